@@ -1,0 +1,310 @@
+#!/usr/bin/env python3
+"""Throughput bench for the Bloom-filter hot path (insert_many + include_many?).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config nstar|1m|100m|10k]
+
+One step = one ``insert_many`` batch + one ``include_many?`` batch of B
+synthetic keys each (key family D: decimal strings of seeded uniform ints,
+bf_100_000_flat.rb:21-22), inputs already resident in HBM, launched through
+the C ABI's device entry points on torch's current stream.  The include?
+batch is 50 % keys of the insert batch and 50 % fresh keys.
+
+Default workload (``nstar``): the north-star filter of BASELINE.json — 1B keys
+at 1 % error, m = 9,585,058,377 bits (1.20 GB), k = 6 — prefilled to 50 % bit
+density, B = 2^24 keys per batch.  It is the configuration the metric's
+"% of HBM random-access roofline" is quoted on; the cache-resident configs
+(1M@1 %, 100M@0.1 %) are reported under ``secondary``.
+
+Multi-GPU (``--gpus N`` under torch.distributed.run): replicated filter, key
+batches sharded per rank (weak scaling).  include? needs no collective; every
+rank's insert batch is all-gathered (RCCL) so all replicas apply every insert.
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402   (imported before libbfhip: one shared HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import pkgload  # noqa: E402
+
+HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md chip table (spec)
+GRANULE = 64               # B per random probe (SURVEY §8 d)
+SEED = 0x5EED
+
+CONFIGS = {
+    # name: (n, error_rate, batch, prefill)
+    "nstar": (10**9, 0.01, 1 << 24, "random"),
+    "100m": (10**8, 0.001, 1 << 24, "random"),
+    "1m": (10**6, 0.01, 1 << 20, "insert"),
+    "10k": (10**4, 0.01, 1 << 14, "insert"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            torch.cuda.set_device(self.local)
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", self.local))
+        else:
+            torch.cuda.set_device(0)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            dist.destroy_process_group()
+
+
+def make_batches(pkg, n_filter: int, batch: int, rank: int):
+    """Insert batch: uniform ints in [0, n); include? batch: half of those + half fresh."""
+    rng = np.random.default_rng([SEED, rank])
+    ins_vals = rng.integers(0, n_filter, size=batch, dtype=np.int64)
+    fresh = rng.integers(n_filter, 2 * n_filter, size=batch - batch // 2, dtype=np.int64)
+    inc_vals = np.concatenate([ins_vals[: batch // 2], fresh])
+    return pkg.keys.pack_decimal(ins_vals), pkg.keys.pack_decimal(inc_vals)
+
+
+def to_dev(buf: np.ndarray, offs: np.ndarray, dev):
+    kb = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
+    ko = torch.from_numpy(offs.view(np.int64)).to(dev)
+    return kb, ko
+
+
+def prefill_random(f, m: int, k: int, rank: int) -> np.ndarray:
+    """50 % bit density over the reachable prefix (a full filter holds 1 - e^{-kn/m} ~ 46.5 %)."""
+    nbytes = (f.reach_bits + 7) // 8
+    rng = np.random.default_rng([SEED, 99, rank])
+    host = np.frombuffer(rng.bytes(nbytes), dtype=np.uint8).copy()
+    tail = f.reach_bits & 7
+    if tail:
+        host[-1] &= (0xFF << (8 - tail)) & 0xFF
+    f.import_redis(host.tobytes() if nbytes < (1 << 20) else memoryview(host))
+    return host
+
+
+def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False):
+    n, p, batch, prefill = CONFIGS[name]
+    B = pkg.Bloomfilter
+    m, k = B.optimal_m(n, p), B.optimal_k(n, B.optimal_m(n, p))
+    dev = torch.device("cuda", D.local)
+    f = pkg.Filter(m, k, device=D.local)
+    t0 = time.time()
+    (ib, io), (pb, po) = make_batches(pkg, n, batch, D.rank)
+    host_bits = None
+    if prefill == "random":
+        host_bits = prefill_random(f, m, k, D.rank)
+    log("[%s] m=%d k=%d batch=%d setup %.1fs" % (name, m, k, batch, time.time() - t0))
+    ikb, iko = to_dev(ib, io, dev)
+    pkb, pko = to_dev(pb, po, dev)
+    out = torch.empty(batch, dtype=torch.uint8, device=dev)
+    gathered = None
+    if D.world > 1:   # replicated mode: every replica applies every rank's inserts
+        gathered = [(torch.empty_like(ikb), torch.empty_like(iko)) for _ in range(D.world)]
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def insert():
+        if gathered is None:
+            f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, stream=sp)
+            return
+        dist.all_gather([g[0] for g in gathered], ikb)
+        dist.all_gather([g[1] for g in gathered], iko)
+        for gk, go in gathered:
+            f.insert_many_dev(gk.data_ptr(), go.data_ptr(), batch, stream=sp)
+
+    def include():
+        f.include_many_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), stream=sp)
+
+    for _ in range(warmup):
+        insert()
+        include()
+    D.barrier()
+    torch.cuda.synchronize()
+    ev = []
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
+        insert()
+        e[1].record(stream)
+        include()
+        e[2].record(stream)
+        ev.append(e)
+    torch.cuda.synchronize()
+    D.barrier()
+    wall = time.perf_counter() - t_start
+    wall = D.max(wall)
+    ins_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    inc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    # sanity: members must all be found (no false negatives)
+    got = out.cpu().numpy()
+    assert got[: batch // 2].all(), "false negative in the include? batch"
+    fp_rate = float(got[batch // 2:].mean())
+    Lmean = float(po[-1]) / batch
+    res = {
+        "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3),
+        "wall_s": wall, "steps": steps,
+        "keys_per_s": 2 * batch * D.world * steps / wall,
+        "insert": {"kernel_ms": ins_ms, "keys_per_s": batch * D.world / (ins_ms / 1e3) if gathered is None
+                   else batch * D.world / (ins_ms / 1e3),
+                   "algo_bytes_per_key": Lmean + 8 + 2 * k * GRANULE},
+        "include": {"kernel_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
+                    "algo_bytes_per_key": Lmean + 8 + 1 + k * GRANULE,
+                    "observed_fp_rate": fp_rate},
+        "bitset_bytes": f.device_bytes,
+    }
+    if want_host:
+        # PCIe-inclusive rate of the host-pointer entry points (H2D keys + D2H answers).
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        f.insert_many(ib, io)
+        t_ins = time.perf_counter() - t
+        t = time.perf_counter()
+        f.include_many(pb, po)
+        t_inc = time.perf_counter() - t
+        res["host_api"] = {"insert_keys_per_s": batch / t_ins, "include_keys_per_s": batch / t_inc}
+    f.close()
+    return res, (ib, io, pb, po, host_bits, m, k)
+
+
+def cpu_baseline(data, budget_s: float = 12.0):
+    """Oracle (C restatement, OpenMP) on the host cores, bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O   # the checker, here the timed CPU baseline ("port")
+    ib, io, pb, po, host_bits, m, k = data
+    orc = O.COracle()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    bits = host_bits.copy() if host_bits is not None else orc.new_bitset(m, k)
+    done = 0
+    t0 = time.perf_counter()
+    n_total = len(io) - 1
+    chunk = 1 << 20
+    i = 0
+    while time.perf_counter() - t0 < budget_s and i < n_total:
+        j = min(i + chunk, n_total)
+        sub_o = io[i:j + 1]
+        orc.insert_many_omp(bits, m, k, ib, sub_o, threads)
+        sub_p = po[i:j + 1]
+        orc.include_many_omp(bits, m, k, pb, sub_p, threads)
+        done += 2 * (j - i)
+        i = j
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "keys/s", "cores": threads, "kind": "port",
+            "sample": "%d insert + %d include? keys (first %d keys of each batch) on the same filter, "
+                      "oracle/bf_oracle.c with OpenMP, %.1f s" % (done // 2, done // 2, done // 2, dt)}
+
+
+def load_traffic(workload: str):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+        return t.get(workload)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="nstar", choices=sorted(CONFIGS))
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    D = Dist()
+    pkg = pkgload.load()
+    main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1))
+    secondary = {}
+    if D.world == 1 and not args.no_secondary:
+        for name in ("1m", "100m"):
+            if name != args.config:
+                r, _ = time_config(pkg, D, name, max(3, args.steps // 2), 1)
+                secondary[name] = {"keys_per_s": r["keys_per_s"],
+                                   "insert_keys_per_s": r["insert"]["keys_per_s"],
+                                   "include_keys_per_s": r["include"]["keys_per_s"],
+                                   "m": r["m"], "k": r["k"], "batch": r["batch"]}
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(data)
+    D.close()
+    if D.rank != 0:
+        return
+
+    ins, inc = main_res["insert"], main_res["include"]
+    dom_name = "insert" if ins["kernel_ms"] >= inc["kernel_ms"] else "include"
+    dom = main_res[dom_name]
+    per_launch_keys = main_res["batch"]
+    algo = dom["algo_bytes_per_key"] * per_launch_keys
+    achieved = algo / (dom["kernel_ms"] / 1e3)
+    traffic = load_traffic(args.config)
+    n, p, batch, _ = CONFIGS[args.config]
+    line = {
+        "metric": "keys/sec (insert, include?) per GPU and whole node; % of HBM random-access roofline",
+        "value": main_res["keys_per_s"],
+        "unit": "keys/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": main_res["wall_s"] / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: decimal-string keys of seeded uniform ints (bf_100_000_flat.rb shape); "
+                "filter prefilled to 50% random bit density",
+        "config": {"workload": "%s: %d keys @ %g error, m=%d bits, k=%d, batch=%d keys insert_many + %d keys "
+                               "include_many? per step (50%% members)" % (args.config, n, p, main_res["m"],
+                                                                          main_res["k"], batch, batch),
+                   "global_batch": 2 * batch * D.world,
+                   "parallelism": "replicated x%d (include? sharded, insert all-gathered)" % D.world
+                   if D.world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                     "traffic": traffic.get(dom_name) if isinstance(traffic, dict) else None,
+                     "algo_bytes_per_key": dom["algo_bytes_per_key"], "keys_per_launch": per_launch_keys,
+                     "kernel_ms": dom["kernel_ms"]},
+        "cpu_baseline": cpu,
+        "ops": {"insert": ins, "include": inc},
+        "host_api": main_res.get("host_api"),
+        "secondary": secondary or None,
+        "reference_published_keys_per_s": {"ruby_insert": 5103, "ruby_include": 4322,
+                                           "lua_insert": 6235, "lua_include": 5712,
+                                           "source": "reference README.md:80-95, 1M items, hardware unstated"},
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

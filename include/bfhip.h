@@ -1,0 +1,117 @@
+/*
+ * bfhip.h — C ABI of libbfhip.so, the MI355X Bloom-filter engine behind
+ * `Redis::Bloomfilter.new(..., driver: 'hip')`.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, and
+ * returns an int status (BF_OK = 0).  No exceptions cross the ABI.  The
+ * library owns device memory and streams; the caller owns every buffer it
+ * passes (read/written during the call only).  Calls on one handle are
+ * serialised by an internal mutex; different handles are independent.
+ *
+ * Reference interface each entry point replaces (paths relative to the
+ * reference repository kontera-technologies/redis-bloomfilter @ 1.1.2):
+ *
+ *   bf_create          Redis::BloomfilterDriver::Ruby#initialize  lib/bloomfilter_driver/ruby.rb:10-12
+ *                      (m = options[:bits], k = options[:hashes] from
+ *                       lib/redis/bloomfilter.rb:27-28)
+ *   bf_destroy         (driver object going out of scope)
+ *   bf_insert_many     Ruby#insert / #set, one key per call          ruby.rb:15-17, 57-63
+ *                      (k pipelined SETBIT; `any_new` = !found, which drives EXPIRE at ruby.rb:62)
+ *   bf_include_many    Ruby#include?                                  ruby.rb:20-30
+ *   bf_indexes_many    Ruby#indexes_for (protected)                   ruby.rb:41-55
+ *   bf_clear           Ruby#clear (DEL key_name)                      ruby.rb:33-35
+ *   bf_export_redis    GET key_name — the Redis string SETBIT builds  ruby.rb:59 (SETBIT layout)
+ *   bf_import_redis    SET key_name — load a string written by the ruby driver
+ *   bf_optimal_m/_k    Redis::Bloomfilter.optimal_m / optimal_k       lib/redis/bloomfilter.rb:50-58
+ *   bf_version         Redis::Bloomfilter.version                     lib/redis/bloomfilter/version.rb:6-8
+ *
+ * Device-resident variants (`*_dev`) take device pointers and a hipStream_t
+ * (as void*, NULL = the handle's stream) and do not synchronise; they are
+ * what bench.py times and what the multi-GPU layer composes.
+ *
+ * Bit layout (identical to the Redis string written by SETBIT): bit offset o
+ * lives in byte o >> 3 under mask 0x80 >> (o & 7).  On the device the bytes
+ * are viewed as little-endian 32-bit words: word o >> 5, mask
+ * 1u << ((o ^ 7) & 31).  Export is therefore a memcpy of the trimmed prefix.
+ */
+#ifndef BFHIP_H
+#define BFHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes */
+#define BF_OK       0
+#define BF_EINVAL   1   /* bad argument: m == 0 (the ref raises ZeroDivisionError at ruby.rb:51), k == 0, NULL */
+#define BF_ENOMEM   2   /* device or host allocation failed */
+#define BF_EDEVICE  3   /* HIP runtime error / no device */
+#define BF_ERCCL    4   /* reserved: collective failure (multi-GPU layer) */
+#define BF_ERANGE   5   /* output buffer too small (bf_export_redis) / string outside the reachable range */
+
+#define BF_MAX_K    64u /* hashes supported per key */
+
+/* ---- import modes */
+#define BF_IMPORT_REPLACE 0u  /* like SET key value            */
+#define BF_IMPORT_OR      1u  /* union with the current filter */
+
+typedef struct bf_handle bf_handle;
+
+typedef struct bf_config {
+    uint32_t struct_size;      /* sizeof(bf_config); 0 => defaults for every field        */
+    int32_t  device;           /* HIP device ordinal; -1 => current device                 */
+    uint64_t batch_keys;       /* keys per internal chunk of host-pointer calls (0 = 1<<22) */
+    uint64_t batch_bytes;      /* key bytes per internal chunk (0 = 64 MiB)                 */
+} bf_config;
+
+/* ---- lifecycle */
+int  bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out);
+int  bf_destroy(bf_handle* h);
+const char* bf_last_error(const bf_handle* h);   /* h == NULL: last error of bf_create on this thread */
+const char* bf_version(void);
+
+/* ---- filter geometry: m, k, and the reachable prefix min(m, k*(2^32-1)+1)
+ *      (ruby.rb:44-51 only ever produces offsets below k*(2^32-1)+1). */
+int  bf_info(const bf_handle* h, uint64_t* m_bits, uint32_t* k, uint64_t* reach_bits,
+             uint64_t* device_bytes);
+
+/* ---- host-pointer batch API.  keys: packed key bytes (`data.to_s`);
+ *      offsets: n+1 byte offsets into key_bytes, key j = [offsets[j], offsets[j+1]).
+ *      offsets[0] need not be 0. */
+int  bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                    uint8_t* any_new /* nullable: 1 iff some bit flipped 0->1 (drives EXPIRE) */,
+                    uint8_t* per_key_new /* nullable, n bytes: 1 iff this key's atomics saw a 0 */);
+int  bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                     uint8_t* out /* n bytes, 0/1 */);
+int  bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                     uint64_t* out /* n*k offsets, key-major */);
+int  bf_clear(bf_handle* h);
+
+/* ---- Redis-string sync.  Export writes the trimmed Redis string (length =
+ *      last nonzero byte + 1, exactly what k SETBITs would have grown the key
+ *      to).  buf == NULL => only *len_out is set.  cap < len => BF_ERANGE. */
+int  bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out);
+int  bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode);
+
+/* ---- device-resident API (device pointers; async on `stream`) */
+int  bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets,
+                        uint64_t n, uint32_t* d_any_new /* nullable: OR-ed with 1 when a bit flips */,
+                        uint8_t* d_per_key_new /* nullable */, void* stream);
+int  bf_include_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets,
+                         uint64_t n, uint8_t* d_out, void* stream);
+int  bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets,
+                         uint64_t n, uint64_t* d_out, void* stream);
+/* The device bitset (Redis byte order, device_bytes long, zero past the reachable prefix). */
+int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
+int  bf_sync(bf_handle* h);
+
+/* ---- sizing helpers with the facade's exact semantics (bloomfilter.rb:50-58) */
+int64_t bf_optimal_m(double n, double error_rate);
+int64_t bf_optimal_k(int64_t n, int64_t m_bits);     /* Integer n: floor division, 0 -> 1 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BFHIP_H */

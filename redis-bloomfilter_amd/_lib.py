@@ -1,0 +1,282 @@
+"""ctypes binding of libbfhip.so (the C ABI in include/bfhip.h).
+
+This is the only way the package reaches the engine: there is no CPU
+fallback.  If the shared library is missing or fails to load, importing the
+driver raises ``BfHipUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+import threading
+from typing import Optional, Tuple
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_LIB = os.path.join(PKG_DIR, "lib", "libbfhip.so")
+
+BF_OK, BF_EINVAL, BF_ENOMEM, BF_EDEVICE, BF_ERCCL, BF_ERANGE = 0, 1, 2, 3, 4, 5
+BF_IMPORT_REPLACE, BF_IMPORT_OR = 0, 1
+BF_MAX_K = 64
+
+_STATUS = {BF_EINVAL: "BF_EINVAL", BF_ENOMEM: "BF_ENOMEM", BF_EDEVICE: "BF_EDEVICE",
+           BF_ERCCL: "BF_ERCCL", BF_ERANGE: "BF_ERANGE"}
+
+
+class BfHipUnavailable(ImportError):
+    """libbfhip.so could not be loaded (not built, or no HIP runtime)."""
+
+
+class BfHipError(RuntimeError):
+    """A non-argument failure reported by the engine (device, memory, collective)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__("%s: %s" % (_STATUS.get(code, "BF_E%d" % code), msg))
+        self.code = code
+
+
+class ArgumentError(ValueError):
+    """Mirror of Ruby's ArgumentError (raised where the reference raises it)."""
+
+
+class bf_config(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("batch_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64)]
+
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+
+# name -> (restype, argtypes); must list every function declared in include/bfhip.h
+SIGNATURES = {
+    "bf_create": (ctypes.c_int, [_u64, _u32, ctypes.POINTER(bf_config), ctypes.POINTER(_vp)]),
+    "bf_destroy": (ctypes.c_int, [_vp]),
+    "bf_last_error": (ctypes.c_char_p, [_vp]),
+    "bf_version": (ctypes.c_char_p, []),
+    "bf_info": (ctypes.c_int, [_vp, _u64p, _u32p, _u64p, _u64p]),
+    "bf_insert_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u8p, _vp]),
+    "bf_include_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "bf_indexes_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "bf_clear": (ctypes.c_int, [_vp]),
+    "bf_export_redis": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
+    "bf_import_redis": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
+    "bf_insert_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "bf_include_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_indexes_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_device_bits": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), _u64p]),
+    "bf_sync": (ctypes.c_int, [_vp]),
+    "bf_optimal_m": (ctypes.c_int64, [ctypes.c_double, ctypes.c_double]),
+    "bf_optimal_k": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return os.environ.get("BFHIP_LIB", DEFAULT_LIB)
+
+
+def _share_torch_runtime() -> None:
+    """Make libbfhip bind to the HIP runtime PyTorch-ROCm already uses.
+
+    torch ships its own ``libamdhip64.so`` (SONAME ``libamdhip64.so.7``) and
+    links it by the unversioned name.  If libbfhip is loaded first, the system
+    runtime comes in under that SONAME and torch later maps a SECOND runtime,
+    after which torch sees no GPU.  Loading torch first lets the dynamic
+    loader satisfy libbfhip's ``libamdhip64.so.7`` with torch's copy: one
+    runtime, shared streams and device pointers.  BFHIP_STANDALONE=1 skips this
+    (e.g. a process that never imports torch).
+    """
+    if os.environ.get("BFHIP_STANDALONE") == "1" or "torch" in sys.modules:
+        return
+    import importlib.util
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
+def load() -> ctypes.CDLL:
+    """Load libbfhip.so once; raise BfHipUnavailable if it cannot be loaded."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        _share_torch_runtime()
+        path = lib_path()
+        if not os.path.exists(path):
+            raise BfHipUnavailable(
+                "libbfhip.so not found at %s — build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (or `make -C redis-bloomfilter_amd/csrc`)" % path)
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:  # missing HIP runtime etc.
+            raise BfHipUnavailable("cannot load %s: %s" % (path, e)) from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def version() -> str:
+    return load().bf_version().decode()
+
+
+def optimal_m(n, error_rate) -> int:
+    return int(load().bf_optimal_m(float(n), float(error_rate)))
+
+
+def optimal_k(n: int, m: int) -> int:
+    return int(load().bf_optimal_k(int(n), int(m)))
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    return a.ctypes.data
+
+
+def _check(code: int, h=None) -> None:
+    if code == BF_OK:
+        return
+    lib = load()
+    msg = lib.bf_last_error(h).decode(errors="replace") if lib else ""
+    if code in (BF_EINVAL, BF_ERANGE):
+        raise ArgumentError("%s: %s" % (_STATUS.get(code), msg))
+    raise BfHipError(code, msg)
+
+
+class Filter:
+    """One device-resident filter (a `bf_handle*`).
+
+    Arrays are numpy: ``keys`` uint8, ``offsets`` uint64 with n+1 entries.
+    The ``*_dev`` methods take raw device addresses (ints), e.g. from
+    ``torch.Tensor.data_ptr()``, and a stream handle (int, 0 = the filter's
+    own stream).
+    """
+
+    def __init__(self, m_bits: int, k: int, device: int = -1, batch_keys: int = 0,
+                 batch_bytes: int = 0):
+        self._lib = load()
+        cfg = bf_config(ctypes.sizeof(bf_config), int(device), int(batch_keys), int(batch_bytes))
+        h = _vp()
+        rc = self._lib.bf_create(int(m_bits), int(k), ctypes.byref(cfg), ctypes.byref(h))
+        _check(rc, None)
+        self._h = h
+        m = ctypes.c_uint64()
+        kk = ctypes.c_uint32()
+        reach = ctypes.c_uint64()
+        devb = ctypes.c_uint64()
+        _check(self._lib.bf_info(h, ctypes.byref(m), ctypes.byref(kk), ctypes.byref(reach),
+                                 ctypes.byref(devb)), h)
+        self.m, self.k, self.reach_bits, self.device_bytes = m.value, kk.value, reach.value, devb.value
+        self.device = int(device)
+
+    # -- lifecycle
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.bf_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        if not self._h:
+            raise ArgumentError("filter is closed")
+        return self._h
+
+    # -- host-pointer batch API
+    @staticmethod
+    def _keys(keys: np.ndarray, offsets: np.ndarray) -> Tuple[np.ndarray, np.ndarray, int]:
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if offsets.ndim != 1 or len(offsets) < 1:
+            raise ArgumentError("offsets must be a 1-D array of n+1 entries")
+        n = len(offsets) - 1
+        if n and int(offsets[-1]) > len(keys):
+            raise ArgumentError("offsets point past the key buffer")
+        if len(keys) == 0:
+            keys = np.zeros(1, np.uint8)
+        return keys, offsets, n
+
+    def insert_many(self, keys: np.ndarray, offsets: np.ndarray, any_new: bool = False,
+                    per_key_new: bool = False):
+        keys, offsets, n = self._keys(keys, offsets)
+        flag = ctypes.c_uint8(0)
+        pk = np.zeros(max(n, 1), np.uint8) if per_key_new else None
+        _check(self._lib.bf_insert_many(self.handle, _ptr(keys), _ptr(offsets), n,
+                                        ctypes.byref(flag) if any_new else None, _ptr(pk)), self._h)
+        return (bool(flag.value) if any_new else None), (pk[:n] if per_key_new else None)
+
+    def include_many(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        keys, offsets, n = self._keys(keys, offsets)
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(self._lib.bf_include_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(out)), self._h)
+        return out[:n]
+
+    def indexes_many(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        keys, offsets, n = self._keys(keys, offsets)
+        out = np.zeros(max(n * self.k, 1), np.uint64)
+        _check(self._lib.bf_indexes_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(out)), self._h)
+        return out[: n * self.k].reshape(n, self.k)
+
+    def clear(self) -> None:
+        _check(self._lib.bf_clear(self.handle), self._h)
+
+    def sync(self) -> None:
+        _check(self._lib.bf_sync(self.handle), self._h)
+
+    # -- Redis string
+    def export_redis(self) -> bytes:
+        n = ctypes.c_uint64(0)
+        _check(self._lib.bf_export_redis(self.handle, None, 0, ctypes.byref(n)), self._h)
+        buf = np.zeros(max(n.value, 1), np.uint8)
+        _check(self._lib.bf_export_redis(self.handle, _ptr(buf), len(buf), ctypes.byref(n)), self._h)
+        return buf[: n.value].tobytes()
+
+    def redis_len(self) -> int:
+        n = ctypes.c_uint64(0)
+        _check(self._lib.bf_export_redis(self.handle, None, 0, ctypes.byref(n)), self._h)
+        return n.value
+
+    def import_redis(self, data: bytes, mode: int = BF_IMPORT_REPLACE) -> None:
+        buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+        _check(self._lib.bf_import_redis(self.handle, _ptr(buf), len(data), int(mode)), self._h)
+
+    # -- device-resident API
+    def insert_many_dev(self, d_keys: int, d_offsets: int, n: int, d_any_new: int = 0,
+                        d_per_key_new: int = 0, stream: int = 0) -> None:
+        _check(self._lib.bf_insert_many_dev(self.handle, d_keys, d_offsets, int(n), d_any_new or None,
+                                            d_per_key_new or None, stream or None), self._h)
+
+    def include_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream: int = 0) -> None:
+        _check(self._lib.bf_include_many_dev(self.handle, d_keys, d_offsets, int(n), d_out,
+                                             stream or None), self._h)
+
+    def indexes_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream: int = 0) -> None:
+        _check(self._lib.bf_indexes_many_dev(self.handle, d_keys, d_offsets, int(n), d_out,
+                                             stream or None), self._h)
+
+    def device_bits(self) -> Tuple[int, int]:
+        p = _vp()
+        nb = ctypes.c_uint64()
+        _check(self._lib.bf_device_bits(self.handle, ctypes.byref(p), ctypes.byref(nb)), self._h)
+        return int(p.value or 0), int(nb.value)

@@ -1,0 +1,496 @@
+// bf_api.cpp — the C ABI declared in include/bfhip.h.
+//
+// Owns the device bitset (one HIP device per handle), a HIP stream, and two
+// staging slots (pinned host + device) used by the host-pointer calls so that
+// packing chunk c+1 on the host overlaps the device work of chunk c.
+#include "bfhip.h"
+#include "bf_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#define BFHIP_VERSION_STR "bfhip 0.1.0 (gfx950; redis-bloomfilter 1.1.2 ruby-driver layout)"
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Slot {
+    uint8_t*  h_keys = nullptr;   // pinned
+    uint64_t* h_off = nullptr;    // pinned, cap_keys + 1
+    uint8_t*  h_out = nullptr;    // pinned, cap_keys (per-key bytes) or cap_keys*k*8 (indexes)
+    uint8_t*  d_keys = nullptr;
+    uint64_t* d_off = nullptr;
+    uint8_t*  d_out = nullptr;
+    uint64_t  cap_bytes = 0;
+    hipEvent_t done = nullptr;
+    // pending result copy-out
+    bool      busy = false;
+    uint8_t*  user_out = nullptr;
+    uint64_t  out_bytes = 0;
+};
+
+}  // namespace
+
+struct bf_handle {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    BfGeom g{};
+    uint64_t m = 0, reach = 0, dev_bytes = 0;
+    uint32_t k = 0;
+    uint64_t cap_keys = 0, cap_bytes = 0;
+    Slot slot[2];
+    bool staging_ready = false;
+    uint32_t* d_flag = nullptr;
+    unsigned long long* d_scan = nullptr;
+    uint32_t* h_flag = nullptr;   // pinned
+    std::string err;
+};
+
+namespace {
+
+int set_err(bf_handle* h, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf; else g_create_error = buf;
+    return code;
+}
+
+#define HIPCHK(h, expr)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err((h), (e_ == hipErrorOutOfMemory ? BF_ENOMEM : BF_EDEVICE),        \
+                           "%s failed: %s", #expr, hipGetErrorString(e_));                   \
+    } while (0)
+
+// Makes the handle's device current for the duration of a call.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = (prev == dev) || hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+int free_staging(bf_handle* h) {
+    for (Slot& s : h->slot) {
+        if (s.done) (void)hipEventSynchronize(s.done);
+        if (s.h_keys) (void)hipHostFree(s.h_keys);
+        if (s.h_off) (void)hipHostFree(s.h_off);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_keys) (void)hipFree(s.d_keys);
+        if (s.d_off) (void)hipFree(s.d_off);
+        if (s.d_out) (void)hipFree(s.d_out);
+        if (s.done) (void)hipEventDestroy(s.done);
+        s = Slot{};
+    }
+    h->staging_ready = false;
+    return BF_OK;
+}
+
+int ensure_staging(bf_handle* h, uint64_t need_bytes) {
+    if (h->staging_ready && h->slot[0].cap_bytes >= need_bytes) return BF_OK;
+    free_staging(h);
+    const uint64_t cap_bytes = round_up(std::max(h->cap_bytes, need_bytes), 4096) + 64;
+    const uint64_t outb = h->cap_keys;   // 1 byte per key; indexes use fewer keys per chunk
+    for (Slot& s : h->slot) {
+        HIPCHK(h, hipHostMalloc((void**)&s.h_keys, cap_bytes, hipHostMallocDefault));
+        HIPCHK(h, hipHostMalloc((void**)&s.h_off, (h->cap_keys + 1) * sizeof(uint64_t), hipHostMallocDefault));
+        HIPCHK(h, hipHostMalloc((void**)&s.h_out, outb, hipHostMallocDefault));
+        HIPCHK(h, hipMalloc((void**)&s.d_keys, cap_bytes));
+        HIPCHK(h, hipMalloc((void**)&s.d_off, (h->cap_keys + 1) * sizeof(uint64_t)));
+        HIPCHK(h, hipMalloc((void**)&s.d_out, outb));
+        HIPCHK(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        s.cap_bytes = cap_bytes - 64;
+    }
+    h->staging_ready = true;
+    return BF_OK;
+}
+
+// Waits for a slot's previous chunk and copies its results to the caller.
+int retire_slot(bf_handle* h, Slot& s) {
+    if (!s.busy) return BF_OK;
+    HIPCHK(h, hipEventSynchronize(s.done));
+    if (s.user_out && s.out_bytes) memcpy(s.user_out, s.h_out, s.out_bytes);
+    s.busy = false;
+    s.user_out = nullptr;
+    s.out_bytes = 0;
+    return BF_OK;
+}
+
+int check_keys_args(bf_handle* h, const void* keys, const uint64_t* offsets, uint64_t n) {
+    if (!h) return BF_EINVAL;
+    if (n == 0) return BF_OK;
+    if (!offsets) return set_err(h, BF_EINVAL, "offsets is NULL");
+    if (!keys && offsets[n] != offsets[0]) return set_err(h, BF_EINVAL, "key_bytes is NULL");
+    return BF_OK;
+}
+
+// Host-pointer driver: chunk, stage, launch, copy results back.
+int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets, uint64_t n,
+             uint8_t* out8, uint64_t* out64, uint8_t* any_new) {
+    int rc = check_keys_args(h, keys, offsets, n);
+    if (rc) return rc;
+    for (uint64_t j = 0; j < n; ++j)
+        if (offsets[j + 1] < offsets[j]) return set_err(h, BF_EINVAL, "offsets must be non-decreasing (j=%llu)", (unsigned long long)j);
+    if (any_new) *any_new = 0;
+    if (n == 0) return BF_OK;
+
+    // Largest single key decides the minimum stage size.
+    uint64_t maxkey = 0;
+    for (uint64_t j = 0; j < n; ++j) maxkey = std::max(maxkey, offsets[j + 1] - offsets[j]);
+    rc = ensure_staging(h, maxkey);
+    if (rc) return rc;
+
+    uint64_t keys_per_chunk = h->cap_keys;
+    if (op == BF_OP_INDEXES) keys_per_chunk = std::max<uint64_t>(1, h->cap_keys / ((uint64_t)h->k * 8));
+    const bool want_flag = (op == BF_OP_INSERT_FLAGS) && any_new;
+    if (want_flag) HIPCHK(h, hipMemsetAsync(h->d_flag, 0, sizeof(uint32_t), h->stream));
+
+    uint64_t i = 0;
+    int c = 0;
+    while (i < n) {
+        Slot& s = h->slot[c & 1];
+        rc = retire_slot(h, s);
+        if (rc) return rc;
+        // chunk [i, j): at most keys_per_chunk keys and s.cap_bytes bytes
+        uint64_t jmax = std::min(n, i + keys_per_chunk);
+        const uint64_t base = offsets[i];
+        uint64_t j;
+        if (offsets[jmax] - base <= s.cap_bytes) {
+            j = jmax;
+        } else {  // binary search the last j with offsets[j] - base <= cap
+            uint64_t lo = i + 1, hi = jmax;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi + 1) / 2;
+                if (offsets[mid] - base <= s.cap_bytes) lo = mid; else hi = mid - 1;
+            }
+            j = lo;
+        }
+        const uint64_t cn = j - i;
+        const uint64_t nbytes = offsets[j] - base;
+        if (nbytes) memcpy(s.h_keys, keys + base, nbytes);
+        memset(s.h_keys + nbytes, 0, 16);
+        memcpy(s.h_off, offsets + i, (cn + 1) * sizeof(uint64_t));
+        HIPCHK(h, hipMemcpyAsync(s.d_keys, s.h_keys, round_up(nbytes + 1, 16), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(s.d_off, s.h_off, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+        uint8_t* d_out8 = (op == BF_OP_INCLUDE || (op == BF_OP_INSERT_FLAGS && out8)) ? s.d_out : nullptr;
+        uint64_t* d_out64 = (op == BF_OP_INDEXES) ? reinterpret_cast<uint64_t*>(s.d_out) : nullptr;
+        HIPCHK(h, bf_launch_keys(op, h->g, s.d_keys, s.d_off, (uint64_t)0 - base, cn, d_out8, d_out64,
+                                 want_flag ? h->d_flag : nullptr, h->stream));
+        s.out_bytes = 0;
+        s.user_out = nullptr;
+        if (d_out8 && out8) {
+            s.out_bytes = cn;
+            s.user_out = out8 + i;
+        } else if (d_out64 && out64) {
+            s.out_bytes = cn * h->k * sizeof(uint64_t);
+            s.user_out = reinterpret_cast<uint8_t*>(out64 + i * h->k);
+        }
+        if (s.out_bytes) HIPCHK(h, hipMemcpyAsync(s.h_out, s.d_out, s.out_bytes, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipEventRecord(s.done, h->stream));
+        s.busy = true;
+        i = j;
+        ++c;
+    }
+    for (Slot& s : h->slot) {
+        rc = retire_slot(h, s);
+        if (rc) return rc;
+    }
+    if (want_flag) {
+        HIPCHK(h, hipMemcpyAsync(h->h_flag, h->d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        *any_new = *h->h_flag ? 1 : 0;
+    }
+    return BF_OK;
+}
+
+hipStream_t pick_stream(bf_handle* h, void* stream) {
+    return stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+}
+
+// Device pointer + 16-byte alignment bias for the kernels.
+const uint8_t* align_keys(const uint8_t* p, uint64_t* bias) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    *bias = a & 15u;
+    return reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
+}
+
+int run_dev(bf_handle* h, BfOp op, const uint8_t* d_keys, const uint64_t* d_offsets, uint64_t n,
+            uint8_t* d_out8, uint64_t* d_out64, uint32_t* d_flag, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (n == 0) return BF_OK;
+    if (!d_offsets || !d_keys) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (op == BF_OP_INCLUDE && !d_out8) return set_err(h, BF_EINVAL, "d_out is NULL");
+    if (op == BF_OP_INDEXES && !d_out64) return set_err(h, BF_EINVAL, "d_out is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    uint64_t bias = 0;
+    const uint8_t* k16 = align_keys(d_keys, &bias);
+    HIPCHK(h, bf_launch_keys(op, h->g, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, pick_stream(h, stream)));
+    return BF_OK;
+}
+
+}  // namespace
+
+// ===================================================================== ABI ==
+extern "C" {
+
+const char* bf_version(void) { return BFHIP_VERSION_STR; }
+
+const char* bf_last_error(const bf_handle* h) {
+    return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int64_t bf_optimal_m(double n, double p) {
+    // lib/redis/bloomfilter.rb:50-52 — left-to-right IEEE double, Float#round (half away from zero).
+    const double v = (-1.0 * n) * std::log(p) / std::pow(std::log(2.0), 2.0);
+    return (int64_t)std::round(v);
+}
+
+int64_t bf_optimal_k(int64_t n, int64_t m) {
+    // lib/redis/bloomfilter.rb:54-58 — Integer floor division, bumped to 1 when 0.
+    if (n == 0) return 0;
+    int64_t q = m / n;
+    if ((m % n != 0) && ((m < 0) != (n < 0))) --q;
+    int64_t h = (int64_t)std::round(std::log(2.0) * (double)q);
+    if (h == 0) h += 1;
+    return h;
+}
+
+int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out) {
+    g_create_error.clear();
+    if (!out) return set_err(nullptr, BF_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (m_bits == 0) return set_err(nullptr, BF_EINVAL, "m_bits == 0 (the ruby driver would raise ZeroDivisionError, ruby.rb:51)");
+    if (k == 0 || k > BF_MAX_K) return set_err(nullptr, BF_EINVAL, "k must be in [1, %u], got %u", BF_MAX_K, k);
+    bf_config c{};
+    if (cfg && cfg->struct_size) {
+        memcpy(&c, cfg, std::min<size_t>(sizeof c, cfg->struct_size));
+    } else {
+        c.device = -1;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(nullptr, BF_EDEVICE, "no HIP device available");
+    int dev = c.device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev >= ndev) return set_err(nullptr, BF_EINVAL, "device %d out of range (%d devices)", dev, ndev);
+
+    bf_handle* h = new (std::nothrow) bf_handle();
+    if (!h) return set_err(nullptr, BF_ENOMEM, "host allocation failed");
+    h->device = dev;
+    h->m = m_bits;
+    h->k = k;
+    const uint64_t maxval = (uint64_t)k * 0xFFFFFFFFull;      // largest offset ruby.rb:51 can produce
+    h->reach = std::min<uint64_t>(m_bits, maxval + 1);
+    h->dev_bytes = round_up((h->reach + 7) / 8, 256);
+    h->cap_keys = c.batch_keys ? c.batch_keys : (1ull << 22);
+    h->cap_bytes = c.batch_bytes ? c.batch_bytes : (64ull << 20);
+
+    DeviceGuard dg(dev);
+    auto fail = [&](int code, const char* what, hipError_t e) {
+        set_err(nullptr, code, "%s: %s", what, hipGetErrorString(e));
+        if (h->g.bits) (void)hipFree(h->g.bits);
+        if (h->d_flag) (void)hipFree(h->d_flag);
+        if (h->d_scan) (void)hipFree(h->d_scan);
+        if (h->h_flag) (void)hipHostFree(h->h_flag);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+        delete h;
+        return code;
+    };
+    if (!dg.ok) return fail(BF_EDEVICE, "hipSetDevice", hipErrorInvalidDevice);
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(BF_EDEVICE, "hipStreamCreate", e);
+    if ((e = hipMalloc((void**)&h->g.bits, h->dev_bytes)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(bitset)", e);
+    if ((e = hipMalloc((void**)&h->d_flag, 256)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(flag)", e);
+    if ((e = hipMalloc((void**)&h->d_scan, 256)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(scan)", e);
+    if ((e = hipHostMalloc((void**)&h->h_flag, 64, hipHostMallocDefault)) != hipSuccess) return fail(BF_ENOMEM, "hipHostMalloc", e);
+    if ((e = hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream)) != hipSuccess) return fail(BF_EDEVICE, "hipMemset", e);
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(BF_EDEVICE, "hipStreamSynchronize", e);
+    h->g.m = m_bits;
+    h->g.inv_m = 1.0 / (double)m_bits;
+    h->g.k = k;
+    h->g.nomod = (m_bits > maxval) ? 1u : 0u;
+    *out = h;
+    return BF_OK;
+}
+
+int bf_destroy(bf_handle* h) {
+    if (!h) return BF_OK;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceGuard dg(h->device);
+        if (h->stream) (void)hipStreamSynchronize(h->stream);
+        free_staging(h);
+        if (h->g.bits) (void)hipFree(h->g.bits);
+        if (h->d_flag) (void)hipFree(h->d_flag);
+        if (h->d_scan) (void)hipFree(h->d_scan);
+        if (h->h_flag) (void)hipHostFree(h->h_flag);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+    }
+    delete h;
+    return BF_OK;
+}
+
+int bf_info(const bf_handle* h, uint64_t* m_bits, uint32_t* k, uint64_t* reach_bits, uint64_t* device_bytes) {
+    if (!h) return BF_EINVAL;
+    if (m_bits) *m_bits = h->m;
+    if (k) *k = h->k;
+    if (reach_bits) *reach_bits = h->reach;
+    if (device_bytes) *device_bytes = h->dev_bytes;
+    return BF_OK;
+}
+
+int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                   uint8_t* any_new, uint8_t* per_key_new) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    const BfOp op = (any_new || per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
+    int rc = run_host(h, op, key_bytes, offsets, n, per_key_new, nullptr, any_new);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n, uint8_t* out) {
+    if (!h) return BF_EINVAL;
+    if (n && !out) return set_err(h, BF_EINVAL, "out is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    return run_host(h, BF_OP_INCLUDE, key_bytes, offsets, n, out, nullptr, nullptr);
+}
+
+int bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n, uint64_t* out) {
+    if (!h) return BF_EINVAL;
+    if (n && !out) return set_err(h, BF_EINVAL, "out is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    return run_host(h, BF_OP_INDEXES, key_bytes, offsets, n, nullptr, out, nullptr);
+}
+
+int bf_clear(bf_handle* h) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+int bf_sync(bf_handle* h) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+int bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+    if (!h || !len_out) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    HIPCHK(h, hipMemsetAsync(h->d_scan, 0, sizeof(unsigned long long), h->stream));
+    HIPCHK(h, bf_launch_last_nonzero(h->g.bits, h->dev_bytes / 4, h->d_scan, h->stream));
+    unsigned long long last = 0;
+    HIPCHK(h, hipMemcpyAsync(h->h_flag, h->d_scan, sizeof last, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    memcpy(&last, h->h_flag, sizeof last);
+    uint64_t len = 0;
+    if (last) {
+        const uint64_t w = last - 1;   // index of the last nonzero 32-bit word
+        uint32_t word = 0;
+        HIPCHK(h, hipMemcpy(&word, h->g.bits + w, 4, hipMemcpyDeviceToHost));
+        int top = 3;
+        while (top > 0 && ((word >> (8 * top)) & 0xFFu) == 0) --top;
+        len = w * 4 + (uint64_t)top + 1;
+    }
+    *len_out = len;
+    if (!buf) return BF_OK;
+    if (cap < len) return set_err(h, BF_ERANGE, "export buffer too small: need %llu bytes", (unsigned long long)len);
+    if (len) HIPCHK(h, hipMemcpy(buf, h->g.bits, len, hipMemcpyDeviceToHost));
+    return BF_OK;
+}
+
+int bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode) {
+    if (!h) return BF_EINVAL;
+    if (mode != BF_IMPORT_REPLACE && mode != BF_IMPORT_OR) return set_err(h, BF_EINVAL, "bad import mode %u", mode);
+    if (len && !buf) return set_err(h, BF_EINVAL, "buf is NULL");
+    const uint64_t max_bytes = (h->reach + 7) / 8;
+    if (len > max_bytes)
+        return set_err(h, BF_ERANGE, "string of %llu bytes exceeds the filter's %llu reachable bytes",
+                       (unsigned long long)len, (unsigned long long)max_bytes);
+    if (len == max_bytes && (h->reach & 7)) {
+        const uint8_t beyond = (uint8_t)(0xFFu >> (h->reach & 7));
+        if (buf[len - 1] & beyond) return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)h->reach);
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    if (mode == BF_IMPORT_REPLACE) {
+        HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (len) HIPCHK(h, hipMemcpy(h->g.bits, buf, len, hipMemcpyHostToDevice));
+        return BF_OK;
+    }
+    if (!len) return BF_OK;
+    const uint64_t tb = round_up(len, 256);
+    uint32_t* tmp = nullptr;
+    HIPCHK(h, hipMalloc((void**)&tmp, tb));
+    hipError_t e = hipMemsetAsync(tmp, 0, tb, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipMemcpy(tmp, buf, len, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = bf_launch_or(h->g.bits, tmp, tb / 4, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return set_err(h, BF_EDEVICE, "import OR failed: %s", hipGetErrorString(e));
+    return BF_OK;
+}
+
+int bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                       uint32_t* d_any_new, uint8_t* d_per_key_new, void* stream) {
+    const BfOp op = (d_any_new || d_per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
+    return run_dev(h, op, d_key_bytes, d_offsets, n, d_per_key_new, nullptr, d_any_new, stream);
+}
+
+int bf_include_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                        uint8_t* d_out, void* stream) {
+    return run_dev(h, BF_OP_INCLUDE, d_key_bytes, d_offsets, n, d_out, nullptr, nullptr, stream);
+}
+
+int bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                        uint64_t* d_out, void* stream) {
+    return run_dev(h, BF_OP_INDEXES, d_key_bytes, d_offsets, n, nullptr, d_out, nullptr, stream);
+}
+
+int bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes) {
+    if (!h) return BF_EINVAL;
+    if (d_bits) *d_bits = h->g.bits;
+    if (device_bytes) *device_bytes = h->dev_bytes;
+    return BF_OK;
+}
+
+}  // extern "C"

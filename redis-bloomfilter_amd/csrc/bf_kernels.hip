@@ -1,0 +1,292 @@
+// bf_kernels.hip — CDNA4 (gfx950) kernels for the Bloom-filter hot path.
+//
+// One lane per key.  A 256-lane workgroup owns 256 consecutive keys:
+//   1. the 257 offsets are read coalesced into LDS;
+//   2. the workgroup's packed key bytes [off[0], off[256]) are staged into LDS
+//      with 16-byte coalesced loads (fallback: per-lane global reads when the
+//      span exceeds the 16 KiB stage);
+//   3. each lane builds its big-endian SHA-1 message words from LDS with
+//      v_alignbyte + v_perm (byte swap) and runs the 80-round compression
+//      (single block for keys <= 55 bytes, the generic multi-block loop otherwise);
+//   4. the k offsets follow ruby.rb:41-55 exactly:
+//        idx_i = (h[i%2] + i*h[2 + (((i + i%2) % 4) / 2)]) mod m
+//      with the modulo done by a double-precision reciprocal + one correction
+//      (no integer divide on the GPU), skipped entirely when m > k*(2^32-1);
+//   5. the op: gather k words and AND (include?), atomic-OR k words (insert),
+//      or store the offsets (indexes_for).
+//
+// Bit o of the filter is bit ((o ^ 7) & 31) of little-endian word o >> 5, i.e.
+// byte o >> 3 under mask 0x80 >> (o & 7) — the Redis SETBIT layout, so the
+// device buffer IS the Redis string.
+#include "bf_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;             // lanes per workgroup = keys per workgroup
+constexpr int kStageBytes = 16384;      // LDS key stage per workgroup
+constexpr int kStageVec = kStageBytes / 16;
+constexpr int kChunk = 8;               // probes issued together per key
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
+
+// FIPS 180-4 SHA-1 compression of one 16-word block; w[] is consumed as the
+// circular message schedule.  Fully unrolled so every w index is static.
+__device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        uint32_t f, kk;
+        if (t < 20)      { f = d ^ (b & (c ^ d));           kk = 0x5A827999u; }  // Ch  -> v_bfi
+        else if (t < 40) { f = b ^ c ^ d;                   kk = 0x6ED9EBA1u; }  // Parity -> v_xor3
+        else if (t < 60) { f = (b & c) | (d & (b | c));     kk = 0x8F1BBCDCu; }  // Maj
+        else             { f = b ^ c ^ d;                   kk = 0xCA62C1D6u; }
+        const uint32_t tmp = rotl(a, 5) + f + e + kk + wt;
+        e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// Word `wi` (big-endian) of the SHA-1-padded message of a key of L bytes whose
+// first byte sits at byte position s of the 32-bit word array `src`.
+template <typename Src>
+__device__ __forceinline__ uint32_t msg_word(Src src, uint32_t s, uint32_t L, uint32_t wi,
+                                             uint32_t total_words) {
+    if (wi == total_words - 1) return L << 3;   // bit length, low word
+    if (wi == total_words - 2) return L >> 29;  // bit length, high word
+    const int valid = (int)L - (int)(4u * wi);  // key bytes left at this word
+    uint32_t x = 0;
+    if (valid > 0) {
+        const uint32_t a = s + 4u * wi;
+        const uint32_t lo = src[a >> 2];
+        const uint32_t hi = src[(a >> 2) + 1];
+        x = __builtin_amdgcn_alignbyte(hi, lo, a & 3u);  // bytes a..a+3, little-endian
+    }
+    if (valid < 4) {
+        if (valid >= 0) {
+            x &= (valid == 0) ? 0u : (0xFFFFFFFFu >> (8 * (4 - valid)));
+            x |= 0x80u << (8 * valid);                // the FIPS padding byte
+        } else {
+            x = 0u;
+        }
+    }
+    return __builtin_bswap32(x);
+}
+
+template <typename Src>
+__device__ __forceinline__ void sha1_key(Src src, uint32_t s, uint32_t L, uint32_t H[5]) {
+    H[0] = 0x67452301u; H[1] = 0xEFCDAB89u; H[2] = 0x98BADCFEu; H[3] = 0x10325476u; H[4] = 0xC3D2E1F0u;
+    const uint32_t nblk = (L + 8u) / 64u + 1u;
+    const uint32_t total = nblk * 16u;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = msg_word(src, s, L, b * 16u + j, total);
+        sha1_compress(H, w);
+    }
+}
+
+// ruby.rb:50-53 for probe i, reduced mod m without an integer divide.
+__device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, uint32_t h1,
+                                                 uint32_t h2, uint32_t h3, uint32_t i) {
+    const uint32_t a = (i & 1u) ? h1 : h0;
+    const uint32_t b = (((i + (i & 1u)) & 3u) >> 1) ? h3 : h2;
+    const uint64_t v = (uint64_t)a + (uint64_t)i * (uint64_t)b;  // < k * 2^32: exact
+    if (g.nomod) return v;
+    // q within +-1 of floor(v/m): v < 2^38 is exact in a double, 1/m carries 2^-53 relative error.
+    const uint64_t q = (uint64_t)((double)v * g.inv_m);
+    int64_t r = (int64_t)(v - q * g.m);
+    if (r < 0) r += (int64_t)g.m;
+    else if ((uint64_t)r >= g.m) r -= (int64_t)g.m;
+    return (uint64_t)r;
+}
+
+template <int OP, typename Src>
+__device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uint32_t L,
+                                       uint64_t key, uint8_t* __restrict__ out8,
+                                       uint64_t* __restrict__ out64, uint32_t& newflag) {
+    uint32_t H[5];
+    sha1_key(src, s, L, H);
+    const uint32_t k = g.k;
+    if constexpr (OP == BF_OP_INDEXES) {
+        for (uint32_t i = 0; i < k; ++i)
+            out64[key * k + i] = probe_offset(g, H[0], H[1], H[2], H[3], i);
+    } else if constexpr (OP == BF_OP_INCLUDE) {
+        uint32_t ok = 1u;
+        for (uint32_t i0 = 0; i0 < k; i0 += kChunk) {
+            uint32_t v[kChunk], sh[kChunk];
+#pragma unroll
+            for (int c = 0; c < kChunk; ++c) {   // issue every load of the chunk first
+                v[c] = 0xFFFFFFFFu; sh[c] = 0;
+                if (i0 + c < k) {
+                    const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + c);
+                    sh[c] = (uint32_t)(o ^ 7u) & 31u;
+                    v[c] = g.bits[o >> 5];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kChunk; ++c) ok &= v[c] >> sh[c];
+        }
+        out8[key] = (uint8_t)(ok & 1u);
+    } else {
+        uint32_t isnew = 0;
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i);
+            const uint32_t mask = 1u << ((uint32_t)(o ^ 7u) & 31u);
+            if constexpr (OP == BF_OP_INSERT_FLAGS) {
+                const uint32_t old = __hip_atomic_fetch_or(g.bits + (o >> 5), mask, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                isnew |= (old & mask) ? 0u : 1u;
+            } else {
+                __hip_atomic_fetch_or(g.bits + (o >> 5), mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if constexpr (OP == BF_OP_INSERT_FLAGS) {
+            if (out8) out8[key] = (uint8_t)isnew;
+            newflag = isnew;
+        }
+    }
+}
+
+template <int OP>
+__global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+                                                         const uint64_t* __restrict__ offsets,
+                                                         uint64_t bias, uint64_t n,
+                                                         uint8_t* __restrict__ out8,
+                                                         uint64_t* __restrict__ out64,
+                                                         uint32_t* __restrict__ any_flag) {
+    __shared__ uint64_t s_off[kBlock + 1];
+    __shared__ uint4 s_stage[kStageVec + 1];   // +1 vector: slack for the `hi` word of the last key
+
+    const uint64_t blk0 = (uint64_t)blockIdx.x * kBlock;
+    const uint32_t t = threadIdx.x;
+    const uint64_t rem = n - blk0;
+    const uint32_t cnt = rem < (uint64_t)kBlock ? (uint32_t)rem : (uint32_t)kBlock;
+
+    if (t < cnt) s_off[t] = offsets[blk0 + t] + bias;
+    if (t == 0) s_off[cnt] = offsets[blk0 + cnt] + bias;
+    __syncthreads();
+
+    const uint64_t start = s_off[0];
+    const uint64_t end = s_off[cnt];
+    const uint64_t abase = start & ~(uint64_t)15;
+    const uint64_t nvec = (end - abase + 15) >> 4;
+    const bool staged = nvec <= (uint64_t)kStageVec;   // workgroup-uniform
+
+    uint32_t newflag = 0;
+    if (staged) {
+        const uint4* gv = reinterpret_cast<const uint4*>(keys16 + abase);
+        for (uint32_t v = t; v < (uint32_t)nvec; v += kBlock) s_stage[v] = gv[v];
+        __syncthreads();
+        if (t < cnt) {
+            const uint32_t s = (uint32_t)(s_off[t] - abase);
+            const uint32_t L = (uint32_t)(s_off[t + 1] - s_off[t]);
+            const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_stage);
+            key_op<OP>(g, sw, s, L, blk0 + t, out8, out64, newflag);
+        }
+    } else if (t < cnt) {
+        // Span too large for the stage (long keys): read each key straight from global.
+        const uint64_t ks = s_off[t];
+        const uint64_t kbase = ks & ~(uint64_t)3;
+        const uint32_t* gw = reinterpret_cast<const uint32_t*>(keys16 + kbase);
+        const uint64_t L64 = s_off[t + 1] - ks;
+        key_op<OP>(g, gw, (uint32_t)(ks - kbase), (uint32_t)L64, blk0 + t, out8, out64, newflag);
+    }
+
+    if constexpr (OP == BF_OP_INSERT_FLAGS) {
+        if (any_flag) {
+            const unsigned long long b = __ballot(newflag != 0);
+            if (b != 0ull && (t & 63u) == (uint32_t)__builtin_ctzll(b))
+                __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void last_nonzero_kernel(const uint4* __restrict__ v, uint64_t nvec,
+                                                           unsigned long long* __restrict__ d_last) {
+    unsigned long long best = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        const uint4 x = v[i];
+        unsigned long long cand = 0;
+        if (x.w) cand = 4 * i + 4;
+        else if (x.z) cand = 4 * i + 3;
+        else if (x.y) cand = 4 * i + 2;
+        else if (x.x) cand = 4 * i + 1;
+        best = cand > best ? cand : best;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63u) == 0 && best) atomicMax(d_last, best);
+}
+
+__global__ __launch_bounds__(256) void or_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                 uint64_t nvec) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        uint4 a = dst[i];
+        const uint4 b = src[i];
+        a.x |= b.x; a.y |= b.y; a.z |= b.z; a.w |= b.w;
+        dst[i] = a;
+    }
+}
+
+uint32_t stream_grid(uint64_t nvec) {
+    uint64_t g = (nvec + 255) / 256;
+    if (g > 2048) g = 2048;   // grid-stride beyond 8 blocks per CU
+    return g ? (uint32_t)g : 1u;
+}
+
+}  // namespace
+
+hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets,
+                          uint64_t bias, uint64_t n, uint8_t* out8, uint64_t* out64,
+                          uint32_t* any_flag, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)blocks), block(kBlock);
+    switch (op) {
+        case BF_OP_INDEXES:
+            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INDEXES>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
+            break;
+        case BF_OP_INCLUDE:
+            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INCLUDE>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
+            break;
+        case BF_OP_INSERT:
+            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INSERT>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
+            break;
+        case BF_OP_INSERT_FLAGS:
+            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INSERT_FLAGS>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_last_nonzero(const uint32_t* words, uint64_t nwords, unsigned long long* d_last,
+                                  hipStream_t s) {
+    const uint64_t nvec = nwords / 4;
+    if (nvec == 0) return hipSuccess;
+    hipLaunchKernelGGL(last_nonzero_kernel, dim3(stream_grid(nvec)), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(words), nvec, d_last);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_or(uint32_t* dst, const uint32_t* src, uint64_t nwords, hipStream_t s) {
+    const uint64_t nvec = nwords / 4;
+    if (nvec == 0) return hipSuccess;
+    hipLaunchKernelGGL(or_kernel, dim3(stream_grid(nvec)), dim3(256), 0, s,
+                       reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), nvec);
+    return hipGetLastError();
+}

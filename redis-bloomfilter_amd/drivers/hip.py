@@ -1,0 +1,141 @@
+"""``Redis::BloomfilterDriver::Hip`` — the MI355X driver, Python host mirror.
+
+Plugs in exactly where lib/bloomfilter_driver/ruby.rb does (duck-typed
+driver: ``__init__(options)``, ``redis`` attribute, ``insert``, ``include``,
+``clear``) and adds ``insert_many`` / ``include_many``.  The filter lives in
+HBM (one ``bf_handle``); Redis keeps the same bitstring the ruby driver writes:
+
+* attach (``driver.redis = r``, bloomfilter.rb:45): if ``key_name`` exists it is
+  imported (a filter written by the ruby driver is readable here) and its TTL
+  is mirrored;
+* ``sync='write_through'`` (default): an insert that flips a bit writes the
+  trimmed device string back with SETRANGE (keeps the key's TTL, grows it like
+  SETBIT would), then EXPIREs when ``expire`` is given — ruby.rb:61-62;
+* ``sync='manual'``: Redis is only touched by ``clear`` (DEL) and by explicit
+  ``flush()`` / ``reload()``; meant for batch jobs on filters too large for a
+  per-call write-back;
+* TTL: the device copy is cleared when the mirrored EXPIRE deadline passes,
+  as the Redis key would have vanished (README.md usage, ruby.rb:62).
+
+Extra options (all optional): ``device`` (HIP ordinal, default current),
+``sync``, ``batch_keys`` / ``batch_bytes`` (host staging chunk sizes).
+"""
+from __future__ import annotations
+
+import time
+from typing import Iterable, Optional
+
+import numpy as np
+
+from .. import keys as _keys
+from .._lib import ArgumentError, BF_IMPORT_REPLACE, Filter
+
+
+class Hip:
+    SYNC_MODES = ("write_through", "manual")
+
+    def __init__(self, options: dict):
+        self.options = options
+        m, k = options.get("bits"), options.get("hashes")
+        if m is None or k is None:
+            raise ArgumentError("options[:bits] and options[:hashes] are required")
+        if m <= 0:
+            # the ruby driver would raise ZeroDivisionError / a Redis error at the first insert
+            raise ArgumentError("filter size in bits must be positive (got %r)" % (m,))
+        self.sync_mode = options.get("sync", "write_through")
+        if self.sync_mode not in self.SYNC_MODES:
+            raise ArgumentError("sync must be one of %s" % (self.SYNC_MODES,))
+        self._clock = options.get("clock", time.monotonic)
+        self.filter = Filter(m, k, device=options.get("device", -1),
+                             batch_keys=options.get("batch_keys", 0),
+                             batch_bytes=options.get("batch_bytes", 0))
+        self._redis = None
+        self._deadline: Optional[float] = None
+
+    # -- attr_accessor :redis (ruby.rb:9); attaching imports the existing key
+    @property
+    def redis(self):
+        return self._redis
+
+    @redis.setter
+    def redis(self, r):
+        self._redis = r
+        if r is not None:
+            self.reload()
+
+    @property
+    def key_name(self) -> str:
+        return self.options["key_name"]
+
+    # -- TTL mirror
+    def _expired(self) -> None:
+        if self._deadline is not None and self._clock() >= self._deadline:
+            self._deadline = None
+            self.filter.clear()
+
+    def _arm(self, expire) -> None:
+        self._deadline = self._clock() + float(expire)
+        if self._redis is not None and self.sync_mode == "write_through":
+            self._redis.expire(self.key_name, expire)
+
+    # -- ruby.rb:15-17 / 57-63
+    def insert(self, data, expire=None):
+        return self.insert_many([data], expire)
+
+    def insert_many(self, keys: Iterable, expire=None) -> bool:
+        """Insert a batch; returns True iff some bit flipped (the ruby driver's !found)."""
+        self._expired()
+        buf, offs = _keys.pack(keys)
+        want = bool(expire) or (self._redis is not None and self.sync_mode == "write_through")
+        any_new, _ = self.filter.insert_many(buf, offs, any_new=want)
+        if any_new:
+            if self._redis is not None and self.sync_mode == "write_through":
+                self.flush()
+            if expire:
+                self._arm(expire)
+        return bool(any_new) if want else None
+
+    # -- ruby.rb:20-30
+    def include(self, key) -> bool:
+        return bool(self.include_many([key])[0])
+
+    def include_many(self, keys: Iterable) -> np.ndarray:
+        """Membership of every key, as a numpy bool array (Ruby: Array<bool>)."""
+        self._expired()
+        buf, offs = _keys.pack(keys)
+        return self.filter.include_many(buf, offs).astype(bool)
+
+    # -- ruby.rb:33-35
+    def clear(self):
+        self.filter.clear()
+        self._deadline = None
+        if self._redis is not None:
+            self._redis.delete(self.key_name)
+
+    # -- Redis sync
+    def flush(self) -> int:
+        """Write the device filter to Redis (SETRANGE 0: keeps TTL, grows like SETBIT)."""
+        data = self.filter.export_redis()
+        if data and self._redis is not None:
+            self._redis.setrange(self.key_name, 0, data)
+        return len(data)
+
+    def reload(self) -> None:
+        """Replace the device filter with the Redis key's current value."""
+        if self._redis is None:
+            return
+        data = self._redis.get(self.key_name)
+        self._deadline = None
+        if data is None:
+            self.filter.clear()
+            return
+        self.filter.import_redis(bytes(data), BF_IMPORT_REPLACE)
+        ttl = self._redis.ttl(self.key_name) if hasattr(self._redis, "ttl") else -1
+        if ttl is not None and ttl > 0:
+            self._deadline = self._clock() + ttl
+
+    def to_redis_string(self) -> bytes:
+        return self.filter.export_redis()
+
+    def close(self):
+        self.filter.close()

@@ -1,0 +1,229 @@
+"""HIP path vs the CPU oracle, through the C ABI (libbfhip.so).
+
+Bit-exact: the k offsets of every key, the Redis string after a fixed insert
+sequence, and every include? answer, against oracle/ (the restatement of
+lib/bloomfilter_driver/ruby.rb:41-63 and lib/redis/bloomfilter.rb:50-58).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RNG_SEED = 0x5EED
+
+
+def rand_keys(rng, n, lo=0, hi=200):
+    lens = rng.integers(lo, hi + 1, size=n)
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    buf = rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)
+    return buf, offs
+
+
+def w8_keys(rng, n):
+    """bf_10_000.rb:8-11 family: 8 distinct lowercase letters."""
+    letters = np.argsort(rng.random((n, 26)), axis=1)[:, :8].astype(np.uint8) + ord("a")
+    buf = letters.reshape(-1).copy()
+    offs = np.arange(0, 8 * n + 1, 8, dtype=np.uint64)
+    return buf, offs
+
+
+def edge_keys():
+    """Every length across the SHA-1 block boundaries (55/56, 63/64, 119/120 ...)."""
+    keys = [bytes((i * 7 + j) & 0xFF for j in range(L)) for i, L in enumerate(range(0, 260))]
+    keys += ["asdlol", "foo", "", "héllo wörld ✓", "a" * 55, "b" * 56, "c" * 64, "d" * 119, "e" * 120]
+    keys += [str(i) for i in (0, 42, 999, 10**9, 2**63)]
+    return keys
+
+
+REGIMES = [
+    (9585, 6),                     # spec 1000@1% (spec:56-57)
+    (95851, 6),                    # 10k@1%
+    (95851, 7),
+    (1, 1),
+    (2, 3),
+    (9585058, 6),                  # 1M@1%
+    (1437758757, 10),              # 100M@0.1%
+    (2**32 + 17, 10),              # 2^32 <= m < k*2^32
+    (9585058377, 6),               # 1B@1% (north star)
+    (13 * 0xFFFFFFFF + 1, 13),     # m == reach (largest m still reduced)
+    (191701167547, 13),            # 10B@0.01%: m > k*(2^32-1), modulo skipped
+    (2**40 + 3, 64),               # k = BF_MAX_K
+]
+
+
+@pytest.mark.parametrize("m,k", REGIMES)
+def test_indexes_match_oracle(pkg, oracle, m, k):
+    rng = np.random.default_rng(RNG_SEED + k)
+    buf, offs = rand_keys(rng, 3000)
+    e_buf, e_offs = pkg.keys.pack(edge_keys())
+    with pkg.Filter(m, k) as f:
+        for b, o in ((buf, offs), (e_buf, e_offs)):
+            got = f.indexes_many(b, o)
+            want = oracle.indexes_many(b, o, m, k)
+            assert got.shape == want.shape
+            np.testing.assert_array_equal(got, want)
+
+
+def test_known_answers(pkg):
+    """SURVEY §7 known answers (Python hashlib + Node crypto restatements)."""
+    cases = {("asdlol", 9585, 6): [5260, 6438, 144, 8807, 5008, 5791],
+             ("foo", 95851, 7): [61181, 74832, 85954, 69596, 70715, 28527, 39649],
+             (42, 9585, 6): [6198, 1190, 536, 3493, 2299, 9036],
+             ("", 9585, 6): [8986, 4917, 7472, 7054, 4436, 1889]}
+    for (key, m, k), want in cases.items():
+        with pkg.Filter(m, k) as f:
+            b, o = pkg.keys.pack([key])
+            assert f.indexes_many(b, o)[0].tolist() == want
+
+
+def _insert_include_roundtrip(pkg, oracle, m, k, ins, probe, **fkw):
+    (ib, io), (pb, po) = ins, probe
+    with pkg.Filter(m, k, **fkw) as f:
+        f.insert_many(ib, io)
+        got_str = f.export_redis()
+        got_inc = f.include_many(pb, po)
+    bits = oracle.new_bitset(m, k)
+    oracle.insert_many(bits, m, k, ib, io)
+    want_str = oracle.redis_string(bits)
+    want_inc = oracle.include_many(bits, m, k, pb, po)
+    assert len(got_str) == len(want_str)
+    assert hashlib.sha1(got_str).hexdigest() == hashlib.sha1(want_str).hexdigest()
+    np.testing.assert_array_equal(got_inc, want_inc)
+    return got_str, got_inc
+
+
+def test_spec_strings(pkg, oracle):
+    """SURVEY §7 pinned strings: 'asdlol' alone; "0".."999" into 1000@1%."""
+    s, _ = _insert_include_roundtrip(pkg, oracle, 9585, 6, pkg.keys.pack(["asdlol"]),
+                                     pkg.keys.pack(["asdlol", "nope"]))
+    assert len(s) == 1101
+    assert hashlib.sha1(s).hexdigest() == "fdb117fe21dea15cb79ef9decc983623b10f8af9"
+    s, _ = _insert_include_roundtrip(pkg, oracle, 9585, 6, pkg.keys.pack([str(i) for i in range(1000)]),
+                                     pkg.keys.pack([str(i) for i in range(2000)]))
+    assert len(s) == 1198
+    assert hashlib.sha1(s).hexdigest() == "5e73e7002948f579501e9a6577af1f9c2c5364f3"
+    assert sum(bin(x).count("1") for x in s) == 4438
+
+
+def test_config_10k_w8(pkg, oracle):
+    rng = np.random.default_rng(RNG_SEED)
+    ins = w8_keys(rng, 10_000)
+    probe = w8_keys(rng, 20_000)
+    _, inc = _insert_include_roundtrip(pkg, oracle, 95851, 6, ins, probe)
+    assert 0 < inc.sum() < len(inc)
+
+
+def test_config_1m_decimal(pkg, oracle):
+    rng = np.random.default_rng(RNG_SEED + 1)
+    vals = rng.integers(0, 10**6, size=10**6)
+    ins = pkg.keys.pack_decimal(vals)
+    probe = pkg.keys.pack_decimal(np.concatenate([vals[:500_000], rng.integers(10**6, 2 * 10**6, 500_000)]))
+    _, inc = _insert_include_roundtrip(pkg, oracle, 9585058, 6, ins, probe)
+    assert inc[:500_000].all()   # no false negatives
+
+
+def test_long_keys_fallback_and_chunking(pkg, oracle):
+    """Workgroup spans > 16 KiB take the global-read path; tiny host chunks force many chunks."""
+    rng = np.random.default_rng(RNG_SEED + 2)
+    ins = rand_keys(rng, 3000, 50, 400)
+    probe = rand_keys(rng, 3000, 0, 400)
+    ib, io = ins
+    probe = (np.concatenate([ib, probe[0]]), np.concatenate([io, probe[1][1:] + io[-1]]))
+    _insert_include_roundtrip(pkg, oracle, 95851, 7, ins, probe)
+    _insert_include_roundtrip(pkg, oracle, 95851, 7, ins, probe, batch_keys=257, batch_bytes=5000)
+
+
+def test_offsets_not_starting_at_zero(pkg, oracle):
+    rng = np.random.default_rng(RNG_SEED + 3)
+    buf, offs = rand_keys(rng, 1000, 0, 40)
+    sub_offs = offs[100:]   # keys 100.. of the same buffer
+    with pkg.Filter(95851, 6) as f:
+        np.testing.assert_array_equal(f.indexes_many(buf, sub_offs),
+                                      oracle.indexes_many(buf, sub_offs, 95851, 6))
+
+
+def test_empty_and_single(pkg):
+    with pkg.Filter(9585, 6) as f:
+        b, o = pkg.keys.pack([])
+        assert f.include_many(b, o).shape == (0,)
+        any_new, _ = f.insert_many(b, o, any_new=True)
+        assert any_new is False
+        assert f.export_redis() == b""
+        b, o = pkg.keys.pack([""])
+        any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
+        assert any_new is True and pk.tolist() == [1]
+        assert f.include_many(b, o).tolist() == [1]
+
+
+def test_any_new_and_per_key(pkg, oracle):
+    rng = np.random.default_rng(RNG_SEED + 4)
+    b, o = pkg.keys.pack_decimal(rng.permutation(10**6)[:5000])
+    with pkg.Filter(9585058377, 6) as f:   # sparse: no intra-batch collisions expected
+        any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
+        assert any_new is True and pk.all()
+        any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
+        assert any_new is False and not pk.any()
+    with pkg.Filter(9585, 6) as f:           # dense: aggregate flag is order independent
+        b, o = pkg.keys.pack([str(i) for i in range(3000)])
+        any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
+        bits = oracle.new_bitset(9585, 6)
+        seq_any, seq_pk = oracle.insert_many(bits, 9585, 6, b, o, per_key=True)
+        assert any_new == seq_any
+        assert pk.sum() >= 1   # per-key flags are arrival-order dependent; only the aggregate is pinned
+
+
+def test_import_export(pkg, oracle):
+    rng = np.random.default_rng(RNG_SEED + 5)
+    ib, io = rand_keys(rng, 2000, 0, 30)
+    bits = oracle.new_bitset(95851, 6)
+    oracle.insert_many(bits, 95851, 6, ib, io)
+    s = oracle.redis_string(bits)
+    with pkg.Filter(95851, 6) as f:
+        f.import_redis(s)
+        assert f.export_redis() == s
+        np.testing.assert_array_equal(f.include_many(ib, io), np.ones(2000, np.uint8))
+        # OR mode: union with a second string
+        jb, jo = rand_keys(rng, 500, 0, 30)
+        bits2 = oracle.new_bitset(95851, 6)
+        oracle.insert_many(bits2, 95851, 6, jb, jo)
+        f.import_redis(oracle.redis_string(bits2), mode=1)
+        union = np.bitwise_or(bits, bits2)
+        assert f.export_redis() == oracle.redis_string(union)
+        # strings reaching past m are rejected (the ruby driver never writes them)
+        with pytest.raises(pkg.ArgumentError):
+            f.import_redis(b"\x00" * ((95851 + 7) // 8) + b"\x01")
+        with pytest.raises(pkg.ArgumentError):
+            f.import_redis(b"\x00" * ((95851 + 7) // 8 - 1) + b"\xff")   # bits >= m in the last byte
+        f.clear()
+        assert f.export_redis() == b""
+
+
+def test_device_api_torch(pkg, oracle):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(RNG_SEED + 6)
+    buf, offs = rand_keys(rng, 4097, 0, 70)
+    dk = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    m, k = 1437758757, 10
+    st = torch.cuda.current_stream().cuda_stream
+    with pkg.Filter(m, k) as f:
+        idx = torch.empty((4097, k), dtype=torch.int64, device="cuda")
+        f.indexes_many_dev(dk.data_ptr(), do.data_ptr(), 4097, idx.data_ptr(), stream=st)
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        f.insert_many_dev(dk.data_ptr(), do.data_ptr(), 4097, flag.data_ptr(), stream=st)
+        out = torch.empty(4097, dtype=torch.uint8, device="cuda")
+        f.include_many_dev(dk.data_ptr(), do.data_ptr(), 4097, out.data_ptr(), stream=st)
+        f.sync()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint64), oracle.indexes_many(buf, offs, m, k))
+        assert int(flag.item()) == 1
+        assert out.cpu().numpy().all()
+        # unaligned device key pointer (offset 3 bytes into the buffer)
+        dk2 = torch.zeros(len(buf) + 3, dtype=torch.uint8, device="cuda")
+        dk2[3:] = dk
+        f.indexes_many_dev(dk2.data_ptr() + 3, do.data_ptr(), 4097, idx.data_ptr(), stream=st)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint64), oracle.indexes_many(buf, offs, m, k))
