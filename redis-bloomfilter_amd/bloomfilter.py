@@ -37,6 +37,15 @@ def _ruby_round(x: float) -> int:
     return int(r) if x >= 0 else -int(r)
 
 
+def _ruby_log(x: float) -> float:
+    """Math.log: log(0) is -Infinity; negative arguments raise Math::DomainError."""
+    if x == 0:
+        return -math.inf
+    if x < 0:
+        raise ValueError('Math::DomainError: Numerical argument is out of domain - "log"')
+    return math.log(x)
+
+
 def driver_name(driver: str) -> str:
     """bloomfilter.rb:77-79: ``'ruby-test'`` -> ``'RubyTest'``, ``'hip'`` -> ``'Hip'``."""
     parts = driver.lower().split("-")
@@ -96,7 +105,7 @@ class Bloomfilter:
     # bloomfilter.rb:50-52
     @staticmethod
     def optimal_m(num_of_elements, false_positive_rate=0.01) -> int:
-        return _ruby_round((-1 * num_of_elements) * math.log(false_positive_rate) / (math.log(2) ** 2))
+        return _ruby_round((-1 * num_of_elements) * _ruby_log(false_positive_rate) / (math.log(2) ** 2))
 
     # bloomfilter.rb:54-58 (Integer division when both are Integers)
     @staticmethod
