@@ -15,9 +15,10 @@ density, B = 2^24 keys per batch.  It is the configuration the metric's
 "% of HBM random-access roofline" is quoted on; the cache-resident configs
 (1M@1 %, 100M@0.1 %) are reported under ``secondary``.
 
-Multi-GPU (``--gpus N`` under torch.distributed.run): replicated filter, key
-batches sharded per rank (weak scaling).  include? needs no collective; every
-rank's insert batch is all-gathered (RCCL) so all replicas apply every insert.
+Multi-GPU (``--gpus N`` under torch.distributed.run): the filter is
+block-partitioned over the N GPUs and every rank brings its own key batches
+(weak scaling); probes travel to their owner GPU by RCCL all-to-all and
+include? answers come back the same way (redis-bloomfilter_amd/distributed.py).
 
 Rank 0 prints ONE JSON line.
 """
@@ -84,19 +85,47 @@ class Dist:
             dist.destroy_process_group()
 
 
-def make_batches(pkg, n_filter: int, batch: int, rank: int):
-    """Insert batch: uniform ints in [0, n); include? batch: half of those + half fresh."""
-    rng = np.random.default_rng([SEED, rank])
-    ins_vals = rng.integers(0, n_filter, size=batch, dtype=np.int64)
-    fresh = rng.integers(n_filter, 2 * n_filter, size=batch - batch // 2, dtype=np.int64)
-    inc_vals = np.concatenate([ins_vals[: batch // 2], fresh])
-    return pkg.keys.pack_decimal(ins_vals), pkg.keys.pack_decimal(inc_vals)
+_POW10 = {}
 
 
-def to_dev(buf: np.ndarray, offs: np.ndarray, dev):
-    kb = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
-    ko = torch.from_numpy(offs.view(np.int64)).to(dev)
-    return kb, ko
+def pack_decimal_dev(vals: torch.Tensor):
+    """``Integer#to_s`` + pack on the device (bench input synthesis, outside the timed region).
+
+    vals: non-negative int64 on the GPU -> (uint8 key bytes + 16 B slack, int64 offsets[n+1])."""
+    dev = vals.device
+    if dev not in _POW10:
+        _POW10[dev] = torch.tensor([10 ** i for i in range(19)], dtype=torch.int64, device=dev)
+    pow10 = _POW10[dev]
+    ndig = torch.searchsorted(pow10, vals, right=True).clamp_(min=1)
+    width = int(ndig.max().item())
+    div = pow10[:width].flip(0)
+    digits = (torch.div(vals[:, None], div[None, :], rounding_mode="floor") % 10 + 48).to(torch.uint8)
+    keep = torch.arange(width, device=dev)[None, :] >= (width - ndig)[:, None]
+    buf = digits[keep]
+    offs = torch.zeros(vals.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(ndig, 0, out=offs[1:])
+    kb = torch.cat([buf, torch.zeros(16, dtype=torch.uint8, device=dev)])
+    return kb, offs
+
+
+def make_batches(n_filter: int, batch: int, rank: int, count: int, dev):
+    """`count` step batches, each a fresh insert batch (uniform ints in [0, n)) and an
+    include? batch of half that step's inserts + half fresh non-members (ints in [n, 2n))."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED * 1000 + rank)
+    out = []
+    for _ in range(count):
+        ins = torch.randint(0, n_filter, (batch,), generator=g, device=dev, dtype=torch.int64)
+        fresh = torch.randint(n_filter, 2 * n_filter, (batch - batch // 2,), generator=g, device=dev,
+                              dtype=torch.int64)
+        inc = torch.cat([ins[: batch // 2], fresh])
+        out.append((pack_decimal_dev(ins), pack_decimal_dev(inc)))
+    return out
+
+
+def to_host(kb: torch.Tensor, ko: torch.Tensor):
+    offs = ko.cpu().numpy().view(np.uint64)
+    return kb.cpu().numpy()[: int(offs[-1])], offs
 
 
 def prefill_random(f, m: int, k: int, rank: int) -> np.ndarray:
@@ -114,49 +143,56 @@ def prefill_random(f, m: int, k: int, rank: int) -> np.ndarray:
 def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False):
     n, p, batch, prefill = CONFIGS[name]
     B = pkg.Bloomfilter
-    m, k = B.optimal_m(n, p), B.optimal_k(n, B.optimal_m(n, p))
+    m = B.optimal_m(n, p)
+    k = B.optimal_k(n, m)
     dev = torch.device("cuda", D.local)
-    f = pkg.Filter(m, k, device=D.local)
     t0 = time.time()
-    (ib, io), (pb, po) = make_batches(pkg, n, batch, D.rank)
+    pf = None
     host_bits = None
-    if prefill == "random":
-        host_bits = prefill_random(f, m, k, D.rank)
+    if D.world == 1:
+        f = pkg.Filter(m, k, device=D.local)
+        if prefill == "random":
+            host_bits = prefill_random(f, m, k, D.rank)
+    else:   # partitioned over the ranks, RCCL all-to-all routing
+        pf = pkg.distributed.PartitionedFilter(m, k, block_log2=20, device=dev)
+        f = pf.engine.filter
+        if prefill == "random":
+            rng = np.random.default_rng([SEED, 99, D.rank])
+            f.shard_import(rng.bytes(f.local_bits // 8))
+    batches = make_batches(n, batch, D.rank, warmup + steps, dev)
+    torch.cuda.synchronize()
     log("[%s] m=%d k=%d batch=%d setup %.1fs" % (name, m, k, batch, time.time() - t0))
-    ikb, iko = to_dev(ib, io, dev)
-    pkb, pko = to_dev(pb, po, dev)
     out = torch.empty(batch, dtype=torch.uint8, device=dev)
-    gathered = None
-    if D.world > 1:   # replicated mode: every replica applies every rank's inserts
-        gathered = [(torch.empty_like(ikb), torch.empty_like(iko)) for _ in range(D.world)]
     stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    sp = stream.cuda_stream   # 0 = the null stream torch uses by default
 
-    def insert():
-        if gathered is None:
+    def insert(bt):
+        ikb, iko = bt[0]
+        if pf is None:
             f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, stream=sp)
-            return
-        dist.all_gather([g[0] for g in gathered], ikb)
-        dist.all_gather([g[1] for g in gathered], iko)
-        for gk, go in gathered:
-            f.insert_many_dev(gk.data_ptr(), go.data_ptr(), batch, stream=sp)
+        else:
+            pf.insert_many_dev(ikb, iko, batch)
 
-    def include():
-        f.include_many_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), stream=sp)
+    def include(bt):
+        pkb, pko = bt[1]
+        if pf is None:
+            f.include_many_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), stream=sp)
+        else:
+            out.copy_(pf.include_many_dev(pkb, pko, batch))
 
-    for _ in range(warmup):
-        insert()
-        include()
+    for bt in batches[:warmup]:
+        insert(bt)
+        include(bt)
     D.barrier()
     torch.cuda.synchronize()
     ev = []
     t_start = time.perf_counter()
-    for _ in range(steps):
+    for bt in batches[warmup:]:
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         e[0].record(stream)
-        insert()
+        insert(bt)
         e[1].record(stream)
-        include()
+        include(bt)
         e[2].record(stream)
         ev.append(e)
     torch.cuda.synchronize()
@@ -165,24 +201,25 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     wall = D.max(wall)
     ins_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     inc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-    # sanity: members must all be found (no false negatives)
+    # sanity: the members (first half of the include? batch) must all be found
     got = out.cpu().numpy()
     assert got[: batch // 2].all(), "false negative in the include? batch"
     fp_rate = float(got[batch // 2:].mean())
-    Lmean = float(po[-1]) / batch
+    Lmean = float(batches[-1][1][1][-1].item()) / batch
     res = {
         "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3),
         "wall_s": wall, "steps": steps,
         "keys_per_s": 2 * batch * D.world * steps / wall,
-        "insert": {"kernel_ms": ins_ms, "keys_per_s": batch * D.world / (ins_ms / 1e3) if gathered is None
-                   else batch * D.world / (ins_ms / 1e3),
+        "insert": {"kernel_ms": ins_ms, "keys_per_s": batch / (ins_ms / 1e3),
                    "algo_bytes_per_key": Lmean + 8 + 2 * k * GRANULE},
         "include": {"kernel_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
                     "algo_bytes_per_key": Lmean + 8 + 1 + k * GRANULE,
                     "observed_fp_rate": fp_rate},
         "bitset_bytes": f.device_bytes,
     }
-    if want_host:
+    ib, io = to_host(*batches[0][0])
+    pb, po = to_host(*batches[0][1])
+    if want_host and pf is None:
         # PCIe-inclusive rate of the host-pointer entry points (H2D keys + D2H answers).
         torch.cuda.synchronize()
         t = time.perf_counter()
@@ -192,7 +229,11 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         f.include_many(pb, po)
         t_inc = time.perf_counter() - t
         res["host_api"] = {"insert_keys_per_s": batch / t_ins, "include_keys_per_s": batch / t_inc}
-    f.close()
+    del batches
+    if pf is not None:
+        pf.close()
+    else:
+        f.close()
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
@@ -288,7 +329,8 @@ def main():
                                "include_many? per step (50%% members)" % (args.config, n, p, main_res["m"],
                                                                           main_res["k"], batch, batch),
                    "global_batch": 2 * batch * D.world,
-                   "parallelism": "replicated x%d (include? sharded, insert all-gathered)" % D.world
+                   "parallelism": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key batches "
+                                  "routed to owner GPUs by RCCL all-to-all)" % D.world
                    if D.world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,

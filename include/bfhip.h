@@ -26,8 +26,9 @@
  *   bf_version         Redis::Bloomfilter.version                     lib/redis/bloomfilter/version.rb:6-8
  *
  * Device-resident variants (`*_dev`) take device pointers and a hipStream_t
- * (as void*, NULL = the handle's stream) and do not synchronise; they are
- * what bench.py times and what the multi-GPU layer composes.
+ * (as void*, used verbatim: NULL is HIP's null stream, bf_stream() gives the
+ * handle's own) and do not synchronise; they are what bench.py times and what
+ * the multi-GPU layer composes.
  *
  * Bit layout (identical to the Redis string written by SETBIT): bit offset o
  * lives in byte o >> 3 under mask 0x80 >> (o & 7).  On the device the bytes
@@ -64,6 +65,16 @@ typedef struct bf_config {
     int32_t  device;           /* HIP device ordinal; -1 => current device                 */
     uint64_t batch_keys;       /* keys per internal chunk of host-pointer calls (0 = 1<<22) */
     uint64_t batch_bytes;      /* key bytes per internal chunk (0 = 64 MiB)                 */
+    /* Partitioned filters (one handle per GPU, one shard each).  Bit offset o of the
+     * reachable prefix belongs to block g = o >> shard_block_log2, owned by shard
+     * g % shard_count; inside the owner it sits at local offset
+     * ((g / shard_count) << shard_block_log2) | (o & (2^shard_block_log2 - 1)).
+     * Block-cyclic, so the probe-dense first 2^32 bits (h0 < 2^32, ruby.rb:51)
+     * spread over every shard. */
+    uint32_t shard_count;      /* 0 or 1 => the handle holds the whole filter; max 255     */
+    uint32_t shard_index;      /* this handle's shard, < shard_count                       */
+    uint32_t shard_block_log2; /* ownership block size, 3..40 (0 => 20: 128 KiB blocks)    */
+    uint32_t reserved;
 } bf_config;
 
 /* ---- lifecycle */
@@ -105,7 +116,37 @@ int  bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
                          uint64_t n, uint64_t* d_out, void* stream);
 /* The device bitset (Redis byte order, device_bytes long, zero past the reachable prefix). */
 int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
-int  bf_sync(bf_handle* h);
+int  bf_stream(bf_handle* h, void** stream);   /* the handle's own (non-blocking) hipStream_t */
+int  bf_sync(bf_handle* h);                    /* synchronise the handle's own stream */
+
+/* ---- partitioned filters (multi-GPU; the collective between the steps is the
+ *      caller's, e.g. RCCL all-to-all through torch.distributed).
+ *
+ *  requester:  bf_route_dev     hash n keys; every probe (j, i) becomes an owner-local
+ *                               offset in d_send, grouped by owner shard: owner s's probes
+ *                               are d_send[displ[s] .. displ[s] + d_counts[s]), displ the
+ *                               exclusive prefix sum of d_counts; d_slot[j*k + i] is the
+ *                               probe's position in d_send.  Needs n*k < 2^32.
+ *  owner:      bf_shard_insert_dev   OR the received local offsets into this shard
+ *              bf_shard_test_dev     one byte (0/1) per received local offset
+ *  requester:  bf_combine_dev   d_out[j] = AND_i d_bits[d_slot[j*k + i]] (include? answer)
+ *
+ *  Works on any handle: on a whole-filter handle shard_count = 1 routes everything to 0.
+ *  d_counts must hold shard_count uint64 and is written, not accumulated. */
+int  bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_index,
+                   uint32_t* block_log2, uint64_t* local_bits);
+int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                  uint64_t* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream);
+int  bf_shard_insert_dev(bf_handle* h, const uint64_t* d_local, uint64_t count,
+                         uint32_t* d_any_new /* nullable */, void* stream);
+int  bf_shard_test_dev(bf_handle* h, const uint64_t* d_local, uint64_t count, uint8_t* d_bits,
+                       void* stream);
+int  bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t n,
+                    uint8_t* d_out, void* stream);
+/* The shard's bytes in local layout (local_bits/8 bytes, untrimmed); the caller
+ * interleaves shards block by block to rebuild the Redis string. */
+int  bf_shard_export(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out);
+int  bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode);
 
 /* ---- sizing helpers with the facade's exact semantics (bloomfilter.rb:50-58) */
 int64_t bf_optimal_m(double n, double error_rate);

@@ -17,5 +17,6 @@ from .bloomfilter import Bloomfilter, DRIVERS, VERSION, driver_name, register_dr
 from .drivers.hip import Hip  # noqa: F401
 from .fakeredis import FakeRedis  # noqa: F401
 from . import keys  # noqa: F401
+from . import distributed  # noqa: F401
 
 register_driver(Hip)

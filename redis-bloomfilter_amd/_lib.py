@@ -43,7 +43,9 @@ class ArgumentError(ValueError):
 
 class bf_config(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
-                ("batch_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64)]
+                ("batch_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
+                ("shard_count", ctypes.c_uint32), ("shard_index", ctypes.c_uint32),
+                ("shard_block_log2", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -71,6 +73,14 @@ SIGNATURES = {
     "bf_indexes_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_device_bits": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), _u64p]),
     "bf_sync": (ctypes.c_int, [_vp]),
+    "bf_stream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "bf_shard_info": (ctypes.c_int, [_vp, _u32p, _u32p, _u32p, _u64p]),
+    "bf_route_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp]),
+    "bf_shard_insert_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
+    "bf_shard_test_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
+    "bf_combine_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_shard_export": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
+    "bf_shard_import": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
     "bf_optimal_m": (ctypes.c_int64, [ctypes.c_double, ctypes.c_double]),
     "bf_optimal_k": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
 }
@@ -158,14 +168,16 @@ class Filter:
 
     Arrays are numpy: ``keys`` uint8, ``offsets`` uint64 with n+1 entries.
     The ``*_dev`` methods take raw device addresses (ints), e.g. from
-    ``torch.Tensor.data_ptr()``, and a stream handle (int, 0 = the filter's
-    own stream).
+    ``torch.Tensor.data_ptr()``, and a hipStream_t as an int (``stream=None``:
+    the filter's own stream; ``0`` is HIP's null stream, e.g. torch's default).
     """
 
     def __init__(self, m_bits: int, k: int, device: int = -1, batch_keys: int = 0,
-                 batch_bytes: int = 0):
+                 batch_bytes: int = 0, shard_count: int = 1, shard_index: int = 0,
+                 shard_block_log2: int = 0):
         self._lib = load()
-        cfg = bf_config(ctypes.sizeof(bf_config), int(device), int(batch_keys), int(batch_bytes))
+        cfg = bf_config(ctypes.sizeof(bf_config), int(device), int(batch_keys), int(batch_bytes),
+                        int(shard_count), int(shard_index), int(shard_block_log2), 0)
         h = _vp()
         rc = self._lib.bf_create(int(m_bits), int(k), ctypes.byref(cfg), ctypes.byref(h))
         _check(rc, None)
@@ -178,6 +190,11 @@ class Filter:
                                  ctypes.byref(devb)), h)
         self.m, self.k, self.reach_bits, self.device_bytes = m.value, kk.value, reach.value, devb.value
         self.device = int(device)
+        sc, si, bl = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        lb = ctypes.c_uint64()
+        _check(self._lib.bf_shard_info(h, ctypes.byref(sc), ctypes.byref(si), ctypes.byref(bl),
+                                       ctypes.byref(lb)), h)
+        self.shard_count, self.shard_index, self.block_log2, self.local_bits = sc.value, si.value, bl.value, lb.value
 
     # -- lifecycle
     def close(self) -> None:
@@ -263,20 +280,57 @@ class Filter:
 
     # -- device-resident API
     def insert_many_dev(self, d_keys: int, d_offsets: int, n: int, d_any_new: int = 0,
-                        d_per_key_new: int = 0, stream: int = 0) -> None:
+                        d_per_key_new: int = 0, stream=None) -> None:
         _check(self._lib.bf_insert_many_dev(self.handle, d_keys, d_offsets, int(n), d_any_new or None,
-                                            d_per_key_new or None, stream or None), self._h)
+                                            d_per_key_new or None, self._s(stream)), self._h)
 
-    def include_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream: int = 0) -> None:
+    def include_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream=None) -> None:
         _check(self._lib.bf_include_many_dev(self.handle, d_keys, d_offsets, int(n), d_out,
-                                             stream or None), self._h)
+                                             self._s(stream)), self._h)
 
-    def indexes_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream: int = 0) -> None:
+    def indexes_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream=None) -> None:
         _check(self._lib.bf_indexes_many_dev(self.handle, d_keys, d_offsets, int(n), d_out,
-                                             stream or None), self._h)
+                                             self._s(stream)), self._h)
+
+    def _s(self, stream):
+        if stream is None:
+            if getattr(self, "_own_stream", None) is None:
+                p = _vp()
+                _check(self._lib.bf_stream(self.handle, ctypes.byref(p)), self._h)
+                self._own_stream = p.value or 0
+            return self._own_stream or None
+        return int(stream) or None
 
     def device_bits(self) -> Tuple[int, int]:
         p = _vp()
         nb = ctypes.c_uint64()
         _check(self._lib.bf_device_bits(self.handle, ctypes.byref(p), ctypes.byref(nb)), self._h)
         return int(p.value or 0), int(nb.value)
+
+    # -- partitioned filters (see include/bfhip.h)
+    def route_dev(self, d_keys: int, d_offsets: int, n: int, d_send: int, d_slot: int, d_counts: int,
+                  stream=None) -> None:
+        _check(self._lib.bf_route_dev(self.handle, d_keys, d_offsets, int(n), d_send, d_slot, d_counts,
+                                      self._s(stream)), self._h)
+
+    def shard_insert_dev(self, d_local: int, count: int, d_any_new: int = 0, stream=None) -> None:
+        _check(self._lib.bf_shard_insert_dev(self.handle, d_local, int(count), d_any_new or None,
+                                             self._s(stream)), self._h)
+
+    def shard_test_dev(self, d_local: int, count: int, d_bits: int, stream=None) -> None:
+        _check(self._lib.bf_shard_test_dev(self.handle, d_local, int(count), d_bits, self._s(stream)), self._h)
+
+    def combine_dev(self, d_bits: int, d_slot: int, n: int, d_out: int, stream=None) -> None:
+        _check(self._lib.bf_combine_dev(self.handle, d_bits, d_slot, int(n), d_out, self._s(stream)), self._h)
+
+    def shard_export(self) -> np.ndarray:
+        n = ctypes.c_uint64(0)
+        _check(self._lib.bf_shard_export(self.handle, None, 0, ctypes.byref(n)), self._h)
+        buf = np.zeros(max(n.value, 1), np.uint8)
+        _check(self._lib.bf_shard_export(self.handle, _ptr(buf), len(buf), ctypes.byref(n)), self._h)
+        return buf[: n.value]
+
+    def shard_import(self, data, mode: int = BF_IMPORT_REPLACE) -> None:
+        buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+        _check(self._lib.bf_shard_import(self.handle, _ptr(buf), len(buf) if len(data) else 0, int(mode)),
+               self._h)

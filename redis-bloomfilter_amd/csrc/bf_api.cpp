@@ -44,6 +44,14 @@ struct bf_handle {
     BfGeom g{};
     uint64_t m = 0, reach = 0, dev_bytes = 0;
     uint32_t k = 0;
+    // partitioned filters: this handle holds shard `shard_index` of `shards`
+    uint32_t shards = 1, shard_index = 0, block_log2 = 20;
+    uint64_t local_bits = 0;
+    // routing scratch (grown on demand)
+    uint64_t* d_tmp_local = nullptr;
+    uint8_t*  d_tmp_owner = nullptr;
+    uint64_t  tmp_cap = 0;
+    unsigned long long* d_cursor = nullptr;
     uint64_t cap_keys = 0, cap_bytes = 0;
     Slot slot[2];
     bool staging_ready = false;
@@ -147,6 +155,8 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
              uint8_t* out8, uint64_t* out64, uint8_t* any_new) {
     int rc = check_keys_args(h, keys, offsets, n);
     if (rc) return rc;
+    if (op != BF_OP_INDEXES && h->shards > 1)
+        return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter: use bf_route_dev");
     for (uint64_t j = 0; j < n; ++j)
         if (offsets[j + 1] < offsets[j]) return set_err(h, BF_EINVAL, "offsets must be non-decreasing (j=%llu)", (unsigned long long)j);
     if (any_new) *any_new = 0;
@@ -221,8 +231,8 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
     return BF_OK;
 }
 
-hipStream_t pick_stream(bf_handle* h, void* stream) {
-    return stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+hipStream_t pick_stream(bf_handle*, void* stream) {
+    return reinterpret_cast<hipStream_t>(stream);   // verbatim: NULL is the null stream
 }
 
 // Device pointer + 16-byte alignment bias for the kernels.
@@ -239,6 +249,8 @@ int run_dev(bf_handle* h, BfOp op, const uint8_t* d_keys, const uint64_t* d_offs
     if (!d_offsets || !d_keys) return set_err(h, BF_EINVAL, "NULL device pointer");
     if (op == BF_OP_INCLUDE && !d_out8) return set_err(h, BF_EINVAL, "d_out is NULL");
     if (op == BF_OP_INDEXES && !d_out64) return set_err(h, BF_EINVAL, "d_out is NULL");
+    if (op != BF_OP_INDEXES && h->shards > 1)
+        return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter: use bf_route_dev");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
@@ -301,7 +313,22 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->k = k;
     const uint64_t maxval = (uint64_t)k * 0xFFFFFFFFull;      // largest offset ruby.rb:51 can produce
     h->reach = std::min<uint64_t>(m_bits, maxval + 1);
-    h->dev_bytes = round_up((h->reach + 7) / 8, 256);
+    h->shards = c.shard_count > 1 ? c.shard_count : 1;
+    h->shard_index = h->shards > 1 ? c.shard_index : 0;
+    h->block_log2 = c.shard_block_log2 ? c.shard_block_log2 : 20;
+    if (h->shards > 255 || h->shard_index >= h->shards || h->block_log2 < 3 || h->block_log2 > 40) {
+        delete h;
+        return set_err(nullptr, BF_EINVAL, "bad shard config (count %u, index %u, block_log2 %u)",
+                       c.shard_count, c.shard_index, c.shard_block_log2);
+    }
+    if (h->shards == 1) {
+        h->local_bits = h->reach;
+    } else {   // blocks g = s, s + P, s + 2P, ... below ceil(reach / 2^b)
+        const uint64_t nblocks = (h->reach + (1ull << h->block_log2) - 1) >> h->block_log2;
+        const uint64_t mine = nblocks > h->shard_index ? (nblocks - 1 - h->shard_index) / h->shards + 1 : 0;
+        h->local_bits = mine << h->block_log2;
+    }
+    h->dev_bytes = round_up(std::max<uint64_t>((h->local_bits + 7) / 8, 1), 256);
     h->cap_keys = c.batch_keys ? c.batch_keys : (1ull << 22);
     h->cap_bytes = c.batch_bytes ? c.batch_bytes : (64ull << 20);
 
@@ -329,6 +356,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.inv_m = 1.0 / (double)m_bits;
     h->g.k = k;
     h->g.nomod = (m_bits > maxval) ? 1u : 0u;
+    h->g.shards = h->shards;
+    h->g.block_log2 = h->block_log2;
     *out = h;
     return BF_OK;
 }
@@ -344,6 +373,9 @@ int bf_destroy(bf_handle* h) {
         if (h->d_flag) (void)hipFree(h->d_flag);
         if (h->d_scan) (void)hipFree(h->d_scan);
         if (h->h_flag) (void)hipHostFree(h->h_flag);
+        if (h->d_tmp_local) (void)hipFree(h->d_tmp_local);
+        if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
+        if (h->d_cursor) (void)hipFree(h->d_cursor);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -408,11 +440,12 @@ int bf_sync(bf_handle* h) {
     return BF_OK;
 }
 
-int bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
-    if (!h || !len_out) return BF_EINVAL;
-    std::lock_guard<std::mutex> lk(h->mu);
-    DeviceGuard dg(h->device);
-    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+}  // extern "C"
+
+namespace {
+
+// Trimmed length of the first `max_bytes` bytes of the device bitset (Redis STRLEN after SETBITs).
+int device_trimmed_len(bf_handle* h, uint64_t* len_out) {
     HIPCHK(h, hipMemsetAsync(h->d_scan, 0, sizeof(unsigned long long), h->stream));
     HIPCHK(h, bf_launch_last_nonzero(h->g.bits, h->dev_bytes / 4, h->d_scan, h->stream));
     unsigned long long last = 0;
@@ -429,27 +462,22 @@ int bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out)
         len = w * 4 + (uint64_t)top + 1;
     }
     *len_out = len;
-    if (!buf) return BF_OK;
-    if (cap < len) return set_err(h, BF_ERANGE, "export buffer too small: need %llu bytes", (unsigned long long)len);
-    if (len) HIPCHK(h, hipMemcpy(buf, h->g.bits, len, hipMemcpyDeviceToHost));
     return BF_OK;
 }
 
-int bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode) {
-    if (!h) return BF_EINVAL;
+// Load `len` bytes (device layout) into the bitset; bits at offsets >= max_bits are refused.
+int import_bytes(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode, uint64_t max_bits) {
     if (mode != BF_IMPORT_REPLACE && mode != BF_IMPORT_OR) return set_err(h, BF_EINVAL, "bad import mode %u", mode);
     if (len && !buf) return set_err(h, BF_EINVAL, "buf is NULL");
-    const uint64_t max_bytes = (h->reach + 7) / 8;
+    const uint64_t max_bytes = (max_bits + 7) / 8;
     if (len > max_bytes)
         return set_err(h, BF_ERANGE, "string of %llu bytes exceeds the filter's %llu reachable bytes",
                        (unsigned long long)len, (unsigned long long)max_bytes);
-    if (len == max_bytes && (h->reach & 7)) {
-        const uint8_t beyond = (uint8_t)(0xFFu >> (h->reach & 7));
-        if (buf[len - 1] & beyond) return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)h->reach);
+    if (len == max_bytes && (max_bits & 7)) {
+        const uint8_t beyond = (uint8_t)(0xFFu >> (max_bits & 7));
+        if (buf[len - 1] & beyond)
+            return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)max_bits);
     }
-    std::lock_guard<std::mutex> lk(h->mu);
-    DeviceGuard dg(h->device);
-    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     if (mode == BF_IMPORT_REPLACE) {
         HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -470,6 +498,141 @@ int bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mod
     return BF_OK;
 }
 
+int ensure_route_scratch(bf_handle* h, uint64_t probes) {
+    if (!h->d_cursor) HIPCHK(h, hipMalloc((void**)&h->d_cursor, 256 * sizeof(unsigned long long)));
+    if (probes <= h->tmp_cap) return BF_OK;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->d_tmp_local) (void)hipFree(h->d_tmp_local);
+    if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
+    h->d_tmp_local = nullptr;
+    h->d_tmp_owner = nullptr;
+    h->tmp_cap = 0;
+    const uint64_t cap = round_up(probes, 1ull << 16);
+    HIPCHK(h, hipMalloc((void**)&h->d_tmp_local, cap * sizeof(uint64_t)));
+    HIPCHK(h, hipMalloc((void**)&h->d_tmp_owner, cap));
+    h->tmp_cap = cap;
+    return BF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+    if (!h || !len_out) return BF_EINVAL;
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_export and interleave blocks");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    uint64_t len = 0;
+    int rc = device_trimmed_len(h, &len);
+    if (rc) return rc;
+    *len_out = len;
+    if (!buf) return BF_OK;
+    if (cap < len) return set_err(h, BF_ERANGE, "export buffer too small: need %llu bytes", (unsigned long long)len);
+    if (len) HIPCHK(h, hipMemcpy(buf, h->g.bits, len, hipMemcpyDeviceToHost));
+    return BF_OK;
+}
+
+int bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode) {
+    if (!h) return BF_EINVAL;
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_import");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    return import_bytes(h, buf, len, mode, h->reach);
+}
+
+int bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_index, uint32_t* block_log2,
+                  uint64_t* local_bits) {
+    if (!h) return BF_EINVAL;
+    if (shard_count) *shard_count = h->shards;
+    if (shard_index) *shard_index = h->shard_index;
+    if (block_log2) *block_log2 = h->block_log2;
+    if (local_bits) *local_bits = h->local_bits;
+    return BF_OK;
+}
+
+int bf_shard_export(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+    if (!h || !len_out) return BF_EINVAL;
+    const uint64_t len = (h->local_bits + 7) / 8;
+    *len_out = len;
+    if (!buf) return BF_OK;
+    if (cap < len) return set_err(h, BF_ERANGE, "export buffer too small: need %llu bytes", (unsigned long long)len);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (len) HIPCHK(h, hipMemcpy(buf, h->g.bits, len, hipMemcpyDeviceToHost));
+    return BF_OK;
+}
+
+int bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    return import_bytes(h, buf, len, mode, h->local_bits);
+}
+
+int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                 uint64_t* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
+    if (n && (!d_key_bytes || !d_offsets || !d_send || !d_slot)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    const uint64_t probes = n * h->k;
+    if (n && probes / n != h->k) return set_err(h, BF_EINVAL, "n*k overflows");
+    if (probes >= (1ull << 32)) return set_err(h, BF_EINVAL, "n*k must be < 2^32 per call (slot indices are 32-bit)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    hipStream_t s = pick_stream(h, stream);
+    int rc = ensure_route_scratch(h, std::max<uint64_t>(probes, 1));
+    if (rc) return rc;
+    auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
+    HIPCHK(h, hipMemsetAsync(counts, 0, h->shards * sizeof(unsigned long long), s));
+    if (n) {
+        uint64_t bias = 0;
+        const uint8_t* k16 = align_keys(d_key_bytes, &bias);
+        HIPCHK(h, bf_launch_keys(BF_OP_ROUTE, h->g, k16, d_offsets, bias, n, h->d_tmp_owner, h->d_tmp_local,
+                                 nullptr, s, counts));
+    }
+    HIPCHK(h, bf_launch_route_scatter(h->d_tmp_local, h->d_tmp_owner, probes, h->shards, counts, h->d_cursor,
+                                      d_send, d_slot, s));
+    return BF_OK;
+}
+
+int bf_shard_insert_dev(bf_handle* h, const uint64_t* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (count && !d_local) return set_err(h, BF_EINVAL, "d_local is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, pick_stream(h, stream)));
+    return BF_OK;
+}
+
+int bf_shard_test_dev(bf_handle* h, const uint64_t* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (count && (!d_local || !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, pick_stream(h, stream)));
+    return BF_OK;
+}
+
+int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t n, uint8_t* d_out,
+                   void* stream) {
+    if (!h) return BF_EINVAL;
+    if (n && (!d_bits || !d_slot || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, pick_stream(h, stream)));
+    return BF_OK;
+}
+
 int bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                        uint32_t* d_any_new, uint8_t* d_per_key_new, void* stream) {
     const BfOp op = (d_any_new || d_per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
@@ -484,6 +647,12 @@ int bf_include_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
 int bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                         uint64_t* d_out, void* stream) {
     return run_dev(h, BF_OP_INDEXES, d_key_bytes, d_offsets, n, nullptr, d_out, nullptr, stream);
+}
+
+int bf_stream(bf_handle* h, void** stream) {
+    if (!h || !stream) return BF_EINVAL;
+    *stream = reinterpret_cast<void*>(h->stream);
+    return BF_OK;
 }
 
 int bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes) {

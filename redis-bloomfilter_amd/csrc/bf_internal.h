@@ -10,6 +10,8 @@ struct BfGeom {
     double    inv_m;   // 1.0 / m, for the division-free modulo
     uint32_t  k;       // hashes per key (options[:hashes], bloomfilter.rb:28)
     uint32_t  nomod;   // 1 iff m > k*(2^32-1): every derived offset is already < m
+    uint32_t  shards;  // partitioned filters: shard count P (1 = whole filter)
+    uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
 };
 
 enum BfOp : int {
@@ -17,6 +19,8 @@ enum BfOp : int {
     BF_OP_INCLUDE      = 1,  // AND of the k bits (ruby.rb:20-30)
     BF_OP_INSERT       = 2,  // OR the k bits in, no per-key result (ruby.rb:57-60)
     BF_OP_INSERT_FLAGS = 3,  // ... and report which keys / whether any bit flipped (ruby.rb:61-62)
+    BF_OP_ROUTE        = 4,  // owner-local offset (out64) + owner shard (out8) per probe,
+                             // per-owner probe counts accumulated into counts[P]
 };
 
 // Keys: byte j of the packed buffer for offset o is keys16[o + bias - 0] where
@@ -24,7 +28,22 @@ enum BfOp : int {
 // the last key byte.  (bias is added modulo 2^64.)
 hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets,
                           uint64_t bias, uint64_t n, uint8_t* out8, uint64_t* out64,
-                          uint32_t* any_flag, hipStream_t s);
+                          uint32_t* any_flag, hipStream_t s,
+                          unsigned long long* counts = nullptr /* BF_OP_ROUTE only */);
+
+// Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
+// pairs by owner into send[], writes each probe's position into slot[].
+// counts[P] must hold the per-owner totals (from BF_OP_ROUTE).
+hipError_t bf_launch_route_scatter(const uint64_t* local, const uint8_t* owner, uint64_t total,
+                                   uint32_t P, const unsigned long long* counts,
+                                   unsigned long long* cursor, uint64_t* send, uint32_t* slot,
+                                   hipStream_t s);
+hipError_t bf_launch_shard_insert(uint32_t* bits, const uint64_t* local, uint64_t count,
+                                  uint32_t* any_flag, hipStream_t s);
+hipError_t bf_launch_shard_test(const uint32_t* bits, const uint64_t* local, uint64_t count,
+                                uint8_t* out, hipStream_t s);
+hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k,
+                             uint8_t* out, hipStream_t s);
 
 // *d_last = 1 + index of the last nonzero 32-bit word in words[0, nwords) (0 if none).
 // d_last must be zeroed before the launch.  nwords must be a multiple of 4.

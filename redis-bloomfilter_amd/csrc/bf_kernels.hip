@@ -107,16 +107,35 @@ __device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, u
     return (uint64_t)r;
 }
 
+// Block-cyclic ownership of partitioned filters (include/bfhip.h, bf_config):
+// block b = o >> block_log2 lives on shard b % P at local block b / P.
+__device__ __forceinline__ void owner_local(const BfGeom& g, uint64_t o, uint32_t& owner, uint64_t& local) {
+    const uint64_t blk = o >> g.block_log2;
+    const uint64_t lblk = blk / g.shards;
+    owner = (uint32_t)(blk - lblk * g.shards);
+    local = (lblk << g.block_log2) | (o & ((1ull << g.block_log2) - 1ull));
+}
+
 template <int OP, typename Src>
 __device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uint32_t L,
                                        uint64_t key, uint8_t* __restrict__ out8,
-                                       uint64_t* __restrict__ out64, uint32_t& newflag) {
+                                       uint64_t* __restrict__ out64, uint32_t& newflag,
+                                       uint32_t* hist) {
     uint32_t H[5];
     sha1_key(src, s, L, H);
     const uint32_t k = g.k;
     if constexpr (OP == BF_OP_INDEXES) {
         for (uint32_t i = 0; i < k; ++i)
             out64[key * k + i] = probe_offset(g, H[0], H[1], H[2], H[3], i);
+    } else if constexpr (OP == BF_OP_ROUTE) {
+        for (uint32_t i = 0; i < k; ++i) {
+            uint32_t owner;
+            uint64_t local;
+            owner_local(g, probe_offset(g, H[0], H[1], H[2], H[3], i), owner, local);
+            out64[key * k + i] = local;
+            out8[key * k + i] = (uint8_t)owner;
+            atomicAdd(hist + owner, 1u);   // LDS histogram
+        }
     } else if constexpr (OP == BF_OP_INCLUDE) {
         uint32_t ok = 1u;
         for (uint32_t i0 = 0; i0 < k; i0 += kChunk) {
@@ -160,9 +179,11 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
                                                          uint64_t bias, uint64_t n,
                                                          uint8_t* __restrict__ out8,
                                                          uint64_t* __restrict__ out64,
-                                                         uint32_t* __restrict__ any_flag) {
+                                                         uint32_t* __restrict__ any_flag,
+                                                         unsigned long long* __restrict__ counts) {
     __shared__ uint64_t s_off[kBlock + 1];
     __shared__ uint4 s_stage[kStageVec + 1];   // +1 vector: slack for the `hi` word of the last key
+    __shared__ uint32_t s_hist[OP == BF_OP_ROUTE ? 256 : 1];
 
     const uint64_t blk0 = (uint64_t)blockIdx.x * kBlock;
     const uint32_t t = threadIdx.x;
@@ -171,6 +192,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
 
     if (t < cnt) s_off[t] = offsets[blk0 + t] + bias;
     if (t == 0) s_off[cnt] = offsets[blk0 + cnt] + bias;
+    if constexpr (OP == BF_OP_ROUTE) s_hist[t] = 0;   // kBlock == 256 bins
     __syncthreads();
 
     const uint64_t start = s_off[0];
@@ -188,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
             const uint32_t s = (uint32_t)(s_off[t] - abase);
             const uint32_t L = (uint32_t)(s_off[t + 1] - s_off[t]);
             const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_stage);
-            key_op<OP>(g, sw, s, L, blk0 + t, out8, out64, newflag);
+            key_op<OP>(g, sw, s, L, blk0 + t, out8, out64, newflag, s_hist);
         }
     } else if (t < cnt) {
         // Span too large for the stage (long keys): read each key straight from global.
@@ -196,7 +218,12 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
         const uint64_t kbase = ks & ~(uint64_t)3;
         const uint32_t* gw = reinterpret_cast<const uint32_t*>(keys16 + kbase);
         const uint64_t L64 = s_off[t + 1] - ks;
-        key_op<OP>(g, gw, (uint32_t)(ks - kbase), (uint32_t)L64, blk0 + t, out8, out64, newflag);
+        key_op<OP>(g, gw, (uint32_t)(ks - kbase), (uint32_t)L64, blk0 + t, out8, out64, newflag, s_hist);
+    }
+
+    if constexpr (OP == BF_OP_ROUTE) {
+        __syncthreads();
+        if (t < g.shards && s_hist[t]) atomicAdd(counts + t, (unsigned long long)s_hist[t]);
     }
 
     if constexpr (OP == BF_OP_INSERT_FLAGS) {
@@ -240,6 +267,102 @@ __global__ __launch_bounds__(256) void or_kernel(uint4* __restrict__ dst, const 
     }
 }
 
+// ---- partitioned filters ---------------------------------------------------
+
+constexpr int kScatterItems = 8;   // probes per lane in the scatter pass
+
+// cursor[s] = exclusive prefix sum of counts (P <= 255: one wave is plenty).
+__global__ void displ_kernel(const unsigned long long* __restrict__ counts, uint32_t P,
+                             unsigned long long* __restrict__ cursor) {
+    if (threadIdx.x == 0) {
+        unsigned long long acc = 0;
+        for (uint32_t s = 0; s < P; ++s) { cursor[s] = acc; acc += counts[s]; }
+    }
+}
+
+// Groups probes by owner: one LDS histogram per workgroup, one global
+// atomicAdd per (workgroup, owner) to reserve a contiguous range, then every
+// probe lands at range base + its LDS rank.
+__global__ __launch_bounds__(256) void route_scatter_kernel(const uint64_t* __restrict__ local,
+                                                            const uint8_t* __restrict__ owner,
+                                                            uint64_t total, uint32_t P,
+                                                            unsigned long long* __restrict__ cursor,
+                                                            uint64_t* __restrict__ send,
+                                                            uint32_t* __restrict__ slot) {
+    __shared__ uint32_t s_cnt[256];
+    __shared__ unsigned long long s_base[256];
+    const uint32_t t = threadIdx.x;
+    s_cnt[t] = 0;
+    __syncthreads();
+    const uint64_t p0 = (uint64_t)blockIdx.x * 256 * kScatterItems;
+    uint32_t own[kScatterItems], rank[kScatterItems];
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const uint64_t p = p0 + (uint64_t)it * 256 + t;
+        own[it] = 0xFFFFFFFFu;
+        if (p < total) {
+            own[it] = owner[p];
+            rank[it] = atomicAdd(s_cnt + own[it], 1u);
+        }
+    }
+    __syncthreads();
+    if (t < P && s_cnt[t]) s_base[t] = atomicAdd(cursor + t, (unsigned long long)s_cnt[t]);
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kScatterItems; ++it) {
+        const uint64_t p = p0 + (uint64_t)it * 256 + t;
+        if (own[it] != 0xFFFFFFFFu) {
+            const unsigned long long pos = s_base[own[it]] + rank[it];
+            send[pos] = local[p];
+            slot[p] = (uint32_t)pos;
+        }
+    }
+}
+
+template <bool FLAGS>
+__global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
+                                                           const uint64_t* __restrict__ local,
+                                                           uint64_t count, uint32_t* __restrict__ any_flag) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t isnew = 0;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < count; p += stride) {
+        const uint64_t o = local[p];
+        const uint32_t mask = 1u << ((uint32_t)(o ^ 7u) & 31u);
+        if constexpr (FLAGS) {
+            const uint32_t old = __hip_atomic_fetch_or(bits + (o >> 5), mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            isnew |= (old & mask) ? 0u : 1u;
+        } else {
+            __hip_atomic_fetch_or(bits + (o >> 5), mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if constexpr (FLAGS) {
+        const unsigned long long b = __ballot(isnew != 0);
+        if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
+            __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits,
+                                                         const uint64_t* __restrict__ local, uint64_t count,
+                                                         uint8_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < count; p += stride) {
+        const uint64_t o = local[p];
+        out[p] = (uint8_t)((bits[o >> 5] >> ((uint32_t)(o ^ 7u) & 31u)) & 1u);
+    }
+}
+
+__global__ __launch_bounds__(256) void combine_kernel(const uint8_t* __restrict__ bits,
+                                                      const uint32_t* __restrict__ slot, uint64_t n,
+                                                      uint32_t k, uint8_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        uint32_t ok = 1u;
+        for (uint32_t i = 0; i < k; ++i) ok &= bits[slot[j * k + i]];
+        out[j] = (uint8_t)ok;
+    }
+}
+
 uint32_t stream_grid(uint64_t nvec) {
     uint64_t g = (nvec + 255) / 256;
     if (g > 2048) g = 2048;   // grid-stride beyond 8 blocks per CU
@@ -250,27 +373,62 @@ uint32_t stream_grid(uint64_t nvec) {
 
 hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets,
                           uint64_t bias, uint64_t n, uint8_t* out8, uint64_t* out64,
-                          uint32_t* any_flag, hipStream_t s) {
+                          uint32_t* any_flag, hipStream_t s, unsigned long long* counts) {
     if (n == 0) return hipSuccess;
     const uint64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const dim3 grid((uint32_t)blocks), block(kBlock);
+#define BF_LAUNCH(OPC) \
+    hipLaunchKernelGGL(bf_keys_kernel<OPC>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag, counts)
     switch (op) {
-        case BF_OP_INDEXES:
-            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INDEXES>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
-            break;
-        case BF_OP_INCLUDE:
-            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INCLUDE>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
-            break;
-        case BF_OP_INSERT:
-            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INSERT>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
-            break;
-        case BF_OP_INSERT_FLAGS:
-            hipLaunchKernelGGL(bf_keys_kernel<BF_OP_INSERT_FLAGS>, grid, block, 0, s, g, keys16, offsets, bias, n, out8, out64, any_flag);
+        case BF_OP_INDEXES: BF_LAUNCH(BF_OP_INDEXES); break;
+        case BF_OP_INCLUDE: BF_LAUNCH(BF_OP_INCLUDE); break;
+        case BF_OP_INSERT: BF_LAUNCH(BF_OP_INSERT); break;
+        case BF_OP_INSERT_FLAGS: BF_LAUNCH(BF_OP_INSERT_FLAGS); break;
+        case BF_OP_ROUTE:
+            if (!counts || g.shards == 0 || g.shards > 255) return hipErrorInvalidValue;
+            BF_LAUNCH(BF_OP_ROUTE);
             break;
         default:
             return hipErrorInvalidValue;
     }
+#undef BF_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_route_scatter(const uint64_t* local, const uint8_t* owner, uint64_t total, uint32_t P,
+                                   const unsigned long long* counts, unsigned long long* cursor,
+                                   uint64_t* send, uint32_t* slot, hipStream_t s) {
+    hipLaunchKernelGGL(displ_kernel, dim3(1), dim3(64), 0, s, counts, P, cursor);
+    if (total == 0) return hipGetLastError();
+    const uint64_t per = 256ull * kScatterItems;
+    const uint64_t blocks = (total + per - 1) / per;
+    hipLaunchKernelGGL(route_scatter_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, local, owner, total, P,
+                       cursor, send, slot);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_shard_insert(uint32_t* bits, const uint64_t* local, uint64_t count, uint32_t* any_flag,
+                                  hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (any_flag)
+        hipLaunchKernelGGL(shard_insert_kernel<true>, dim3(stream_grid(count)), dim3(256), 0, s, bits, local, count, any_flag);
+    else
+        hipLaunchKernelGGL(shard_insert_kernel<false>, dim3(stream_grid(count)), dim3(256), 0, s, bits, local, count, any_flag);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_shard_test(const uint32_t* bits, const uint64_t* local, uint64_t count, uint8_t* out,
+                                hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(shard_test_kernel, dim3(stream_grid(count)), dim3(256), 0, s, bits, local, count, out);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k, uint8_t* out,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(combine_kernel, dim3(stream_grid(n)), dim3(256), 0, s, bits, slot, n, k, out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,251 @@
+"""Multi-GPU filters: one process per GPU, collectives through torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests).
+
+Two layouts (SURVEY §8 e):
+
+``PartitionedFilter`` — the filter's reachable prefix is split block-cyclically
+    over the P ranks (block = 2^block_log2 bits, owner = block % P), so a
+    filter larger than one GPU's HBM (the 200B-key config) fits, and the
+    probe-dense low offsets (h0 < 2^32, ruby.rb:51) spread over every GPU.
+    insert:   route (hash -> owner-local offsets grouped by owner) ->
+              all_to_all(counts) -> all_to_all(offsets) -> owner atomic-OR
+    include?: route -> all_to_all(offsets) -> owner bit test ->
+              reverse all_to_all(1 byte per probe) -> requester AND per key
+    Each rank brings its own key batch (weak scaling); the only data-path
+    collectives are the two all-to-alls the ownership split makes necessary.
+
+``ReplicatedFilter`` — every rank holds the whole filter (read-mostly
+    filters that fit one GPU).  include? is purely local (no collective);
+    insert all-gathers the packed key batches so every replica applies every
+    rank's inserts and the replicas stay byte-identical.
+
+The per-rank compute goes through an *engine* with four primitives (route,
+shard_insert, shard_test, combine); ``HipEngine`` is libbfhip.so's
+``bf_route_dev`` / ``bf_shard_*_dev`` / ``bf_combine_dev``.  The CPU tests
+substitute a numpy engine to exercise this module's exchange logic over gloo.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import keys as _keys
+from ._lib import ArgumentError, Filter
+
+
+def block_owner_local(offsets: np.ndarray, P: int, block_log2: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Host restatement of the ownership map in include/bfhip.h (for tooling and tests)."""
+    o = offsets.astype(np.uint64)
+    blk = o >> np.uint64(block_log2)
+    owner = (blk % np.uint64(P)).astype(np.int64)
+    local = ((blk // np.uint64(P)) << np.uint64(block_log2)) | (o & np.uint64((1 << block_log2) - 1))
+    return owner, local
+
+
+def shard_local_bits(reach_bits: int, P: int, s: int, block_log2: int) -> int:
+    nblocks = (reach_bits + (1 << block_log2) - 1) >> block_log2
+    mine = (nblocks - 1 - s) // P + 1 if nblocks > s else 0
+    return mine << block_log2
+
+
+def interleave_shards(shards: List[np.ndarray], reach_bits: int, block_log2: int) -> bytes:
+    """Rebuild the Redis string (trimmed) from every shard's local bytes."""
+    P = len(shards)
+    bb = (1 << block_log2) // 8
+    nblocks = (reach_bits + (1 << block_log2) - 1) >> block_log2
+    out = np.zeros(nblocks * bb, dtype=np.uint8)
+    view = out.reshape(nblocks, bb)
+    for s, loc in enumerate(shards):
+        cnt = len(range(s, nblocks, P))
+        if cnt:
+            view[s::P] = np.asarray(loc, dtype=np.uint8)[: cnt * bb].reshape(cnt, bb)
+    out = out[: (reach_bits + 7) // 8]
+    nz = np.flatnonzero(out)
+    return out[: nz[-1] + 1].tobytes() if len(nz) else b""
+
+
+def split_shard(data: bytes, P: int, s: int, reach_bits: int, block_log2: int) -> np.ndarray:
+    """Shard s's local bytes of a Redis string (inverse of interleave_shards)."""
+    bb = (1 << block_log2) // 8
+    nblocks = (reach_bits + (1 << block_log2) - 1) >> block_log2
+    full = np.zeros(nblocks * bb, dtype=np.uint8)
+    src = np.frombuffer(data, dtype=np.uint8)
+    if len(src) > (reach_bits + 7) // 8:
+        raise ArgumentError("string of %d bytes exceeds the filter's reachable bytes" % len(src))
+    full[: len(src)] = src
+    return np.ascontiguousarray(full.reshape(nblocks, bb)[s::P]).reshape(-1)
+
+
+class HipEngine:
+    """Per-rank primitives on libbfhip.so (one shard handle on this rank's GPU)."""
+
+    def __init__(self, m: int, k: int, P: int, rank: int, block_log2: int, device: torch.device):
+        self.device = device
+        self.filter = Filter(m, k, device=device.index if device.index is not None else -1,
+                             shard_count=P, shard_index=rank, shard_block_log2=block_log2)
+        self.k, self.P = k, P
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def route(self, kb: torch.Tensor, ko: torch.Tensor, n: int):
+        send = torch.empty(n * self.k, dtype=torch.int64, device=self.device)
+        slot = torch.empty(n * self.k, dtype=torch.int32, device=self.device)
+        counts = torch.empty(self.P, dtype=torch.int64, device=self.device)
+        self.filter.route_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(), slot.data_ptr(),
+                              counts.data_ptr(), stream=self._stream())
+        return send, slot, counts
+
+    def shard_insert(self, local: torch.Tensor) -> None:
+        self.filter.shard_insert_dev(local.data_ptr(), local.numel(), stream=self._stream())
+
+    def shard_test(self, local: torch.Tensor) -> torch.Tensor:
+        out = torch.empty(local.numel(), dtype=torch.uint8, device=self.device)
+        self.filter.shard_test_dev(local.data_ptr(), local.numel(), out.data_ptr(), stream=self._stream())
+        return out
+
+    def combine(self, bits: torch.Tensor, slot: torch.Tensor, n: int) -> torch.Tensor:
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self.filter.combine_dev(bits.data_ptr(), slot.data_ptr(), n, out.data_ptr(), stream=self._stream())
+        return out
+
+    def clear(self) -> None:
+        self.filter.clear() if self.P == 1 else self.filter.shard_import(b"")
+
+    def shard_export(self) -> np.ndarray:
+        torch.cuda.current_stream(self.device).synchronize()
+        return self.filter.shard_export()
+
+    def shard_import(self, local: np.ndarray) -> None:
+        torch.cuda.current_stream(self.device).synchronize()
+        self.filter.shard_import(local.tobytes())
+
+    def close(self):
+        self.filter.close()
+
+
+def _device_batch(keys, device) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    buf, offs = _keys.pack(keys)
+    kb = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(device)
+    ko = torch.from_numpy(offs.view(np.int64)).to(device)
+    return kb, ko, len(offs) - 1
+
+
+class PartitionedFilter:
+    """A filter block-cyclically partitioned over the ranks of a process group."""
+
+    def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None):
+        self.group = group
+        self.P = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.m, self.k, self.block_log2 = int(m), int(k), int(block_log2)
+        self.reach_bits = min(self.m, self.k * 0xFFFFFFFF + 1)
+        if engine is None:
+            device = device or torch.device("cuda", torch.cuda.current_device())
+            engine = HipEngine(self.m, self.k, self.P, self.rank, self.block_log2, device)
+        self.engine = engine
+        self.device = engine.device
+
+    # -- exchange helpers
+    def _exchange(self, send: torch.Tensor, counts: torch.Tensor):
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts, group=self.group)
+        cnt = torch.stack([counts, recv_counts]).cpu()
+        send_splits, recv_splits = cnt[0].tolist(), cnt[1].tolist()
+        recv = torch.empty(sum(recv_splits), dtype=send.dtype, device=send.device)
+        dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group)
+        return recv, send_splits, recv_splits
+
+    # -- device-resident batch API (keys already in device memory)
+    def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
+        send, _, counts = self.engine.route(kb, ko, n)
+        recv, _, _ = self._exchange(send, counts)
+        self.engine.shard_insert(recv)
+
+    def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
+        send, slot, counts = self.engine.route(kb, ko, n)
+        recv, send_splits, recv_splits = self._exchange(send, counts)
+        bits = self.engine.shard_test(recv)
+        back = torch.empty(sum(send_splits), dtype=torch.uint8, device=bits.device)
+        dist.all_to_all_single(back, bits, send_splits, recv_splits, group=self.group)
+        return self.engine.combine(back, slot, n)
+
+    # -- host API (each rank passes its own keys)
+    def insert_many(self, keys: Iterable) -> None:
+        kb, ko, n = _device_batch(keys, self.device)
+        self.insert_many_dev(kb, ko, n)
+
+    def include_many(self, keys: Iterable) -> np.ndarray:
+        kb, ko, n = _device_batch(keys, self.device)
+        return self.include_many_dev(kb, ko, n).cpu().numpy().astype(bool)
+
+    def clear(self) -> None:
+        self.engine.clear()
+
+    # -- Redis string (collective: every rank must call)
+    def export_redis(self) -> bytes:
+        local = self.engine.shard_export()
+        parts: List[Optional[np.ndarray]] = [None] * self.P
+        dist.all_gather_object(parts, local, group=self.group)
+        return interleave_shards(parts, self.reach_bits, self.block_log2)
+
+    def import_redis(self, data: bytes) -> None:
+        self.engine.shard_import(split_shard(data, self.P, self.rank, self.reach_bits, self.block_log2))
+
+    def close(self):
+        self.engine.close()
+
+
+class ReplicatedFilter:
+    """Every rank holds the whole filter; include? is local, insert is all-gathered."""
+
+    def __init__(self, m: int, k: int, group=None, device=None):
+        self.group = group
+        self.P = dist.get_world_size(group)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.filter = Filter(m, k, device=self.device.index)
+        self.k = k
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
+        sizes = torch.tensor([kb.numel(), n], dtype=torch.int64, device=self.device)
+        all_sizes = [torch.empty_like(sizes) for _ in range(self.P)]
+        dist.all_gather(all_sizes, sizes, group=self.group)
+        all_sizes = torch.stack(all_sizes).cpu().tolist()
+        max_b = max(s[0] for s in all_sizes)
+        max_n = max(s[1] for s in all_sizes)
+        kb_p = torch.zeros(max_b, dtype=torch.uint8, device=self.device)
+        kb_p[: kb.numel()] = kb
+        ko_p = torch.zeros(max_n + 1, dtype=torch.int64, device=self.device)
+        ko_p[: n + 1] = ko[: n + 1]
+        gk = [torch.empty_like(kb_p) for _ in range(self.P)]
+        go = [torch.empty_like(ko_p) for _ in range(self.P)]
+        dist.all_gather(gk, kb_p, group=self.group)
+        dist.all_gather(go, ko_p, group=self.group)
+        for (nbytes, cnt), k_t, o_t in zip(all_sizes, gk, go):
+            self.filter.insert_many_dev(k_t.data_ptr(), o_t.data_ptr(), cnt, stream=self._stream())
+
+    def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self.filter.include_many_dev(kb.data_ptr(), ko.data_ptr(), n, out.data_ptr(), stream=self._stream())
+        return out
+
+    def insert_many(self, keys: Iterable) -> None:
+        kb, ko, n = _device_batch(keys, self.device)
+        self.insert_many_dev(kb, ko, n)
+
+    def include_many(self, keys: Iterable) -> np.ndarray:
+        kb, ko, n = _device_batch(keys, self.device)
+        return self.include_many_dev(kb, ko, n).cpu().numpy().astype(bool)
+
+    def export_redis(self) -> bytes:
+        torch.cuda.current_stream(self.device).synchronize()
+        return self.filter.export_redis()
+
+    def close(self):
+        self.filter.close()

@@ -1,0 +1,74 @@
+"""One rank of the multi-process partitioned-filter test (launched by
+tests/test_distributed.py through torch.distributed.run, gloo on CPU).
+
+The exchange logic under test is redis-bloomfilter_amd/distributed.py; the
+per-rank primitives come from a numpy engine built on the oracle (test
+infrastructure), since this container has no GPU.  Rank 0 checks the
+assembled Redis string and every include? answer against a single-filter
+oracle run over all ranks' keys.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("BFHIP_STANDALONE", "1")
+
+import pkgload  # noqa: E402
+import oracle as O  # noqa: E402  (checker / reference engine only)
+
+pkg = pkgload.load()
+from redis_bloomfilter_amd import distributed as D  # noqa: E402
+from ref_engine import NumpyEngine  # noqa: E402
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, P = dist.get_rank(), dist.get_world_size()
+    cfg = json.loads(os.environ["BF_DIST_CFG"])
+    m, k, b = cfg["m"], cfg["k"], cfg["block_log2"]
+    orc = O.COracle()
+    pf = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    rng = np.random.default_rng([cfg["seed"], rank])
+    mine = [("r%d-%d" % (rank, int(v))) for v in rng.integers(0, 10**9, cfg["n"])]
+    pf.insert_many(mine)
+    probe = ["r%d-%d" % (r, int(v)) for r in range(P)
+             for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, cfg["n"])]
+    probe += ["fresh-%d-%d" % (rank, i) for i in range(cfg["n"])]
+    got = pf.include_many(probe)
+    s = pf.export_redis()
+    # round trip: a fresh partitioned filter loaded from the string answers identically
+    pf2 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    pf2.import_redis(s)
+    got2 = pf2.include_many(probe)
+    ok = True
+    if rank == 0 or True:
+        all_keys = [("r%d-%d" % (r, int(v))) for r in range(P)
+                    for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, cfg["n"])]
+        ib, io = O.pack_keys(all_keys)
+        bits = orc.new_bitset(m, k)
+        orc.insert_many(bits, m, k, ib, io)
+        want_s = orc.redis_string(bits)
+        pb, po = O.pack_keys(probe)
+        want = orc.include_many(bits, m, k, pb, po).astype(bool)
+        ok = (s == want_s) and bool((got == want).all()) and bool((got2 == want).all())
+        if not ok:
+            print("rank %d MISMATCH: string %s (%d vs %d bytes), include %d diffs" %
+                  (rank, s == want_s, len(s), len(want_s), int((got != want).sum())), flush=True)
+    flag = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print("DIST_RESULT", "ok" if flag.item() == 1 else "fail", flush=True)
+    dist.destroy_process_group()
+    sys.exit(0 if flag.item() == 1 else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,111 @@
+"""Partitioned-filter primitives on the GPU (route / shard insert / shard test /
+combine through the C ABI), with P shards simulated in one process on one
+MI355X, plus the torch.distributed layer at world size 1 over RCCL.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+
+def dev_batch(pkg, torch, keys):
+    buf, offs = pkg.keys.pack(keys)
+    kb = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).cuda()
+    ko = torch.from_numpy(offs.view(np.int64)).cuda()
+    return kb, ko, len(offs) - 1, buf, offs
+
+
+@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20)])
+def test_simulated_partition(pkg, oracle, m, k, P, b):
+    import torch
+    D = pkg.distributed
+    dev = torch.device("cuda", 0)
+    shards = [D.HipEngine(m, k, P, s, b, dev) for s in range(P)]
+    rng = np.random.default_rng(9)
+    per_rank = [["p%d-%d" % (r, int(v)) for v in rng.integers(0, 10**9, 4000)] for r in range(P)]
+    routed = []
+    for r in range(P):
+        kb, ko, n, buf, offs = dev_batch(pkg, torch, per_rank[r])
+        send, slot, counts = shards[r].route(kb, ko, n)
+        torch.cuda.synchronize()
+        # route invariants vs the oracle: every probe lands in its owner's segment at the right local offset
+        idx = oracle.indexes_many(buf, offs, m, k).reshape(-1)
+        owner, local = D.block_owner_local(idx, P, b)
+        c = counts.cpu().numpy()
+        assert c.tolist() == np.bincount(owner, minlength=P).tolist()
+        s_np = send.cpu().numpy().view(np.uint64)
+        sl = slot.cpu().numpy().astype(np.int64)
+        assert sorted(sl.tolist()) == list(range(n * k))
+        np.testing.assert_array_equal(s_np[sl], local)
+        displ = np.concatenate([[0], np.cumsum(c)[:-1]])
+        seg_owner = np.searchsorted(np.cumsum(c), sl, side="right")
+        np.testing.assert_array_equal(seg_owner, owner)
+        routed.append((send, slot, c, displ, n))
+    # exchange: owner s receives every rank's segment s
+    for s in range(P):
+        recv = torch.cat([send[int(d[s]):int(d[s] + c[s])] for send, _, c, d, _ in routed])
+        shards[s].shard_insert(recv)
+    torch.cuda.synchronize()
+    ib, io = pkg.keys.pack([x for r in range(P) for x in per_rank[r]])
+    bits = oracle.new_bitset(m, k)
+    oracle.insert_many(bits, m, k, ib, io)
+    want_str = oracle.redis_string(bits)
+    got_str = D.interleave_shards([e.shard_export() for e in shards], shards[0].filter.reach_bits, b)
+    assert got_str == want_str
+    # include?: members of every rank + fresh keys, answered via owners and combined
+    probe = per_rank[0][:2000] + per_rank[P - 1][:2000] + ["fresh%d" % i for i in range(4000)]
+    kb, ko, n, pb, po = dev_batch(pkg, torch, probe)
+    send, slot, counts = shards[1 % P].route(kb, ko, n)
+    c = counts.cpu().numpy()
+    d = np.concatenate([[0], np.cumsum(c)[:-1]])
+    back = torch.empty(n * k, dtype=torch.uint8, device=dev)
+    for s in range(P):
+        seg = send[int(d[s]):int(d[s] + c[s])]
+        back[int(d[s]):int(d[s] + c[s])] = shards[s].shard_test(seg)
+    got = shards[1 % P].combine(back, slot, n).cpu().numpy()
+    want = oracle.include_many(bits, m, k, pb, po)
+    np.testing.assert_array_equal(got, want)
+    for e in shards:
+        e.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_torch_distributed_world1(pkg, oracle):
+    """PartitionedFilter and ReplicatedFilter over RCCL (world size 1) match a single filter."""
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        D = pkg.distributed
+        m, k = 9585058, 6
+        keys = ["k%d" % i for i in range(50_000)]
+        probe = keys[:20_000] + ["x%d" % i for i in range(20_000)]
+        ib, io = pkg.keys.pack(keys)
+        pb, po = pkg.keys.pack(probe)
+        bits = oracle.new_bitset(m, k)
+        oracle.insert_many(bits, m, k, ib, io)
+        want = oracle.include_many(bits, m, k, pb, po).astype(bool)
+        for cls, kw in ((D.PartitionedFilter, {"block_log2": 16}), (D.ReplicatedFilter, {})):
+            f = cls(m, k, **kw)
+            f.insert_many(keys)
+            np.testing.assert_array_equal(f.include_many(probe), want)
+            assert f.export_redis() == oracle.redis_string(bits)
+            f.close()
+    finally:
+        dist.destroy_process_group()
