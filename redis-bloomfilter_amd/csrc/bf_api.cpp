@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -46,6 +47,7 @@ struct bf_handle {
     uint32_t k = 0;
     // partitioned filters: this handle holds shard `shard_index` of `shards`
     uint32_t shards = 1, shard_index = 0, block_log2 = 20;
+    uint32_t mem_kind = 0;   // bitset allocation: 0 coarse-grained, 1 uncached, 2 fine-grained
     uint64_t local_bits = 0;
     // routing scratch (grown on demand)
     uint64_t* d_tmp_local = nullptr;
@@ -95,6 +97,21 @@ struct DeviceGuard {
 };
 
 uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// Probe-policy defaults, measured on MI355X with tools/ab_policies.py (profiles/
+// ab_policies_r01.jsonl): include? loads ceil(k/4) probes before its first
+// early-exit check (1B@1%: 1.82 -> 1.39 ms per 2^24 keys), insert loads the k
+// words and atomics only the unset bits (5.13 -> 3.30 ms).  The environment
+// overrides exist for A/B runs and never change results.
+uint32_t default_first_round(uint32_t k) { return (k + 3) / 4; }
+constexpr uint32_t kDefaultInsertTest = 1;
+constexpr uint32_t kDefaultMemKind = 0;
+
+uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = getenv(name);
+    if (!v || !*v) return dflt;
+    return (uint32_t)strtoul(v, nullptr, 10);
+}
 
 int free_staging(bf_handle* h) {
     for (Slot& s : h->slot) {
@@ -346,7 +363,13 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     if (!dg.ok) return fail(BF_EDEVICE, "hipSetDevice", hipErrorInvalidDevice);
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(BF_EDEVICE, "hipStreamCreate", e);
-    if ((e = hipMalloc((void**)&h->g.bits, h->dev_bytes)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(bitset)", e);
+    // Bitset memory kind (A/B knob): 0 coarse-grained hipMalloc, 1 uncached (MTYPE UC),
+    // 2 fine-grained.
+    h->mem_kind = env_u32("BFHIP_BITS_MEM", kDefaultMemKind);
+    if (h->mem_kind == 1) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocUncached);
+    else if (h->mem_kind == 2) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocFinegrained);
+    else e = hipMalloc((void**)&h->g.bits, h->dev_bytes);
+    if (e != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(bitset)", e);
     if ((e = hipMalloc((void**)&h->d_flag, 256)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(flag)", e);
     if ((e = hipMalloc((void**)&h->d_scan, 256)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(scan)", e);
     if ((e = hipHostMalloc((void**)&h->h_flag, 64, hipHostMallocDefault)) != hipSuccess) return fail(BF_ENOMEM, "hipHostMalloc", e);
@@ -358,6 +381,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.nomod = (m_bits > maxval) ? 1u : 0u;
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
+    h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k));
+    h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     *out = h;
     return BF_OK;
 }

@@ -12,6 +12,9 @@ struct BfGeom {
     uint32_t  nomod;   // 1 iff m > k*(2^32-1): every derived offset is already < m
     uint32_t  shards;  // partitioned filters: shard count P (1 = whole filter)
     uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
+    // probe policies (tuning; results are identical for every setting)
+    uint32_t  first_round;  // include?: probes loaded before the first early-exit check (0 = all k)
+    uint32_t  insert_test;  // insert: 1 = load the k words first, atomic-OR only the unset bits
 };
 
 enum BfOp : int {

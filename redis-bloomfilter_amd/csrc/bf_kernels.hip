@@ -137,13 +137,19 @@ __device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uin
             atomicAdd(hist + owner, 1u);   // LDS histogram
         }
     } else if constexpr (OP == BF_OP_INCLUDE) {
+        // Rounds of up to kChunk independent loads; after the first round (first_round
+        // probes) a lane whose AND already failed stops issuing loads — ruby.rb:23's
+        // early exit, which only ever saves bandwidth, never changes the answer.
         uint32_t ok = 1u;
-        for (uint32_t i0 = 0; i0 < k; i0 += kChunk) {
+        uint32_t i0 = 0;
+        uint32_t rend = (g.first_round && g.first_round < k) ? g.first_round : k;
+        while (i0 < k) {
+            const uint32_t e = (i0 + kChunk < rend) ? i0 + kChunk : rend;
             uint32_t v[kChunk], sh[kChunk];
 #pragma unroll
-            for (int c = 0; c < kChunk; ++c) {   // issue every load of the chunk first
+            for (int c = 0; c < kChunk; ++c) {   // issue every load of the round first
                 v[c] = 0xFFFFFFFFu; sh[c] = 0;
-                if (i0 + c < k) {
+                if (i0 + c < e) {
                     const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + c);
                     sh[c] = (uint32_t)(o ^ 7u) & 31u;
                     v[c] = g.bits[o >> 5];
@@ -151,19 +157,39 @@ __device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uin
             }
 #pragma unroll
             for (int c = 0; c < kChunk; ++c) ok &= v[c] >> sh[c];
+            i0 = e;
+            rend = k;
+            if (!(ok & 1u)) break;
         }
         out8[key] = (uint8_t)(ok & 1u);
     } else {
         uint32_t isnew = 0;
-        for (uint32_t i = 0; i < k; ++i) {
-            const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i);
-            const uint32_t mask = 1u << ((uint32_t)(o ^ 7u) & 31u);
-            if constexpr (OP == BF_OP_INSERT_FLAGS) {
-                const uint32_t old = __hip_atomic_fetch_or(g.bits + (o >> 5), mask, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                isnew |= (old & mask) ? 0u : 1u;
-            } else {
-                __hip_atomic_fetch_or(g.bits + (o >> 5), mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t i0 = 0; i0 < k; i0 += kChunk) {
+            uint64_t w[kChunk];
+            uint32_t mask[kChunk], v[kChunk];
+#pragma unroll
+            for (int c = 0; c < kChunk; ++c) {
+                w[c] = 0; mask[c] = 0; v[c] = 0;
+                if (i0 + c < k) {
+                    const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + c);
+                    w[c] = o >> 5;
+                    mask[c] = 1u << ((uint32_t)(o ^ 7u) & 31u);
+                    // test-then-set: a 1 seen here is final (bits only go 0 -> 1 within a
+                    // launch); a stale 0 just costs an atomic that then reports the truth.
+                    if (g.insert_test) v[c] = g.bits[w[c]];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kChunk; ++c) {
+                if (mask[c] && !(v[c] & mask[c])) {
+                    if constexpr (OP == BF_OP_INSERT_FLAGS) {
+                        const uint32_t old = __hip_atomic_fetch_or(g.bits + w[c], mask[c], __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        isnew |= (old & mask[c]) ? 0u : 1u;
+                    } else {
+                        __hip_atomic_fetch_or(g.bits + w[c], mask[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
             }
         }
         if constexpr (OP == BF_OP_INSERT_FLAGS) {

@@ -61,7 +61,10 @@ def interleave_shards(shards: List[np.ndarray], reach_bits: int, block_log2: int
     for s, loc in enumerate(shards):
         cnt = len(range(s, nblocks, P))
         if cnt:
-            view[s::P] = np.asarray(loc, dtype=np.uint8)[: cnt * bb].reshape(cnt, bb)
+            arr = np.asarray(loc, dtype=np.uint8)[: cnt * bb]
+            if len(arr) < cnt * bb:   # a whole-filter handle (P == 1) stops at the reachable prefix
+                arr = np.concatenate([arr, np.zeros(cnt * bb - len(arr), np.uint8)])
+            view[s::P] = arr.reshape(cnt, bb)
     out = out[: (reach_bits + 7) // 8]
     nz = np.flatnonzero(out)
     return out[: nz[-1] + 1].tobytes() if len(nz) else b""
@@ -121,7 +124,7 @@ class HipEngine:
 
     def shard_import(self, local: np.ndarray) -> None:
         torch.cuda.current_stream(self.device).synchronize()
-        self.filter.shard_import(local.tobytes())
+        self.filter.shard_import(local[: (self.filter.local_bits + 7) // 8].tobytes())
 
     def close(self):
         self.filter.close()

@@ -1,0 +1,195 @@
+# frozen_string_literal: true
+
+# Redis::BloomfilterDriver::Hip — the MI355X driver for the redis-bloomfilter gem.
+#
+# Drop-in next to lib/bloomfilter_driver/ruby.rb and lua.rb: the facade
+# resolves `driver: 'hip'` to this class through `const_get`
+# (lib/redis/bloomfilter.rb:43, driver_name at :77-79), passes the whole
+# options hash (with :bits and :hashes, :25-28) and then sets `redis=` (:45).
+#
+# The filter lives in HBM behind libbfhip.so (include/bfhip.h); Ruby talks to
+# it through FFI with `blocking: true`, so the GVL is released during device
+# work.  Redis keeps the same bitstring the ruby driver writes (SETBIT layout,
+# MSB-first), so the two drivers read each other's filters:
+#   * attaching (`redis=`) imports an existing key and its TTL;
+#   * sync: :write_through (default) writes the device string back with
+#     SETRANGE after an insert that flipped a bit (SETRANGE keeps the TTL and
+#     grows the string exactly like SETBIT), then EXPIREs iff a bit flipped and
+#     an expire was given (ruby.rb:61-62);
+#   * sync: :manual leaves Redis alone until #flush.
+# Extra options: :device (HIP ordinal), :sync, :batch_keys, :batch_bytes.
+require 'ffi'
+
+class Redis
+  module BloomfilterDriver
+    # FFI binding of include/bfhip.h (host-pointer entry points only).
+    module HipFFI
+      extend FFI::Library
+      ffi_lib ENV.fetch('BFHIP_LIB', File.expand_path('../../../lib/libbfhip.so', __dir__))
+
+      BF_OK = 0
+      BF_EINVAL = 1
+      BF_ERANGE = 5
+      BF_IMPORT_REPLACE = 0
+
+      # struct bf_config (include/bfhip.h)
+      class Config < FFI::Struct
+        layout :struct_size, :uint32, :device, :int32, :batch_keys, :uint64, :batch_bytes, :uint64,
+               :shard_count, :uint32, :shard_index, :uint32, :shard_block_log2, :uint32, :reserved, :uint32
+      end
+
+      attach_function :bf_version, [], :string
+      attach_function :bf_last_error, [:pointer], :string
+      attach_function :bf_create, %i[uint64 uint32 pointer pointer], :int, blocking: true
+      attach_function :bf_destroy, [:pointer], :int, blocking: true
+      attach_function :bf_insert_many, %i[pointer pointer pointer uint64 pointer pointer], :int, blocking: true
+      attach_function :bf_include_many, %i[pointer pointer pointer uint64 pointer], :int, blocking: true
+      attach_function :bf_clear, [:pointer], :int, blocking: true
+      attach_function :bf_export_redis, %i[pointer pointer uint64 pointer], :int, blocking: true
+      attach_function :bf_import_redis, %i[pointer pointer uint64 uint32], :int, blocking: true
+    end
+
+    class Hip
+      attr_reader :redis
+
+      def initialize(options = {})
+        @options = options
+        bits = options[:bits]
+        # ruby.rb:51 would raise ZeroDivisionError on the first insert
+        raise ArgumentError, 'filter size in bits must be positive' unless bits.is_a?(Integer) && bits.positive?
+
+        @sync = (options[:sync] || :write_through).to_sym
+        raise ArgumentError, 'sync must be :write_through or :manual' unless %i[write_through manual].include?(@sync)
+
+        cfg = HipFFI::Config.new
+        cfg[:struct_size] = HipFFI::Config.size
+        cfg[:device] = options.fetch(:device, -1)
+        cfg[:batch_keys] = options.fetch(:batch_keys, 0)
+        cfg[:batch_bytes] = options.fetch(:batch_bytes, 0)
+        out = FFI::MemoryPointer.new(:pointer)
+        check(HipFFI.bf_create(bits, options[:hashes], cfg, out), nil)
+        @handle = FFI::AutoPointer.new(out.read_pointer, HipFFI.method(:bf_destroy))
+        @deadline = nil
+      end
+
+      # attr_accessor :redis (ruby.rb:9); attaching loads the existing filter.
+      def redis=(redis)
+        @redis = redis
+        reload if redis
+      end
+
+      # ruby.rb:15-17
+      def insert(data, expire = nil)
+        insert_many([data], expire)
+      end
+
+      # Batched insert; returns true iff some bit flipped (the ruby driver's !found).
+      def insert_many(keys, expire = nil)
+        expire_if_due
+        buf, offs, n = pack(keys)
+        flag = FFI::MemoryPointer.new(:uint8)
+        check(HipFFI.bf_insert_many(@handle, buf, offs, n, flag, nil))
+        changed = flag.read_uint8 == 1
+        if changed
+          flush if @redis && @sync == :write_through
+          if expire
+            @deadline = now + expire
+            @redis.expire(@options[:key_name], expire) if @redis && @sync == :write_through
+          end
+        end
+        changed
+      end
+
+      # ruby.rb:20-30
+      def include?(key)
+        include_many?([key]).first
+      end
+
+      def include_many?(keys)
+        expire_if_due
+        buf, offs, n = pack(keys)
+        out = FFI::MemoryPointer.new(:uint8, [n, 1].max)
+        check(HipFFI.bf_include_many(@handle, buf, offs, n, out))
+        out.read_array_of_uint8(n).map { |b| b == 1 }
+      end
+
+      # ruby.rb:33-35
+      def clear
+        check(HipFFI.bf_clear(@handle))
+        @deadline = nil
+        @redis&.del(@options[:key_name])
+      end
+
+      # Device filter -> Redis (SETRANGE 0: keeps the TTL, grows like SETBIT).
+      def flush
+        str = export
+        @redis.setrange(@options[:key_name], 0, str) if @redis && !str.empty?
+        str.bytesize
+      end
+
+      # Redis -> device filter (replace).
+      def reload
+        str = @redis.get(@options[:key_name])
+        @deadline = nil
+        if str.nil?
+          check(HipFFI.bf_clear(@handle))
+          return
+        end
+        mem = FFI::MemoryPointer.new(:uint8, [str.bytesize, 1].max)
+        mem.put_bytes(0, str)
+        check(HipFFI.bf_import_redis(@handle, mem, str.bytesize, HipFFI::BF_IMPORT_REPLACE))
+        ttl = @redis.ttl(@options[:key_name])
+        @deadline = now + ttl if ttl.positive?
+      end
+
+      def export
+        len = FFI::MemoryPointer.new(:uint64)
+        check(HipFFI.bf_export_redis(@handle, nil, 0, len))
+        n = len.read_uint64
+        buf = FFI::MemoryPointer.new(:uint8, [n, 1].max)
+        check(HipFFI.bf_export_redis(@handle, buf, n, len))
+        buf.read_bytes(n)
+      end
+
+      private
+
+      # `data.to_s` bytes (ruby.rb:42), packed as (bytes, uint64 offsets[n+1]).
+      def pack(keys)
+        strs = keys.map { |k| k.to_s.b }
+        n = strs.size
+        total = strs.sum(&:bytesize)
+        buf = FFI::MemoryPointer.new(:uint8, [total, 1].max)
+        offs = FFI::MemoryPointer.new(:uint64, n + 1)
+        pos = 0
+        offsets = [0]
+        strs.each do |s|
+          buf.put_bytes(pos, s) unless s.empty?
+          pos += s.bytesize
+          offsets << pos
+        end
+        offs.write_array_of_uint64(offsets)
+        [buf, offs, n]
+      end
+
+      def expire_if_due
+        return unless @deadline && now >= @deadline
+
+        @deadline = nil
+        check(HipFFI.bf_clear(@handle))
+      end
+
+      def now
+        Process.clock_gettime(Process::CLOCK_MONOTONIC)
+      end
+
+      def check(rc, handle = @handle)
+        return if rc == HipFFI::BF_OK
+
+        msg = HipFFI.bf_last_error(handle)
+        raise ArgumentError, msg if [HipFFI::BF_EINVAL, HipFFI::BF_ERANGE].include?(rc)
+
+        raise "bfhip error #{rc}: #{msg}"
+      end
+    end
+  end
+end

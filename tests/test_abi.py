@@ -22,6 +22,37 @@ def test_header_functions_listed_in_binding(pkg):
         "include/bfhip.h and _lib.SIGNATURES disagree"
 
 
+def header_arity():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for name, args in re.findall(r"\b(bf_[a-z_0-9]+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
+        args = args.strip()
+        out[name] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ruby_ffi_binding_matches_header():
+    """redis-bloomfilter_amd/ruby/.../hip.rb attaches only declared functions, with the right arity
+    (Ruby is not installed here, so this static check stands in for running it)."""
+    rb = open(os.path.join(ROOT, "redis-bloomfilter_amd", "ruby", "lib", "bloomfilter_driver", "hip.rb")).read()
+    arity = header_arity()
+    attached = re.findall(r"attach_function :(bf_\w+),\s*(%i\[[^\]]*\]|\[[^\]]*\])", rb)
+    assert len(attached) >= 9
+    for name, args in attached:
+        assert name in arity, name
+        if args.startswith("%i["):
+            n = len(args[3:-1].split())
+        else:
+            inner = args[1:-1].strip()
+            n = 0 if not inner else inner.count(",") + 1
+        assert n == arity[name], (name, n, arity[name])
+    # the FFI struct layout lists bf_config's fields in order
+    cfg = re.search(r"typedef struct bf_config \{(.*?)\} bf_config;", open(HEADER).read(), re.S).group(1)
+    fields = re.findall(r"\b(?:uint32_t|int32_t|uint64_t)\s+(\w+);", cfg)
+    layout = re.findall(r":(\w+), :(?:u?int\d+)", re.search(r"layout (.*?)\n\s*end", rb, re.S).group(1))
+    assert layout == fields
+
+
 def test_library_exports_every_symbol(pkg):
     lib = pkg._lib.load()
     for name in declared_functions():

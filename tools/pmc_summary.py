@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (tools/pmc_passes.sh) per hot kernel.
+
+    python tools/pmc_summary.py gpurun_out/pmc_* [--batch 16777216] [--json out.json]
+
+Keeps only the bench's timed launches (Grid_Size == batch) of the insert
+(bf_keys_kernel<2|3>) and include? (bf_keys_kernel<1>) kernels, averages each
+counter per launch, and derives HBM bytes per launch the way rocprofv3's own
+FETCH_SIZE / WRITE_SIZE expressions do (read requests weighted 32/64/128 B by
+TCC_EA0_RDREQ_32B / TCC_BUBBLE; write requests 32/64 B by TCC_EA0_WRREQ_64B).
+Atomic requests (TCC_EA0_ATOMIC) are reported separately, as 64 B each.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+KERNELS = {"include": re.compile(r"bf_keys_kernel<1>"), "insert": re.compile(r"bf_keys_kernel<[23]>")}
+
+
+def load(dirs, batch):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for d in dirs:
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            seen = set()
+            for r in csv.DictReader(open(path)):
+                if int(r["Grid_Size"]) != batch:
+                    continue
+                for name, rx in KERNELS.items():
+                    if rx.search(r["Kernel_Name"]):
+                        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                        key = (path, r["Dispatch_Id"])
+                        if key not in seen:
+                            seen.add(key)
+                            dur[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    return acc, dur
+
+
+def derive(c):
+    g = lambda n: (sum(c[n]) / len(c[n])) if c.get(n) else None  # noqa: E731
+    out = {k: g(k) for k in sorted(c)}
+    rd, rd32, bub = g("TCC_EA0_RDREQ_sum"), g("TCC_EA0_RDREQ_32B_sum"), g("TCC_BUBBLE_sum")
+    if rd is not None and rd32 is not None and bub is not None:
+        out["read_bytes"] = bub * 128 + (rd - bub - rd32) * 64 + rd32 * 32
+    wr, wr64 = g("TCC_EA0_WRREQ_sum"), g("TCC_EA0_WRREQ_64B_sum")
+    if wr is not None and wr64 is not None:
+        out["write_bytes"] = (wr - wr64) * 32 + wr64 * 64
+    if g("FETCH_SIZE") is not None:
+        out["FETCH_SIZE_bytes"] = g("FETCH_SIZE") * 1024
+    if g("WRITE_SIZE") is not None:
+        out["WRITE_SIZE_bytes"] = g("WRITE_SIZE") * 1024
+    at = g("TCC_EA0_ATOMIC_sum")
+    if at is not None:
+        out["atomic_bytes"] = at * 64
+    tot = sum(out.get(k) or 0 for k in ("read_bytes", "write_bytes", "atomic_bytes"))
+    out["hbm_bytes"] = tot if tot else None
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--workload", default="nstar")
+    ap.add_argument("--json")
+    args = ap.parse_args()
+    acc, dur = load([d for d in args.dirs if os.path.isdir(d)], args.batch)
+    res = {}
+    for name in KERNELS:
+        if name not in acc:
+            continue
+        d = derive(acc[name])
+        d["launches_counted"] = max(len(v) for v in acc[name].values())
+        d["profiled_ms_mean"] = sum(dur[name]) / len(dur[name]) if dur[name] else None
+        d["keys_per_launch"] = args.batch
+        if d.get("hbm_bytes"):
+            d["hbm_bytes_per_key"] = d["hbm_bytes"] / args.batch
+        res[name] = d
+    out = {args.workload: res}
+    txt = json.dumps(out, indent=1, sort_keys=True)
+    print(txt)
+    if args.json:
+        with open(args.json, "w") as fh:
+            fh.write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()
