@@ -282,11 +282,12 @@ def main():
     ap.add_argument("--config", default="nstar", choices=sorted(CONFIGS))
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
     args = ap.parse_args()
 
     D = Dist()
     pkg = pkgload.load()
-    main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1))
+    main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api))
     secondary = {}
     if D.world == 1 and not args.no_secondary:
         for name in ("1m", "100m"):

@@ -45,18 +45,21 @@ def derive(c):
     out = {k: g(k) for k in sorted(c)}
     rd, rd32, bub = g("TCC_EA0_RDREQ_sum"), g("TCC_EA0_RDREQ_32B_sum"), g("TCC_BUBBLE_sum")
     if rd is not None and rd32 is not None and bub is not None:
-        out["read_bytes"] = bub * 128 + (rd - bub - rd32) * 64 + rd32 * 32
+        # rocprofv3's FETCH_SIZE expression: on gfx950 it tallies 128-B requests at 64 B
+        # (MI355X_MICROARCH.md §HBM), kept for comparison only.
+        out["read_bytes_fetch_size_formula"] = bub * 128 + (rd - bub - rd32) * 64 + rd32 * 32
+    r128, r64 = g("TCC_EA0_RDREQ_128B_sum"), g("TCC_EA0_RDREQ_64B_sum")
+    if r128 is not None and r64 is not None and rd32 is not None:
+        # gfx950 correction: weight each request by the size the fabric actually moved.
+        out["read_bytes"] = r128 * 128 + r64 * 64 + rd32 * 32
     wr, wr64 = g("TCC_EA0_WRREQ_sum"), g("TCC_EA0_WRREQ_64B_sum")
     if wr is not None and wr64 is not None:
-        out["write_bytes"] = (wr - wr64) * 32 + wr64 * 64
+        out["write_bytes"] = (wr - wr64) * 32 + wr64 * 64   # atomics are counted here (32 B each)
     if g("FETCH_SIZE") is not None:
         out["FETCH_SIZE_bytes"] = g("FETCH_SIZE") * 1024
     if g("WRITE_SIZE") is not None:
         out["WRITE_SIZE_bytes"] = g("WRITE_SIZE") * 1024
-    at = g("TCC_EA0_ATOMIC_sum")
-    if at is not None:
-        out["atomic_bytes"] = at * 64
-    tot = sum(out.get(k) or 0 for k in ("read_bytes", "write_bytes", "atomic_bytes"))
+    tot = sum(out.get(k) or 0 for k in ("read_bytes", "write_bytes"))
     out["hbm_bytes"] = tot if tot else None
     return out
 
@@ -79,6 +82,8 @@ def main():
         d["keys_per_launch"] = args.batch
         if d.get("hbm_bytes"):
             d["hbm_bytes_per_key"] = d["hbm_bytes"] / args.batch
+            if d.get("profiled_ms_mean"):
+                d["hbm_GBps_profiled"] = d["hbm_bytes"] / (d["profiled_ms_mean"] / 1e3) / 1e9
         res[name] = d
     out = {args.workload: res}
     txt = json.dumps(out, indent=1, sort_keys=True)
