@@ -54,6 +54,13 @@ struct bf_handle {
     uint8_t*  d_tmp_owner = nullptr;
     uint64_t  tmp_cap = 0;
     unsigned long long* d_cursor = nullptr;
+    // binned-insert scratch (grown on demand) and policy: 0 never, 1 always, 2 auto
+    uint32_t binned_mode = 2;
+    uint32_t* d_bin_counts = nullptr;
+    uint32_t* d_bin_totals = nullptr;
+    uint32_t* d_bin_bases = nullptr;
+    uint32_t* d_binned = nullptr;
+    uint64_t bin_counts_cap = 0, bin_bins_cap = 0, binned_cap = 0;
     uint64_t cap_keys = 0, cap_bytes = 0;
     Slot slot[2];
     bool staging_ready = false;
@@ -106,6 +113,8 @@ uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 uint32_t default_first_round(uint32_t k) { return (k + 3) / 4; }
 constexpr uint32_t kDefaultInsertTest = 1;
 constexpr uint32_t kDefaultMemKind = 0;
+constexpr uint32_t kDefaultBinnedMode = 2;     // auto
+constexpr double kBinnedCostRatio = 3.0;       // random line-fill bytes vs bitset bytes
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
     const char* v = getenv(name);
@@ -167,6 +176,64 @@ int check_keys_args(bf_handle* h, const void* keys, const uint64_t* offsets, uin
     return BF_OK;
 }
 
+// Binned insert: worth it when the batch's random line fills (~128 B per probe)
+// clearly exceed one streaming pass over a bitset that lives beyond L2.
+bool use_binned(const bf_handle* h, uint64_t n, bool per_key, BfBinPlan* plan) {
+    if (per_key || h->binned_mode == 0 || h->shards > 1) return false;
+    if (!bf_binned_plan(h->dev_bytes, n, h->k, plan)) return false;
+    if (h->binned_mode == 1) return true;
+    return h->dev_bytes >= (64ull << 20) &&
+           (double)n * (double)h->k * 128.0 > kBinnedCostRatio * (double)h->dev_bytes;
+}
+
+int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p) {
+    const uint64_t need_counts = (uint64_t)p.nblocks * p.nbins;
+    const uint64_t need_bins = (uint64_t)p.nbins + 1;
+    if (need_counts <= h->bin_counts_cap && need_bins <= h->bin_bins_cap && p.probes <= h->binned_cap) return BF_OK;
+    (void)hipDeviceSynchronize();
+    if (need_counts > h->bin_counts_cap) {
+        if (h->d_bin_counts) (void)hipFree(h->d_bin_counts);
+        h->d_bin_counts = nullptr;
+        h->bin_counts_cap = 0;
+        HIPCHK(h, hipMalloc((void**)&h->d_bin_counts, need_counts * 4));
+        h->bin_counts_cap = need_counts;
+    }
+    if (need_bins > h->bin_bins_cap) {
+        if (h->d_bin_totals) (void)hipFree(h->d_bin_totals);
+        if (h->d_bin_bases) (void)hipFree(h->d_bin_bases);
+        h->d_bin_totals = h->d_bin_bases = nullptr;
+        h->bin_bins_cap = 0;
+        HIPCHK(h, hipMalloc((void**)&h->d_bin_totals, need_bins * 4));
+        HIPCHK(h, hipMalloc((void**)&h->d_bin_bases, need_bins * 4));
+        h->bin_bins_cap = need_bins;
+    }
+    if (p.probes > h->binned_cap) {
+        if (h->d_binned) (void)hipFree(h->d_binned);
+        h->d_binned = nullptr;
+        h->binned_cap = 0;
+        const uint64_t cap = round_up(p.probes, 1ull << 20);
+        HIPCHK(h, hipMalloc((void**)&h->d_binned, cap * 4));
+        h->binned_cap = cap;
+    }
+    return BF_OK;
+}
+
+// Every keyed launch goes through here: inserts take the binned path when it pays.
+int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, uint64_t bias, uint64_t n,
+              uint8_t* out8, uint64_t* out64, uint32_t* flag, hipStream_t s) {
+    BfBinPlan plan;
+    if ((op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS) && use_binned(h, n, out8 != nullptr, &plan)) {
+        int rc = ensure_bin_scratch(h, plan);
+        if (rc) return rc;
+        HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_counts,
+                                          h->d_bin_totals, h->d_bin_bases, h->d_binned,
+                                          op == BF_OP_INSERT_FLAGS ? flag : nullptr, s));
+        return BF_OK;
+    }
+    HIPCHK(h, bf_launch_keys(op, h->g, k16, offs, bias, n, out8, out64, flag, s));
+    return BF_OK;
+}
+
 // Host-pointer driver: chunk, stage, launch, copy results back.
 int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets, uint64_t n,
              uint8_t* out8, uint64_t* out64, uint8_t* any_new) {
@@ -219,8 +286,9 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
         HIPCHK(h, hipMemcpyAsync(s.d_off, s.h_off, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
         uint8_t* d_out8 = (op == BF_OP_INCLUDE || (op == BF_OP_INSERT_FLAGS && out8)) ? s.d_out : nullptr;
         uint64_t* d_out64 = (op == BF_OP_INDEXES) ? reinterpret_cast<uint64_t*>(s.d_out) : nullptr;
-        HIPCHK(h, bf_launch_keys(op, h->g, s.d_keys, s.d_off, (uint64_t)0 - base, cn, d_out8, d_out64,
-                                 want_flag ? h->d_flag : nullptr, h->stream));
+        rc = launch_op(h, op, s.d_keys, s.d_off, (uint64_t)0 - base, cn, d_out8, d_out64,
+                       want_flag ? h->d_flag : nullptr, h->stream);
+        if (rc) return rc;
         s.out_bytes = 0;
         s.user_out = nullptr;
         if (d_out8 && out8) {
@@ -273,8 +341,7 @@ int run_dev(bf_handle* h, BfOp op, const uint8_t* d_keys, const uint64_t* d_offs
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     uint64_t bias = 0;
     const uint8_t* k16 = align_keys(d_keys, &bias);
-    HIPCHK(h, bf_launch_keys(op, h->g, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, pick_stream(h, stream)));
-    return BF_OK;
+    return launch_op(h, op, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, pick_stream(h, stream));
 }
 
 }  // namespace
@@ -383,6 +450,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.block_log2 = h->block_log2;
     h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k));
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
+    h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     *out = h;
     return BF_OK;
 }
@@ -401,6 +469,10 @@ int bf_destroy(bf_handle* h) {
         if (h->d_tmp_local) (void)hipFree(h->d_tmp_local);
         if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
         if (h->d_cursor) (void)hipFree(h->d_cursor);
+        if (h->d_bin_counts) (void)hipFree(h->d_bin_counts);
+        if (h->d_bin_totals) (void)hipFree(h->d_bin_totals);
+        if (h->d_bin_bases) (void)hipFree(h->d_bin_bases);
+        if (h->d_binned) (void)hipFree(h->d_binned);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;

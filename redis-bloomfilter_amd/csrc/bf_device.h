@@ -1,0 +1,137 @@
+// bf_device.h — device-side building blocks shared by the kernels: SHA-1 over
+// LDS-staged packed keys, the ruby driver's offset derivation, the ownership
+// map of partitioned filters, and the workgroup key-tile stager.
+#pragma once
+#include "bf_internal.h"
+
+namespace bfdev {
+
+constexpr int kBlock = 256;             // lanes per workgroup = keys per workgroup
+constexpr int kStageBytes = 16384;      // LDS key stage per workgroup
+constexpr int kStageVec = kStageBytes / 16;
+constexpr int kChunk = 8;               // probes issued together per key
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
+
+// FIPS 180-4 SHA-1 compression of one 16-word block; w[] is consumed as the
+// circular message schedule.  Fully unrolled so every w index is static.
+__device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        uint32_t f, kk;
+        if (t < 20)      { f = d ^ (b & (c ^ d));           kk = 0x5A827999u; }  // Ch  -> v_bfi
+        else if (t < 40) { f = b ^ c ^ d;                   kk = 0x6ED9EBA1u; }  // Parity -> v_xor3
+        else if (t < 60) { f = (b & c) | (d & (b | c));     kk = 0x8F1BBCDCu; }  // Maj
+        else             { f = b ^ c ^ d;                   kk = 0xCA62C1D6u; }
+        const uint32_t tmp = rotl(a, 5) + f + e + kk + wt;
+        e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// Word `wi` (big-endian) of the SHA-1-padded message of a key of L bytes whose
+// first byte sits at byte position s of the 32-bit word array `src`.
+template <typename Src>
+__device__ __forceinline__ uint32_t msg_word(Src src, uint32_t s, uint32_t L, uint32_t wi,
+                                             uint32_t total_words) {
+    if (wi == total_words - 1) return L << 3;   // bit length, low word
+    if (wi == total_words - 2) return L >> 29;  // bit length, high word
+    const int valid = (int)L - (int)(4u * wi);  // key bytes left at this word
+    uint32_t x = 0;
+    if (valid > 0) {
+        const uint32_t a = s + 4u * wi;
+        const uint32_t lo = src[a >> 2];
+        const uint32_t hi = src[(a >> 2) + 1];
+        x = __builtin_amdgcn_alignbyte(hi, lo, a & 3u);  // bytes a..a+3, little-endian
+    }
+    if (valid < 4) {
+        if (valid >= 0) {
+            x &= (valid == 0) ? 0u : (0xFFFFFFFFu >> (8 * (4 - valid)));
+            x |= 0x80u << (8 * valid);                // the FIPS padding byte
+        } else {
+            x = 0u;
+        }
+    }
+    return __builtin_bswap32(x);
+}
+
+template <typename Src>
+__device__ __forceinline__ void sha1_key(Src src, uint32_t s, uint32_t L, uint32_t H[5]) {
+    H[0] = 0x67452301u; H[1] = 0xEFCDAB89u; H[2] = 0x98BADCFEu; H[3] = 0x10325476u; H[4] = 0xC3D2E1F0u;
+    const uint32_t nblk = (L + 8u) / 64u + 1u;
+    const uint32_t total = nblk * 16u;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = msg_word(src, s, L, b * 16u + j, total);
+        sha1_compress(H, w);
+    }
+}
+
+// ruby.rb:50-53 for probe i, reduced mod m without an integer divide.
+__device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, uint32_t h1,
+                                                 uint32_t h2, uint32_t h3, uint32_t i) {
+    const uint32_t a = (i & 1u) ? h1 : h0;
+    const uint32_t b = (((i + (i & 1u)) & 3u) >> 1) ? h3 : h2;
+    const uint64_t v = (uint64_t)a + (uint64_t)i * (uint64_t)b;  // < k * 2^32: exact
+    if (g.nomod) return v;
+    // q within +-1 of floor(v/m): v < 2^38 is exact in a double, 1/m carries 2^-53 relative error.
+    const uint64_t q = (uint64_t)((double)v * g.inv_m);
+    int64_t r = (int64_t)(v - q * g.m);
+    if (r < 0) r += (int64_t)g.m;
+    else if ((uint64_t)r >= g.m) r -= (int64_t)g.m;
+    return (uint64_t)r;
+}
+
+// Block-cyclic ownership of partitioned filters (include/bfhip.h, bf_config):
+// block b = o >> block_log2 lives on shard b % P at local block b / P.
+__device__ __forceinline__ void owner_local(const BfGeom& g, uint64_t o, uint32_t& owner, uint64_t& local) {
+    const uint64_t blk = o >> g.block_log2;
+    const uint64_t lblk = blk / g.shards;
+    owner = (uint32_t)(blk - lblk * g.shards);
+    local = (lblk << g.block_log2) | (o & ((1ull << g.block_log2) - 1ull));
+}
+
+
+// Stages one tile of up to TILE consecutive keys (offsets + packed bytes) into
+// LDS and hands each lane its key: f(lane, src_words, start_byte, len).  When the
+// tile's bytes exceed the stage, lanes read their key straight from global.
+// Ends with a barrier, so the caller may restage the same LDS right after.
+template <int TILE, int STAGE_VEC, typename F>
+__device__ __forceinline__ void for_key_tile(const uint8_t* __restrict__ keys16,
+                                             const uint64_t* __restrict__ offsets, uint64_t bias,
+                                             uint64_t tile0, uint32_t cnt, uint64_t* s_off,
+                                             uint4* s_stage, F&& f) {
+    const uint32_t t = threadIdx.x;
+    if (t < cnt) s_off[t] = offsets[tile0 + t] + bias;
+    if (t == 0) s_off[cnt] = offsets[tile0 + cnt] + bias;
+    __syncthreads();
+    const uint64_t start = s_off[0];
+    const uint64_t end = s_off[cnt];
+    const uint64_t abase = start & ~(uint64_t)15;
+    const uint64_t nvec = (end - abase + 15) >> 4;
+    if (nvec <= (uint64_t)STAGE_VEC) {   // workgroup-uniform
+        const uint4* gv = reinterpret_cast<const uint4*>(keys16 + abase);
+        for (uint32_t v = t; v < (uint32_t)nvec; v += TILE) s_stage[v] = gv[v];
+        __syncthreads();
+        if (t < cnt)
+            f(t, reinterpret_cast<const uint32_t*>(s_stage), (uint32_t)(s_off[t] - abase),
+              (uint32_t)(s_off[t + 1] - s_off[t]));
+    } else if (t < cnt) {
+        const uint64_t ks = s_off[t];
+        const uint64_t kbase = ks & ~(uint64_t)3;
+        f(t, reinterpret_cast<const uint32_t*>(keys16 + kbase), (uint32_t)(ks - kbase),
+          (uint32_t)(s_off[t + 1] - ks));
+    }
+    __syncthreads();
+}
+
+}  // namespace bfdev

@@ -18,103 +18,11 @@
 // Bit o of the filter is bit ((o ^ 7) & 31) of little-endian word o >> 5, i.e.
 // byte o >> 3 under mask 0x80 >> (o & 7) — the Redis SETBIT layout, so the
 // device buffer IS the Redis string.
-#include "bf_internal.h"
+#include "bf_device.h"
 
 namespace {
 
-constexpr int kBlock = 256;             // lanes per workgroup = keys per workgroup
-constexpr int kStageBytes = 16384;      // LDS key stage per workgroup
-constexpr int kStageVec = kStageBytes / 16;
-constexpr int kChunk = 8;               // probes issued together per key
-
-__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
-
-// FIPS 180-4 SHA-1 compression of one 16-word block; w[] is consumed as the
-// circular message schedule.  Fully unrolled so every w index is static.
-__device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
-#pragma unroll
-    for (int t = 0; t < 80; ++t) {
-        uint32_t wt;
-        if (t < 16) {
-            wt = w[t];
-        } else {
-            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
-            w[t & 15] = wt;
-        }
-        uint32_t f, kk;
-        if (t < 20)      { f = d ^ (b & (c ^ d));           kk = 0x5A827999u; }  // Ch  -> v_bfi
-        else if (t < 40) { f = b ^ c ^ d;                   kk = 0x6ED9EBA1u; }  // Parity -> v_xor3
-        else if (t < 60) { f = (b & c) | (d & (b | c));     kk = 0x8F1BBCDCu; }  // Maj
-        else             { f = b ^ c ^ d;                   kk = 0xCA62C1D6u; }
-        const uint32_t tmp = rotl(a, 5) + f + e + kk + wt;
-        e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
-    }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
-}
-
-// Word `wi` (big-endian) of the SHA-1-padded message of a key of L bytes whose
-// first byte sits at byte position s of the 32-bit word array `src`.
-template <typename Src>
-__device__ __forceinline__ uint32_t msg_word(Src src, uint32_t s, uint32_t L, uint32_t wi,
-                                             uint32_t total_words) {
-    if (wi == total_words - 1) return L << 3;   // bit length, low word
-    if (wi == total_words - 2) return L >> 29;  // bit length, high word
-    const int valid = (int)L - (int)(4u * wi);  // key bytes left at this word
-    uint32_t x = 0;
-    if (valid > 0) {
-        const uint32_t a = s + 4u * wi;
-        const uint32_t lo = src[a >> 2];
-        const uint32_t hi = src[(a >> 2) + 1];
-        x = __builtin_amdgcn_alignbyte(hi, lo, a & 3u);  // bytes a..a+3, little-endian
-    }
-    if (valid < 4) {
-        if (valid >= 0) {
-            x &= (valid == 0) ? 0u : (0xFFFFFFFFu >> (8 * (4 - valid)));
-            x |= 0x80u << (8 * valid);                // the FIPS padding byte
-        } else {
-            x = 0u;
-        }
-    }
-    return __builtin_bswap32(x);
-}
-
-template <typename Src>
-__device__ __forceinline__ void sha1_key(Src src, uint32_t s, uint32_t L, uint32_t H[5]) {
-    H[0] = 0x67452301u; H[1] = 0xEFCDAB89u; H[2] = 0x98BADCFEu; H[3] = 0x10325476u; H[4] = 0xC3D2E1F0u;
-    const uint32_t nblk = (L + 8u) / 64u + 1u;
-    const uint32_t total = nblk * 16u;
-    for (uint32_t b = 0; b < nblk; ++b) {
-        uint32_t w[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = msg_word(src, s, L, b * 16u + j, total);
-        sha1_compress(H, w);
-    }
-}
-
-// ruby.rb:50-53 for probe i, reduced mod m without an integer divide.
-__device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, uint32_t h1,
-                                                 uint32_t h2, uint32_t h3, uint32_t i) {
-    const uint32_t a = (i & 1u) ? h1 : h0;
-    const uint32_t b = (((i + (i & 1u)) & 3u) >> 1) ? h3 : h2;
-    const uint64_t v = (uint64_t)a + (uint64_t)i * (uint64_t)b;  // < k * 2^32: exact
-    if (g.nomod) return v;
-    // q within +-1 of floor(v/m): v < 2^38 is exact in a double, 1/m carries 2^-53 relative error.
-    const uint64_t q = (uint64_t)((double)v * g.inv_m);
-    int64_t r = (int64_t)(v - q * g.m);
-    if (r < 0) r += (int64_t)g.m;
-    else if ((uint64_t)r >= g.m) r -= (int64_t)g.m;
-    return (uint64_t)r;
-}
-
-// Block-cyclic ownership of partitioned filters (include/bfhip.h, bf_config):
-// block b = o >> block_log2 lives on shard b % P at local block b / P.
-__device__ __forceinline__ void owner_local(const BfGeom& g, uint64_t o, uint32_t& owner, uint64_t& local) {
-    const uint64_t blk = o >> g.block_log2;
-    const uint64_t lblk = blk / g.shards;
-    owner = (uint32_t)(blk - lblk * g.shards);
-    local = (lblk << g.block_log2) | (o & ((1ull << g.block_log2) - 1ull));
-}
+using namespace bfdev;
 
 template <int OP, typename Src>
 __device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uint32_t L,

@@ -227,3 +227,22 @@ def test_device_api_torch(pkg, oracle):
         f.indexes_many_dev(dk2.data_ptr() + 3, do.data_ptr(), 4097, idx.data_ptr(), stream=st)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint64), oracle.indexes_many(buf, offs, m, k))
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("m,k,n", [(95851, 6, 20_000), (9585058, 6, 300_000), (1437758757, 10, 200_000),
+                                   (2**32 + 17, 7, 100_000)])
+def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
+    """BFHIP_INSERT_BINNED=1 forces the binned (count/scan/scatter/apply) insert; 0 the direct one."""
+    monkeypatch.setenv("BFHIP_INSERT_BINNED", mode)
+    rng = np.random.default_rng(RNG_SEED + 7)
+    ins = rand_keys(rng, n, 0, 24)
+    probe = rand_keys(rng, 20_000, 0, 24)
+    ib, io = ins
+    probe = (np.concatenate([ib, probe[0]]), np.concatenate([io[:5001], probe[1][1:] + io[5000]]))
+    s, _ = _insert_include_roundtrip(pkg, oracle, m, k, ins, probe)
+    with pkg.Filter(m, k) as f:                       # any_new through the binned path
+        any1, _ = f.insert_many(ib, io, any_new=True)
+        any2, _ = f.insert_many(ib, io, any_new=True)
+        assert (any1, any2) == (True, False)
+        assert f.export_redis() == s
