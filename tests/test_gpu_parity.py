@@ -239,7 +239,7 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
     ins = rand_keys(rng, n, 0, 24)
     probe = rand_keys(rng, 20_000, 0, 24)
     ib, io = ins
-    probe = (np.concatenate([ib, probe[0]]), np.concatenate([io[:5001], probe[1][1:] + io[5000]]))
+    probe = (np.concatenate([ib, probe[0]]), np.concatenate([io[:5001], probe[1][1:] + io[-1]]))
     s, _ = _insert_include_roundtrip(pkg, oracle, m, k, ins, probe)
     with pkg.Filter(m, k) as f:                       # any_new through the binned path
         any1, _ = f.insert_many(ib, io, any_new=True)
