@@ -140,7 +140,7 @@ def prefill_random(f, m: int, k: int, rank: int) -> np.ndarray:
     return host
 
 
-def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False):
+def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto"):
     n, p, batch, prefill = CONFIGS[name]
     B = pkg.Bloomfilter
     m = B.optimal_m(n, p)
@@ -149,7 +149,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     t0 = time.time()
     pf = None
     host_bits = None
-    if D.world == 1:
+    if mode == "auto":
+        mode = "single" if D.world == 1 else "partitioned"
+    if mode == "single":
         f = pkg.Filter(m, k, device=D.local)
         if prefill == "random":
             host_bits = prefill_random(f, m, k, D.rank)
@@ -283,11 +285,14 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
+    ap.add_argument("--mode", default="auto", choices=["auto", "single", "partitioned"],
+                    help="auto: single GPU at N=1, partitioned over the ranks at N>1")
     args = ap.parse_args()
 
     D = Dist()
     pkg = pkgload.load()
-    main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api))
+    main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
+                                  mode=args.mode)
     secondary = {}
     if D.world == 1 and not args.no_secondary:
         for name in ("1m", "100m"):
@@ -332,7 +337,7 @@ def main():
                    "global_batch": 2 * batch * D.world,
                    "parallelism": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key batches "
                                   "routed to owner GPUs by RCCL all-to-all)" % D.world
-                   if D.world > 1 else "single GPU"},
+                   if (D.world > 1 or args.mode == "partitioned") else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic.get(dom_name) if isinstance(traffic, dict) else None,

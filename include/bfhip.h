@@ -74,8 +74,12 @@ typedef struct bf_config {
     uint32_t shard_count;      /* 0 or 1 => the handle holds the whole filter; max 255     */
     uint32_t shard_index;      /* this handle's shard, < shard_count                       */
     uint32_t shard_block_log2; /* ownership block size, 3..40 (0 => 20: 128 KiB blocks)    */
-    uint32_t reserved;
+    uint32_t flags;            /* BF_FLAG_* */
 } bf_config;
+
+/* bf_config.flags */
+#define BF_FLAG_ROUTE32 1u     /* routed owner-local offsets (d_send / d_local) are uint32, halving the
+                                  all-to-all bytes; needs every shard's local_bits <= 2^32 (else BF_EINVAL) */
 
 /* ---- lifecycle */
 int  bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out);
@@ -136,10 +140,11 @@ int  bf_sync(bf_handle* h);                    /* synchronise the handle's own s
 int  bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_index,
                    uint32_t* block_log2, uint64_t* local_bits);
 int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
-                  uint64_t* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream);
-int  bf_shard_insert_dev(bf_handle* h, const uint64_t* d_local, uint64_t count,
+                  void* d_send /* uint64[n*k], or uint32 with BF_FLAG_ROUTE32 */, uint32_t* d_slot,
+                  uint64_t* d_counts, void* stream);
+int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
-int  bf_shard_test_dev(bf_handle* h, const uint64_t* d_local, uint64_t count, uint8_t* d_bits,
+int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,
                        void* stream);
 int  bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t n,
                     uint8_t* d_out, void* stream);

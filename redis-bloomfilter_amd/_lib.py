@@ -19,6 +19,7 @@ DEFAULT_LIB = os.path.join(PKG_DIR, "lib", "libbfhip.so")
 
 BF_OK, BF_EINVAL, BF_ENOMEM, BF_EDEVICE, BF_ERCCL, BF_ERANGE = 0, 1, 2, 3, 4, 5
 BF_IMPORT_REPLACE, BF_IMPORT_OR = 0, 1
+BF_FLAG_ROUTE32 = 1
 BF_MAX_K = 64
 
 _STATUS = {BF_EINVAL: "BF_EINVAL", BF_ENOMEM: "BF_ENOMEM", BF_EDEVICE: "BF_EDEVICE",
@@ -45,7 +46,7 @@ class bf_config(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("batch_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
                 ("shard_count", ctypes.c_uint32), ("shard_index", ctypes.c_uint32),
-                ("shard_block_log2", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("shard_block_log2", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -174,10 +175,11 @@ class Filter:
 
     def __init__(self, m_bits: int, k: int, device: int = -1, batch_keys: int = 0,
                  batch_bytes: int = 0, shard_count: int = 1, shard_index: int = 0,
-                 shard_block_log2: int = 0):
+                 shard_block_log2: int = 0, flags: int = 0):
         self._lib = load()
         cfg = bf_config(ctypes.sizeof(bf_config), int(device), int(batch_keys), int(batch_bytes),
-                        int(shard_count), int(shard_index), int(shard_block_log2), 0)
+                        int(shard_count), int(shard_index), int(shard_block_log2), int(flags))
+        self.route32 = bool(flags & BF_FLAG_ROUTE32)
         h = _vp()
         rc = self._lib.bf_create(int(m_bits), int(k), ctypes.byref(cfg), ctypes.byref(h))
         _check(rc, None)

@@ -48,6 +48,7 @@ struct bf_handle {
     // partitioned filters: this handle holds shard `shard_index` of `shards`
     uint32_t shards = 1, shard_index = 0, block_log2 = 20;
     uint32_t mem_kind = 0;   // bitset allocation: 0 coarse-grained, 1 uncached, 2 fine-grained
+    bool route32 = false;    // BF_FLAG_ROUTE32
     uint64_t local_bits = 0;
     // routing scratch (grown on demand)
     uint64_t* d_tmp_local = nullptr;
@@ -413,6 +414,16 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
         h->local_bits = mine << h->block_log2;
     }
     h->dev_bytes = round_up(std::max<uint64_t>((h->local_bits + 7) / 8, 1), 256);
+    h->route32 = (c.flags & BF_FLAG_ROUTE32) != 0;
+    if (h->route32) {   // the largest shard (index 0) must address its bits in 32 bits
+        const uint64_t nblocks = (h->reach + (1ull << h->block_log2) - 1) >> h->block_log2;
+        const uint64_t biggest = h->shards == 1 ? h->reach : (((nblocks - 1) / h->shards + 1) << h->block_log2);
+        if (biggest > (1ull << 32)) {
+            delete h;
+            return set_err(nullptr, BF_EINVAL, "BF_FLAG_ROUTE32 needs shards of <= 2^32 bits (largest: %llu)",
+                           (unsigned long long)biggest);
+        }
+    }
     h->cap_keys = c.batch_keys ? c.batch_keys : (1ull << 22);
     h->cap_bytes = c.batch_bytes ? c.batch_bytes : (64ull << 20);
 
@@ -448,6 +459,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.nomod = (m_bits > maxval) ? 1u : 0u;
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
+    h->g.route32 = h->route32 ? 1u : 0u;
     h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k));
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
@@ -673,7 +685,7 @@ int bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mod
 }
 
 int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
-                 uint64_t* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream) {
+                 void* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream) {
     if (!h) return BF_EINVAL;
     if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
     if (n && (!d_key_bytes || !d_offsets || !d_send || !d_slot)) return set_err(h, BF_EINVAL, "NULL device pointer");
@@ -695,27 +707,27 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
                                  nullptr, s, counts));
     }
     HIPCHK(h, bf_launch_route_scatter(h->d_tmp_local, h->d_tmp_owner, probes, h->shards, counts, h->d_cursor,
-                                      d_send, d_slot, s));
+                                      d_send, d_slot, h->route32, s));
     return BF_OK;
 }
 
-int bf_shard_insert_dev(bf_handle* h, const uint64_t* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
+int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
     if (!h) return BF_EINVAL;
     if (count && !d_local) return set_err(h, BF_EINVAL, "d_local is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, pick_stream(h, stream)));
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, h->route32, pick_stream(h, stream)));
     return BF_OK;
 }
 
-int bf_shard_test_dev(bf_handle* h, const uint64_t* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
+int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
     if (!h) return BF_EINVAL;
     if (count && (!d_local || !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, pick_stream(h, stream)));
+    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, h->route32, pick_stream(h, stream)));
     return BF_OK;
 }
 

@@ -15,6 +15,7 @@ struct BfGeom {
     // probe policies (tuning; results are identical for every setting)
     uint32_t  first_round;  // include?: probes loaded before the first early-exit check (0 = all k)
     uint32_t  insert_test;  // insert: 1 = load the k words first, atomic-OR only the unset bits
+    uint32_t  route32;      // BF_FLAG_ROUTE32: routed owner-local offsets are uint32
 };
 
 enum BfOp : int {
@@ -52,14 +53,15 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
 // pairs by owner into send[], writes each probe's position into slot[].
 // counts[P] must hold the per-owner totals (from BF_OP_ROUTE).
-hipError_t bf_launch_route_scatter(const uint64_t* local, const uint8_t* owner, uint64_t total,
+// `local` (tmp, from BF_OP_ROUTE) and `send` hold uint64, or uint32 when route32.
+hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint64_t total,
                                    uint32_t P, const unsigned long long* counts,
-                                   unsigned long long* cursor, uint64_t* send, uint32_t* slot,
-                                   hipStream_t s);
-hipError_t bf_launch_shard_insert(uint32_t* bits, const uint64_t* local, uint64_t count,
-                                  uint32_t* any_flag, hipStream_t s);
-hipError_t bf_launch_shard_test(const uint32_t* bits, const uint64_t* local, uint64_t count,
-                                uint8_t* out, hipStream_t s);
+                                   unsigned long long* cursor, void* send, uint32_t* slot,
+                                   bool route32, hipStream_t s);
+hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count,
+                                  uint32_t* any_flag, bool route32, hipStream_t s);
+hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count,
+                                uint8_t* out, bool route32, hipStream_t s);
 hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k,
                              uint8_t* out, hipStream_t s);
 

@@ -40,7 +40,8 @@ __device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uin
             uint32_t owner;
             uint64_t local;
             owner_local(g, probe_offset(g, H[0], H[1], H[2], H[3], i), owner, local);
-            out64[key * k + i] = local;
+            if (g.route32) reinterpret_cast<uint32_t*>(out64)[key * k + i] = (uint32_t)local;
+            else out64[key * k + i] = local;
             out8[key * k + i] = (uint8_t)owner;
             atomicAdd(hist + owner, 1u);   // LDS histogram
         }
@@ -217,11 +218,12 @@ __global__ void displ_kernel(const unsigned long long* __restrict__ counts, uint
 // Groups probes by owner: one LDS histogram per workgroup, one global
 // atomicAdd per (workgroup, owner) to reserve a contiguous range, then every
 // probe lands at range base + its LDS rank.
-__global__ __launch_bounds__(256) void route_scatter_kernel(const uint64_t* __restrict__ local,
+template <typename Off>
+__global__ __launch_bounds__(256) void route_scatter_kernel(const Off* __restrict__ local,
                                                             const uint8_t* __restrict__ owner,
                                                             uint64_t total, uint32_t P,
                                                             unsigned long long* __restrict__ cursor,
-                                                            uint64_t* __restrict__ send,
+                                                            Off* __restrict__ send,
                                                             uint32_t* __restrict__ slot) {
     __shared__ uint32_t s_cnt[256];
     __shared__ unsigned long long s_base[256];
@@ -253,9 +255,9 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const uint64_t* __re
     }
 }
 
-template <bool FLAGS>
+template <bool FLAGS, typename Off>
 __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
-                                                           const uint64_t* __restrict__ local,
+                                                           const Off* __restrict__ local,
                                                            uint64_t count, uint32_t* __restrict__ any_flag) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t isnew = 0;
@@ -276,8 +278,9 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
     }
 }
 
+template <typename Off>
 __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits,
-                                                         const uint64_t* __restrict__ local, uint64_t count,
+                                                         const Off* __restrict__ local, uint64_t count,
                                                          uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < count; p += stride) {
@@ -330,32 +333,48 @@ hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const
     return hipGetLastError();
 }
 
-hipError_t bf_launch_route_scatter(const uint64_t* local, const uint8_t* owner, uint64_t total, uint32_t P,
+hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint64_t total, uint32_t P,
                                    const unsigned long long* counts, unsigned long long* cursor,
-                                   uint64_t* send, uint32_t* slot, hipStream_t s) {
+                                   void* send, uint32_t* slot, bool route32, hipStream_t s) {
     hipLaunchKernelGGL(displ_kernel, dim3(1), dim3(64), 0, s, counts, P, cursor);
     if (total == 0) return hipGetLastError();
     const uint64_t per = 256ull * kScatterItems;
-    const uint64_t blocks = (total + per - 1) / per;
-    hipLaunchKernelGGL(route_scatter_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, local, owner, total, P,
-                       cursor, send, slot);
-    return hipGetLastError();
-}
-
-hipError_t bf_launch_shard_insert(uint32_t* bits, const uint64_t* local, uint64_t count, uint32_t* any_flag,
-                                  hipStream_t s) {
-    if (count == 0) return hipSuccess;
-    if (any_flag)
-        hipLaunchKernelGGL(shard_insert_kernel<true>, dim3(stream_grid(count)), dim3(256), 0, s, bits, local, count, any_flag);
+    const dim3 grid((uint32_t)((total + per - 1) / per));
+    if (route32)
+        hipLaunchKernelGGL(route_scatter_kernel<uint32_t>, grid, dim3(256), 0, s, static_cast<const uint32_t*>(local),
+                           owner, total, P, cursor, static_cast<uint32_t*>(send), slot);
     else
-        hipLaunchKernelGGL(shard_insert_kernel<false>, dim3(stream_grid(count)), dim3(256), 0, s, bits, local, count, any_flag);
+        hipLaunchKernelGGL(route_scatter_kernel<uint64_t>, grid, dim3(256), 0, s, static_cast<const uint64_t*>(local),
+                           owner, total, P, cursor, static_cast<uint64_t*>(send), slot);
     return hipGetLastError();
 }
 
-hipError_t bf_launch_shard_test(const uint32_t* bits, const uint64_t* local, uint64_t count, uint8_t* out,
-                                hipStream_t s) {
+template <typename Off>
+static void launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag, hipStream_t s) {
+    const Off* l = static_cast<const Off*>(local);
+    if (any_flag)
+        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count, any_flag);
+    else
+        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count, any_flag);
+}
+
+hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag,
+                                  bool route32, hipStream_t s) {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(shard_test_kernel, dim3(stream_grid(count)), dim3(256), 0, s, bits, local, count, out);
+    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, s);
+    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, s);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count, uint8_t* out,
+                                bool route32, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (route32)
+        hipLaunchKernelGGL(shard_test_kernel<uint32_t>, dim3(stream_grid(count)), dim3(256), 0, s, bits,
+                           static_cast<const uint32_t*>(local), count, out);
+    else
+        hipLaunchKernelGGL(shard_test_kernel<uint64_t>, dim3(stream_grid(count)), dim3(256), 0, s, bits,
+                           static_cast<const uint64_t*>(local), count, out);
     return hipGetLastError();
 }
 

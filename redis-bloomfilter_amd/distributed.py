@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from . import keys as _keys
-from ._lib import ArgumentError, Filter
+from ._lib import BF_FLAG_ROUTE32, ArgumentError, Filter
 
 
 def block_owner_local(offsets: np.ndarray, P: int, block_log2: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -87,15 +87,20 @@ class HipEngine:
 
     def __init__(self, m: int, k: int, P: int, rank: int, block_log2: int, device: torch.device):
         self.device = device
+        reach = min(m, k * 0xFFFFFFFF + 1)
+        # 32-bit owner-local offsets halve the all-to-all bytes whenever every shard fits 2^32 bits
+        route32 = shard_local_bits(reach, P, 0, block_log2) <= (1 << 32)
         self.filter = Filter(m, k, device=device.index if device.index is not None else -1,
-                             shard_count=P, shard_index=rank, shard_block_log2=block_log2)
+                             shard_count=P, shard_index=rank, shard_block_log2=block_log2,
+                             flags=BF_FLAG_ROUTE32 if route32 else 0)
         self.k, self.P = k, P
+        self.offset_dtype = torch.int32 if route32 else torch.int64
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def route(self, kb: torch.Tensor, ko: torch.Tensor, n: int):
-        send = torch.empty(n * self.k, dtype=torch.int64, device=self.device)
+        send = torch.empty(n * self.k, dtype=self.offset_dtype, device=self.device)
         slot = torch.empty(n * self.k, dtype=torch.int32, device=self.device)
         counts = torch.empty(self.P, dtype=torch.int64, device=self.device)
         self.filter.route_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(), slot.data_ptr(),

@@ -35,7 +35,7 @@ class Redis
       # struct bf_config (include/bfhip.h)
       class Config < FFI::Struct
         layout :struct_size, :uint32, :device, :int32, :batch_keys, :uint64, :batch_bytes, :uint64,
-               :shard_count, :uint32, :shard_index, :uint32, :shard_block_log2, :uint32, :reserved, :uint32
+               :shard_count, :uint32, :shard_index, :uint32, :shard_block_log2, :uint32, :flags, :uint32
       end
 
       attach_function :bf_version, [], :string

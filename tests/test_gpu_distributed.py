@@ -40,7 +40,9 @@ def test_simulated_partition(pkg, oracle, m, k, P, b):
         owner, local = D.block_owner_local(idx, P, b)
         c = counts.cpu().numpy()
         assert c.tolist() == np.bincount(owner, minlength=P).tolist()
-        s_np = send.cpu().numpy().view(np.uint64)
+        s_np = send.cpu().numpy()   # int32 when the shards fit 2^32 bits (BF_FLAG_ROUTE32)
+        s_np = s_np.view(np.uint32).astype(np.uint64) if s_np.dtype == np.int32 else s_np.view(np.uint64)
+        assert (s_np.dtype, send.dtype == torch.int32) == (np.uint64, shards[r].filter.route32)
         sl = slot.cpu().numpy().astype(np.int64)
         assert sorted(sl.tolist()) == list(range(n * k))
         np.testing.assert_array_equal(s_np[sl], local)
@@ -109,3 +111,11 @@ def test_torch_distributed_world1(pkg, oracle):
             f.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_route32_needs_small_shards(pkg):
+    with pytest.raises(pkg.ArgumentError, match="ROUTE32"):
+        pkg.Filter(191701167547, 13, shard_count=2, shard_index=0, flags=pkg._lib.BF_FLAG_ROUTE32)
+    f = pkg.Filter(9585058377, 6, shard_count=2, shard_index=1, flags=pkg._lib.BF_FLAG_ROUTE32)
+    assert f.route32 and f.local_bits <= 1 << 32
+    f.close()
