@@ -50,6 +50,8 @@ CONFIGS = {
     "100m": (10**8, 0.001, 1 << 24, "random"),
     "1m": (10**6, 0.01, 1 << 20, "insert"),
     "10k": (10**4, 0.01, 1 << 14, "insert"),
+    # hash-bound probe: the 1M@1% (L2-resident) filter driven with 2^24-key batches
+    "1m_big": (10**6, 0.01, 1 << 24, "insert"),
 }
 
 
@@ -58,12 +60,21 @@ def log(*a):
 
 
 class Dist:
-    def __init__(self):
+    def __init__(self, need_group: bool = False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world > 1:
+        self.group = self.world > 1 or need_group
+        if self.group:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if self.world == 1:
+                import socket
+                sk = socket.socket()
+                sk.bind(("127.0.0.1", 0))
+                os.environ.setdefault("MASTER_PORT", str(sk.getsockname()[1]))
+                sk.close()
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
             torch.cuda.set_device(self.local)
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", self.local))
         else:
@@ -81,7 +92,7 @@ class Dist:
         return float(t.item())
 
     def close(self):
-        if self.world > 1:
+        if self.group:
             dist.destroy_process_group()
 
 
@@ -277,6 +288,10 @@ def load_traffic(workload: str):
 
 
 def main():
+    # Libraries (RCCL's version banner, HIP) may write to stdout; the contract is ONE JSON
+    # line there, so fd 1 goes to stderr for the run and the JSON to the original stdout.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -289,7 +304,7 @@ def main():
                     help="auto: single GPU at N=1, partitioned over the ranks at N>1")
     args = ap.parse_args()
 
-    D = Dist()
+    D = Dist(need_group=(args.mode == "partitioned"))
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
                                   mode=args.mode)
@@ -351,7 +366,7 @@ def main():
                                            "lua_insert": 6235, "lua_include": 5712,
                                            "source": "reference README.md:80-95, 1M items, hardware unstated"},
     }
-    print(json.dumps(line), flush=True)
+    print(json.dumps(line), file=json_out, flush=True)
 
 
 if __name__ == "__main__":

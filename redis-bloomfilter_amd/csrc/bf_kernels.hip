@@ -259,16 +259,35 @@ template <bool FLAGS, typename Off>
 __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
                                                            const Off* __restrict__ local,
                                                            uint64_t count, uint32_t* __restrict__ any_flag) {
+    // Test-then-set as in the direct insert: 4 probes per lane in flight, an atomic
+    // only for bits still 0 (a 1 seen here is final within the launch).
+    constexpr int U = 4;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t isnew = 0;
-    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < count; p += stride) {
-        const uint64_t o = local[p];
-        const uint32_t mask = 1u << ((uint32_t)(o ^ 7u) & 31u);
-        if constexpr (FLAGS) {
-            const uint32_t old = __hip_atomic_fetch_or(bits + (o >> 5), mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            isnew |= (old & mask) ? 0u : 1u;
-        } else {
-            __hip_atomic_fetch_or(bits + (o >> 5), mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < count; p0 += U * stride) {
+        uint64_t w[U];
+        uint32_t mask[U], v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t p = p0 + u * stride;
+            mask[u] = 0; v[u] = 0; w[u] = 0;
+            if (p < count) {
+                const uint64_t o = local[p];
+                w[u] = o >> 5;
+                mask[u] = 1u << ((uint32_t)(o ^ 7u) & 31u);
+                v[u] = bits[w[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (mask[u] && !(v[u] & mask[u])) {
+                if constexpr (FLAGS) {
+                    const uint32_t old = __hip_atomic_fetch_or(bits + w[u], mask[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    isnew |= (old & mask[u]) ? 0u : 1u;
+                } else {
+                    __hip_atomic_fetch_or(bits + w[u], mask[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
     }
     if constexpr (FLAGS) {
@@ -282,10 +301,25 @@ template <typename Off>
 __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits,
                                                          const Off* __restrict__ local, uint64_t count,
                                                          uint8_t* __restrict__ out) {
+    constexpr int U = 4;   // 4 independent probe loads per lane in flight
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < count; p += stride) {
-        const uint64_t o = local[p];
-        out[p] = (uint8_t)((bits[o >> 5] >> ((uint32_t)(o ^ 7u) & 31u)) & 1u);
+    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < count; p0 += U * stride) {
+        uint32_t v[U], sh[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t p = p0 + u * stride;
+            v[u] = 0; sh[u] = 0;
+            if (p < count) {
+                const uint64_t o = local[p];
+                sh[u] = (uint32_t)(o ^ 7u) & 31u;
+                v[u] = bits[o >> 5];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t p = p0 + u * stride;
+            if (p < count) out[p] = (uint8_t)((v[u] >> sh[u]) & 1u);
+        }
     }
 }
 

@@ -116,6 +116,6 @@ def test_torch_distributed_world1(pkg, oracle):
 def test_route32_needs_small_shards(pkg):
     with pytest.raises(pkg.ArgumentError, match="ROUTE32"):
         pkg.Filter(191701167547, 13, shard_count=2, shard_index=0, flags=pkg._lib.BF_FLAG_ROUTE32)
-    f = pkg.Filter(9585058377, 6, shard_count=2, shard_index=1, flags=pkg._lib.BF_FLAG_ROUTE32)
+    f = pkg.Filter(9585058377, 6, shard_count=4, shard_index=1, flags=pkg._lib.BF_FLAG_ROUTE32)
     assert f.route32 and f.local_bits <= 1 << 32
     f.close()
