@@ -61,7 +61,8 @@ struct bf_handle {
     uint32_t* d_bin_totals = nullptr;
     uint32_t* d_bin_bases = nullptr;
     uint32_t* d_binned = nullptr;
-    uint64_t bin_counts_cap = 0, bin_bins_cap = 0, binned_cap = 0;
+    void* d_digests = nullptr;   // 16 B per key: the count pass's SHA-1 words for the scatter pass
+    uint64_t bin_counts_cap = 0, bin_bins_cap = 0, binned_cap = 0, digest_cap = 0;
     uint64_t cap_keys = 0, cap_bytes = 0;
     Slot slot[2];
     bool staging_ready = false;
@@ -187,10 +188,12 @@ bool use_binned(const bf_handle* h, uint64_t n, bool per_key, BfBinPlan* plan) {
            (double)n * (double)h->k * 128.0 > kBinnedCostRatio * (double)h->dev_bytes;
 }
 
-int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p) {
+int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p, uint64_t n) {
     const uint64_t need_counts = (uint64_t)p.nblocks * p.nbins;
     const uint64_t need_bins = (uint64_t)p.nbins + 1;
-    if (need_counts <= h->bin_counts_cap && need_bins <= h->bin_bins_cap && p.probes <= h->binned_cap) return BF_OK;
+    if (need_counts <= h->bin_counts_cap && need_bins <= h->bin_bins_cap && p.probes <= h->binned_cap &&
+        n <= h->digest_cap)
+        return BF_OK;
     (void)hipDeviceSynchronize();
     if (need_counts > h->bin_counts_cap) {
         if (h->d_bin_counts) (void)hipFree(h->d_bin_counts);
@@ -216,6 +219,14 @@ int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p) {
         HIPCHK(h, hipMalloc((void**)&h->d_binned, cap * 4));
         h->binned_cap = cap;
     }
+    if (n > h->digest_cap) {
+        if (h->d_digests) (void)hipFree(h->d_digests);
+        h->d_digests = nullptr;
+        h->digest_cap = 0;
+        const uint64_t cap = round_up(n, 1ull << 16);
+        HIPCHK(h, hipMalloc(&h->d_digests, cap * 16));
+        h->digest_cap = cap;
+    }
     return BF_OK;
 }
 
@@ -224,10 +235,10 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
               uint8_t* out8, uint64_t* out64, uint32_t* flag, hipStream_t s) {
     BfBinPlan plan;
     if ((op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS) && use_binned(h, n, out8 != nullptr, &plan)) {
-        int rc = ensure_bin_scratch(h, plan);
+        int rc = ensure_bin_scratch(h, plan, n);
         if (rc) return rc;
         HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_counts,
-                                          h->d_bin_totals, h->d_bin_bases, h->d_binned,
+                                          h->d_bin_totals, h->d_bin_bases, h->d_binned, h->d_digests,
                                           op == BF_OP_INSERT_FLAGS ? flag : nullptr, s));
         return BF_OK;
     }
@@ -457,6 +468,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.inv_m = 1.0 / (double)m_bits;
     h->g.k = k;
     h->g.nomod = (m_bits > maxval) ? 1u : 0u;
+    h->g.mod_f32 = (m_bits >= (1ull << 17)) ? 1u : 0u;
+    h->g.inv_m_f = (float)(1.0 / (double)m_bits);
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
     h->g.route32 = h->route32 ? 1u : 0u;
@@ -485,6 +498,7 @@ int bf_destroy(bf_handle* h) {
         if (h->d_bin_totals) (void)hipFree(h->d_bin_totals);
         if (h->d_bin_bases) (void)hipFree(h->d_bin_bases);
         if (h->d_binned) (void)hipFree(h->d_binned);
+        if (h->d_digests) (void)hipFree(h->d_digests);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;

@@ -4,14 +4,26 @@
 #pragma once
 #include "bf_internal.h"
 
+#include <type_traits>
+
 namespace bfdev {
 
 constexpr int kBlock = 256;             // lanes per workgroup = keys per workgroup
 constexpr int kStageBytes = 16384;      // LDS key stage per workgroup
 constexpr int kStageVec = kStageBytes / 16;
 constexpr int kChunk = 8;               // probes issued together per key
+constexpr int kStageSlackVec = 5;       // LDS slack (16-B vectors) past a key stage
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
+
+// a ^ b ^ c in ONE gfx950 v_bitop3_b32 (truth table 0x96).  hipcc (ROCm 7.2)
+// emits two v_xor_b32 for this pattern; SHA-1 has 40 parity rounds and 64
+// schedule steps that each need it.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // FIPS 180-4 SHA-1 compression of one 16-word block; w[] is consumed as the
 // circular message schedule.  Fully unrolled so every w index is static.
@@ -23,14 +35,14 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
         if (t < 16) {
             wt = w[t];
         } else {
-            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
             w[t & 15] = wt;
         }
         uint32_t f, kk;
-        if (t < 20)      { f = d ^ (b & (c ^ d));           kk = 0x5A827999u; }  // Ch  -> v_bfi
-        else if (t < 40) { f = b ^ c ^ d;                   kk = 0x6ED9EBA1u; }  // Parity -> v_xor3
+        if (t < 20)      { f = d ^ (b & (c ^ d));           kk = 0x5A827999u; }  // Ch  -> v_bitop3 0xac
+        else if (t < 40) { f = xor3(b, c, d);               kk = 0x6ED9EBA1u; }  // Parity
         else if (t < 60) { f = (b & c) | (d & (b | c));     kk = 0x8F1BBCDCu; }  // Maj
-        else             { f = b ^ c ^ d;                   kk = 0xCA62C1D6u; }
+        else             { f = xor3(b, c, d);               kk = 0xCA62C1D6u; }
         const uint32_t tmp = rotl(a, 5) + f + e + kk + wt;
         e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
     }
@@ -76,6 +88,59 @@ __device__ __forceinline__ void sha1_key(Src src, uint32_t s, uint32_t L, uint32
     }
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, off);
+        x = x > y ? x : y;
+    }
+    return __builtin_amdgcn_readfirstlane(x);
+}
+
+// SHA-1 of a key staged in LDS.  Waves whose keys all fit one block (L <= 55:
+// every key family the benches and the reference's tests use) build the 16
+// message words branch-free: word j < L/4 is key data, word L/4 carries the
+// tail bytes + the 0x80 pad, later words are zero, w15 = 8L.  The wave-uniform
+// max of L/4 bounds the loop, so short keys read and build only a few words.
+// Needs 64 B of readable LDS slack past the stage.  Other waves: sha1_key.
+__device__ __forceinline__ void sha1_key_staged(const uint32_t* src, uint32_t s, uint32_t L, uint32_t H[5]) {
+    if (__ballot(L > 55u) != 0ull) {   // wave-uniform
+        sha1_key(src, s, L, H);
+        return;
+    }
+    H[0] = 0x67452301u; H[1] = 0xEFCDAB89u; H[2] = 0x98BADCFEu; H[3] = 0x10325476u; H[4] = 0xC3D2E1F0u;
+    const uint32_t pw = L >> 2;
+    const uint32_t pb = (L & 3u) * 8u;
+    const uint32_t keep = (1u << pb) - 1u;   // key-data bytes of the pad word
+    const uint32_t pad = 0x80u << pb;
+    const uint32_t lim = wave_max_u32(pw);   // words above lim are zero in every lane
+    const uint32_t base = s >> 2;
+    const uint32_t sh = s & 3u;
+    uint32_t w[16];
+    uint32_t lo = src[base];
+#pragma unroll
+    for (uint32_t j = 0; j < 14; ++j) {
+        uint32_t x = 0u;
+        if (j <= lim) {
+            const uint32_t hi = src[base + j + 1];
+            const uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+            x = __builtin_bswap32(j < pw ? d : (j == pw ? ((d & keep) | pad) : 0u));
+        }
+        w[j] = x;
+    }
+    w[14] = 0u;
+    w[15] = L << 3;
+    sha1_compress(H, w);
+}
+
+// Dispatch: keys staged in LDS take the branch-free path, global reads the generic one.
+template <bool STAGED>
+__device__ __forceinline__ void sha1_any(const uint32_t* src, uint32_t s, uint32_t L, uint32_t H[5]) {
+    if constexpr (STAGED) sha1_key_staged(src, s, L, H);
+    else sha1_key(src, s, L, H);
+}
+
 // ruby.rb:50-53 for probe i, reduced mod m without an integer divide.
 __device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, uint32_t h1,
                                                  uint32_t h2, uint32_t h3, uint32_t i) {
@@ -83,6 +148,17 @@ __device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, u
     const uint32_t b = (((i + (i & 1u)) & 3u) >> 1) ? h3 : h2;
     const uint64_t v = (uint64_t)a + (uint64_t)i * (uint64_t)b;  // < k * 2^32: exact
     if (g.nomod) return v;
+    if (g.mod_f32) {
+        // m >= 2^17 (set at create): q = v/m < 2^21 (v < 2^38), and a float32 estimate
+        // (relative error <= 2^-22) is off by at most one after truncation; the remainder
+        // is then fixed exactly in 64-bit integers.
+        const float vf = __builtin_fmaf((float)(uint32_t)(v >> 32), 4294967296.0f, (float)(uint32_t)v);
+        const uint32_t q = (uint32_t)(vf * g.inv_m_f);
+        int64_t r = (int64_t)(v - (uint64_t)q * g.m);
+        if (r < 0) r += (int64_t)g.m;
+        else if ((uint64_t)r >= g.m) r -= (int64_t)g.m;
+        return (uint64_t)r;
+    }
     // q within +-1 of floor(v/m): v < 2^38 is exact in a double, 1/m carries 2^-53 relative error.
     const uint64_t q = (uint64_t)((double)v * g.inv_m);
     int64_t r = (int64_t)(v - q * g.m);
@@ -123,12 +199,12 @@ __device__ __forceinline__ void for_key_tile(const uint8_t* __restrict__ keys16,
         for (uint32_t v = t; v < (uint32_t)nvec; v += TILE) s_stage[v] = gv[v];
         __syncthreads();
         if (t < cnt)
-            f(t, reinterpret_cast<const uint32_t*>(s_stage), (uint32_t)(s_off[t] - abase),
+            f(std::true_type{}, t, reinterpret_cast<const uint32_t*>(s_stage), (uint32_t)(s_off[t] - abase),
               (uint32_t)(s_off[t + 1] - s_off[t]));
     } else if (t < cnt) {
         const uint64_t ks = s_off[t];
         const uint64_t kbase = ks & ~(uint64_t)3;
-        f(t, reinterpret_cast<const uint32_t*>(keys16 + kbase), (uint32_t)(ks - kbase),
+        f(std::false_type{}, t, reinterpret_cast<const uint32_t*>(keys16 + kbase), (uint32_t)(ks - kbase),
           (uint32_t)(s_off[t + 1] - ks));
     }
     __syncthreads();

@@ -10,6 +10,8 @@ struct BfGeom {
     double    inv_m;   // 1.0 / m, for the division-free modulo
     uint32_t  k;       // hashes per key (options[:hashes], bloomfilter.rb:28)
     uint32_t  nomod;   // 1 iff m > k*(2^32-1): every derived offset is already < m
+    uint32_t  mod_f32; // 1 iff m >= 2^17: the quotient is estimated in float32 (else float64)
+    float     inv_m_f; // (float)(1.0 / m)
     uint32_t  shards;  // partitioned filters: shard count P (1 = whole filter)
     uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
     // probe policies (tuning; results are identical for every setting)
@@ -48,7 +50,7 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, BfBinPlan* pl
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                    uint32_t* counts, uint32_t* totals, uint32_t* bases, uint32_t* binned,
-                                   uint32_t* any_flag, hipStream_t s);
+                                   void* digests /* 16 B per key */, uint32_t* any_flag, hipStream_t s);
 
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
 // pairs by owner into send[], writes each probe's position into slot[].

@@ -24,13 +24,13 @@ namespace {
 
 using namespace bfdev;
 
-template <int OP, typename Src>
-__device__ __forceinline__ void key_op(const BfGeom& g, Src src, uint32_t s, uint32_t L,
+template <int OP, bool STAGED>
+__device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uint32_t s, uint32_t L,
                                        uint64_t key, uint8_t* __restrict__ out8,
                                        uint64_t* __restrict__ out64, uint32_t& newflag,
                                        uint32_t* hist) {
     uint32_t H[5];
-    sha1_key(src, s, L, H);
+    sha1_any<STAGED>(src, s, L, H);
     const uint32_t k = g.k;
     if constexpr (OP == BF_OP_INDEXES) {
         for (uint32_t i = 0; i < k; ++i)
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
                                                          uint32_t* __restrict__ any_flag,
                                                          unsigned long long* __restrict__ counts) {
     __shared__ uint64_t s_off[kBlock + 1];
-    __shared__ uint4 s_stage[kStageVec + 1];   // +1 vector: slack for the `hi` word of the last key
+    __shared__ uint4 s_stage[kStageVec + kStageSlackVec];   // slack: sha1_key_staged reads up to 64 B past a key
     __shared__ uint32_t s_hist[OP == BF_OP_ROUTE ? 256 : 1];
 
     const uint64_t blk0 = (uint64_t)blockIdx.x * kBlock;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
             const uint32_t s = (uint32_t)(s_off[t] - abase);
             const uint32_t L = (uint32_t)(s_off[t + 1] - s_off[t]);
             const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_stage);
-            key_op<OP>(g, sw, s, L, blk0 + t, out8, out64, newflag, s_hist);
+            key_op<OP, true>(g, sw, s, L, blk0 + t, out8, out64, newflag, s_hist);
         }
     } else if (t < cnt) {
         // Span too large for the stage (long keys): read each key straight from global.
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
         const uint64_t kbase = ks & ~(uint64_t)3;
         const uint32_t* gw = reinterpret_cast<const uint32_t*>(keys16 + kbase);
         const uint64_t L64 = s_off[t + 1] - ks;
-        key_op<OP>(g, gw, (uint32_t)(ks - kbase), (uint32_t)L64, blk0 + t, out8, out64, newflag, s_hist);
+        key_op<OP, false>(g, gw, (uint32_t)(ks - kbase), (uint32_t)L64, blk0 + t, out8, out64, newflag, s_hist);
     }
 
     if constexpr (OP == BF_OP_ROUTE) {

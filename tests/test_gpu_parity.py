@@ -51,6 +51,9 @@ REGIMES = [
     (13 * 0xFFFFFFFF + 1, 13),     # m == reach (largest m still reduced)
     (191701167547, 13),            # 10B@0.01%: m > k*(2^32-1), modulo skipped
     (2**40 + 3, 64),               # k = BF_MAX_K
+    # float32-quotient modulo boundaries (m >= 2^17) and the float64 path below it
+    (2**17 - 1, 13), (2**17, 13), (2**17 + 1, 64), (2**32 - 1, 13), (2**32, 6), (2**32 + 1, 64),
+    (999999999989, 64), (3, 64), (131071 * 7, 9),
 ]
 
 
