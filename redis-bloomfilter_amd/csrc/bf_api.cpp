@@ -57,12 +57,9 @@ struct bf_handle {
     unsigned long long* d_cursor = nullptr;
     // binned-insert scratch (grown on demand) and policy: 0 never, 1 always, 2 auto
     uint32_t binned_mode = 2;
-    uint32_t* d_bin_counts = nullptr;
-    uint32_t* d_bin_totals = nullptr;
-    uint32_t* d_bin_bases = nullptr;
-    uint32_t* d_binned = nullptr;
-    void* d_digests = nullptr;   // 16 B per key: the count pass's SHA-1 words for the scatter pass
-    uint64_t bin_counts_cap = 0, bin_bins_cap = 0, binned_cap = 0, digest_cap = 0;
+    uint32_t bin_region_log2 = 19;   // preferred region (LDS image) size of the apply pass
+    void* d_bin_scratch = nullptr;   // digests, probe arrays and histograms of one binned launch
+    uint64_t bin_scratch_cap = 0;
     uint64_t cap_keys = 0, cap_bytes = 0;
     Slot slot[2];
     bool staging_ready = false;
@@ -116,6 +113,7 @@ uint32_t default_first_round(uint32_t k) { return (k + 3) / 4; }
 constexpr uint32_t kDefaultInsertTest = 1;
 constexpr uint32_t kDefaultMemKind = 0;
 constexpr uint32_t kDefaultBinnedMode = 2;     // auto
+constexpr uint32_t kDefaultBinRegionLog2 = 19; // 64 KiB LDS image per apply workgroup
 constexpr double kBinnedCostRatio = 3.0;       // random line-fill bytes vs bitset bytes
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
@@ -182,51 +180,21 @@ int check_keys_args(bf_handle* h, const void* keys, const uint64_t* offsets, uin
 // clearly exceed one streaming pass over a bitset that lives beyond L2.
 bool use_binned(const bf_handle* h, uint64_t n, bool per_key, BfBinPlan* plan) {
     if (per_key || h->binned_mode == 0 || h->shards > 1) return false;
-    if (!bf_binned_plan(h->dev_bytes, n, h->k, plan)) return false;
+    if (!bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, plan)) return false;
     if (h->binned_mode == 1) return true;
     return h->dev_bytes >= (64ull << 20) &&
            (double)n * (double)h->k * 128.0 > kBinnedCostRatio * (double)h->dev_bytes;
 }
 
-int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p, uint64_t n) {
-    const uint64_t need_counts = (uint64_t)p.nblocks * p.nbins;
-    const uint64_t need_bins = (uint64_t)p.nbins + 1;
-    if (need_counts <= h->bin_counts_cap && need_bins <= h->bin_bins_cap && p.probes <= h->binned_cap &&
-        n <= h->digest_cap)
-        return BF_OK;
-    (void)hipDeviceSynchronize();
-    if (need_counts > h->bin_counts_cap) {
-        if (h->d_bin_counts) (void)hipFree(h->d_bin_counts);
-        h->d_bin_counts = nullptr;
-        h->bin_counts_cap = 0;
-        HIPCHK(h, hipMalloc((void**)&h->d_bin_counts, need_counts * 4));
-        h->bin_counts_cap = need_counts;
-    }
-    if (need_bins > h->bin_bins_cap) {
-        if (h->d_bin_totals) (void)hipFree(h->d_bin_totals);
-        if (h->d_bin_bases) (void)hipFree(h->d_bin_bases);
-        h->d_bin_totals = h->d_bin_bases = nullptr;
-        h->bin_bins_cap = 0;
-        HIPCHK(h, hipMalloc((void**)&h->d_bin_totals, need_bins * 4));
-        HIPCHK(h, hipMalloc((void**)&h->d_bin_bases, need_bins * 4));
-        h->bin_bins_cap = need_bins;
-    }
-    if (p.probes > h->binned_cap) {
-        if (h->d_binned) (void)hipFree(h->d_binned);
-        h->d_binned = nullptr;
-        h->binned_cap = 0;
-        const uint64_t cap = round_up(p.probes, 1ull << 20);
-        HIPCHK(h, hipMalloc((void**)&h->d_binned, cap * 4));
-        h->binned_cap = cap;
-    }
-    if (n > h->digest_cap) {
-        if (h->d_digests) (void)hipFree(h->d_digests);
-        h->d_digests = nullptr;
-        h->digest_cap = 0;
-        const uint64_t cap = round_up(n, 1ull << 16);
-        HIPCHK(h, hipMalloc(&h->d_digests, cap * 16));
-        h->digest_cap = cap;
-    }
+int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p) {
+    if (p.scratch_bytes <= h->bin_scratch_cap) return BF_OK;
+    (void)hipDeviceSynchronize();   // earlier launches may still use the old buffer
+    if (h->d_bin_scratch) (void)hipFree(h->d_bin_scratch);
+    h->d_bin_scratch = nullptr;
+    h->bin_scratch_cap = 0;
+    const uint64_t cap = round_up(p.scratch_bytes, 16ull << 20);
+    HIPCHK(h, hipMalloc(&h->d_bin_scratch, cap));
+    h->bin_scratch_cap = cap;
     return BF_OK;
 }
 
@@ -235,10 +203,9 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
               uint8_t* out8, uint64_t* out64, uint32_t* flag, hipStream_t s) {
     BfBinPlan plan;
     if ((op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS) && use_binned(h, n, out8 != nullptr, &plan)) {
-        int rc = ensure_bin_scratch(h, plan, n);
+        int rc = ensure_bin_scratch(h, plan);
         if (rc) return rc;
-        HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_counts,
-                                          h->d_bin_totals, h->d_bin_bases, h->d_binned, h->d_digests,
+        HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_scratch,
                                           op == BF_OP_INSERT_FLAGS ? flag : nullptr, s));
         return BF_OK;
     }
@@ -476,6 +443,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k));
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
+    h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);
     *out = h;
     return BF_OK;
 }
@@ -494,11 +462,7 @@ int bf_destroy(bf_handle* h) {
         if (h->d_tmp_local) (void)hipFree(h->d_tmp_local);
         if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
         if (h->d_cursor) (void)hipFree(h->d_cursor);
-        if (h->d_bin_counts) (void)hipFree(h->d_bin_counts);
-        if (h->d_bin_totals) (void)hipFree(h->d_bin_totals);
-        if (h->d_bin_bases) (void)hipFree(h->d_bin_bases);
-        if (h->d_binned) (void)hipFree(h->d_binned);
-        if (h->d_digests) (void)hipFree(h->d_digests);
+        if (h->d_bin_scratch) (void)hipFree(h->d_bin_scratch);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;

@@ -37,20 +37,25 @@ hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const
                           uint32_t* any_flag, hipStream_t s,
                           unsigned long long* counts = nullptr /* BF_OP_ROUTE only */);
 
-// Binned insert (bf_binned.hip): plan + launch.  Scratch sizes: counts
-// nblocks*nbins u32, totals nbins u32, bases nbins+1 u32, binned probes u32.
+// Binned insert (bf_binned.hip): plan + launch.  The launch carves every
+// intermediate (digests, two probe arrays, histograms) out of one device
+// scratch buffer of plan.scratch_bytes.
 struct BfBinPlan {
     uint32_t region_log2;   // 2^region_log2 bits per region (LDS image in the apply pass)
     uint32_t nbins;         // regions covering the bitset
-    uint32_t nblocks;       // workgroups of the count / scatter passes (fixed key ranges)
+    uint32_t rel_log2;      // superbin = 2^rel_log2 consecutive regions (level-1 partition)
+    uint32_t nsup;          // superbins covering the bitset (<= 256)
+    uint32_t nblocks;       // workgroups of the count / level-1 passes (fixed key ranges)
     uint64_t chunk;         // keys per workgroup
-    uint64_t probes;        // n * k
+    uint64_t probes;        // n * k (< 2^32)
+    uint64_t scratch_bytes; // device scratch the launch needs
 };
-bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, BfBinPlan* plan);
+// false: the batch / filter shape is outside the binned path (k > 16, more than
+// 2^32 probes, or a bitset beyond 24576 regions of 2^20 bits).
+bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, BfBinPlan* plan);
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
-                                   uint32_t* counts, uint32_t* totals, uint32_t* bases, uint32_t* binned,
-                                   void* digests /* 16 B per key */, uint32_t* any_flag, hipStream_t s);
+                                   void* scratch, uint32_t* any_flag, hipStream_t s);
 
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
 // pairs by owner into send[], writes each probe's position into slot[].

@@ -249,3 +249,36 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
         any2, _ = f.insert_many(ib, io, any_new=True)
         assert (any1, any2) == (True, False)
         assert f.export_redis() == s
+
+
+@pytest.mark.parametrize("rl", ["19", "20"])
+@pytest.mark.parametrize("case", ["dup", "tiny", "long", "k16", "nstar"])
+def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
+    """Forced binned insert on shapes that stress its partition passes: one key repeated
+    (every probe in <= k regions, one superbin run per tile holding thousands of probes),
+    a few keys over the 1.2 GB north-star filter (a level-2 chunk spanning every superbin:
+    the per-probe cursor path), keys past the single-block SHA-1 (multi-block hash in the
+    count pass), k = 16 (one key per lane in the level-1 pass), and a 200k-key batch on the
+    north-star filter; both region sizes (64 KiB / 128 KiB LDS images)."""
+    monkeypatch.setenv("BFHIP_INSERT_BINNED", "1")
+    monkeypatch.setenv("BFHIP_BIN_REGION_LOG2", rl)
+    rng = np.random.default_rng(RNG_SEED + 8)
+    if case == "dup":
+        m, k = 1437758757, 10
+        ins = pkg.keys.pack(["same-key"] * 60_000 + [str(i) for i in range(100)])
+    elif case == "tiny":
+        m, k = 9585058377, 6
+        ins = rand_keys(rng, 37, 0, 20)
+    elif case == "long":
+        m, k = 1437758757, 6
+        ins = rand_keys(rng, 20_000, 56, 300)
+    elif case == "k16":
+        m, k = 2**32 + 17, 16
+        ins = rand_keys(rng, 30_000, 0, 24)
+    else:
+        m, k = 9585058377, 6
+        ins = pkg.keys.pack_decimal(rng.integers(0, 10**9, size=200_000))
+    ib, io = ins
+    extra = rand_keys(rng, 5_000, 0, 24)
+    probe = (np.concatenate([ib, extra[0]]), np.concatenate([io, extra[1][1:] + io[-1]]))
+    _insert_include_roundtrip(pkg, oracle, m, k, ins, probe)
