@@ -196,6 +196,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     for bt in batches[:warmup]:
         insert(bt)
         include(bt)
+    prof = pf.engine.filter if pf is not None else f
+    prof.profile(True)      # per-kernel HIP events, recorded on the launch stream inside the timed region
+    prof.profile_read(reset=True)
     D.barrier()
     torch.cuda.synchronize()
     ev = []
@@ -214,21 +217,44 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     wall = D.max(wall)
     ins_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     inc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    kernels = {name: {"ms": tot / cnt, "launches": cnt} for name, (tot, cnt) in prof.profile_read(reset=True).items()}
+    prof.profile(False)
+    plan = f.insert_plan(batch) if pf is None else {"binned": False, "scratch_bytes": 0}
     # sanity: the members (first half of the include? batch) must all be found
     got = out.cpu().numpy()
     assert got[: batch // 2].all(), "false negative in the include? batch"
     fp_rate = float(got[batch // 2:].mean())
     Lmean = float(batches[-1][1][1][-1].item()) / batch
+    P = batch * k
+    bitset = f.device_bytes
+    # algorithmic bytes per launch of each kernel (SURVEY §8 d for the random-access kernels;
+    # the binned insert's kernels by the arrays each one must read and write)
+    algo = {
+        "bf_keys_kernel<INCLUDE>": batch * (Lmean + 8 + 1 + k * GRANULE),
+        "bf_keys_kernel<INSERT>": batch * (Lmean + 8 + 2 * k * GRANULE),
+        "bf_keys_kernel<INSERT_FLAGS>": batch * (Lmean + 8 + 2 * k * GRANULE + 1),
+        "bin_count": batch * (Lmean + 8 + 16),
+        "bin_part1": batch * 16 + P * 4,
+        "bin_part2": P * 8,
+        "bin_apply": P * 4 + 2 * bitset,
+    }
+    for name, kt in kernels.items():
+        if name in algo:
+            kt["algo_bytes"] = algo[name]
+            kt["GBps"] = algo[name] / (kt["ms"] / 1e3) / 1e9
     res = {
         "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3),
         "wall_s": wall, "steps": steps,
         "keys_per_s": 2 * batch * D.world * steps / wall,
-        "insert": {"kernel_ms": ins_ms, "keys_per_s": batch / (ins_ms / 1e3),
-                   "algo_bytes_per_key": Lmean + 8 + 2 * k * GRANULE},
-        "include": {"kernel_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
+        "insert": {"op_ms": ins_ms, "keys_per_s": batch / (ins_ms / 1e3),
+                   "path": "binned" if plan["binned"] else "direct",
+                   "algo_bytes_per_key": (Lmean + 8 + 2 * bitset / batch) if plan["binned"]
+                   else (Lmean + 8 + 2 * k * GRANULE)},
+        "include": {"op_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
                     "algo_bytes_per_key": Lmean + 8 + 1 + k * GRANULE,
                     "observed_fp_rate": fp_rate},
-        "bitset_bytes": f.device_bytes,
+        "kernels": kernels,
+        "bitset_bytes": bitset,
     }
     ib, io = to_host(*batches[0][0])
     pb, po = to_host(*batches[0][1])
@@ -250,8 +276,10 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
-def cpu_baseline(data, budget_s: float = 12.0):
-    """Oracle (C restatement, OpenMP) on the host cores, bounded sample of the same workload."""
+def cpu_baseline(data, budget_s: float = 10.0):
+    """Oracle (C restatement, OpenMP) on the host cores, bounded sample of the same workload:
+    the first step's insert and include? batches, in 2^20-key chunks, passed over again
+    until ~budget_s of CPU work is done."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O   # the checker, here the timed CPU baseline ("port")
     ib, io, pb, po, host_bits, m, k = data
@@ -263,28 +291,30 @@ def cpu_baseline(data, budget_s: float = 12.0):
     n_total = len(io) - 1
     chunk = 1 << 20
     i = 0
-    while time.perf_counter() - t0 < budget_s and i < n_total:
+    while time.perf_counter() - t0 < budget_s:
         j = min(i + chunk, n_total)
         sub_o = io[i:j + 1]
         orc.insert_many_omp(bits, m, k, ib, sub_o, threads)
         sub_p = po[i:j + 1]
         orc.include_many_omp(bits, m, k, pb, sub_p, threads)
         done += 2 * (j - i)
-        i = j
+        i = j if j < n_total else 0
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "keys/s", "cores": threads, "kind": "port",
-            "sample": "%d insert + %d include? keys (first %d keys of each batch) on the same filter, "
-                      "oracle/bf_oracle.c with OpenMP, %.1f s" % (done // 2, done // 2, done // 2, dt)}
+            "sample": "%d insert + %d include? keys (the first step's %d-key batches, repeated) on the same "
+                      "prefilled filter, oracle/bf_oracle.c with OpenMP, %.1f s" % (done // 2, done // 2, n_total, dt)}
 
 
-def load_traffic(workload: str):
+def load_traffic(workload: str, kernel: str):
+    """PMC-measured HBM bytes per launch of `kernel` (profiles/pmc_traffic.json, tools/pmc_summary.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            t = json.load(fh)
-        return t.get(workload)
+            t = json.load(fh).get(workload) or {}
     except (OSError, ValueError):
         return None
+    rec = t.get(kernel)
+    return rec.get("hbm_bytes_per_launch") if isinstance(rec, dict) else None
 
 
 def main():
@@ -325,12 +355,12 @@ def main():
         return
 
     ins, inc = main_res["insert"], main_res["include"]
-    dom_name = "insert" if ins["kernel_ms"] >= inc["kernel_ms"] else "include"
-    dom = main_res[dom_name]
-    per_launch_keys = main_res["batch"]
-    algo = dom["algo_bytes_per_key"] * per_launch_keys
-    achieved = algo / (dom["kernel_ms"] / 1e3)
-    traffic = load_traffic(args.config)
+    # dominant kernel: the largest total time per step among the kernels the ops launched
+    kern = main_res["kernels"]
+    dom_name = max(kern, key=lambda nm: kern[nm]["ms"] * kern[nm]["launches"])
+    dom = kern[dom_name]
+    achieved = dom["algo_bytes"] / (dom["ms"] / 1e3) if "algo_bytes" in dom else None
+    traffic = load_traffic(args.config, dom_name)
     n, p, batch, _ = CONFIGS[args.config]
     line = {
         "metric": "keys/sec (insert, include?) per GPU and whole node; % of HBM random-access roofline",
@@ -353,13 +383,15 @@ def main():
                    "parallelism": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key batches "
                                   "routed to owner GPUs by RCCL all-to-all)" % D.world
                    if (D.world > 1 or args.mode == "partitioned") else "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                     "traffic": traffic.get(dom_name) if isinstance(traffic, dict) else None,
-                     "algo_bytes_per_key": dom["algo_bytes_per_key"], "keys_per_launch": per_launch_keys,
-                     "kernel_ms": dom["kernel_ms"]},
+        "roofline": {"bound": "hbm", "kernel": dom_name,
+                     "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK if achieved else None,
+                     "traffic": traffic, "algo_bytes": dom.get("algo_bytes"), "keys_per_launch": batch,
+                     "kernel_ms": dom["ms"], "timing": "HIP events on the launch stream around each kernel, "
+                                                       "inside the timed region (bf_profile)"},
         "cpu_baseline": cpu,
         "ops": {"insert": ins, "include": inc},
+        "kernels": kern,
         "host_api": main_res.get("host_api"),
         "secondary": secondary or None,
         "reference_published_keys_per_s": {"ruby_insert": 5103, "ruby_include": 4322,

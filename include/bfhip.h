@@ -97,7 +97,9 @@ int  bf_info(const bf_handle* h, uint64_t* m_bits, uint32_t* k, uint64_t* reach_
  *      offsets[0] need not be 0. */
 int  bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                     uint8_t* any_new /* nullable: 1 iff some bit flipped 0->1 (drives EXPIRE) */,
-                    uint8_t* per_key_new /* nullable, n bytes: 1 iff this key's atomics saw a 0 */);
+                    uint8_t* per_key_new /* nullable, n bytes: 1 iff, inserting the keys one by one in
+                                            batch order (ruby.rb:57-61), this key flipped a bit; its
+                                            complement is include?-before-insert (bf_10_000.rb:37) */);
 int  bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                      uint8_t* out /* n bytes, 0/1 */);
 int  bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
@@ -120,6 +122,21 @@ int  bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
                          uint64_t n, uint64_t* d_out, void* stream);
 /* The device bitset (Redis byte order, device_bytes long, zero past the reachable prefix). */
 int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
+/* How an insert batch of n keys will run (no launch): *binned = 1 for the binned
+ * (hash, partition, per-region LDS apply) pipeline, 0 for the direct test-then-atomic
+ * kernel; *scratch_bytes = device scratch the binned pipeline allocates for it.
+ * The choice never changes results; BFHIP_INSERT_BINNED=0/1 forces it. */
+int  bf_insert_plan(const bf_handle* h, uint64_t n, uint32_t* binned, uint64_t* scratch_bytes);
+
+/* ---- per-kernel timing.  While enabled, every keyed launch (insert / include? /
+ *      indexes, host or device API) records HIP events on its stream between its
+ *      kernels; bf_profile_read waits for them and returns, per kernel name, the
+ *      summed duration and launch count (names in BF_PROFILE_NAME_LEN-byte slots).
+ *      *n_out = kernels known (may exceed cap).  reset != 0 clears the totals. */
+#define BF_PROFILE_NAME_LEN 64
+int  bf_profile(bf_handle* h, uint32_t enable);
+int  bf_profile_read(bf_handle* h, char* names, double* total_ms, uint64_t* launches, uint32_t cap,
+                     uint32_t* n_out, uint32_t reset);
 int  bf_stream(bf_handle* h, void** stream);   /* the handle's own (non-blocking) hipStream_t */
 int  bf_sync(bf_handle* h);                    /* synchronise the handle's own stream */
 

@@ -21,6 +21,7 @@ BF_OK, BF_EINVAL, BF_ENOMEM, BF_EDEVICE, BF_ERCCL, BF_ERANGE = 0, 1, 2, 3, 4, 5
 BF_IMPORT_REPLACE, BF_IMPORT_OR = 0, 1
 BF_FLAG_ROUTE32 = 1
 BF_MAX_K = 64
+PROFILE_NAME_LEN = 64   # BF_PROFILE_NAME_LEN
 
 _STATUS = {BF_EINVAL: "BF_EINVAL", BF_ENOMEM: "BF_ENOMEM", BF_EDEVICE: "BF_EDEVICE",
            BF_ERCCL: "BF_ERCCL", BF_ERANGE: "BF_ERANGE"}
@@ -73,6 +74,9 @@ SIGNATURES = {
     "bf_include_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_indexes_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_device_bits": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), _u64p]),
+    "bf_insert_plan": (ctypes.c_int, [_vp, _u64, _u32p, _u64p]),
+    "bf_profile": (ctypes.c_int, [_vp, _u32]),
+    "bf_profile_read": (ctypes.c_int, [_vp, _vp, _vp, _vp, _u32, _u32p, _u32]),
     "bf_sync": (ctypes.c_int, [_vp]),
     "bf_stream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "bf_shard_info": (ctypes.c_int, [_vp, _u32p, _u32p, _u32p, _u64p]),
@@ -302,6 +306,31 @@ class Filter:
                 self._own_stream = p.value or 0
             return self._own_stream or None
         return int(stream) or None
+
+    def insert_plan(self, n: int) -> dict:
+        """How an insert of n keys runs: {"binned": bool, "scratch_bytes": int} (bf_insert_plan)."""
+        b, sb = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(self._lib.bf_insert_plan(self.handle, int(n), ctypes.byref(b), ctypes.byref(sb)), self._h)
+        return {"binned": bool(b.value), "scratch_bytes": int(sb.value)}
+
+    def profile(self, enable: bool) -> None:
+        """Per-kernel HIP-event timing of every keyed launch (bf_profile)."""
+        _check(self._lib.bf_profile(self.handle, 1 if enable else 0), self._h)
+
+    def profile_read(self, reset: bool = True) -> dict:
+        """{kernel name: (total ms, launches)} since the last reset (bf_profile_read)."""
+        cap = 32
+        names = ctypes.create_string_buffer(cap * PROFILE_NAME_LEN)
+        ms = np.zeros(cap, np.float64)
+        cnt = np.zeros(cap, np.uint64)
+        n = ctypes.c_uint32()
+        _check(self._lib.bf_profile_read(self.handle, names, _ptr(ms), _ptr(cnt), cap, ctypes.byref(n),
+                                         1 if reset else 0), self._h)
+        out = {}
+        for i in range(min(n.value, cap)):
+            raw = names.raw[i * PROFILE_NAME_LEN:(i + 1) * PROFILE_NAME_LEN]
+            out[raw.split(b"\0", 1)[0].decode()] = (float(ms[i]), int(cnt[i]))
+        return out
 
     def device_bits(self) -> Tuple[int, int]:
         p = _vp()

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #define BFHIP_VERSION_STR "bfhip 0.1.0 (gfx950; redis-bloomfilter 1.1.2 ruby-driver layout)"
 
@@ -66,6 +67,11 @@ struct bf_handle {
     uint32_t* d_flag = nullptr;
     unsigned long long* d_scan = nullptr;
     uint32_t* h_flag = nullptr;   // pinned
+    // per-kernel timing (bf_profile): event sets awaiting harvest, recycled sets, totals
+    bool profile = false;
+    std::vector<BfMarks> prof_pending, prof_free;
+    struct ProfAcc { std::string name; double ms; uint64_t launches; };
+    std::vector<ProfAcc> prof_acc;
     std::string err;
 };
 
@@ -186,30 +192,93 @@ bool use_binned(const bf_handle* h, uint64_t n, bool per_key, BfBinPlan* plan) {
            (double)n * (double)h->k * 128.0 > kBinnedCostRatio * (double)h->dev_bytes;
 }
 
-int ensure_bin_scratch(bf_handle* h, const BfBinPlan& p) {
-    if (p.scratch_bytes <= h->bin_scratch_cap) return BF_OK;
+// Device scratch shared by the binned and the sequential insert paths (grown on demand).
+int ensure_scratch(bf_handle* h, uint64_t bytes) {
+    if (bytes <= h->bin_scratch_cap) return BF_OK;
     (void)hipDeviceSynchronize();   // earlier launches may still use the old buffer
     if (h->d_bin_scratch) (void)hipFree(h->d_bin_scratch);
     h->d_bin_scratch = nullptr;
     h->bin_scratch_cap = 0;
-    const uint64_t cap = round_up(p.scratch_bytes, 16ull << 20);
+    const uint64_t cap = round_up(bytes, 16ull << 20);
     HIPCHK(h, hipMalloc(&h->d_bin_scratch, cap));
     h->bin_scratch_cap = cap;
     return BF_OK;
 }
 
+// bf_profile: an event set per keyed launch, harvested by bf_profile_read.
+BfMarks* prof_begin(bf_handle* h, hipStream_t s) {
+    if (!h->profile) return nullptr;
+    BfMarks mk{};
+    if (!h->prof_free.empty()) {
+        mk = h->prof_free.back();
+        h->prof_free.pop_back();
+    } else {
+        for (hipEvent_t& e : mk.ev)
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    }
+    mk.used = 0;
+    if (hipEventRecord(mk.ev[0], s) != hipSuccess) {
+        h->prof_free.push_back(mk);
+        return nullptr;
+    }
+    h->prof_pending.push_back(mk);
+    return &h->prof_pending.back();
+}
+
+int prof_harvest(bf_handle* h) {
+    for (BfMarks& mk : h->prof_pending) {
+        if (mk.used > 0) HIPCHK(h, hipEventSynchronize(mk.ev[mk.used]));
+        for (int i = 0; i < mk.used; ++i) {
+            float ms = 0.f;
+            HIPCHK(h, hipEventElapsedTime(&ms, mk.ev[i], mk.ev[i + 1]));
+            auto it = std::find_if(h->prof_acc.begin(), h->prof_acc.end(),
+                                   [&](const bf_handle::ProfAcc& a) { return a.name == mk.names[i]; });
+            if (it == h->prof_acc.end()) h->prof_acc.push_back({mk.names[i], (double)ms, 1});
+            else { it->ms += ms; it->launches += 1; }
+        }
+        h->prof_free.push_back(mk);
+    }
+    h->prof_pending.clear();
+    return BF_OK;
+}
+
+const char* op_kernel_name(BfOp op) {
+    switch (op) {
+        case BF_OP_INDEXES: return "bf_keys_kernel<INDEXES>";
+        case BF_OP_INCLUDE: return "bf_keys_kernel<INCLUDE>";
+        case BF_OP_INSERT: return "bf_keys_kernel<INSERT>";
+        case BF_OP_INSERT_FLAGS: return "bf_keys_kernel<INSERT_FLAGS>";
+        default: return "bf_keys_kernel<ROUTE>";
+    }
+}
+
 // Every keyed launch goes through here: inserts take the binned path when it pays.
 int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, uint64_t bias, uint64_t n,
               uint8_t* out8, uint64_t* out64, uint32_t* flag, hipStream_t s) {
-    BfBinPlan plan;
-    if ((op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS) && use_binned(h, n, out8 != nullptr, &plan)) {
-        int rc = ensure_bin_scratch(h, plan);
+    if (op == BF_OP_INSERT_FLAGS && out8) {
+        // Per-key flags: exact sequential semantics (bf_seq.hip), chunk after chunk in stream order.
+        const uint64_t chunk = bf_seq_chunk_keys(h->k);
+        int rc = ensure_scratch(h, bf_seq_scratch_bytes(std::min(n, chunk), h->k, nullptr));
         if (rc) return rc;
-        HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_scratch,
-                                          op == BF_OP_INSERT_FLAGS ? flag : nullptr, s));
+        for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+            const uint64_t cn = std::min(chunk, n - c0);
+            BfMarks* mk = prof_begin(h, s);
+            HIPCHK(h, bf_launch_insert_seq(h->g, k16, offs + c0, bias, cn, h->d_bin_scratch, out8 + c0, flag, s, mk));
+        }
         return BF_OK;
     }
+    BfBinPlan plan;
+    if ((op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS) && use_binned(h, n, out8 != nullptr, &plan)) {
+        int rc = ensure_scratch(h, plan.scratch_bytes);
+        if (rc) return rc;
+        BfMarks* mk = prof_begin(h, s);
+        HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_scratch,
+                                          op == BF_OP_INSERT_FLAGS ? flag : nullptr, s, mk));
+        return BF_OK;
+    }
+    BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_keys(op, h->g, k16, offs, bias, n, out8, out64, flag, s));
+    bf_mark(mk, s, op_kernel_name(op));
     return BF_OK;
 }
 
@@ -463,6 +532,9 @@ int bf_destroy(bf_handle* h) {
         if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
         if (h->d_cursor) (void)hipFree(h->d_cursor);
         if (h->d_bin_scratch) (void)hipFree(h->d_bin_scratch);
+        (void)prof_harvest(h);   // waits for marks recorded on caller streams
+        for (BfMarks& mk : h->prof_free)
+            for (hipEvent_t e : mk.ev) (void)hipEventDestroy(e);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -678,14 +750,17 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     if (rc) return rc;
     auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
     HIPCHK(h, hipMemsetAsync(counts, 0, h->shards * sizeof(unsigned long long), s));
+    BfMarks* mk = prof_begin(h, s);
     if (n) {
         uint64_t bias = 0;
         const uint8_t* k16 = align_keys(d_key_bytes, &bias);
         HIPCHK(h, bf_launch_keys(BF_OP_ROUTE, h->g, k16, d_offsets, bias, n, h->d_tmp_owner, h->d_tmp_local,
                                  nullptr, s, counts));
+        bf_mark(mk, s, op_kernel_name(BF_OP_ROUTE));
     }
     HIPCHK(h, bf_launch_route_scatter(h->d_tmp_local, h->d_tmp_owner, probes, h->shards, counts, h->d_cursor,
                                       d_send, d_slot, h->route32, s));
+    bf_mark(mk, s, "route_scatter");
     return BF_OK;
 }
 
@@ -695,7 +770,10 @@ int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint3
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, h->route32, pick_stream(h, stream)));
+    hipStream_t s = pick_stream(h, stream);
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, h->route32, s));
+    bf_mark(mk, s, "shard_insert");
     return BF_OK;
 }
 
@@ -705,7 +783,10 @@ int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, h->route32, pick_stream(h, stream)));
+    hipStream_t s = pick_stream(h, stream);
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, h->route32, s));
+    bf_mark(mk, s, "shard_test");
     return BF_OK;
 }
 
@@ -716,7 +797,10 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, pick_stream(h, stream)));
+    hipStream_t s = pick_stream(h, stream);
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, s));
+    bf_mark(mk, s, "combine");
     return BF_OK;
 }
 
@@ -746,6 +830,42 @@ int bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes) {
     if (!h) return BF_EINVAL;
     if (d_bits) *d_bits = h->g.bits;
     if (device_bytes) *device_bytes = h->dev_bytes;
+    return BF_OK;
+}
+
+int bf_profile(bf_handle* h, uint32_t enable) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    int rc = prof_harvest(h);
+    h->profile = enable != 0;
+    return rc;
+}
+
+int bf_profile_read(bf_handle* h, char* names, double* total_ms, uint64_t* launches, uint32_t cap,
+                    uint32_t* n_out, uint32_t reset) {
+    if (!h || !n_out) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    int rc = prof_harvest(h);
+    if (rc) return rc;
+    *n_out = (uint32_t)h->prof_acc.size();
+    for (uint32_t i = 0; i < cap && i < h->prof_acc.size(); ++i) {
+        const bf_handle::ProfAcc& a = h->prof_acc[i];
+        if (names) snprintf(names + (size_t)i * BF_PROFILE_NAME_LEN, BF_PROFILE_NAME_LEN, "%s", a.name.c_str());
+        if (total_ms) total_ms[i] = a.ms;
+        if (launches) launches[i] = a.launches;
+    }
+    if (reset) h->prof_acc.clear();
+    return BF_OK;
+}
+
+int bf_insert_plan(const bf_handle* h, uint64_t n, uint32_t* binned, uint64_t* scratch_bytes) {
+    if (!h) return BF_EINVAL;
+    BfBinPlan plan{};
+    const bool b = n > 0 && use_binned(h, n, false, &plan);
+    if (binned) *binned = b ? 1u : 0u;
+    if (scratch_bytes) *scratch_bytes = b ? plan.scratch_bytes : 0;
     return BF_OK;
 }
 

@@ -38,12 +38,14 @@ constexpr int kTile = 1024;                   // lanes of the count / partition 
 constexpr int kTileStageVec = 32768 / 16;     // 32 KiB LDS key stage (count pass)
 constexpr uint32_t kMaxBins = 24576;          // region histogram capacity (96 KiB)
 constexpr uint32_t kMaxSup = 256;             // superbins (u8 tags in part1)
-constexpr uint32_t kMaxBlocks = 256;          // count / part1 workgroups (one per CU)
-constexpr uint32_t kP1Probes = 16384;         // probes per part1 tile
-constexpr int kP1Slots = 16;                  // probes per lane per part1 tile (k <= 16)
+constexpr uint32_t kMaxBlocks = 512;          // count / part1 workgroups (two per CU)
+constexpr uint32_t kP1Probes = 12288;         // probes per part1 tile (64 KiB of LDS: two workgroups per CU)
+constexpr int kP1Slots = 12;                  // probes per lane per part1 tile (k <= 12)
+constexpr uint32_t kP1TwoKeys = 6;            // k <= 6: two keys per lane per tile
 constexpr uint32_t kP2Probes = 8192;          // probes per part2 workgroup
 constexpr int kP2PerLane = kP2Probes / kTile;
-constexpr uint32_t kP2Bins = 1024;            // local region bins per part2 workgroup
+constexpr uint32_t kP2Bins = 512;             // local region bins per part2 workgroup (52 KiB: three per CU)
+constexpr uint32_t kApplyLanes = 1024;
 
 // Exclusive prefix sum of v over the workgroup (blockDim.x a multiple of 64,
 // at most 1024 lanes); *total gets the workgroup sum.  s_w: 16 words of LDS.
@@ -131,8 +133,8 @@ __global__ __launch_bounds__(1024) void bin_colsum_kernel(const uint32_t* __rest
     }
 }
 
-// scnt[b][sb] -> exclusive prefix over b, in place.  One workgroup (256 lanes) per superbin.
-__global__ __launch_bounds__(256) void bin_supscan_kernel(uint32_t* __restrict__ scnt, uint32_t nblocks,
+// scnt[b][sb] -> exclusive prefix over b, in place.  One workgroup (kMaxBlocks lanes) per superbin.
+__global__ __launch_bounds__(kMaxBlocks) void bin_supscan_kernel(uint32_t* __restrict__ scnt, uint32_t nblocks,
                                                           uint32_t nsup) {
     __shared__ uint32_t s_w[16];
     const uint32_t t = threadIdx.x, sb = blockIdx.x;
@@ -185,23 +187,26 @@ __global__ __launch_bounds__(kTile) void bin_part1_kernel(BfGeom g, const uint4*
     if (t < kMaxSup) s_cnt[t] = 0;
     __syncthreads();
     const uint32_t k = g.k;
-    const uint32_t kpl = k <= 8 ? 2u : 1u;          // keys per lane per tile
+    const uint32_t kpl = k <= kP1TwoKeys ? 2u : 1u;   // keys per lane per tile
     const uint32_t tile_keys = kTile * kpl;
     const uint64_t smask = (1ull << sup_log2) - 1ull;
     const uint64_t k0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t k1 = (k0 + chunk < n) ? k0 + chunk : n;
+    // digests of the next tile are loaded while the current one is sorted and written
+    uint4 N0 = make_uint4(0, 0, 0, 0), N1 = make_uint4(0, 0, 0, 0);
+    if (k0 + t < k1) N0 = digests[k0 + t];
+    if (kpl == 2 && k0 + kTile + t < k1) N1 = digests[k0 + kTile + t];
     for (uint64_t tile0 = k0; tile0 < k1; tile0 += tile_keys) {
         const uint32_t tk = (uint32_t)((k1 - tile0) < (uint64_t)tile_keys ? (k1 - tile0) : tile_keys);
         // A: probes of this lane's keys -> (superbin, rank in the tile's superbin run)
         const bool live0 = t < tk;
         const bool live1 = kpl == 2 && kTile + t < tk;
-        const uint4 H0 = live0 ? digests[tile0 + t] : make_uint4(0, 0, 0, 0);
-        const uint4 H1 = live1 ? digests[tile0 + kTile + t] : make_uint4(0, 0, 0, 0);
+        const uint4 H0 = N0, H1 = N1;
         uint32_t tag[kP1Slots], loc[kP1Slots];
 #pragma unroll
         for (int q = 0; q < kP1Slots; ++q) {
-            const bool second = kpl == 2 && q >= 8;
-            const uint32_t i = kpl == 2 ? (uint32_t)(q & 7) : (uint32_t)q;
+            const bool second = kpl == 2 && q >= (int)kP1TwoKeys;
+            const uint32_t i = kpl == 2 ? (second ? (uint32_t)q - kP1TwoKeys : (uint32_t)q) : (uint32_t)q;
             const bool live = i < k && (second ? live1 : live0);
             tag[q] = 0xFFFFFFFFu;
             loc[q] = 0;
@@ -214,6 +219,9 @@ __global__ __launch_bounds__(kTile) void bin_part1_kernel(BfGeom g, const uint4*
             }
         }
         __syncthreads();
+        const uint64_t nx = tile0 + tile_keys;
+        if (nx + t < k1) N0 = digests[nx + t];
+        if (kpl == 2 && nx + kTile + t < k1) N1 = digests[nx + kTile + t];
         // B: tile-local run bases, global run bases; cursors advance past this tile
         const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
         const uint32_t ex = block_excl_scan(c, s_w, nullptr);
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(kTile) void bin_part2_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ cursor,
                                                           uint32_t* __restrict__ level2) {
     __shared__ uint32_t s_sbb[kMaxSup + 1];
-    __shared__ uint32_t s_cnt[kP2Bins], s_lbase[kP2Bins], s_gdst[kP2Bins];
+    __shared__ uint32_t s_cnt[kP2Bins], s_gdst[kP2Bins];   // s_cnt becomes the local run bases
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_first, s_last;
     __shared__ uint32_t s_sorted[kP2Probes];
@@ -264,7 +272,7 @@ __global__ __launch_bounds__(kTile) void bin_part2_kernel(const uint32_t* __rest
         const uint32_t r = t << rel_log2;
         s_sbb[t] = bases[r < nbins ? r : nbins];
     }
-    s_cnt[t] = 0;   // kP2Bins == kTile
+    if (t < kP2Bins) s_cnt[t] = 0;
     __syncthreads();
     if (t < 2) {   // superbin of p0 (lane 0) / of p1 - 1 (lane 1): last sb with s_sbb[sb] <= p
         const uint32_t p = t ? p1 - 1 : p0;
@@ -313,15 +321,15 @@ __global__ __launch_bounds__(kTile) void bin_part2_kernel(const uint32_t* __rest
     }
     __syncthreads();
     const uint32_t cnt = t < range ? s_cnt[t] : 0u;
-    const uint32_t ex = block_excl_scan(cnt, s_w, nullptr);
-    s_lbase[t] = ex;
+    const uint32_t ex = block_excl_scan(cnt, s_w, nullptr);   // its barriers order the s_cnt reads first
+    if (t < kP2Bins) s_cnt[t] = ex;
     if (cnt) s_gdst[t] = atomicAdd(cursor + rfirst + t, cnt);
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < kP2PerLane; ++c) {
         if (tag[c] != 0xFFFFFFFFu) {
             const uint32_t lr = tag[c] >> 16;
-            const uint32_t d = s_lbase[lr] + (tag[c] & 0xFFFFu);
+            const uint32_t d = s_cnt[lr] + (tag[c] & 0xFFFFu);
             s_sorted[d] = loc[c] & rmask;
             s_lr[d] = (uint16_t)lr;
         }
@@ -329,7 +337,7 @@ __global__ __launch_bounds__(kTile) void bin_part2_kernel(const uint32_t* __rest
     __syncthreads();
     for (uint32_t j = t; j < p1 - p0; j += kTile) {
         const uint32_t lr = s_lr[j];
-        level2[s_gdst[lr] + (j - s_lbase[lr])] = s_sorted[j];
+        level2[s_gdst[lr] + (j - s_cnt[lr])] = s_sorted[j];
     }
 }
 
@@ -346,10 +354,24 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
     const uint32_t r = blockIdx.x;
+    const uint64_t v0 = (uint64_t)r * kVec;
+    const uint64_t nvec = nwords / 4;
+    uint4* gv = reinterpret_cast<uint4*>(bits);
+    const uint32_t pb = bases[r], p1 = bases[r + 1];
+    // Dense region (at least one probe per 16-B vector on average; most vectors are
+    // touched): its bitset vectors are loaded first, so that read overlaps the probe
+    // pass.  Sparse region: only the touched vectors are read, after the probe pass.
+    const bool dense = p1 - pb >= kVec;   // workgroup-uniform
+    uint4 old[kPer];
+#pragma unroll
+    for (uint32_t c = 0; c < kPer; ++c) {
+        const uint32_t v = c * LANES + t;
+        old[c] = make_uint4(0, 0, 0, 0);
+        if (dense && v0 + v < nvec) old[c] = gv[v0 + v];
+    }
     for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    const uint32_t p1 = bases[r + 1];
-    for (uint32_t p = bases[r] + t; p < p1; p += kLoads * LANES) {   // kLoads loads in flight per lane
+    for (uint32_t p = pb + t; p < p1; p += kLoads * LANES) {   // kLoads loads in flight per lane
         uint32_t l[kLoads];
 #pragma unroll
         for (int c = 0; c < kLoads; ++c) l[c] = (p + c * LANES < p1) ? binned[p + c * LANES] : 0xFFFFFFFFu;
@@ -358,16 +380,12 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
             if (l[c] != 0xFFFFFFFFu) atomicOr(s_mask + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
     }
     __syncthreads();
-    const uint64_t v0 = (uint64_t)r * kVec;
-    const uint64_t nvec = nwords / 4;
-    uint4* gv = reinterpret_cast<uint4*>(bits);
-    uint4 msk[kPer], old[kPer];
+    uint4 msk[kPer];
 #pragma unroll
-    for (uint32_t c = 0; c < kPer; ++c) {   // every touched vector's load issues before any store
+    for (uint32_t c = 0; c < kPer; ++c) {   // sparse: every touched vector's load issues before any store
         const uint32_t v = c * LANES + t;
         msk[c] = s_mask4[v];
-        old[c] = make_uint4(0, 0, 0, 0);
-        if (v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) old[c] = gv[v0 + v];
+        if (!dense && v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) old[c] = gv[v0 + v];
     }
     uint32_t fresh = 0;
 #pragma unroll
@@ -413,7 +431,7 @@ Carve carve(const BfBinPlan& p, uint64_t n, void* base) {
 }  // namespace
 
 bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kP1Slots || n == 0) return false;
+    if (k == 0 || k > (uint32_t)kP1Slots || n == 0) return false;   // k > 12: the direct insert
     const uint64_t bits = bitset_bytes * 8;
     const uint32_t order[2] = {pref_region_log2 == 20 ? 20u : 19u, pref_region_log2 == 20 ? 19u : 20u};
     for (uint32_t rl : order) {
@@ -427,7 +445,7 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
         plan->nsup = (uint32_t)((nbins + (1ull << rel) - 1) >> rel);
         const uint64_t per_block = 2ull * kTile * 16;   // >= 16 tiles per workgroup
         uint64_t blocks = (n + per_block - 1) / per_block;
-        if (blocks > kMaxBlocks) blocks = kMaxBlocks;    // one per CU (137 KiB of LDS each)
+        if (blocks > kMaxBlocks) blocks = kMaxBlocks;
         if (blocks == 0) blocks = 1;
         plan->nblocks = (uint32_t)blocks;
         plan->chunk = ((n + blocks - 1) / blocks + kTile - 1) / kTile * kTile;
@@ -441,26 +459,33 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
 
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
-                                   void* scratch, uint32_t* any_flag, hipStream_t s) {
+                                   void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
     if (n == 0) return hipSuccess;
     const Carve c = carve(p, n, scratch);
     const uint32_t P = (uint32_t)p.probes;
     hipLaunchKernelGGL(bin_count_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.chunk,
                        p.region_log2, p.nbins, p.rel_log2, p.nsup, c.counts, c.scnt, c.digests);
+    bf_mark(mk, s, "bin_count");
     hipLaunchKernelGGL(bin_colsum_kernel, dim3((p.nbins + 63) / 64), dim3(1024), 0, s, c.counts, p.nblocks, p.nbins,
                        c.totals);
-    hipLaunchKernelGGL(bin_supscan_kernel, dim3(p.nsup), dim3(256), 0, s, c.scnt, p.nblocks, p.nsup);
+    bf_mark(mk, s, "bin_colsum");
+    hipLaunchKernelGGL(bin_supscan_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.scnt, p.nblocks, p.nsup);
+    bf_mark(mk, s, "bin_supscan");
     hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, s, c.totals, p.nbins, c.bases, c.cursor);
+    bf_mark(mk, s, "bin_scan");
     hipLaunchKernelGGL(bin_part1_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, c.digests, n, p.chunk,
                        p.region_log2 + p.rel_log2, p.rel_log2, p.nsup, p.nbins, c.scnt, c.bases, c.level1);
+    bf_mark(mk, s, "bin_part1");
     hipLaunchKernelGGL(bin_part2_kernel, dim3((P + kP2Probes - 1) / kP2Probes), dim3(kTile), 0, s, c.level1, P,
                        c.bases, p.nbins, p.nsup, p.region_log2, p.rel_log2, c.cursor, c.level2);
+    bf_mark(mk, s, "bin_part2");
     const uint64_t nwords = bitset_bytes / 4;
     if (p.region_log2 == 19)
-        hipLaunchKernelGGL((bin_apply_kernel<19, 512>), dim3(p.nbins), dim3(512), 0, s, g.bits, nwords, c.level2,
-                           c.bases, any_flag);
+        hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.bases, any_flag);
     else
-        hipLaunchKernelGGL((bin_apply_kernel<20, 1024>), dim3(p.nbins), dim3(1024), 0, s, g.bits, nwords, c.level2,
-                           c.bases, any_flag);
+        hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.bases, any_flag);
+    bf_mark(mk, s, "bin_apply");
     return hipGetLastError();
 }

@@ -18,7 +18,11 @@ struct BfGeom {
     uint32_t  first_round;  // include?: probes loaded before the first early-exit check (0 = all k)
     uint32_t  insert_test;  // insert: 1 = load the k words first, atomic-OR only the unset bits
     uint32_t  route32;      // BF_FLAG_ROUTE32: routed owner-local offsets are uint32
+    uint8_t*  dirty;        // nullable: one byte per 2^kDirtyShiftBits-bit block, set to 1 when an
+                            // insert may have changed the block (bf_track_dirty)
 };
+
+constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = 64 KiB of the Redis string
 
 enum BfOp : int {
     BF_OP_INDEXES      = 0,  // write the k offsets of each key (ruby.rb:41-55)
@@ -50,12 +54,39 @@ struct BfBinPlan {
     uint64_t probes;        // n * k (< 2^32)
     uint64_t scratch_bytes; // device scratch the launch needs
 };
+// Optional per-kernel timing: when a BfMarks is passed, a launcher records
+// marks->ev[i] after its i-th kernel (ev[0] before the first), named names[i].
+struct BfMarks {
+    static constexpr int kMax = 12;
+    hipEvent_t ev[kMax + 1];
+    const char* names[kMax];
+    int used;   // kernels marked
+};
+inline void bf_mark(BfMarks* mk, hipStream_t s, const char* name) {
+    if (!mk || mk->used >= BfMarks::kMax) return;
+    mk->names[mk->used] = name;
+    (void)hipEventRecord(mk->ev[++mk->used], s);
+}
 // false: the batch / filter shape is outside the binned path (k > 16, more than
 // 2^32 probes, or a bitset beyond 24576 regions of 2^20 bits).
 bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, BfBinPlan* plan);
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
-                                   void* scratch, uint32_t* any_flag, hipStream_t s);
+                                   void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
+
+// Exact sequential per-key results (bf_seq.hip): batches of at most
+// bf_seq_chunk_keys(k) keys, scratch of bf_seq_scratch_bytes(n, k).  Probe
+// indices i0 .. i0+k-1 (0 for the ruby driver, 1 for the Lua scripts).
+uint64_t bf_seq_chunk_keys(uint32_t k);
+uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t* slots);
+hipError_t bf_launch_seq_candidates(const BfGeom& g, uint32_t i0, const uint8_t* keys16, const uint64_t* offsets,
+                                    uint64_t bias, uint64_t n, void* scratch, hipStream_t s);
+// new(j) -> out8 / any_flag (nullable) for j < n; ORs the 0-probes of keys j < limit into g.bits.
+hipError_t bf_launch_seq_mark(const BfGeom& g, uint32_t i0, uint64_t n, uint64_t limit, void* scratch,
+                              uint8_t* out8, uint32_t* any_flag, hipStream_t s);
+hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets, uint64_t bias,
+                                uint64_t n, void* scratch, uint8_t* out8, uint32_t* any_flag, hipStream_t s,
+                                BfMarks* marks = nullptr);
 
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
 // pairs by owner into send[], writes each probe's position into slot[].

@@ -1,0 +1,182 @@
+// bf_seq.hip — exact sequential per-key results for a batch insert.
+//
+// The ruby driver inserts one key per call: SETBIT k times, found = every old
+// bit was 1 (ruby.rb:57-61).  Run over a batch in order, key j is "new" iff one
+// of its bits was 0 before the batch AND no earlier key of the batch set it.
+// With first(b) = the smallest batch index whose probes include bit b:
+//
+//     new(j)  <=>  exists probe b of j:  prebit(b) == 0  and  first(b) == j
+//
+// (first(b) <= j always holds for j's own probes).  Two kernels per chunk:
+//   1. seq_candidates: hash (shared SHA-1 / ruby.rb:41-55 derivation), test every
+//      probe against the pre-batch bitset; for each 0 bit record the min index in
+//      a global open-addressing table keyed by bit offset (atomicCAS claim +
+//      atomicMin); keep the digest and the key's mask of 0-probes;
+//   2. seq_mark: new(j) from the table, then OR the 0-probes of keys j < limit in.
+// Chunks run in stream order, so chunk c+1 tests against chunk c's bits: the
+// result is that of inserting every key one by one.  "Found before its own
+// insert" — what bf_10_000.rb and the spec's test_error_rate compare include?
+// against — is !new(j).  The probe indices are i0 .. i0+k-1: 0-based for the
+// ruby driver (ruby.rb:50), 1-based for the Lua scripts (add.lua:37).
+#include "bf_device.h"
+
+using namespace bfdev;
+
+namespace {
+
+constexpr int kSeqTile = 256;
+constexpr int kSeqStageVec = 16384 / 16;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {   // SplitMix64 finalizer
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+__global__ __launch_bounds__(kSeqTile) void seq_candidates_kernel(BfGeom g, uint32_t i0,
+                                                                  const uint8_t* __restrict__ keys16,
+                                                                  const uint64_t* __restrict__ offsets, uint64_t bias,
+                                                                  uint64_t n, unsigned long long* __restrict__ tkeys,
+                                                                  uint32_t* __restrict__ tvals, uint64_t tmask,
+                                                                  uint4* __restrict__ digests,
+                                                                  unsigned long long* __restrict__ cand) {
+    __shared__ uint64_t s_off[kSeqTile + 1];
+    __shared__ uint4 s_stage[kSeqStageVec + kStageSlackVec];
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kSeqTile;
+    const uint32_t cnt = (uint32_t)((n - tile0) < (uint64_t)kSeqTile ? (n - tile0) : kSeqTile);
+    for_key_tile<kSeqTile, kSeqStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage,
+        [&](auto staged, uint32_t lane, const uint32_t* src, uint32_t s, uint32_t L) {
+            uint32_t H[5];
+            sha1_any<decltype(staged)::value>(src, s, L, H);
+            const uint32_t j = (uint32_t)(tile0 + lane);
+            digests[j] = make_uint4(H[0], H[1], H[2], H[3]);
+            unsigned long long cm = 0;
+            for (uint32_t i = 0; i < g.k; ++i) {
+                const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + i);
+                if ((g.bits[o >> 5] >> ((uint32_t)(o ^ 7u) & 31u)) & 1u) continue;
+                cm |= 1ull << i;
+                const unsigned long long key = o + 1;   // 0 marks an empty slot
+                uint64_t slot = mix64(o) & tmask;
+                for (;;) {   // the table holds <= half its slots: a free or matching slot exists
+                    const unsigned long long cur = atomicCAS(tkeys + slot, 0ull, key);
+                    if (cur == 0ull || cur == key) {
+                        atomicMin(tvals + slot, j);
+                        break;
+                    }
+                    slot = (slot + 1) & tmask;
+                }
+            }
+            cand[j] = cm;
+        });
+}
+
+// out8 / any_flag (nullable) get new(j) for j < n; the 0-probes of keys j < limit are ORed in.
+__global__ __launch_bounds__(256) void seq_mark_kernel(BfGeom g, uint32_t i0, uint64_t n, uint64_t limit,
+                                                       const unsigned long long* __restrict__ tkeys,
+                                                       const uint32_t* __restrict__ tvals, uint64_t tmask,
+                                                       const uint4* __restrict__ digests,
+                                                       const unsigned long long* __restrict__ cand,
+                                                       uint8_t* __restrict__ out8, uint32_t* __restrict__ any_flag) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t isnew = 0;
+    if (j < n) {
+        unsigned long long cm = cand[j];
+        if (cm) {
+            const uint4 H = digests[j];
+            while (cm) {
+                const uint32_t i = (uint32_t)__builtin_ctzll(cm);
+                cm &= cm - 1;
+                const uint64_t o = probe_offset(g, H.x, H.y, H.z, H.w, i0 + i);
+                const unsigned long long key = o + 1;
+                uint64_t slot = mix64(o) & tmask;
+                while (tkeys[slot] != key) slot = (slot + 1) & tmask;   // inserted by seq_candidates
+                isnew |= tvals[slot] == (uint32_t)j ? 1u : 0u;
+                if (j < limit) {
+                    __hip_atomic_fetch_or(g.bits + (o >> 5), 1u << ((uint32_t)(o ^ 7u) & 31u), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    if (g.dirty) g.dirty[o >> kDirtyShiftBits] = 1;
+                }
+            }
+        }
+        if (out8) out8[j] = (uint8_t)isnew;
+    }
+    if (any_flag) {
+        const unsigned long long b = __ballot(isnew != 0 && j < limit);
+        if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
+            __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
+
+struct SeqCarve {
+    unsigned long long* tkeys;
+    uint32_t* tvals;
+    uint4* digests;
+    unsigned long long* cand;
+    uint64_t slots;
+};
+
+SeqCarve seq_carve(void* scratch, uint64_t n, uint32_t k) {
+    SeqCarve c{};
+    (void)bf_seq_scratch_bytes(n, k, &c.slots);
+    uint8_t* at = static_cast<uint8_t*>(scratch);
+    c.tkeys = reinterpret_cast<unsigned long long*>(at);
+    at += align256(c.slots * 8);
+    c.tvals = reinterpret_cast<uint32_t*>(at);
+    at += align256(c.slots * 4);
+    c.digests = reinterpret_cast<uint4*>(at);
+    at += align256(n * 16);
+    c.cand = reinterpret_cast<unsigned long long*>(at);
+    return c;
+}
+
+}  // namespace
+
+uint64_t bf_seq_chunk_keys(uint32_t k) {
+    const uint64_t c = (1ull << 25) / (k ? k : 1);   // table <= 2^26 slots (768 MiB)
+    return c < (1ull << 22) ? (c ? c : 1) : (1ull << 22);
+}
+
+uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t* slots) {
+    uint64_t s = 1024;
+    while (s < 2 * n * (uint64_t)k) s <<= 1;
+    if (slots) *slots = s;
+    return align256(s * 8) + align256(s * 4) + align256(n * 16) + align256(n * 8);
+}
+
+hipError_t bf_launch_seq_candidates(const BfGeom& g, uint32_t i0, const uint8_t* keys16, const uint64_t* offsets,
+                                    uint64_t bias, uint64_t n, void* scratch, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const SeqCarve c = seq_carve(scratch, n, g.k);
+    hipError_t e;
+    if ((e = hipMemsetAsync(c.tkeys, 0, c.slots * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(c.tvals, 0xFF, c.slots * 4, s)) != hipSuccess) return e;
+    const uint32_t blocks = (uint32_t)((n + kSeqTile - 1) / kSeqTile);
+    hipLaunchKernelGGL(seq_candidates_kernel, dim3(blocks), dim3(kSeqTile), 0, s, g, i0, keys16, offsets, bias, n,
+                       c.tkeys, c.tvals, c.slots - 1, c.digests, c.cand);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_seq_mark(const BfGeom& g, uint32_t i0, uint64_t n, uint64_t limit, void* scratch, uint8_t* out8,
+                              uint32_t* any_flag, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const SeqCarve c = seq_carve(scratch, n, g.k);
+    hipLaunchKernelGGL(seq_mark_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, g, i0, n, limit,
+                       c.tkeys, c.tvals, c.slots - 1, c.digests, c.cand, out8, any_flag);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets, uint64_t bias,
+                                uint64_t n, void* scratch, uint8_t* out8, uint32_t* any_flag, hipStream_t s,
+                                BfMarks* mk) {
+    hipError_t e = bf_launch_seq_candidates(g, 0, keys16, offsets, bias, n, scratch, s);
+    if (e != hipSuccess) return e;
+    bf_mark(mk, s, "seq_candidates");
+    e = bf_launch_seq_mark(g, 0, n, n, scratch, out8, any_flag, s);
+    bf_mark(mk, s, "seq_mark");
+    return e;
+}

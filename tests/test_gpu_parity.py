@@ -169,13 +169,63 @@ def test_any_new_and_per_key(pkg, oracle):
         assert any_new is True and pk.all()
         any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
         assert any_new is False and not pk.any()
-    with pkg.Filter(9585, 6) as f:           # dense: aggregate flag is order independent
+    with pkg.Filter(9585, 6) as f:           # dense: per-key flags follow the keys' order exactly
         b, o = pkg.keys.pack([str(i) for i in range(3000)])
         any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
         bits = oracle.new_bitset(9585, 6)
         seq_any, seq_pk = oracle.insert_many(bits, 9585, 6, b, o, per_key=True)
         assert any_new == seq_any
-        assert pk.sum() >= 1   # per-key flags are arrival-order dependent; only the aggregate is pinned
+        np.testing.assert_array_equal(pk, seq_pk)
+        assert f.export_redis() == oracle.redis_string(bits)
+
+
+@pytest.mark.parametrize("m,k,n,chunk", [(9585, 6, 5000, 0), (95851, 7, 40_000, 0), (95851, 7, 40_000, 997),
+                                         (2**32 + 17, 13, 20_000, 0), (9585058377, 6, 100_000, 0),
+                                         (1000, 64, 300, 0)])
+def test_per_key_new_is_sequential(pkg, oracle, m, k, n, chunk):
+    """per_key_new[j] == 1 iff inserting the batch key by key (ruby.rb:57-61), key j flipped a
+    bit: exact against the oracle's sequential loop, with repeated keys, dense filters
+    (many keys sharing bits within the batch), host chunks (batch_keys) and a prefilled filter."""
+    rng = np.random.default_rng(RNG_SEED + 9)
+    vals = rng.integers(0, n // 2, size=n)                 # ~half the batch repeats earlier keys
+    b, o = pkg.keys.pack_decimal(vals)
+    pre_b, pre_o = pkg.keys.pack_decimal(rng.integers(10**6, 2 * 10**6, size=n // 4))
+    bits = oracle.new_bitset(m, k)
+    oracle.insert_many(bits, m, k, pre_b, pre_o)
+    want_any, want_pk = oracle.insert_many(bits, m, k, b, o, per_key=True)
+    with pkg.Filter(m, k, batch_keys=chunk) as f:
+        f.insert_many(pre_b, pre_o)
+        any_new, pk = f.insert_many(b, o, any_new=True, per_key_new=True)
+        np.testing.assert_array_equal(pk, want_pk)
+        assert any_new == bool(want_any)
+        assert f.export_redis() == oracle.redis_string(bits)
+
+
+def test_spec_error_rate_as_one_batch(pkg, oracle):
+    """spec/redis_bloomfilter_spec.rb:7-17 (test_error_rate) and bf_10_000.rb:34-43 ask include?
+    before each insert; found-before-insert is !per_key_new, so one batched call reproduces the
+    per-key loop's error count exactly."""
+    rng = np.random.default_rng(RNG_SEED + 10)
+    elems = 180
+    vals = rng.integers(0, elems, size=elems)
+    b, o = pkg.keys.pack_decimal(vals)
+    m = pkg.Bloomfilter.optimal_m(100, 0.02)
+    k = pkg.Bloomfilter.optimal_k(100, m)
+    with pkg.Filter(m, k) as f:
+        _, pk = f.insert_many(b, o, per_key_new=True)
+    found = pk == 0
+    bits = oracle.new_bitset(m, k)
+    visited, errors, want_errors = set(), 0, 0
+    for j, v in enumerate(vals.tolist()):
+        kb, ko = pkg.keys.pack([v])
+        seq_found = bool(oracle.include_many(bits, m, k, kb, ko)[0])
+        oracle.insert_many(bits, m, k, kb, ko)
+        assert found[j] == seq_found
+        errors += found[j] != (v in visited)
+        want_errors += seq_found != (v in visited)
+        visited.add(v)
+    assert errors == want_errors
+    assert round(errors / elems, 2) <= 0.02                # spec:104
 
 
 def test_import_export(pkg, oracle):
@@ -252,13 +302,13 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
 
 
 @pytest.mark.parametrize("rl", ["19", "20"])
-@pytest.mark.parametrize("case", ["dup", "tiny", "long", "k16", "nstar"])
+@pytest.mark.parametrize("case", ["dup", "tiny", "long", "k12", "nstar"])
 def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     """Forced binned insert on shapes that stress its partition passes: one key repeated
     (every probe in <= k regions, one superbin run per tile holding thousands of probes),
     a few keys over the 1.2 GB north-star filter (a level-2 chunk spanning every superbin:
     the per-probe cursor path), keys past the single-block SHA-1 (multi-block hash in the
-    count pass), k = 16 (one key per lane in the level-1 pass), and a 200k-key batch on the
+    count pass), k = 12 (the largest k the binned path takes: one key per lane, every probe slot used), and a 200k-key batch on the
     north-star filter; both region sizes (64 KiB / 128 KiB LDS images)."""
     monkeypatch.setenv("BFHIP_INSERT_BINNED", "1")
     monkeypatch.setenv("BFHIP_BIN_REGION_LOG2", rl)
@@ -272,8 +322,8 @@ def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     elif case == "long":
         m, k = 1437758757, 6
         ins = rand_keys(rng, 20_000, 56, 300)
-    elif case == "k16":
-        m, k = 2**32 + 17, 16
+    elif case == "k12":
+        m, k = 2**32 + 17, 12
         ins = rand_keys(rng, 30_000, 0, 24)
     else:
         m, k = 9585058377, 6

@@ -4,7 +4,7 @@
 # per pass), kernel trace kept separate; outputs under gpurun_out/pmc_<tag>/.
 # Summarise with: python tools/pmc_summary.py gpurun_out/pmc_* > profiles/...
 export TMPDIR=/tmp
-CMD="python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline"
+CMD="python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api"
 run() {   # tag, counters...
     local tag=$1; shift
     timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_${tag} -o run -- $CMD \

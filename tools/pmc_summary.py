@@ -3,12 +3,13 @@
 
     python tools/pmc_summary.py gpurun_out/pmc_* [--batch 16777216] [--json out.json]
 
-Keeps only the bench's timed launches (Grid_Size == batch) of the insert
-(bf_keys_kernel<2|3>) and include? (bf_keys_kernel<1>) kernels, averages each
-counter per launch, and derives HBM bytes per launch the way rocprofv3's own
-FETCH_SIZE / WRITE_SIZE expressions do (read requests weighted 32/64/128 B by
-TCC_EA0_RDREQ_32B / TCC_BUBBLE; write requests 32/64 B by TCC_EA0_WRREQ_64B).
-Atomic requests (TCC_EA0_ATOMIC) are reported separately, as 64 B each.
+Keeps the bench's launches of the hot kernels — the direct include? / insert
+kernels (bf_keys_kernel<1|2|3>, only launches over a full batch: Grid_Size ==
+batch) and the binned insert pipeline's kernels — averages each counter per
+launch, and derives HBM bytes per launch with the gfx950 correction (read
+requests weighted 128/64/32 B by TCC_EA0_RDREQ_128B / _64B / _32B; write
+requests 64/32 B by TCC_EA0_WRREQ_64B).  Keys of the output are the kernel
+names bench.py's bf_profile timing uses.
 """
 import argparse
 import collections
@@ -18,7 +19,16 @@ import json
 import os
 import re
 
-KERNELS = {"include": re.compile(r"bf_keys_kernel<1>"), "insert": re.compile(r"bf_keys_kernel<[23]>")}
+KERNELS = {
+    "bf_keys_kernel<INCLUDE>": re.compile(r"bf_keys_kernel<1>"),
+    "bf_keys_kernel<INSERT>": re.compile(r"bf_keys_kernel<2>"),
+    "bf_keys_kernel<INSERT_FLAGS>": re.compile(r"bf_keys_kernel<3>"),
+    "bin_count": re.compile(r"bin_count_kernel"),
+    "bin_part1": re.compile(r"bin_part1_kernel"),
+    "bin_part2": re.compile(r"bin_part2_kernel"),
+    "bin_apply": re.compile(r"bin_apply_kernel"),
+}
+FULL_BATCH = ("bf_keys_kernel",)   # grid = one lane per key: keep full-batch launches only
 
 
 def load(dirs, batch):
@@ -28,10 +38,10 @@ def load(dirs, batch):
         for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             seen = set()
             for r in csv.DictReader(open(path)):
-                if int(r["Grid_Size"]) != batch:
-                    continue
                 for name, rx in KERNELS.items():
                     if rx.search(r["Kernel_Name"]):
+                        if name.startswith(FULL_BATCH) and int(r["Grid_Size"]) != batch:
+                            continue
                         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
                         key = (path, r["Dispatch_Id"])
                         if key not in seen:
@@ -80,6 +90,7 @@ def main():
         d["launches_counted"] = max(len(v) for v in acc[name].values())
         d["profiled_ms_mean"] = sum(dur[name]) / len(dur[name]) if dur[name] else None
         d["keys_per_launch"] = args.batch
+        d["hbm_bytes_per_launch"] = d.get("hbm_bytes")
         if d.get("hbm_bytes"):
             d["hbm_bytes_per_key"] = d["hbm_bytes"] / args.batch
             if d.get("profiled_ms_mean"):
