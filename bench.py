@@ -220,6 +220,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     kernels = {name: {"ms": tot / cnt, "launches": cnt} for name, (tot, cnt) in prof.profile_read(reset=True).items()}
     prof.profile(False)
     plan = f.insert_plan(batch) if pf is None else {"binned": False, "scratch_bytes": 0}
+    inc_binned = "bin_test" in kernels
     # sanity: the members (first half of the include? batch) must all be found
     got = out.cpu().numpy()
     assert got[: batch // 2].all(), "false negative in the include? batch"
@@ -233,10 +234,12 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         "bf_keys_kernel<INCLUDE>": batch * (Lmean + 8 + 1 + k * GRANULE),
         "bf_keys_kernel<INSERT>": batch * (Lmean + 8 + 2 * k * GRANULE),
         "bf_keys_kernel<INSERT_FLAGS>": batch * (Lmean + 8 + 2 * k * GRANULE + 1),
-        "bin_count": batch * (Lmean + 8 + 16),
-        "bin_part1": batch * 16 + P * 4,
-        "bin_part2": P * 8,
+        # binned path (bf_binned.hip): keys in, probe arrays written / read once, the bitset
+        # streamed once (read + write for insert, read for include?)
+        "bin_front": batch * (Lmean + 8) + P * 4 * (2 if inc_binned else 1) + (batch if inc_binned else 0),
+        "bin_mid": P * 4 * 3 + (P * 4 * 2 if inc_binned else 0),
         "bin_apply": P * 4 + 2 * bitset,
+        "bin_test": P * 8 + bitset,
     }
     for name, kt in kernels.items():
         if name in algo:
@@ -251,7 +254,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
                    "algo_bytes_per_key": (Lmean + 8 + 2 * bitset / batch) if plan["binned"]
                    else (Lmean + 8 + 2 * k * GRANULE)},
         "include": {"op_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
-                    "algo_bytes_per_key": Lmean + 8 + 1 + k * GRANULE,
+                    "path": "binned" if inc_binned else "direct",
+                    "algo_bytes_per_key": (Lmean + 8 + 1 + bitset / batch) if inc_binned
+                    else (Lmean + 8 + 1 + k * GRANULE),
                     "observed_fp_rate": fp_rate},
         "kernels": kernels,
         "bitset_bytes": bitset,

@@ -58,6 +58,7 @@ struct bf_handle {
     unsigned long long* d_cursor = nullptr;
     // binned-insert scratch (grown on demand) and policy: 0 never, 1 always, 2 auto
     uint32_t binned_mode = 2;
+    uint32_t include_binned_mode = 2;   // the same policy for include?
     uint32_t bin_region_log2 = 19;   // preferred region (LDS image) size of the apply pass
     void* d_bin_scratch = nullptr;   // digests, probe arrays and histograms of one binned launch
     uint64_t bin_scratch_cap = 0;
@@ -119,6 +120,10 @@ uint32_t default_first_round(uint32_t k) { return (k + 3) / 4; }
 constexpr uint32_t kDefaultInsertTest = 1;
 constexpr uint32_t kDefaultMemKind = 0;
 constexpr uint32_t kDefaultBinnedMode = 2;     // auto
+// include? stays on the direct kernel by default: at 1B@1% (2^24 keys) the binned
+// include? measured 1.92 ms against 1.48 ms direct (hash 0.76 + partition 0.43 +
+// region test 0.69); BFHIP_INCLUDE_BINNED=1/2 turns it on.
+constexpr uint32_t kDefaultIncludeBinnedMode = 0;
 constexpr uint32_t kDefaultBinRegionLog2 = 19; // 64 KiB LDS image per apply workgroup
 constexpr double kBinnedCostRatio = 3.0;       // random line-fill bytes vs bitset bytes
 
@@ -182,12 +187,13 @@ int check_keys_args(bf_handle* h, const void* keys, const uint64_t* offsets, uin
     return BF_OK;
 }
 
-// Binned insert: worth it when the batch's random line fills (~128 B per probe)
-// clearly exceed one streaming pass over a bitset that lives beyond L2.
-bool use_binned(const bf_handle* h, uint64_t n, bool per_key, BfBinPlan* plan) {
-    if (per_key || h->binned_mode == 0 || h->shards > 1) return false;
-    if (!bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, plan)) return false;
-    if (h->binned_mode == 1) return true;
+// Binned insert / include?: worth it when the batch's random line fills (~128 B
+// per probe) clearly exceed one streaming pass over a bitset that lives beyond L2.
+bool use_binned(const bf_handle* h, uint64_t n, bool include, BfBinPlan* plan) {
+    const uint32_t mode = include ? h->include_binned_mode : h->binned_mode;
+    if (mode == 0 || h->shards > 1) return false;
+    if (!bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, include, plan)) return false;
+    if (mode == 1) return true;
     return h->dev_bytes >= (64ull << 20) &&
            (double)n * (double)h->k * 128.0 > kBinnedCostRatio * (double)h->dev_bytes;
 }
@@ -267,13 +273,25 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
         }
         return BF_OK;
     }
+    // Binned insert / include?, in sub-batches of at most bf_binned_max_keys keys.
+    const bool is_insert = op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS;
     BfBinPlan plan;
-    if ((op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS) && use_binned(h, n, out8 != nullptr, &plan)) {
-        int rc = ensure_scratch(h, plan.scratch_bytes);
-        if (rc) return rc;
-        BfMarks* mk = prof_begin(h, s);
-        HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs, bias, n, h->d_bin_scratch,
-                                          op == BF_OP_INSERT_FLAGS ? flag : nullptr, s, mk));
+    const uint64_t sub = bf_binned_max_keys(h->k);
+    if ((is_insert || op == BF_OP_INCLUDE) && use_binned(h, std::min(n, sub), !is_insert, &plan)) {
+        for (uint64_t c0 = 0; c0 < n; c0 += sub) {
+            const uint64_t cn = std::min(sub, n - c0);
+            if (cn != std::min(n, sub) && !bf_binned_plan(h->dev_bytes, cn, h->k, h->bin_region_log2, !is_insert, &plan))
+                return set_err(h, BF_EINVAL, "binned plan failed for a tail of %llu keys", (unsigned long long)cn);
+            int rc = ensure_scratch(h, plan.scratch_bytes);
+            if (rc) return rc;
+            BfMarks* mk = prof_begin(h, s);
+            if (is_insert)
+                HIPCHK(h, bf_launch_insert_binned(h->g, plan, h->dev_bytes, k16, offs + c0, bias, cn, h->d_bin_scratch,
+                                                  op == BF_OP_INSERT_FLAGS ? flag : nullptr, s, mk));
+            else
+                HIPCHK(h, bf_launch_include_binned(h->g, plan, h->dev_bytes, k16, offs + c0, bias, cn,
+                                                   h->d_bin_scratch, out8 + c0, s, mk));
+        }
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
@@ -513,6 +531,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);
+    h->include_binned_mode = env_u32("BFHIP_INCLUDE_BINNED", kDefaultIncludeBinnedMode);
     *out = h;
     return BF_OK;
 }

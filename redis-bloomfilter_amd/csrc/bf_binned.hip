@@ -1,50 +1,56 @@
-// bf_binned.hip — binned ("sweep") insert for filters far larger than L2.
+// bf_binned.hip — binned ("sweep") insert and include? for filters far larger than L2.
 //
-// The direct insert (bf_kernels.hip) costs every probe a random 128-B DRAM
-// line fill (test) and, for bits still 0, a memory-side atomic.  When a batch
-// carries many probes per filter line that is far more traffic than streaming
-// the filter once.  This path sorts the batch's probes by filter region with
-// two LDS-sorted partition passes whose global writes are coalesced runs, then
-// ORs each region in LDS and streams it once:
+// The direct kernels (bf_kernels.hip) cost every probe a random 128-B DRAM
+// line fill (plus, for insert, a memory-side atomic per bit still 0).  When a
+// batch carries many probes per filter line, streaming the filter once is far
+// cheaper.  This path sorts the batch's probes by filter region and then walks
+// the filter region by region, each region held in LDS:
 //
-//   1. bin_count    hashes every key (ruby.rb:41-55 derivation, shared with the
-//                   direct kernels), stores its 4 digest words (16 B/key) and
-//                   histograms its probes by 2^rl-bit region in LDS.  Workgroup
-//                   w owns a fixed key range; it writes its region counts and
-//                   its superbin counts (superbin = 2^rel consecutive regions).
-//   2. bin_colsum   region totals (column sums over the workgroups);
-//      bin_supscan  per superbin, the exclusive prefix over workgroups (each
-//                   workgroup's exact write window inside the superbin);
-//      bin_scan     region bases (exclusive prefix of the totals) + cursors.
-//   3. bin_part1    re-derives the probes from the digests, tile by tile; per
-//                   tile an LDS counting sort by superbin, then each superbin's
-//                   run is written contiguously (level-1 array, superbin-local
-//                   u32 offsets).
-//   4. bin_part2    per 8192-probe chunk of the level-1 array: LDS counting sort
-//                   by region, one returning atomic per (chunk, region) reserves
-//                   the run, coalesced writes (level-2 array, region-local u32).
-//   5. bin_apply    one workgroup per region ORs its probes into an LDS image of
-//                   the region (LDS atomics), then read-OR-writes the region's
-//                   touched 16-B vectors of the bitset — plain stores, since no
-//                   other workgroup owns that region.
-// Result: the same bitset as atomic OR (OR is idempotent and commutative).
+//   1. bin_front    hashes every key (ruby.rb:41-55 derivation, shared with the
+//                   direct kernels) and, per tile of 1024-2048 keys, counting-
+//                   sorts the tile's probes by superbin (2^rel consecutive
+//                   regions) in LDS.  The sorted tile is written contiguously at
+//                   its fixed place (tile * keys * k), with a table of its
+//                   superbin run boundaries; each workgroup also totals its
+//                   probes per superbin.  include? carries each probe's key
+//                   index and presets the answers to 1.
+//   2. bin_group_sum / bin_group_scan: superbin totals per group of 64
+//                   front workgroups; the exclusive prefix over (superbin,
+//                   group) gives each group's window in the level-2 array, cut
+//                   into chunk blocks of 8192 probes.
+//   3. bin_mid      one workgroup per chunk block gathers its probes from the
+//                   superbin's runs in the group's tiles, counting-sorts them by
+//                   region in LDS and writes the block contiguously (region-local
+//                   offsets) with its table of region boundaries.
+//   4. bin_apply    (insert) one workgroup per region gathers the region's run
+//                   from every chunk block of its superbin, ORs the probes into
+//                   an LDS image of the region, then read-OR-writes the touched
+//                   16-B vectors of the bitset — plain stores: no other
+//                   workgroup owns the region.
+//      bin_test     (include?) loads the region into LDS and clears the answer
+//                   of every key with a probe on a 0 bit.
+// The insert result equals atomic OR (idempotent, commutative); the include?
+// answer is the AND of the key's k bits (ruby.rb:20-30) without the early exit.
 #include "bf_device.h"
 
 using namespace bfdev;
 
 namespace {
 
-constexpr int kTile = 1024;                   // lanes of the count / partition workgroups
-constexpr int kTileStageVec = 32768 / 16;     // 32 KiB LDS key stage (count pass)
-constexpr uint32_t kMaxBins = 24576;          // region histogram capacity (96 KiB)
-constexpr uint32_t kMaxSup = 256;             // superbins (u8 tags in part1)
-constexpr uint32_t kMaxBlocks = 512;          // count / part1 workgroups (two per CU)
-constexpr uint32_t kP1Probes = 12288;         // probes per part1 tile (64 KiB of LDS: two workgroups per CU)
-constexpr int kP1Slots = 12;                  // probes per lane per part1 tile (k <= 12)
-constexpr uint32_t kP1TwoKeys = 6;            // k <= 6: two keys per lane per tile
-constexpr uint32_t kP2Probes = 8192;          // probes per part2 workgroup
-constexpr int kP2PerLane = kP2Probes / kTile;
-constexpr uint32_t kP2Bins = 512;             // local region bins per part2 workgroup (52 KiB: three per CU)
+constexpr int kTile = 1024;                   // lanes per workgroup of the front / mid passes
+constexpr int kStageVec = 16384 / 16;         // 16 KiB LDS key stage per 1024-key sub-tile
+constexpr uint32_t kMaxSup = 256;             // superbins (8-bit superbin in the sort tags)
+constexpr uint32_t kMaxRel = 8;               // <= 256 regions per superbin
+constexpr uint32_t kMaxBlocks = 512;          // front workgroups
+constexpr uint32_t kGroupBlocks = 64;         // front workgroups per group (one wave in bin_group_sum)
+constexpr uint32_t kTileProbes = 12288;       // probes per front tile (LDS sort buffer)
+constexpr int kSlots = 12;                    // probes per lane per tile (k <= 12)
+constexpr uint32_t kTwoKeys = 6;              // k <= 6: two keys per lane per tile
+constexpr uint32_t kMaxTilesPerBlock = 16;    // <= 1024 tiles per group: one run-table pass in bin_mid
+constexpr uint32_t kBlockProbes = 8192;       // probes per level-2 chunk block (one bin_mid workgroup)
+constexpr int kChunkPerLane = kBlockProbes / kTile;
+constexpr uint32_t kRunsPerPass = 1024;       // run-table entries per gather pass (one lane each)
+constexpr uint32_t kMidParts = 2;             // bin_mid workgroups per level-2 window
 constexpr uint32_t kApplyLanes = 1024;
 
 // Exclusive prefix sum of v over the workgroup (blockDim.x a multiple of 64,
@@ -76,137 +82,63 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     return r;
 }
 
-__global__ __launch_bounds__(kTile) void bin_count_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+template <bool KEYS>
+__global__ __launch_bounds__(kTile) void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
                                                           const uint64_t* __restrict__ offsets, uint64_t bias,
-                                                          uint64_t n, uint64_t chunk, uint32_t region_log2,
-                                                          uint32_t nbins, uint32_t rel_log2, uint32_t nsup,
-                                                          uint32_t* __restrict__ counts, uint32_t* __restrict__ scnt,
-                                                          uint4* __restrict__ digests) {
-    __shared__ uint32_t s_hist[kMaxBins];
+                                                          uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
+                                                          uint32_t sup_log2, uint32_t nsup,
+                                                          uint32_t* __restrict__ level1,
+                                                          uint32_t* __restrict__ level1_key,
+                                                          uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt,
+                                                          uint8_t* __restrict__ out8) {
     __shared__ uint64_t s_off[kTile + 1];
-    __shared__ uint4 s_stage[kTileStageVec + kStageSlackVec];
-    const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < nbins; i += kTile) s_hist[i] = 0;
-    __syncthreads();
-    const uint64_t k0 = (uint64_t)blockIdx.x * chunk;
-    const uint64_t k1 = (k0 + chunk < n) ? k0 + chunk : n;
-    for (uint64_t tile0 = k0; tile0 < k1; tile0 += kTile) {
-        const uint32_t cnt = (uint32_t)((k1 - tile0) < (uint64_t)kTile ? (k1 - tile0) : kTile);
-        for_key_tile<kTile, kTileStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage,
-            [&](auto staged, uint32_t lane, const uint32_t* src, uint32_t s, uint32_t L) {
-                uint32_t H[5];
-                sha1_any<decltype(staged)::value>(src, s, L, H);
-                digests[tile0 + lane] = make_uint4(H[0], H[1], H[2], H[3]);   // for the partition pass
-                for (uint32_t i = 0; i < g.k; ++i)
-                    atomicAdd(s_hist + (uint32_t)(probe_offset(g, H[0], H[1], H[2], H[3], i) >> region_log2), 1u);
-            });
-    }
-    uint32_t* row = counts + (uint64_t)blockIdx.x * nbins;
-    for (uint32_t i = t; i < nbins; i += kTile) row[i] = s_hist[i];
-    for (uint32_t sb = t; sb < nsup; sb += kTile) {
-        const uint32_t r0 = sb << rel_log2;
-        const uint32_t r1 = (r0 + (1u << rel_log2) < nbins) ? r0 + (1u << rel_log2) : nbins;
-        uint32_t sum = 0;
-        for (uint32_t r = r0; r < r1; ++r) sum += s_hist[r];
-        scnt[(uint64_t)blockIdx.x * nsup + sb] = sum;
-    }
-}
-
-// totals[r] = sum over workgroups b of counts[b][r].  64 regions x 16 row groups per workgroup.
-__global__ __launch_bounds__(1024) void bin_colsum_kernel(const uint32_t* __restrict__ counts, uint32_t nblocks,
-                                                          uint32_t nbins, uint32_t* __restrict__ totals) {
-    __shared__ uint32_t s_part[16][64];
-    const uint32_t x = threadIdx.x & 63u, y = threadIdx.x >> 6;
-    const uint32_t r = blockIdx.x * 64 + x;
-    uint32_t sum = 0;
-    if (r < nbins) {
-#pragma unroll 8
-        for (uint32_t b = y; b < nblocks; b += 16) sum += counts[(uint64_t)b * nbins + r];
-    }
-    s_part[y][x] = sum;
-    __syncthreads();
-    if (y == 0 && r < nbins) {
-        uint32_t tot = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) tot += s_part[j][x];
-        totals[r] = tot;
-    }
-}
-
-// scnt[b][sb] -> exclusive prefix over b, in place.  One workgroup (kMaxBlocks lanes) per superbin.
-__global__ __launch_bounds__(kMaxBlocks) void bin_supscan_kernel(uint32_t* __restrict__ scnt, uint32_t nblocks,
-                                                          uint32_t nsup) {
+    __shared__ uint4 s_stage[kStageVec + kStageSlackVec];
+    __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
-    const uint32_t t = threadIdx.x, sb = blockIdx.x;
-    const uint32_t v = t < nblocks ? scnt[(uint64_t)t * nsup + sb] : 0u;
-    const uint32_t ex = block_excl_scan(v, s_w, nullptr);
-    if (t < nblocks) scnt[(uint64_t)t * nsup + sb] = ex;
-}
-
-// bases[r] = exclusive prefix of totals, bases[nbins] = total probes, cursor[r] = bases[r].
-// One workgroup; the totals pass through LDS so every global access is coalesced.
-__global__ __launch_bounds__(1024) void bin_scan_kernel(const uint32_t* __restrict__ totals, uint32_t nbins,
-                                                        uint32_t* __restrict__ bases, uint32_t* __restrict__ cursor) {
-    __shared__ uint32_t s_v[kMaxBins];
-    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_sorted[kTileProbes];
+    __shared__ uint32_t s_key[KEYS ? kTileProbes : 1];
     const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < nbins; i += 1024) s_v[i] = totals[i];
-    __syncthreads();
-    const uint32_t per = (nbins + 1023) / 1024;
-    const uint32_t b0 = t * per;
-    uint32_t sum = 0;
-    for (uint32_t i = 0; i < per; ++i)
-        if (b0 + i < nbins) sum += s_v[b0 + i];
-    uint32_t total;
-    uint32_t run = block_excl_scan(sum, s_w, &total);
-    for (uint32_t i = 0; i < per; ++i)
-        if (b0 + i < nbins) { const uint32_t c = s_v[b0 + i]; s_v[b0 + i] = run; run += c; }
-    __syncthreads();
-    for (uint32_t i = t; i < nbins; i += 1024) { bases[i] = s_v[i]; cursor[i] = s_v[i]; }
-    if (t == 0) bases[nbins] = total;
-}
-
-// Level 1: probes grouped by superbin.  Workgroup w walks the key range of the
-// count pass's workgroup w; its run inside superbin sb starts at
-// bases[sb << rel] + scnt[w][sb] and grows tile by tile.
-__global__ __launch_bounds__(kTile) void bin_part1_kernel(BfGeom g, const uint4* __restrict__ digests, uint64_t n,
-                                                          uint64_t chunk, uint32_t sup_log2, uint32_t rel_log2,
-                                                          uint32_t nsup, uint32_t nbins,
-                                                          const uint32_t* __restrict__ scnt,
-                                                          const uint32_t* __restrict__ bases,
-                                                          uint32_t* __restrict__ level1) {
-    __shared__ uint32_t s_cur[kMaxSup], s_cnt[kMaxSup], s_lbase[kMaxSup], s_gdst[kMaxSup];
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_sorted[kP1Probes];
-    __shared__ uint8_t s_sb[kP1Probes];
-    const uint32_t t = threadIdx.x;
-    if (t < nsup) {
-        const uint32_t r = t << rel_log2;
-        s_cur[t] = bases[r < nbins ? r : nbins] + scnt[(uint64_t)blockIdx.x * nsup + t];
+    if (t < kMaxSup) {
+        s_cnt[t] = 0;
+        s_gcnt[t] = 0;
     }
-    if (t < kMaxSup) s_cnt[t] = 0;
     __syncthreads();
     const uint32_t k = g.k;
-    const uint32_t kpl = k <= kP1TwoKeys ? 2u : 1u;   // keys per lane per tile
-    const uint32_t tile_keys = kTile * kpl;
+    const uint32_t kpl = tile_keys / kTile;   // 1 or 2 keys per lane
     const uint64_t smask = (1ull << sup_log2) - 1ull;
-    const uint64_t k0 = (uint64_t)blockIdx.x * chunk;
-    const uint64_t k1 = (k0 + chunk < n) ? k0 + chunk : n;
-    // digests of the next tile are loaded while the current one is sorted and written
-    uint4 N0 = make_uint4(0, 0, 0, 0), N1 = make_uint4(0, 0, 0, 0);
-    if (k0 + t < k1) N0 = digests[k0 + t];
-    if (kpl == 2 && k0 + kTile + t < k1) N1 = digests[k0 + kTile + t];
-    for (uint64_t tile0 = k0; tile0 < k1; tile0 += tile_keys) {
-        const uint32_t tk = (uint32_t)((k1 - tile0) < (uint64_t)tile_keys ? (k1 - tile0) : tile_keys);
-        // A: probes of this lane's keys -> (superbin, rank in the tile's superbin run)
+    const uint64_t ntiles = (n + tile_keys - 1) / tile_keys;
+    const uint64_t tb0 = (uint64_t)blockIdx.x * tiles_per_block;
+    const uint64_t tb1 = (tb0 + tiles_per_block < ntiles) ? tb0 + tiles_per_block : ntiles;
+    for (uint64_t tile = tb0; tile < tb1; ++tile) {
+        const uint64_t key0 = tile * tile_keys;
+        const uint32_t tk = (uint32_t)((n - key0) < (uint64_t)tile_keys ? (n - key0) : tile_keys);
+        uint4 H0 = make_uint4(0, 0, 0, 0), H1 = make_uint4(0, 0, 0, 0);
+        for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off, s_stage,
+            [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                uint32_t H[5];
+                sha1_any<decltype(staged)::value>(src, s, L, H);
+                H0 = make_uint4(H[0], H[1], H[2], H[3]);
+            });
+        if (tk > (uint32_t)kTile) {   // workgroup-uniform: the second key of each lane
+            for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0 + kTile, tk - kTile, s_off, s_stage,
+                [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                    uint32_t H[5];
+                    sha1_any<decltype(staged)::value>(src, s, L, H);
+                    H1 = make_uint4(H[0], H[1], H[2], H[3]);
+                });
+        }
         const bool live0 = t < tk;
         const bool live1 = kpl == 2 && kTile + t < tk;
-        const uint4 H0 = N0, H1 = N1;
-        uint32_t tag[kP1Slots], loc[kP1Slots];
+        if constexpr (KEYS) {   // include?: every answer starts true; bin_test clears it
+            if (live0) out8[key0 + t] = 1;
+            if (live1) out8[key0 + kTile + t] = 1;
+        }
+        // A: each probe -> (superbin, rank inside the tile's superbin run)
+        uint32_t tag[kSlots], loc[kSlots];
 #pragma unroll
-        for (int q = 0; q < kP1Slots; ++q) {
-            const bool second = kpl == 2 && q >= (int)kP1TwoKeys;
-            const uint32_t i = kpl == 2 ? (second ? (uint32_t)q - kP1TwoKeys : (uint32_t)q) : (uint32_t)q;
+        for (int q = 0; q < kSlots; ++q) {
+            const bool second = kpl == 2 && q >= (int)kTwoKeys;
+            const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
             const bool live = i < k && (second ? live1 : live0);
             tag[q] = 0xFFFFFFFFu;
             loc[q] = 0;
@@ -219,149 +151,293 @@ __global__ __launch_bounds__(kTile) void bin_part1_kernel(BfGeom g, const uint4*
             }
         }
         __syncthreads();
-        const uint64_t nx = tile0 + tile_keys;
-        if (nx + t < k1) N0 = digests[nx + t];
-        if (kpl == 2 && nx + kTile + t < k1) N1 = digests[nx + kTile + t];
-        // B: tile-local run bases, global run bases; cursors advance past this tile
+        // B: run boundaries of the tile (lane nsup writes the tile's probe count)
         const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
         const uint32_t ex = block_excl_scan(c, s_w, nullptr);
+        if (t <= nsup) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [superbin][tile]
         if (t < kMaxSup) {
             s_lbase[t] = ex;
-            if (c) { s_gdst[t] = s_cur[t]; s_cur[t] += c; }
+            s_gcnt[t] += c;
             s_cnt[t] = 0;
         }
         __syncthreads();
-        // C: counting-sort the tile in LDS
+        // C: counting sort in LDS
 #pragma unroll
-        for (int q = 0; q < kP1Slots; ++q) {
+        for (int q = 0; q < kSlots; ++q) {
             if (tag[q] != 0xFFFFFFFFu) {
-                const uint32_t sb = tag[q] >> 16;
-                const uint32_t d = s_lbase[sb] + (tag[q] & 0xFFFFu);
+                const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
                 s_sorted[d] = loc[q];
-                s_sb[d] = (uint8_t)sb;
+                if constexpr (KEYS) {
+                    const bool second = kpl == 2 && q >= (int)kTwoKeys;
+                    s_key[d] = (uint32_t)(key0 + (second ? kTile + t : t));
+                }
             }
         }
         __syncthreads();
-        // D: consecutive lanes write consecutive slots of each superbin run
+        // D: the sorted tile, contiguous at its fixed place
+        const uint64_t seg = key0 * k;
         const uint32_t tp = tk * k;
         for (uint32_t j = t; j < tp; j += kTile) {
-            const uint32_t sb = s_sb[j];
-            level1[s_gdst[sb] + (j - s_lbase[sb])] = s_sorted[j];
+            level1[seg + j] = s_sorted[j];
+            if constexpr (KEYS) level1_key[seg + j] = s_key[j];
+        }
+        // the next tile's first LDS writes (staging, then s_sorted) follow barriers
+    }
+    if (t < nsup) gcnt[(uint64_t)blockIdx.x * nsup + t] = s_gcnt[t];
+}
+
+// gsum[sb][q] = probes of superbin sb in the tiles of front workgroups [64q, 64q + 64).
+// One workgroup per superbin, one wave per group.
+__global__ __launch_bounds__(kMaxBlocks) void bin_group_sum_kernel(const uint32_t* __restrict__ gcnt,
+                                                                   uint32_t nblocks, uint32_t nsup, uint32_t nq,
+                                                                   uint32_t* __restrict__ gsum) {
+    const uint32_t w = threadIdx.x, sb = blockIdx.x;
+    uint32_t v = w < nblocks ? gcnt[(uint64_t)w * nsup + sb] : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    const uint32_t q = w / kGroupBlocks;
+    if ((w & 63u) == 0 && q < nq) gsum[sb * nq + q] = v;
+}
+
+// base[i]: exclusive prefix of gsum over windows i = (superbin, group); base[N] =
+// all probes.  cb_base[i]: first chunk block of window i (ceil(size / kBlockProbes)
+// blocks each), cb_base[N] = all blocks; cb_window[b] / cb_start[b]: the window
+// and level-2 position of chunk block b.  One workgroup (N <= 2048).
+__global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __restrict__ gsum, uint32_t N,
+                                                              uint32_t* __restrict__ base,
+                                                              uint32_t* __restrict__ cb_base,
+                                                              uint32_t* __restrict__ cb_window,
+                                                              uint32_t* __restrict__ cb_start) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x;
+    const uint32_t a = 2 * t < N ? gsum[2 * t] : 0u;
+    const uint32_t b = 2 * t + 1 < N ? gsum[2 * t + 1] : 0u;
+    const uint32_t ca = (a + kBlockProbes - 1) / kBlockProbes, cb = (b + kBlockProbes - 1) / kBlockProbes;
+    uint32_t total, ctotal;
+    const uint32_t ex = block_excl_scan(a + b, s_w, &total);
+    const uint32_t cex = block_excl_scan(ca + cb, s_w, &ctotal);
+    if (2 * t < N) {
+        base[2 * t] = ex;
+        cb_base[2 * t] = cex;
+    }
+    if (2 * t + 1 < N) {
+        base[2 * t + 1] = ex + a;
+        cb_base[2 * t + 1] = cex + ca;
+    }
+    if (t == 0) {
+        base[N] = total;
+        cb_base[N] = ctotal;
+    }
+    for (uint32_t c = 0; c < ca; ++c) {
+        cb_window[cex + c] = 2 * t;
+        cb_start[cex + c] = ex + c * kBlockProbes;
+    }
+    for (uint32_t c = 0; c < cb; ++c) {
+        cb_window[cex + ca + c] = 2 * t + 1;
+        cb_start[cex + ca + c] = ex + a + c * kBlockProbes;
+    }
+}
+
+// Last run whose start is <= f in an LDS run table of nt >= 1 ascending starts.
+__device__ __forceinline__ uint32_t run_of(const uint32_t* s_pre, uint32_t nt, uint32_t f) {
+    uint32_t lo = 0, hi = nt - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= f) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// One workgroup per (window, part): window w = (superbin sb, group q)
+// concatenates superbin sb's runs from the group's tiles in tile order; it is
+// cut into chunk blocks of kBlockProbes, and part p of kMidParts takes an equal
+// share of them.  The run table is built once; each block's loads are issued
+// while the previous block is sorted and written.
+template <bool KEYS>
+__global__ __launch_bounds__(kTile) void bin_mid_kernel(const uint32_t* __restrict__ level1,
+                                                        const uint32_t* __restrict__ level1_key,
+                                                        const uint16_t* __restrict__ stab, uint64_t ntiles,
+                                                        uint32_t tile_keys, uint32_t k, uint32_t tiles_per_group,
+                                                        uint32_t nsup, uint32_t nq, uint32_t region_log2,
+                                                        uint32_t rel_log2, const uint32_t* __restrict__ base,
+                                                        const uint32_t* __restrict__ cb_base, uint64_t max_chunks,
+                                                        uint16_t* __restrict__ tabs, uint32_t* __restrict__ level2,
+                                                        uint32_t* __restrict__ level2_key) {
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
+    __shared__ uint32_t s_cnt[1u << kMaxRel];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_sorted[kBlockProbes];
+    __shared__ uint32_t s_key[KEYS ? kBlockProbes : 1];
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = blockIdx.x / kMidParts, part = blockIdx.x - w * kMidParts;
+    const uint32_t sb = w / nq, q = w - sb * nq;
+    const uint32_t wbase = base[w];
+    const uint32_t E = base[w + 1] - wbase;
+    const uint32_t nblk = (E + kBlockProbes - 1) / kBlockProbes;
+    const uint32_t c_lo = (uint32_t)((uint64_t)nblk * part / kMidParts);
+    const uint32_t c_hi = (uint32_t)((uint64_t)nblk * (part + 1) / kMidParts);
+    if (c_lo >= c_hi) return;   // workgroup-uniform
+    const uint32_t b0 = cb_base[w];
+    const uint32_t R = 1u << rel_log2;
+    const uint32_t rmask = (1u << region_log2) - 1u;
+    // run table of the group's tiles (consecutive lanes, consecutive tiles: coalesced)
+    const uint64_t tlo = (uint64_t)q * tiles_per_group;
+    const uint64_t thi = (tlo + tiles_per_group < ntiles) ? tlo + tiles_per_group : ntiles;
+    const uint32_t nt = (uint32_t)(thi - tlo);   // <= kRunsPerPass (plan)
+    uint32_t len = 0, st = 0;
+    if (t < nt) {
+        const uint32_t a = stab[(uint64_t)sb * ntiles + tlo + t];
+        len = stab[(uint64_t)(sb + 1) * ntiles + tlo + t] - a;
+        st = (uint32_t)((tlo + t) * tile_keys * k) + a;
+    }
+    const uint32_t ex = block_excl_scan(len, s_w, nullptr);
+    if (t < nt) {
+        s_pre[t] = ex;
+        s_gst[t] = st;
+    }
+    __syncthreads();
+    // Wave v of the block takes entries [f0 + 512v, f0 + 512v + 512): one binary
+    // search per wave, then each lane walks the run table forward (runs are
+    // ~tile probes / superbins long, so a step of 64 entries crosses at most a few).
+    auto load = [&](uint32_t f0, uint32_t* lv, uint32_t* kv) {
+        const uint32_t fw = f0 + (t >> 6) * (64u * kChunkPerLane);
+        uint32_t i = run_of(s_pre, nt, fw < E ? fw : E - 1);
+#pragma unroll
+        for (int u = 0; u < kChunkPerLane; ++u) {
+            const uint32_t f = fw + u * 64 + (t & 63u);
+            lv[u] = 0xFFFFFFFFu;   // never a superbin-local offset (< 2^28)
+            kv[u] = 0;
+            if (f < E) {
+                while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
+                const uint32_t idx = s_gst[i] + (f - s_pre[i]);
+                lv[u] = level1[idx];
+                if constexpr (KEYS) kv[u] = level1_key[idx];
+            }
+        }
+    };
+    uint32_t lv[kChunkPerLane], kv[kChunkPerLane];
+    load(c_lo * kBlockProbes, lv, kv);
+    for (uint32_t c = c_lo; c < c_hi; ++c) {
+        const uint32_t f0 = c * kBlockProbes;
+        const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
+        if (t < R) s_cnt[t] = 0;
+        __syncthreads();   // also orders the previous block's reads of s_sorted / s_cnt
+        uint32_t tag[kChunkPerLane];
+#pragma unroll
+        for (int u = 0; u < kChunkPerLane; ++u) {
+            tag[u] = 0xFFFFFFFFu;
+            if (lv[u] != 0xFFFFFFFFu) {
+                const uint32_t r = lv[u] >> region_log2;
+                tag[u] = (r << 16) | atomicAdd(s_cnt + r, 1u);
+            }
+        }
+        uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
+        if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
+        __syncthreads();
+        const uint32_t cn = t < R ? s_cnt[t] : 0u;
+        const uint32_t cex = block_excl_scan(cn, s_w, nullptr);   // its barriers order the s_cnt reads first
+        if (t <= R) tabs[(uint64_t)t * max_chunks + b0 + c] = (uint16_t)cex;   // [region][block]
+        if (t < R) s_cnt[t] = cex;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kChunkPerLane; ++u) {
+            if (tag[u] != 0xFFFFFFFFu) {
+                const uint32_t d = s_cnt[tag[u] >> 16] + (tag[u] & 0xFFFFu);
+                s_sorted[d] = lv[u] & rmask;
+                if constexpr (KEYS) s_key[d] = kv[u];
+            }
+        }
+        __syncthreads();
+        const uint32_t out0 = wbase + f0;
+        for (uint32_t j = t; j < f1 - f0; j += kTile) {
+            level2[out0 + j] = s_sorted[j];
+            if constexpr (KEYS) level2_key[out0 + j] = s_key[j];
+        }
+        if (c + 1 < c_hi) {
+#pragma unroll
+            for (int u = 0; u < kChunkPerLane; ++u) {
+                lv[u] = nlv[u];
+                kv[u] = nkv[u];
+            }
         }
     }
 }
 
-// Level 2: one chunk of the level-1 array, grouped by region.  The chunk's
-// superbins are found from the superbin bases; each (chunk, region) run is
-// reserved with one atomic on the region's cursor.
-__global__ __launch_bounds__(kTile) void bin_part2_kernel(const uint32_t* __restrict__ level1, uint32_t P,
-                                                          const uint32_t* __restrict__ bases, uint32_t nbins,
-                                                          uint32_t nsup, uint32_t region_log2, uint32_t rel_log2,
-                                                          uint32_t* __restrict__ cursor,
-                                                          uint32_t* __restrict__ level2) {
-    __shared__ uint32_t s_sbb[kMaxSup + 1];
-    __shared__ uint32_t s_cnt[kP2Bins], s_gdst[kP2Bins];   // s_cnt becomes the local run bases
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_first, s_last;
-    __shared__ uint32_t s_sorted[kP2Probes];
-    __shared__ uint16_t s_lr[kP2Probes];
-    const uint32_t t = threadIdx.x;
-    const uint32_t p0 = blockIdx.x * kP2Probes;
-    const uint32_t p1 = (P - p0 < kP2Probes) ? P : p0 + kP2Probes;
-    if (t <= nsup) {
-        const uint32_t r = t << rel_log2;
-        s_sbb[t] = bases[r < nbins ? r : nbins];
-    }
-    if (t < kP2Bins) s_cnt[t] = 0;
-    __syncthreads();
-    if (t < 2) {   // superbin of p0 (lane 0) / of p1 - 1 (lane 1): last sb with s_sbb[sb] <= p
-        const uint32_t p = t ? p1 - 1 : p0;
-        uint32_t lo = 0, hi = nsup - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_sbb[mid] <= p) lo = mid; else hi = mid - 1;
+// Region r's probes: one run in each chunk block of its superbin.  Calls
+// visit(idx) for every level-2 index of the region (kLoads per lane in flight
+// through the caller's batching); run tables in LDS, passes of kRunsPerPass
+// blocks.  Contains barriers: every lane must call it.
+template <int kLoads, typename Visit>
+__device__ __forceinline__ void for_region_probes(const uint32_t* __restrict__ cb_base,
+                                                  const uint32_t* __restrict__ cb_start,
+                                                  const uint16_t* __restrict__ tabs, uint64_t max_chunks, uint32_t r,
+                                                  uint32_t nq, uint32_t rel_log2, uint32_t* s_pre, uint32_t* s_gst,
+                                                  uint32_t* s_w, Visit&& visit) {
+    const uint32_t R = 1u << rel_log2;
+    const uint32_t sb = r >> rel_log2, rl = r & (R - 1u);
+    const uint32_t t = threadIdx.x, lanes = blockDim.x;
+    const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
+    for (uint32_t p0 = bb0; p0 < bb1; p0 += kRunsPerPass) {
+        const uint32_t nt = (bb1 - p0 < kRunsPerPass) ? bb1 - p0 : kRunsPerPass;
+        uint32_t len = 0, st = 0;
+        if (t < nt) {   // consecutive lanes, consecutive blocks: coalesced
+            const uint32_t a = tabs[(uint64_t)rl * max_chunks + p0 + t];
+            len = tabs[(uint64_t)(rl + 1) * max_chunks + p0 + t] - a;
+            st = cb_start[p0 + t] + a;
         }
-        if (t) s_last = lo; else s_first = lo;
-    }
-    __syncthreads();
-    const uint32_t sb_first = s_first, sb_last = s_last;
-    const uint32_t rfirst = sb_first << rel_log2;
-    const uint32_t range = (sb_last - sb_first + 1) << rel_log2;
-    const uint32_t rmask = (1u << region_log2) - 1u;
-    uint32_t loc[kP2PerLane];
+        uint32_t E;
+        const uint32_t ex = block_excl_scan(len, s_w, &E);
+        if (t < nt) {
+            s_pre[t] = ex;
+            s_gst[t] = st;
+        }
+        __syncthreads();
+        // wave v takes kLoads * 64 consecutive entries per step: one binary search per
+        // wave and step, then each lane walks the run table forward
+        const uint32_t span = kLoads * 64u;
+        for (uint32_t fb = 0; fb < E; fb += span * (lanes >> 6)) {
+            const uint32_t fw = fb + (t >> 6) * span;
+            uint32_t i = run_of(s_pre, nt, fw < E ? fw : E - 1);
+            uint32_t idx[kLoads];
 #pragma unroll
-    for (int c = 0; c < kP2PerLane; ++c) {
-        const uint32_t p = p0 + c * kTile + t;
-        loc[c] = p < p1 ? level1[p] : 0u;
-    }
-    if (range > kP2Bins) {   // workgroup-uniform: many sparse superbins in one chunk
-#pragma unroll
-        for (int c = 0; c < kP2PerLane; ++c) {
-            const uint32_t p = p0 + c * kTile + t;
-            if (p < p1) {
-                uint32_t sb = sb_first;
-                while (p >= s_sbb[sb + 1]) ++sb;
-                const uint32_t r = (sb << rel_log2) + (loc[c] >> region_log2);
-                level2[atomicAdd(cursor + r, 1u)] = loc[c] & rmask;
+            for (int c = 0; c < kLoads; ++c) {
+                const uint32_t f = fw + c * 64 + (t & 63u);
+                idx[c] = 0xFFFFFFFFu;
+                if (f < E) {
+                    while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
+                    idx[c] = s_gst[i] + (f - s_pre[i]);
+                }
             }
+            visit(idx);
         }
-        return;
-    }
-    uint32_t tag[kP2PerLane];
-#pragma unroll
-    for (int c = 0; c < kP2PerLane; ++c) {
-        const uint32_t p = p0 + c * kTile + t;
-        tag[c] = 0xFFFFFFFFu;
-        if (p < p1) {
-            uint32_t sb = sb_first;
-            while (p >= s_sbb[sb + 1]) ++sb;
-            const uint32_t lr = ((sb - sb_first) << rel_log2) + (loc[c] >> region_log2);
-            tag[c] = (lr << 16) | atomicAdd(s_cnt + lr, 1u);
-        }
-    }
-    __syncthreads();
-    const uint32_t cnt = t < range ? s_cnt[t] : 0u;
-    const uint32_t ex = block_excl_scan(cnt, s_w, nullptr);   // its barriers order the s_cnt reads first
-    if (t < kP2Bins) s_cnt[t] = ex;
-    if (cnt) s_gdst[t] = atomicAdd(cursor + rfirst + t, cnt);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < kP2PerLane; ++c) {
-        if (tag[c] != 0xFFFFFFFFu) {
-            const uint32_t lr = tag[c] >> 16;
-            const uint32_t d = s_cnt[lr] + (tag[c] & 0xFFFFu);
-            s_sorted[d] = loc[c] & rmask;
-            s_lr[d] = (uint16_t)lr;
-        }
-    }
-    __syncthreads();
-    for (uint32_t j = t; j < p1 - p0; j += kTile) {
-        const uint32_t lr = s_lr[j];
-        level2[s_gdst[lr] + (j - s_cnt[lr])] = s_sorted[j];
+        __syncthreads();   // the next pass rewrites the run table
     }
 }
 
 template <uint32_t RLOG2, uint32_t LANES>
 __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
-                                                          const uint32_t* __restrict__ binned,
-                                                          const uint32_t* __restrict__ bases,
-                                                          uint32_t* __restrict__ any_flag) {
+                                                          const uint32_t* __restrict__ level2,
+                                                          const uint32_t* __restrict__ cb_base,
+                                                          const uint32_t* __restrict__ cb_start,
+                                                          const uint16_t* __restrict__ tabs, uint64_t max_chunks,
+                                                          uint32_t nq, uint32_t rel_log2, uint32_t dense,
+                                                          uint32_t* __restrict__ any_flag,
+                                                          uint8_t* __restrict__ dirty) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
     constexpr uint32_t kPer = kVec / LANES;
     constexpr int kLoads = 8;
     static_assert(kPer * LANES == kVec, "region must tile the workgroup");
     __shared__ uint4 s_mask4[kVec];
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
     const uint32_t r = blockIdx.x;
     const uint64_t v0 = (uint64_t)r * kVec;
     const uint64_t nvec = nwords / 4;
     uint4* gv = reinterpret_cast<uint4*>(bits);
-    const uint32_t pb = bases[r], p1 = bases[r + 1];
-    // Dense region (at least one probe per 16-B vector on average; most vectors are
-    // touched): its bitset vectors are loaded first, so that read overlaps the probe
-    // pass.  Sparse region: only the touched vectors are read, after the probe pass.
-    const bool dense = p1 - pb >= kVec;   // workgroup-uniform
+    // Dense batch (at least one probe per 16-B vector on average: most vectors are
+    // touched): the region's vectors are loaded first, so that read overlaps the
+    // probe pass.  Sparse batch: only the touched vectors are read, after it.
     uint4 old[kPer];
 #pragma unroll
     for (uint32_t c = 0; c < kPer; ++c) {
@@ -371,15 +447,15 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     }
     for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    for (uint32_t p = pb + t; p < p1; p += kLoads * LANES) {   // kLoads loads in flight per lane
-        uint32_t l[kLoads];
+    for_region_probes<kLoads>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
+        [&](const uint32_t* idx) {
+            uint32_t l[kLoads];
 #pragma unroll
-        for (int c = 0; c < kLoads; ++c) l[c] = (p + c * LANES < p1) ? binned[p + c * LANES] : 0xFFFFFFFFu;
+            for (int c = 0; c < kLoads; ++c) l[c] = idx[c] != 0xFFFFFFFFu ? level2[idx[c]] : 0xFFFFFFFFu;
 #pragma unroll
-        for (int c = 0; c < kLoads; ++c)
-            if (l[c] != 0xFFFFFFFFu) atomicOr(s_mask + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
-    }
-    __syncthreads();
+            for (int c = 0; c < kLoads; ++c)
+                if (l[c] != 0xFFFFFFFFu) atomicOr(s_mask + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
+        });
     uint4 msk[kPer];
 #pragma unroll
     for (uint32_t c = 0; c < kPer; ++c) {   // sparse: every touched vector's load issues before any store
@@ -392,8 +468,11 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     for (uint32_t c = 0; c < kPer; ++c) {
         const uint32_t v = c * LANES + t;
         if (v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) {
-            fresh |= (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) | (msk[c].w & ~old[c].w);
+            const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
+                                (msk[c].w & ~old[c].w);
+            fresh |= fr;
             gv[v0 + v] = make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z, old[c].w | msk[c].w);
+            if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
         }
     }
     if (any_flag) {
@@ -403,55 +482,141 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     }
 }
 
+// include?: the region in LDS; a probe on a 0 bit clears its key's answer.
+template <uint32_t RLOG2, uint32_t LANES>
+__global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restrict__ bits, uint64_t nwords,
+                                                         const uint32_t* __restrict__ level2,
+                                                         const uint32_t* __restrict__ level2_key,
+                                                         const uint32_t* __restrict__ cb_base,
+                                                         const uint32_t* __restrict__ cb_start,
+                                                         const uint16_t* __restrict__ tabs, uint64_t max_chunks,
+                                                         uint32_t nq, uint32_t rel_log2, uint8_t* __restrict__ out8) {
+    constexpr uint32_t kVec = 1u << (RLOG2 - 7);
+    constexpr int kLoads = 8;
+    __shared__ uint4 s_bits4[kVec];
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
+    const uint32_t* s_bits = reinterpret_cast<const uint32_t*>(s_bits4);
+    const uint32_t t = threadIdx.x;
+    const uint64_t v0 = (uint64_t)blockIdx.x * kVec;
+    const uint64_t nvec = nwords / 4;
+    const uint4* gv = reinterpret_cast<const uint4*>(bits);
+    for (uint32_t v = t; v < kVec; v += LANES) s_bits4[v] = v0 + v < nvec ? gv[v0 + v] : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for_region_probes<kLoads>(cb_base, cb_start, tabs, max_chunks, blockIdx.x, nq, rel_log2, s_pre, s_gst, s_w,
+        [&](const uint32_t* idx) {
+            uint32_t l[kLoads], key[kLoads];
+#pragma unroll
+            for (int c = 0; c < kLoads; ++c) {
+                l[c] = 0xFFFFFFFFu;
+                key[c] = 0;
+                if (idx[c] != 0xFFFFFFFFu) {
+                    l[c] = level2[idx[c]];
+                    key[c] = level2_key[idx[c]];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kLoads; ++c)
+                if (l[c] != 0xFFFFFFFFu && !((s_bits[l[c] >> 5] >> ((l[c] ^ 7u) & 31u)) & 1u)) out8[key[c]] = 0;
+        });
+}
+
 uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Carve {
-    uint32_t *counts, *scnt, *totals, *bases, *cursor, *level1, *level2;
-    uint4* digests;
+    uint32_t *level1, *level1_key, *level2, *level2_key, *gcnt, *gsum, *base, *cb_base, *cb_window, *cb_start;
+    uint16_t *stab, *tabs;
     uint64_t bytes;
 };
 
-Carve carve(const BfBinPlan& p, uint64_t n, void* base) {
+Carve carve(const BfBinPlan& p, void* at0) {
     Carve c{};
-    uint8_t* at = static_cast<uint8_t*>(base);
+    uint8_t* at = static_cast<uint8_t*>(at0);
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) { uint8_t* q = at ? at + off : nullptr; off += align256(bytes); return q; };
-    c.digests = reinterpret_cast<uint4*>(take(n * 16));
+    const uint64_t N = (uint64_t)p.nsup * p.ngroups;
     c.level1 = reinterpret_cast<uint32_t*>(take(p.probes * 4));
     c.level2 = reinterpret_cast<uint32_t*>(take(p.probes * 4));
-    c.counts = reinterpret_cast<uint32_t*>(take((uint64_t)p.nblocks * p.nbins * 4));
-    c.scnt = reinterpret_cast<uint32_t*>(take((uint64_t)p.nblocks * p.nsup * 4));
-    c.totals = reinterpret_cast<uint32_t*>(take((uint64_t)p.nbins * 4));
-    c.bases = reinterpret_cast<uint32_t*>(take((uint64_t)(p.nbins + 1) * 4));
-    c.cursor = reinterpret_cast<uint32_t*>(take((uint64_t)p.nbins * 4));
+    c.level1_key = p.with_keys ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
+    c.level2_key = p.with_keys ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
+    c.stab = reinterpret_cast<uint16_t*>(take(p.ntiles * (p.nsup + 1) * 2));   // [superbin][tile]
+    c.gcnt = reinterpret_cast<uint32_t*>(take((uint64_t)p.nblocks * p.nsup * 4));
+    c.gsum = reinterpret_cast<uint32_t*>(take(N * 4));
+    c.base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
+    c.cb_base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
+    c.cb_window = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
+    c.cb_start = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
+    c.tabs = reinterpret_cast<uint16_t*>(take(p.max_chunks * ((1ull << p.rel_log2) + 1) * 2));   // [region][block]
     c.bytes = off;
     return c;
 }
 
+// bin_front .. bin_mid: the batch's probes in region-sorted chunk blocks.
+hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c, const uint8_t* keys16,
+                            const uint64_t* offsets, uint64_t bias, uint64_t n, uint8_t* out8, hipStream_t s,
+                            BfMarks* mk) {
+    const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
+    if (p.with_keys)
+        hipLaunchKernelGGL(bin_front_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                           p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
+                           out8);
+    else
+        hipLaunchKernelGGL(bin_front_kernel<false>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                           p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
+                           out8);
+    bf_mark(mk, s, "bin_front");
+    hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
+                       p.ngroups, c.gsum);
+    hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
+                       c.cb_base, c.cb_window, c.cb_start);
+    bf_mark(mk, s, "bin_group");
+    const uint32_t tiles_per_group = kGroupBlocks * p.tiles_per_block;
+    if (p.with_keys)
+        hipLaunchKernelGGL(bin_mid_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, c.level1,
+                           c.level1_key, c.stab, p.ntiles, p.tile_keys, g.k, tiles_per_group, p.nsup, p.ngroups,
+                           p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           c.level2_key);
+    else
+        hipLaunchKernelGGL(bin_mid_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, c.level1,
+                           c.level1_key, c.stab, p.ntiles, p.tile_keys, g.k, tiles_per_group, p.nsup, p.ngroups,
+                           p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           c.level2_key);
+    bf_mark(mk, s, "bin_mid");
+    return hipGetLastError();
+}
+
 }  // namespace
 
-bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kP1Slots || n == 0) return false;   // k > 12: the direct insert
+uint64_t bf_binned_max_keys(uint32_t k) {
+    return (uint64_t)kMaxBlocks * kMaxTilesPerBlock * (k <= kTwoKeys ? 2 * kTile : kTile);
+}
+
+bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
+                    BfBinPlan* plan) {
+    if (k == 0 || k > (uint32_t)kSlots || n == 0 || n > bf_binned_max_keys(k)) return false;
+    const uint64_t probes = n * k;
+    if (probes >= (1ull << 32)) return false;
     const uint64_t bits = bitset_bytes * 8;
     const uint32_t order[2] = {pref_region_log2 == 20 ? 20u : 19u, pref_region_log2 == 20 ? 19u : 20u};
     for (uint32_t rl : order) {
         const uint64_t nbins = (bits + (1ull << rl) - 1) >> rl;
-        if (nbins > kMaxBins) continue;
         uint32_t rel = 0;
         while (((nbins + (1ull << rel) - 1) >> rel) > kMaxSup) ++rel;
-        plan->region_log2 = rl;
-        plan->nbins = (uint32_t)nbins;
-        plan->rel_log2 = rel;
-        plan->nsup = (uint32_t)((nbins + (1ull << rel) - 1) >> rel);
-        const uint64_t per_block = 2ull * kTile * 16;   // >= 16 tiles per workgroup
-        uint64_t blocks = (n + per_block - 1) / per_block;
-        if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-        if (blocks == 0) blocks = 1;
-        plan->nblocks = (uint32_t)blocks;
-        plan->chunk = ((n + blocks - 1) / blocks + kTile - 1) / kTile * kTile;
-        plan->probes = n * k;
-        if (plan->probes >= (1ull << 32)) return false;
-        plan->scratch_bytes = carve(*plan, n, nullptr).bytes;
+        if (rel > kMaxRel) continue;
+        BfBinPlan p{};
+        p.region_log2 = rl;
+        p.nbins = (uint32_t)nbins;
+        p.rel_log2 = rel;
+        p.nsup = (uint32_t)((nbins + (1ull << rel) - 1) >> rel);
+        p.with_keys = with_keys;
+        p.tile_keys = k <= kTwoKeys ? 2 * kTile : kTile;
+        p.ntiles = (n + p.tile_keys - 1) / p.tile_keys;
+        p.tiles_per_block = (uint32_t)((p.ntiles + kMaxBlocks - 1) / kMaxBlocks);
+        p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
+        p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
+        p.probes = probes;
+        p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
+        p.scratch_bytes = carve(p, nullptr).bytes;
+        *plan = p;
         return true;
     }
     return false;
@@ -461,31 +626,43 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                    void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
     if (n == 0) return hipSuccess;
-    const Carve c = carve(p, n, scratch);
-    const uint32_t P = (uint32_t)p.probes;
-    hipLaunchKernelGGL(bin_count_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.chunk,
-                       p.region_log2, p.nbins, p.rel_log2, p.nsup, c.counts, c.scnt, c.digests);
-    bf_mark(mk, s, "bin_count");
-    hipLaunchKernelGGL(bin_colsum_kernel, dim3((p.nbins + 63) / 64), dim3(1024), 0, s, c.counts, p.nblocks, p.nbins,
-                       c.totals);
-    bf_mark(mk, s, "bin_colsum");
-    hipLaunchKernelGGL(bin_supscan_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.scnt, p.nblocks, p.nsup);
-    bf_mark(mk, s, "bin_supscan");
-    hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, s, c.totals, p.nbins, c.bases, c.cursor);
-    bf_mark(mk, s, "bin_scan");
-    hipLaunchKernelGGL(bin_part1_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, c.digests, n, p.chunk,
-                       p.region_log2 + p.rel_log2, p.rel_log2, p.nsup, p.nbins, c.scnt, c.bases, c.level1);
-    bf_mark(mk, s, "bin_part1");
-    hipLaunchKernelGGL(bin_part2_kernel, dim3((P + kP2Probes - 1) / kP2Probes), dim3(kTile), 0, s, c.level1, P,
-                       c.bases, p.nbins, p.nsup, p.region_log2, p.rel_log2, c.cursor, c.level2);
-    bf_mark(mk, s, "bin_part2");
+    if (p.with_keys) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, nullptr, s, mk);
+    if (e != hipSuccess) return e;
     const uint64_t nwords = bitset_bytes / 4;
+    const uint32_t dense = p.probes >= (uint64_t)p.nbins * (1ull << (p.region_log2 - 7)) ? 1u : 0u;
     if (p.region_log2 == 19)
         hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
-                           nwords, c.level2, c.bases, any_flag);
+                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
+                           any_flag,
+                           g.dirty);
     else
         hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
-                           nwords, c.level2, c.bases, any_flag);
+                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
+                           any_flag,
+                           g.dirty);
     bf_mark(mk, s, "bin_apply");
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
+                                    void* scratch, uint8_t* out8, hipStream_t s, BfMarks* mk) {
+    if (n == 0) return hipSuccess;
+    if (!p.with_keys || !out8) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, out8, s, mk);
+    if (e != hipSuccess) return e;
+    const uint64_t nwords = bitset_bytes / 4;
+    if (p.region_log2 == 19)
+        hipLaunchKernelGGL((bin_test_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
+                           p.rel_log2, out8);
+    else
+        hipLaunchKernelGGL((bin_test_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
+                           p.rel_log2, out8);
+    bf_mark(mk, s, "bin_test");
     return hipGetLastError();
 }

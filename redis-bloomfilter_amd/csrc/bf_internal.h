@@ -42,16 +42,21 @@ hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const
                           unsigned long long* counts = nullptr /* BF_OP_ROUTE only */);
 
 // Binned insert (bf_binned.hip): plan + launch.  The launch carves every
-// intermediate (digests, two probe arrays, histograms) out of one device
+// intermediate (probe arrays, run tables, histograms) out of one device
 // scratch buffer of plan.scratch_bytes.
 struct BfBinPlan {
-    uint32_t region_log2;   // 2^region_log2 bits per region (LDS image in the apply pass)
+    uint32_t region_log2;   // 2^region_log2 bits per region (LDS image in the apply / test pass)
     uint32_t nbins;         // regions covering the bitset
     uint32_t rel_log2;      // superbin = 2^rel_log2 consecutive regions (level-1 partition)
     uint32_t nsup;          // superbins covering the bitset (<= 256)
-    uint32_t nblocks;       // workgroups of the count / level-1 passes (fixed key ranges)
-    uint64_t chunk;         // keys per workgroup
+    bool     with_keys;     // include?: probes carry their key index
+    uint32_t tile_keys;     // keys per front tile (2048 for k <= 6, else 1024)
+    uint64_t ntiles;        // front tiles
+    uint32_t tiles_per_block;
+    uint32_t nblocks;       // front workgroups (<= 512)
+    uint32_t ngroups;       // groups of 64 front workgroups (level-2 windows per superbin)
     uint64_t probes;        // n * k (< 2^32)
+    uint64_t max_chunks;    // bound on level-2 chunk blocks (bin_mid grid)
     uint64_t scratch_bytes; // device scratch the launch needs
 };
 // Optional per-kernel timing: when a BfMarks is passed, a launcher records
@@ -67,12 +72,19 @@ inline void bf_mark(BfMarks* mk, hipStream_t s, const char* name) {
     mk->names[mk->used] = name;
     (void)hipEventRecord(mk->ev[++mk->used], s);
 }
-// false: the batch / filter shape is outside the binned path (k > 16, more than
-// 2^32 probes, or a bitset beyond 24576 regions of 2^20 bits).
-bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, BfBinPlan* plan);
+// Largest batch one binned launch takes (larger batches go in sub-batches).
+uint64_t bf_binned_max_keys(uint32_t k);
+// false: the batch / filter shape is outside the binned path (k > 12, more than
+// bf_binned_max_keys keys, or a bitset beyond 65536 regions of 2^20 bits).
+bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
+                    BfBinPlan* plan);
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                    void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
+// plan.with_keys must be set; out8 gets the n answers.
+hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
+                                    void* scratch, uint8_t* out8, hipStream_t s, BfMarks* marks = nullptr);
 
 // Exact sequential per-key results (bf_seq.hip): batches of at most
 // bf_seq_chunk_keys(k) keys, scratch of bf_seq_scratch_bytes(n, k).  Probe

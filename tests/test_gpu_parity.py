@@ -286,8 +286,10 @@ def test_device_api_torch(pkg, oracle):
 @pytest.mark.parametrize("m,k,n", [(95851, 6, 20_000), (9585058, 6, 300_000), (1437758757, 10, 200_000),
                                    (2**32 + 17, 7, 100_000)])
 def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
-    """BFHIP_INSERT_BINNED=1 forces the binned (count/scan/scatter/apply) insert; 0 the direct one."""
+    """BFHIP_INSERT_BINNED / BFHIP_INCLUDE_BINNED = 1 force the binned (front/mid/apply|test)
+    insert and include?; 0 the direct kernels."""
     monkeypatch.setenv("BFHIP_INSERT_BINNED", mode)
+    monkeypatch.setenv("BFHIP_INCLUDE_BINNED", mode)
     rng = np.random.default_rng(RNG_SEED + 7)
     ins = rand_keys(rng, n, 0, 24)
     probe = rand_keys(rng, 20_000, 0, 24)
@@ -304,13 +306,14 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
 @pytest.mark.parametrize("rl", ["19", "20"])
 @pytest.mark.parametrize("case", ["dup", "tiny", "long", "k12", "nstar"])
 def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
-    """Forced binned insert on shapes that stress its partition passes: one key repeated
+    """Forced binned insert and include? on shapes that stress their partition passes: one key repeated
     (every probe in <= k regions, one superbin run per tile holding thousands of probes),
     a few keys over the 1.2 GB north-star filter (a level-2 chunk spanning every superbin:
     the per-probe cursor path), keys past the single-block SHA-1 (multi-block hash in the
     count pass), k = 12 (the largest k the binned path takes: one key per lane, every probe slot used), and a 200k-key batch on the
     north-star filter; both region sizes (64 KiB / 128 KiB LDS images)."""
     monkeypatch.setenv("BFHIP_INSERT_BINNED", "1")
+    monkeypatch.setenv("BFHIP_INCLUDE_BINNED", "1")
     monkeypatch.setenv("BFHIP_BIN_REGION_LOG2", rl)
     rng = np.random.default_rng(RNG_SEED + 8)
     if case == "dup":
