@@ -83,7 +83,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 }
 
 template <bool KEYS>
-__global__ __launch_bounds__(kTile) void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
                                                           const uint64_t* __restrict__ offsets, uint64_t bias,
                                                           uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
                                                           uint32_t sup_log2, uint32_t nsup,
