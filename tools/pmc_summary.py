@@ -23,10 +23,10 @@ KERNELS = {
     "bf_keys_kernel<INCLUDE>": re.compile(r"bf_keys_kernel<1>"),
     "bf_keys_kernel<INSERT>": re.compile(r"bf_keys_kernel<2>"),
     "bf_keys_kernel<INSERT_FLAGS>": re.compile(r"bf_keys_kernel<3>"),
-    "bin_count": re.compile(r"bin_count_kernel"),
-    "bin_part1": re.compile(r"bin_part1_kernel"),
-    "bin_part2": re.compile(r"bin_part2_kernel"),
+    "bin_front": re.compile(r"bin_front_kernel"),
+    "bin_mid": re.compile(r"bin_mid_kernel"),
     "bin_apply": re.compile(r"bin_apply_kernel"),
+    "bin_test": re.compile(r"bin_test_kernel"),
 }
 FULL_BATCH = ("bf_keys_kernel",)   # grid = one lane per key: keep full-batch launches only
 
