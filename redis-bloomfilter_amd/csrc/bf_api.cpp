@@ -790,6 +790,29 @@ int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint3
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     hipStream_t s = pick_stream(h, stream);
+    // Binned when the routed probes' random line fills clearly exceed a streaming pass
+    // over the shard (same policy and knob as the whole-filter insert).
+    BfBinPlan plan;
+    const uint64_t sub = bf_binned_max_offsets();
+    const bool binned = h->binned_mode != 0 &&
+                        bf_binned_plan_offsets(h->dev_bytes, std::min(count, sub), h->bin_region_log2, &plan) &&
+                        (h->binned_mode == 1 || (h->dev_bytes >= (64ull << 20) &&
+                                                 (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
+    if (binned) {
+        const size_t esz = h->route32 ? 4 : 8;
+        for (uint64_t c0 = 0; c0 < count; c0 += sub) {
+            const uint64_t cn = std::min(sub, count - c0);
+            if (cn != std::min(count, sub) && !bf_binned_plan_offsets(h->dev_bytes, cn, h->bin_region_log2, &plan))
+                return set_err(h, BF_EINVAL, "binned plan failed for a tail of %llu offsets", (unsigned long long)cn);
+            int rc = ensure_scratch(h, plan.scratch_bytes);
+            if (rc) return rc;
+            BfMarks* mk = prof_begin(h, s);
+            HIPCHK(h, bf_launch_shard_insert_binned(h->g, plan, h->dev_bytes,
+                                                    static_cast<const uint8_t*>(d_local) + c0 * esz, h->route32, cn,
+                                                    h->d_bin_scratch, d_any_new, s, mk));
+        }
+        return BF_OK;
+    }
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, h->route32, s));
     bf_mark(mk, s, "shard_insert");

@@ -83,7 +83,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 }
 
 template <bool KEYS>
-__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+__device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                           const uint64_t* __restrict__ offsets, uint64_t bias,
                                                           uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
                                                           uint32_t sup_log2, uint32_t nsup,
@@ -186,6 +186,82 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (t < nsup) gcnt[(uint64_t)blockIdx.x * nsup + t] = s_gcnt[t];
 }
 
+// insert: 8 waves per SIMD (2 workgroups per CU: 77 KiB of LDS, <= 64 VGPRs)
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
+                      uint64_t bias, uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block, uint32_t sup_log2,
+                      uint32_t nsup, uint32_t* __restrict__ level1, uint32_t* __restrict__ level1_key,
+                      uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint8_t* __restrict__ out8) {
+    bin_front_body<false>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1, level1_key,
+                          stab, gcnt, out8);
+}
+
+// include?: key indices ride along (123 KiB of LDS: one workgroup per CU)
+__global__ __launch_bounds__(kTile)
+void bin_front_keys_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
+                           uint64_t bias, uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block, uint32_t sup_log2,
+                           uint32_t nsup, uint32_t* __restrict__ level1, uint32_t* __restrict__ level1_key,
+                           uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint8_t* __restrict__ out8) {
+    bin_front_body<true>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1, level1_key,
+                         stab, gcnt, out8);
+}
+
+// Owner side of a partitioned filter: the probes arrive as shard-local offsets
+// (already hashed and routed), so the front pass only sorts them by superbin,
+// 12288 per tile, into the same level-1 layout bin_mid reads.
+template <typename Off>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uint32_t tiles_per_block,
+                              uint32_t sup_log2, uint32_t nsup, uint32_t* __restrict__ level1,
+                              uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_sorted[kTileProbes];
+    const uint32_t t = threadIdx.x;
+    if (t < kMaxSup) {
+        s_cnt[t] = 0;
+        s_gcnt[t] = 0;
+    }
+    __syncthreads();
+    const uint64_t smask = (1ull << sup_log2) - 1ull;
+    const uint64_t ntiles = (count + kTileProbes - 1) / kTileProbes;
+    const uint64_t tb0 = (uint64_t)blockIdx.x * tiles_per_block;
+    const uint64_t tb1 = (tb0 + tiles_per_block < ntiles) ? tb0 + tiles_per_block : ntiles;
+    for (uint64_t tile = tb0; tile < tb1; ++tile) {
+        const uint64_t p0 = tile * kTileProbes;
+        const uint32_t tp = (uint32_t)((count - p0) < (uint64_t)kTileProbes ? (count - p0) : kTileProbes);
+        uint32_t tag[kSlots], loc[kSlots];
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {   // coalesced: slot q of lane t is entry q * 1024 + t
+            const uint32_t j = (uint32_t)q * kTile + t;
+            tag[q] = 0xFFFFFFFFu;
+            loc[q] = 0;
+            if (j < tp) {
+                const uint64_t o = (uint64_t)local[p0 + j];
+                const uint32_t sb = (uint32_t)(o >> sup_log2);
+                tag[q] = (sb << 16) | atomicAdd(s_cnt + sb, 1u);
+                loc[q] = (uint32_t)(o & smask);
+            }
+        }
+        __syncthreads();
+        const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
+        const uint32_t ex = block_excl_scan(c, s_w, nullptr);
+        if (t <= nsup) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [superbin][tile]
+        if (t < kMaxSup) {
+            s_lbase[t] = ex;
+            s_gcnt[t] += c;
+            s_cnt[t] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q)
+            if (tag[q] != 0xFFFFFFFFu) s_sorted[s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu)] = loc[q];
+        __syncthreads();
+        for (uint32_t j = t; j < tp; j += kTile) level1[p0 + j] = s_sorted[j];
+    }
+    if (t < nsup) gcnt[(uint64_t)blockIdx.x * nsup + t] = s_gcnt[t];
+}
+
 // gsum[sb][q] = probes of superbin sb in the tiles of front workgroups [64q, 64q + 64).
 // One workgroup per superbin, one wave per group.
 __global__ __launch_bounds__(kMaxBlocks) void bin_group_sum_kernel(const uint32_t* __restrict__ gcnt,
@@ -257,7 +333,7 @@ template <bool KEYS>
 __global__ __launch_bounds__(kTile) void bin_mid_kernel(const uint32_t* __restrict__ level1,
                                                         const uint32_t* __restrict__ level1_key,
                                                         const uint16_t* __restrict__ stab, uint64_t ntiles,
-                                                        uint32_t tile_keys, uint32_t k, uint32_t tiles_per_group,
+                                                        uint32_t tile_probes, uint32_t tiles_per_group,
                                                         uint32_t nsup, uint32_t nq, uint32_t region_log2,
                                                         uint32_t rel_log2, const uint32_t* __restrict__ base,
                                                         const uint32_t* __restrict__ cb_base, uint64_t max_chunks,
@@ -288,7 +364,7 @@ __global__ __launch_bounds__(kTile) void bin_mid_kernel(const uint32_t* __restri
     if (t < nt) {
         const uint32_t a = stab[(uint64_t)sb * ntiles + tlo + t];
         len = stab[(uint64_t)(sb + 1) * ntiles + tlo + t] - a;
-        st = (uint32_t)((tlo + t) * tile_keys * k) + a;
+        st = (uint32_t)((tlo + t) * tile_probes) + a;
     }
     const uint32_t ex = block_excl_scan(len, s_w, nullptr);
     if (t < nt) {
@@ -550,20 +626,8 @@ Carve carve(const BfBinPlan& p, void* at0) {
     return c;
 }
 
-// bin_front .. bin_mid: the batch's probes in region-sorted chunk blocks.
-hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c, const uint8_t* keys16,
-                            const uint64_t* offsets, uint64_t bias, uint64_t n, uint8_t* out8, hipStream_t s,
-                            BfMarks* mk) {
-    const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
-    if (p.with_keys)
-        hipLaunchKernelGGL(bin_front_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
-                           p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
-                           out8);
-    else
-        hipLaunchKernelGGL(bin_front_kernel<false>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
-                           p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
-                           out8);
-    bf_mark(mk, s, "bin_front");
+// bin_group_sum .. bin_mid over the level-1 array a front pass wrote.
+hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c, hipStream_t s, BfMarks* mk) {
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
                        p.ngroups, c.gsum);
     hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
@@ -572,16 +636,33 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
     const uint32_t tiles_per_group = kGroupBlocks * p.tiles_per_block;
     if (p.with_keys)
         hipLaunchKernelGGL(bin_mid_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, c.level1,
-                           c.level1_key, c.stab, p.ntiles, p.tile_keys, g.k, tiles_per_group, p.nsup, p.ngroups,
+                           c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
     else
         hipLaunchKernelGGL(bin_mid_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, c.level1,
-                           c.level1_key, c.stab, p.ntiles, p.tile_keys, g.k, tiles_per_group, p.nsup, p.ngroups,
+                           c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
     bf_mark(mk, s, "bin_mid");
     return hipGetLastError();
+}
+
+// bin_front .. bin_mid: the batch's probes in region-sorted chunk blocks.
+hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c, const uint8_t* keys16,
+                            const uint64_t* offsets, uint64_t bias, uint64_t n, uint8_t* out8, hipStream_t s,
+                            BfMarks* mk) {
+    const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
+    if (p.with_keys)
+        hipLaunchKernelGGL(bin_front_keys_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                           p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
+                           out8);
+    else
+        hipLaunchKernelGGL(bin_front_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                           p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
+                           out8);
+    bf_mark(mk, s, "bin_front");
+    return launch_groups_mid(g, p, c, s, mk);
 }
 
 }  // namespace
@@ -590,9 +671,13 @@ uint64_t bf_binned_max_keys(uint32_t k) {
     return (uint64_t)kMaxBlocks * kMaxTilesPerBlock * (k <= kTwoKeys ? 2 * kTile : kTile);
 }
 
-bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
-                    BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kSlots || n == 0 || n > bf_binned_max_keys(k)) return false;
+uint64_t bf_binned_max_offsets() { return (uint64_t)kMaxBlocks * kMaxTilesPerBlock * kTileProbes; }
+
+namespace {
+
+// n units of k probes each, tile_units per front tile.
+bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_units, uint32_t pref_region_log2,
+                 bool with_keys, BfBinPlan* plan) {
     const uint64_t probes = n * k;
     if (probes >= (1ull << 32)) return false;
     const uint64_t bits = bitset_bytes * 8;
@@ -608,8 +693,9 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
         p.rel_log2 = rel;
         p.nsup = (uint32_t)((nbins + (1ull << rel) - 1) >> rel);
         p.with_keys = with_keys;
-        p.tile_keys = k <= kTwoKeys ? 2 * kTile : kTile;
-        p.ntiles = (n + p.tile_keys - 1) / p.tile_keys;
+        p.tile_keys = tile_units;
+        p.tile_probes = tile_units * k;
+        p.ntiles = (n + tile_units - 1) / tile_units;
         p.tiles_per_block = (uint32_t)((p.ntiles + kMaxBlocks - 1) / kMaxBlocks);
         p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
         p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
@@ -622,6 +708,39 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
     return false;
 }
 
+}  // namespace
+
+bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
+                    BfBinPlan* plan) {
+    if (k == 0 || k > (uint32_t)kSlots || n == 0 || n > bf_binned_max_keys(k)) return false;
+    return plan_common(bitset_bytes, n, k, k <= kTwoKeys ? 2 * kTile : kTile, pref_region_log2, with_keys, plan);
+}
+
+bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan) {
+    if (count == 0 || count > bf_binned_max_offsets()) return false;
+    return plan_common(bitset_bytes, count, 1, kTileProbes, pref_region_log2, false, plan);
+}
+
+namespace {
+
+hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes,
+                        uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
+    const uint64_t nwords = bitset_bytes / 4;
+    const uint32_t dense = p.probes >= (uint64_t)p.nbins * (1ull << (p.region_log2 - 7)) ? 1u : 0u;
+    if (p.region_log2 == 19)
+        hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
+                           any_flag, g.dirty);
+    else
+        hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
+                           any_flag, g.dirty);
+    bf_mark(mk, s, "bin_apply");
+    return hipGetLastError();
+}
+
+}  // namespace
+
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                    void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
@@ -630,20 +749,27 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
     const Carve c = carve(p, scratch);
     hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, nullptr, s, mk);
     if (e != hipSuccess) return e;
-    const uint64_t nwords = bitset_bytes / 4;
-    const uint32_t dense = p.probes >= (uint64_t)p.nbins * (1ull << (p.region_log2 - 7)) ? 1u : 0u;
-    if (p.region_log2 == 19)
-        hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
-                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag,
-                           g.dirty);
+    return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
+}
+
+hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                         const void* local, bool route32, uint64_t count, void* scratch,
+                                         uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
+    if (count == 0) return hipSuccess;
+    const Carve c = carve(p, scratch);
+    const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
+    if (route32)
+        hipLaunchKernelGGL(bin_front_offsets_kernel<uint32_t>, dim3(p.nblocks), dim3(kTile), 0, s,
+                           static_cast<const uint32_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
+                           c.stab, c.gcnt);
     else
-        hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
-                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag,
-                           g.dirty);
-    bf_mark(mk, s, "bin_apply");
-    return hipGetLastError();
+        hipLaunchKernelGGL(bin_front_offsets_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
+                           static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
+                           c.stab, c.gcnt);
+    bf_mark(mk, s, "bin_front_offsets");
+    hipError_t e = launch_groups_mid(g, p, c, s, mk);
+    if (e != hipSuccess) return e;
+    return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
 }
 
 hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,

@@ -51,6 +51,7 @@ struct BfBinPlan {
     uint32_t nsup;          // superbins covering the bitset (<= 256)
     bool     with_keys;     // include?: probes carry their key index
     uint32_t tile_keys;     // keys per front tile (2048 for k <= 6, else 1024)
+    uint32_t tile_probes;   // probes per full front tile (level-1 segment stride)
     uint64_t ntiles;        // front tiles
     uint32_t tiles_per_block;
     uint32_t nblocks;       // front workgroups (<= 512)
@@ -81,6 +82,13 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                    void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
+// Owner side of a partitioned filter: `count` routed shard-local offsets (uint32
+// when route32, else uint64) ORed into the shard through the same pipeline.
+uint64_t bf_binned_max_offsets();
+bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan);
+hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                         const void* local, bool route32, uint64_t count, void* scratch,
+                                         uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
 // plan.with_keys must be set; out8 gets the n answers.
 hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                     const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,

@@ -22,9 +22,12 @@ def dev_batch(pkg, torch, keys):
     return kb, ko, len(offs) - 1, buf, offs
 
 
+@pytest.mark.parametrize("binned", ["0", "1"])
 @pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20)])
-def test_simulated_partition(pkg, oracle, m, k, P, b):
+def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
+    """binned=1 forces the owner-side binned insert (offsets front pass + region apply)."""
     import torch
+    monkeypatch.setenv("BFHIP_INSERT_BINNED", binned)
     D = pkg.distributed
     dev = torch.device("cuda", 0)
     shards = [D.HipEngine(m, k, P, s, b, dev) for s in range(P)]
