@@ -146,18 +146,22 @@ int  bf_sync(bf_handle* h);                    /* synchronise the handle's own s
  *  requester:  bf_route_dev     hash n keys; every probe (j, i) becomes an owner-local
  *                               offset in d_send, grouped by owner shard: owner s's probes
  *                               are d_send[displ[s] .. displ[s] + d_counts[s]), displ the
- *                               exclusive prefix sum of d_counts; d_slot[j*k + i] is the
- *                               probe's position in d_send.  Needs n*k < 2^32.
+ *                               exclusive prefix sum of d_counts; d_slot[p] (nullable: an
+ *                               insert does not need it) is the index j of the key that
+ *                               send entry p belongs to.  Needs n*k < 2^32.
  *  owner:      bf_shard_insert_dev   OR the received local offsets into this shard
  *              bf_shard_test_dev     one byte (0/1) per received local offset
- *  requester:  bf_combine_dev   d_out[j] = AND_i d_bits[d_slot[j*k + i]] (include? answer)
+ *  requester:  bf_combine_dev   d_bits[p] = the owner's answer for send entry p (returned in
+ *                               send order); d_out[j] = AND of d_bits[p] over the k entries
+ *                               with d_slot[p] == j (include? answer)
  *
  *  Works on any handle: on a whole-filter handle shard_count = 1 routes everything to 0.
  *  d_counts must hold shard_count uint64 and is written, not accumulated. */
 int  bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_index,
                    uint32_t* block_log2, uint64_t* local_bits);
 int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
-                  void* d_send /* uint64[n*k], or uint32 with BF_FLAG_ROUTE32 */, uint32_t* d_slot,
+                  void* d_send /* uint64[n*k], or uint32 with BF_FLAG_ROUTE32 */,
+                  uint32_t* d_slot /* nullable, n*k */,
                   uint64_t* d_counts, void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);

@@ -341,7 +341,7 @@ class Filter:
     # -- partitioned filters (see include/bfhip.h)
     def route_dev(self, d_keys: int, d_offsets: int, n: int, d_send: int, d_slot: int, d_counts: int,
                   stream=None) -> None:
-        _check(self._lib.bf_route_dev(self.handle, d_keys, d_offsets, int(n), d_send, d_slot, d_counts,
+        _check(self._lib.bf_route_dev(self.handle, d_keys, d_offsets, int(n), d_send, d_slot or None, d_counts,
                                       self._s(stream)), self._h)
 
     def shard_insert_dev(self, d_local: int, count: int, d_any_new: int = 0, stream=None) -> None:

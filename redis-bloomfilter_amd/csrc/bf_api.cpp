@@ -757,7 +757,7 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
                  void* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream) {
     if (!h) return BF_EINVAL;
     if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
-    if (n && (!d_key_bytes || !d_offsets || !d_send || !d_slot)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
     const uint64_t probes = n * h->k;
     if (n && probes / n != h->k) return set_err(h, BF_EINVAL, "n*k overflows");
     if (probes >= (1ull << 32)) return set_err(h, BF_EINVAL, "n*k must be < 2^32 per call (slot indices are 32-bit)");
@@ -765,9 +765,21 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     hipStream_t s = pick_stream(h, stream);
+    auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
+    BfBinPlan plan;
+    if (h->binned_mode != 0 && bf_route_plan(n, h->k, h->shards, !h->route32, d_slot != nullptr, &plan)) {
+        // fused: hash + per-tile LDS sort by owner, then one owner-major gather
+        int rc = ensure_scratch(h, plan.scratch_bytes);
+        if (rc) return rc;
+        uint64_t bias = 0;
+        const uint8_t* k16 = align_keys(d_key_bytes, &bias);
+        BfMarks* mk = prof_begin(h, s);
+        HIPCHK(h, bf_launch_route_fused(h->g, plan, !h->route32, k16, d_offsets, bias, n, h->d_bin_scratch, d_send,
+                                        d_slot, counts, s, mk));
+        return BF_OK;
+    }
     int rc = ensure_route_scratch(h, std::max<uint64_t>(probes, 1));
     if (rc) return rc;
-    auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
     HIPCHK(h, hipMemsetAsync(counts, 0, h->shards * sizeof(unsigned long long), s));
     BfMarks* mk = prof_begin(h, s);
     if (n) {
@@ -777,8 +789,8 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
                                  nullptr, s, counts));
         bf_mark(mk, s, op_kernel_name(BF_OP_ROUTE));
     }
-    HIPCHK(h, bf_launch_route_scatter(h->d_tmp_local, h->d_tmp_owner, probes, h->shards, counts, h->d_cursor,
-                                      d_send, d_slot, h->route32, s));
+    HIPCHK(h, bf_launch_route_scatter(h->d_tmp_local, h->d_tmp_owner, probes, h->shards, h->k, counts,
+                                      h->d_cursor, d_send, d_slot, h->route32, s));
     bf_mark(mk, s, "route_scatter");
     return BF_OK;
 }

@@ -283,8 +283,10 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
                                                               uint32_t* __restrict__ base,
                                                               uint32_t* __restrict__ cb_base,
                                                               uint32_t* __restrict__ cb_window,
-                                                              uint32_t* __restrict__ cb_start) {
+                                                              uint32_t* __restrict__ cb_start, uint32_t nq,
+                                                              unsigned long long* __restrict__ totals) {
     __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_base[2049], s_cb[2049];
     const uint32_t t = threadIdx.x;
     const uint32_t a = 2 * t < N ? gsum[2 * t] : 0u;
     const uint32_t b = 2 * t + 1 < N ? gsum[2 * t + 1] : 0u;
@@ -304,13 +306,31 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
         base[N] = total;
         cb_base[N] = ctotal;
     }
-    for (uint32_t c = 0; c < ca; ++c) {
-        cb_window[cex + c] = 2 * t;
-        cb_start[cex + c] = ex + c * kBlockProbes;
+    if (totals) {   // per-bucket (superbin / owner) probe totals; zeroed by the caller
+        if (a) atomicAdd(totals + (2 * t) / nq, (unsigned long long)a);
+        if (b) atomicAdd(totals + (2 * t + 1) / nq, (unsigned long long)b);
     }
-    for (uint32_t c = 0; c < cb; ++c) {
-        cb_window[cex + ca + c] = 2 * t + 1;
-        cb_start[cex + ca + c] = ex + a + c * kBlockProbes;
+    // every block's window and level-2 start, all lanes over all blocks (a window
+    // may hold thousands of blocks): the window is the last one starting at or
+    // before the block
+    if (2 * t < N) {
+        s_base[2 * t] = ex;
+        s_cb[2 * t] = cex;
+    }
+    if (2 * t + 1 < N) {
+        s_base[2 * t + 1] = ex + a;
+        s_cb[2 * t + 1] = cex + ca;
+    }
+    if (t == 0) s_cb[N] = ctotal;
+    __syncthreads();
+    for (uint32_t blk = t; blk < ctotal; blk += 1024) {
+        uint32_t lo = 0, hi = N - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_cb[mid] <= blk) lo = mid; else hi = mid - 1;
+        }
+        cb_window[blk] = lo;
+        cb_start[blk] = s_base[lo] + (blk - s_cb[lo]) * kBlockProbes;
     }
 }
 
@@ -322,6 +342,170 @@ __device__ __forceinline__ uint32_t run_of(const uint32_t* s_pre, uint32_t nt, u
         if (s_pre[mid] <= f) lo = mid; else hi = mid - 1;
     }
     return lo;
+}
+
+// Requester side of a partitioned filter (bf_route_dev): hash, then per tile an
+// LDS counting sort of the tile's probes by owner shard (block-cyclic map of
+// include/bfhip.h), written contiguously at the tile's fixed place with the
+// tile's owner run table [owner][tile]; per-workgroup owner totals.  WIDE: the
+// owner-local offsets need more than 32 bits (their high byte is kept apart);
+// SLOT: each probe carries its key index.
+template <bool WIDE, bool SLOT>
+__global__ __launch_bounds__(kTile) void route_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+                                                            const uint64_t* __restrict__ offsets, uint64_t bias,
+                                                            uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
+                                                            uint32_t P, uint32_t* __restrict__ lo1,
+                                                            uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1,
+                                                            uint16_t* __restrict__ stab,
+                                                            uint32_t* __restrict__ gcnt) {
+    __shared__ uint64_t s_off[kTile + 1];
+    __shared__ uint4 s_stage[kStageVec + kStageSlackVec];
+    __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_lo[kTileProbes];
+    __shared__ uint8_t s_hi[WIDE ? kTileProbes : 1];
+    __shared__ uint32_t s_key[SLOT ? kTileProbes : 1];
+    const uint32_t t = threadIdx.x;
+    if (t < kMaxSup) {
+        s_cnt[t] = 0;
+        s_gcnt[t] = 0;
+    }
+    __syncthreads();
+    const uint32_t k = g.k;
+    const uint32_t kpl = tile_keys / kTile;
+    const uint64_t ntiles = (n + tile_keys - 1) / tile_keys;
+    const uint64_t tb0 = (uint64_t)blockIdx.x * tiles_per_block;
+    const uint64_t tb1 = (tb0 + tiles_per_block < ntiles) ? tb0 + tiles_per_block : ntiles;
+    for (uint64_t tile = tb0; tile < tb1; ++tile) {
+        const uint64_t key0 = tile * tile_keys;
+        const uint32_t tk = (uint32_t)((n - key0) < (uint64_t)tile_keys ? (n - key0) : tile_keys);
+        uint4 H0 = make_uint4(0, 0, 0, 0), H1 = make_uint4(0, 0, 0, 0);
+        for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off, s_stage,
+            [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                uint32_t H[5];
+                sha1_any<decltype(staged)::value>(src, s, L, H);
+                H0 = make_uint4(H[0], H[1], H[2], H[3]);
+            });
+        if (tk > (uint32_t)kTile) {
+            for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0 + kTile, tk - kTile, s_off, s_stage,
+                [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                    uint32_t H[5];
+                    sha1_any<decltype(staged)::value>(src, s, L, H);
+                    H1 = make_uint4(H[0], H[1], H[2], H[3]);
+                });
+        }
+        const bool live0 = t < tk;
+        const bool live1 = kpl == 2 && kTile + t < tk;
+        uint32_t tag[kSlots], lo[kSlots];
+        uint8_t hi[kSlots];
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+            const bool second = kpl == 2 && q >= (int)kTwoKeys;
+            const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
+            const bool live = i < k && (second ? live1 : live0);
+            tag[q] = 0xFFFFFFFFu;
+            lo[q] = 0;
+            hi[q] = 0;
+            if (live) {
+                const uint4 H = second ? H1 : H0;
+                uint32_t owner;
+                uint64_t local;
+                owner_local(g, probe_offset(g, H.x, H.y, H.z, H.w, i), owner, local);
+                tag[q] = (owner << 16) | atomicAdd(s_cnt + owner, 1u);
+                lo[q] = (uint32_t)local;
+                hi[q] = (uint8_t)(local >> 32);
+            }
+        }
+        __syncthreads();
+        const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
+        const uint32_t ex = block_excl_scan(c, s_w, nullptr);
+        if (t <= P) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [owner][tile]
+        if (t < kMaxSup) {
+            s_lbase[t] = ex;
+            s_gcnt[t] += c;
+            s_cnt[t] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+            if (tag[q] != 0xFFFFFFFFu) {
+                const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
+                s_lo[d] = lo[q];
+                if constexpr (WIDE) s_hi[d] = hi[q];
+                if constexpr (SLOT) {
+                    const bool second = kpl == 2 && q >= (int)kTwoKeys;
+                    s_key[d] = (uint32_t)(key0 + (second ? kTile + t : t));
+                }
+            }
+        }
+        __syncthreads();
+        const uint64_t seg = key0 * k;
+        const uint32_t tp = tk * k;
+        for (uint32_t j = t; j < tp; j += kTile) {
+            lo1[seg + j] = s_lo[j];
+            if constexpr (WIDE) hi1[seg + j] = s_hi[j];
+            if constexpr (SLOT) key1[seg + j] = s_key[j];
+        }
+    }
+    if (t < P) gcnt[(uint64_t)blockIdx.x * P + t] = s_gcnt[t];
+}
+
+// One workgroup per 8192-probe block of an (owner, group) window (the grid is an
+// upper bound; spare workgroups exit): the owner's runs from the group's tiles
+// are copied, in order, to the window's place in the send buffer (owner-major,
+// so owner s's probes are one contiguous all-to-all segment).  Block-granular
+// so that the parallelism does not depend on the number of owners.
+template <bool WIDE, bool SLOT>
+__global__ __launch_bounds__(kTile) void route_gather_kernel(const uint32_t* __restrict__ lo1,
+                                                             const uint8_t* __restrict__ hi1,
+                                                             const uint32_t* __restrict__ key1,
+                                                             const uint16_t* __restrict__ stab, uint64_t ntiles,
+                                                             uint32_t tile_probes, uint32_t tiles_per_group,
+                                                             uint32_t nowners, uint32_t nq,
+                                                             const uint32_t* __restrict__ base,
+                                                             const uint32_t* __restrict__ cb_base,
+                                                             const uint32_t* __restrict__ cb_window,
+                                                             void* __restrict__ send, uint32_t* __restrict__ slot) {
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x, b = blockIdx.x;
+    if (b >= cb_base[nowners * nq]) return;   // workgroup-uniform
+    const uint32_t w = cb_window[b];
+    const uint32_t owner = w / nq, q = w - owner * nq;
+    const uint32_t wbase = base[w];
+    const uint32_t E = base[w + 1] - wbase;
+    const uint32_t f0 = (b - cb_base[w]) * kBlockProbes;
+    const uint32_t f_end = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
+    const uint64_t tlo = (uint64_t)q * tiles_per_group;
+    const uint64_t thi = (tlo + tiles_per_group < ntiles) ? tlo + tiles_per_group : ntiles;
+    const uint32_t nt = (uint32_t)(thi - tlo);
+    uint32_t len = 0, st = 0;
+    if (t < nt) {
+        const uint32_t a = stab[(uint64_t)owner * ntiles + tlo + t];
+        len = stab[(uint64_t)(owner + 1) * ntiles + tlo + t] - a;
+        st = (uint32_t)((tlo + t) * tile_probes) + a;
+    }
+    const uint32_t ex = block_excl_scan(len, s_w, nullptr);
+    if (t < nt) {
+        s_pre[t] = ex;
+        s_gst[t] = st;
+    }
+    __syncthreads();
+    const uint32_t fw = f0 + (t >> 6) * (64u * kChunkPerLane);
+    uint32_t i = run_of(s_pre, nt, fw < f_end ? fw : f_end - 1);
+#pragma unroll
+    for (int u = 0; u < kChunkPerLane; ++u) {
+        const uint32_t f = fw + u * 64 + (t & 63u);
+        if (f < f_end) {
+            while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
+            const uint32_t idx = s_gst[i] + (f - s_pre[i]);
+            if constexpr (WIDE)
+                static_cast<uint64_t*>(send)[wbase + f] = ((uint64_t)hi1[idx] << 32) | lo1[idx];
+            else
+                static_cast<uint32_t*>(send)[wbase + f] = lo1[idx];
+            if constexpr (SLOT) slot[wbase + f] = key1[idx];
+        }
+    }
 }
 
 // One workgroup per (window, part): window w = (superbin sb, group q)
@@ -631,7 +815,7 @@ hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
                        p.ngroups, c.gsum);
     hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
-                       c.cb_base, c.cb_window, c.cb_start);
+                       c.cb_base, c.cb_window, c.cb_start, p.ngroups, (unsigned long long*)nullptr);
     bf_mark(mk, s, "bin_group");
     const uint32_t tiles_per_group = kGroupBlocks * p.tiles_per_block;
     if (p.with_keys)
@@ -790,5 +974,90 @@ hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_
                            nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
                            p.rel_log2, out8);
     bf_mark(mk, s, "bin_test");
+    return hipGetLastError();
+}
+
+// ---- partitioned filters, requester side ---------------------------------
+
+namespace {
+
+struct RouteCarve {
+    uint32_t *lo1, *key1, *gcnt, *gsum, *base, *cb_base, *cb_window, *cb_start;
+    uint8_t* hi1;
+    uint16_t* stab;
+    uint64_t bytes;
+};
+
+RouteCarve route_carve(const BfBinPlan& p, bool wide, bool with_slot, void* at0) {
+    RouteCarve c{};
+    uint8_t* at = static_cast<uint8_t*>(at0);
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) { uint8_t* q = at ? at + off : nullptr; off += align256(bytes); return q; };
+    const uint64_t N = (uint64_t)p.nsup * p.ngroups;
+    c.lo1 = reinterpret_cast<uint32_t*>(take(p.probes * 4));
+    c.hi1 = wide ? take(p.probes) : nullptr;
+    c.key1 = with_slot ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
+    c.stab = reinterpret_cast<uint16_t*>(take(p.ntiles * (p.nsup + 1) * 2));
+    c.gcnt = reinterpret_cast<uint32_t*>(take((uint64_t)p.nblocks * p.nsup * 4));
+    c.gsum = reinterpret_cast<uint32_t*>(take(N * 4));
+    c.base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
+    c.cb_base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
+    c.cb_window = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
+    c.cb_start = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
+    c.bytes = off;
+    return c;
+}
+
+}  // namespace
+
+bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan) {
+    if (k == 0 || k > (uint32_t)kSlots || n == 0 || n > bf_binned_max_keys(k) || shards == 0 || shards > kMaxSup)
+        return false;
+    const uint64_t probes = n * k;
+    if (probes >= (1ull << 32)) return false;
+    BfBinPlan p{};
+    p.nsup = shards;   // buckets = owner shards
+    p.tile_keys = k <= kTwoKeys ? 2 * kTile : kTile;
+    p.tile_probes = p.tile_keys * k;
+    p.ntiles = (n + p.tile_keys - 1) / p.tile_keys;
+    p.tiles_per_block = (uint32_t)((p.ntiles + kMaxBlocks - 1) / kMaxBlocks);
+    p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
+    p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
+    p.probes = probes;
+    p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
+    p.scratch_bytes = route_carve(p, wide, with_slot, nullptr).bytes;
+    *plan = p;
+    return true;
+}
+
+hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
+                                 const uint64_t* offsets, uint64_t bias, uint64_t n, void* scratch, void* send,
+                                 uint32_t* slot, unsigned long long* counts, hipStream_t s, BfMarks* mk) {
+    const RouteCarve c = route_carve(p, wide, slot != nullptr, scratch);
+    hipError_t e;
+    if ((e = hipMemsetAsync(counts, 0, (uint64_t)p.nsup * sizeof(unsigned long long), s)) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+#define BF_ROUTE_FRONT(W, S)                                                                                      \
+    hipLaunchKernelGGL((route_front_kernel<W, S>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, \
+                       p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt)
+    if (wide) { if (slot) BF_ROUTE_FRONT(true, true); else BF_ROUTE_FRONT(true, false); }
+    else { if (slot) BF_ROUTE_FRONT(false, true); else BF_ROUTE_FRONT(false, false); }
+#undef BF_ROUTE_FRONT
+    bf_mark(mk, s, "route_front");
+    hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
+                       p.ngroups, c.gsum);
+    hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
+                       c.cb_base, c.cb_window, c.cb_start, p.ngroups, counts);
+    bf_mark(mk, s, "route_group");
+    const uint32_t tiles_per_group = kGroupBlocks * p.tiles_per_block;
+    const dim3 grid((uint32_t)p.max_chunks);
+#define BF_ROUTE_GATHER(W, S)                                                                                    \
+    hipLaunchKernelGGL((route_gather_kernel<W, S>), grid, dim3(kTile), 0, s, c.lo1, c.hi1, c.key1, c.stab,       \
+                       p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups, c.base, c.cb_base,          \
+                       c.cb_window, send, slot)
+    if (wide) { if (slot) BF_ROUTE_GATHER(true, true); else BF_ROUTE_GATHER(true, false); }
+    else { if (slot) BF_ROUTE_GATHER(false, true); else BF_ROUTE_GATHER(false, false); }
+#undef BF_ROUTE_GATHER
+    bf_mark(mk, s, "route_gather");
     return hipGetLastError();
 }

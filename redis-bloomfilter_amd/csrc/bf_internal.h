@@ -108,18 +108,29 @@ hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const ui
                                 uint64_t n, void* scratch, uint8_t* out8, uint32_t* any_flag, hipStream_t s,
                                 BfMarks* marks = nullptr);
 
+// Partitioned filters, requester side, fused (bf_binned.hip): hash + per-tile
+// LDS sort by owner, then an owner-major gather into send[] (uint64 entries when
+// wide, else uint32) and slot[] (key index of each send entry, nullable);
+// counts[s] = probes for owner s.  Needs n <= bf_binned_max_keys(k), k <= 12.
+bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan);
+hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
+                                 const uint64_t* offsets, uint64_t bias, uint64_t n, void* scratch, void* send,
+                                 uint32_t* slot, unsigned long long* counts, hipStream_t s,
+                                 BfMarks* marks = nullptr);
+
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
-// pairs by owner into send[], writes each probe's position into slot[].
+// pairs by owner into send[]; slot[pos] (nullable) = key index (probe / k) of send entry pos.
 // counts[P] must hold the per-owner totals (from BF_OP_ROUTE).
 // `local` (tmp, from BF_OP_ROUTE) and `send` hold uint64, or uint32 when route32.
 hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint64_t total,
-                                   uint32_t P, const unsigned long long* counts,
+                                   uint32_t P, uint32_t k, const unsigned long long* counts,
                                    unsigned long long* cursor, void* send, uint32_t* slot,
                                    bool route32, hipStream_t s);
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count,
                                   uint32_t* any_flag, bool route32, hipStream_t s);
 hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count,
                                 uint8_t* out, bool route32, hipStream_t s);
+// out[j] = AND of bits[p] over the n*k send entries p with slot[p] == j.
 hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k,
                              uint8_t* out, hipStream_t s);
 

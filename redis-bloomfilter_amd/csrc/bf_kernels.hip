@@ -221,7 +221,7 @@ __global__ void displ_kernel(const unsigned long long* __restrict__ counts, uint
 template <typename Off>
 __global__ __launch_bounds__(256) void route_scatter_kernel(const Off* __restrict__ local,
                                                             const uint8_t* __restrict__ owner,
-                                                            uint64_t total, uint32_t P,
+                                                            uint64_t total, uint32_t P, uint32_t k,
                                                             unsigned long long* __restrict__ cursor,
                                                             Off* __restrict__ send,
                                                             uint32_t* __restrict__ slot) {
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const Off* __restric
         if (own[it] != 0xFFFFFFFFu) {
             const unsigned long long pos = s_base[own[it]] + rank[it];
             send[pos] = local[p];
-            slot[p] = (uint32_t)pos;
+            if (slot) slot[pos] = (uint32_t)(p / k);   // key index of send entry pos
         }
     }
 }
@@ -323,15 +323,14 @@ __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restr
     }
 }
 
+// out[] preset to 1: a probe whose owner answered 0 clears its key's answer (every
+// writer stores the same 0, so no atomics are needed).
 __global__ __launch_bounds__(256) void combine_kernel(const uint8_t* __restrict__ bits,
-                                                      const uint32_t* __restrict__ slot, uint64_t n,
-                                                      uint32_t k, uint8_t* __restrict__ out) {
+                                                      const uint32_t* __restrict__ slot, uint64_t total,
+                                                      uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-        uint32_t ok = 1u;
-        for (uint32_t i = 0; i < k; ++i) ok &= bits[slot[j * k + i]];
-        out[j] = (uint8_t)ok;
-    }
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += stride)
+        if (!bits[p]) out[slot[p]] = 0;
 }
 
 uint32_t stream_grid(uint64_t nvec) {
@@ -368,7 +367,7 @@ hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const
 }
 
 hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint64_t total, uint32_t P,
-                                   const unsigned long long* counts, unsigned long long* cursor,
+                                   uint32_t k, const unsigned long long* counts, unsigned long long* cursor,
                                    void* send, uint32_t* slot, bool route32, hipStream_t s) {
     hipLaunchKernelGGL(displ_kernel, dim3(1), dim3(64), 0, s, counts, P, cursor);
     if (total == 0) return hipGetLastError();
@@ -376,10 +375,10 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
     const dim3 grid((uint32_t)((total + per - 1) / per));
     if (route32)
         hipLaunchKernelGGL(route_scatter_kernel<uint32_t>, grid, dim3(256), 0, s, static_cast<const uint32_t*>(local),
-                           owner, total, P, cursor, static_cast<uint32_t*>(send), slot);
+                           owner, total, P, k, cursor, static_cast<uint32_t*>(send), slot);
     else
         hipLaunchKernelGGL(route_scatter_kernel<uint64_t>, grid, dim3(256), 0, s, static_cast<const uint64_t*>(local),
-                           owner, total, P, cursor, static_cast<uint64_t*>(send), slot);
+                           owner, total, P, k, cursor, static_cast<uint64_t*>(send), slot);
     return hipGetLastError();
 }
 
@@ -415,7 +414,10 @@ hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_
 hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k, uint8_t* out,
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(combine_kernel, dim3(stream_grid(n)), dim3(256), 0, s, bits, slot, n, k, out);
+    hipError_t e = hipMemsetAsync(out, 1, n, s);
+    if (e != hipSuccess) return e;
+    const uint64_t total = n * k;
+    hipLaunchKernelGGL(combine_kernel, dim3(stream_grid(total)), dim3(256), 0, s, bits, slot, total, out);
     return hipGetLastError();
 }
 

@@ -99,12 +99,14 @@ class HipEngine:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def route(self, kb: torch.Tensor, ko: torch.Tensor, n: int):
+    def route(self, kb: torch.Tensor, ko: torch.Tensor, n: int, want_slot: bool = True):
+        """Probes grouped by owner (send), per-owner counts, and (for include?) the key
+        index of every send entry (slot)."""
         send = torch.empty(n * self.k, dtype=self.offset_dtype, device=self.device)
-        slot = torch.empty(n * self.k, dtype=torch.int32, device=self.device)
+        slot = torch.empty(n * self.k, dtype=torch.int32, device=self.device) if want_slot else None
         counts = torch.empty(self.P, dtype=torch.int64, device=self.device)
-        self.filter.route_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(), slot.data_ptr(),
-                              counts.data_ptr(), stream=self._stream())
+        self.filter.route_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
+                              slot.data_ptr() if want_slot else 0, counts.data_ptr(), stream=self._stream())
         return send, slot, counts
 
     def shard_insert(self, local: torch.Tensor) -> None:
@@ -169,7 +171,7 @@ class PartitionedFilter:
 
     # -- device-resident batch API (keys already in device memory)
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
-        send, _, counts = self.engine.route(kb, ko, n)
+        send, _, counts = self.engine.route(kb, ko, n, want_slot=False)
         recv, _, _ = self._exchange(send, counts)
         self.engine.shard_insert(recv)
 

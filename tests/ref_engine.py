@@ -22,16 +22,15 @@ class NumpyEngine:
         self.local_bits = D.shard_local_bits(reach, P, rank, block_log2)
         self.bits = np.zeros((self.local_bits + 7) // 8, np.uint8)
 
-    def route(self, kb, ko, n):
+    def route(self, kb, ko, n, want_slot=True):
         buf = kb.numpy()
         offs = ko.numpy().view(np.uint64)
         idx = self.orc.indexes_many(buf, offs, self.m, self.k).reshape(-1)
         owner, local = D.block_owner_local(idx, self.P, self.b)
         order = np.argsort(owner, kind="stable")
-        slot = np.empty(n * self.k, np.int32)
-        slot[order] = np.arange(n * self.k, dtype=np.int32)
+        slot = (np.arange(n * self.k, dtype=np.int64) // self.k)[order].astype(np.int32)   # key of each send entry
         counts = np.bincount(owner, minlength=self.P).astype(np.int64)
-        return (torch.from_numpy(local[order].view(np.int64).copy()), torch.from_numpy(slot),
+        return (torch.from_numpy(local[order].view(np.int64).copy()), torch.from_numpy(slot) if want_slot else None,
                 torch.from_numpy(counts))
 
     def shard_insert(self, local):
@@ -46,8 +45,9 @@ class NumpyEngine:
         return torch.from_numpy(b.astype(np.uint8))
 
     def combine(self, bits, slot, n):
-        b = bits.numpy()[slot.numpy().astype(np.int64)].reshape(n, self.k)
-        return torch.from_numpy(b.all(axis=1).astype(np.uint8))
+        out = np.ones(n, np.uint8)
+        out[slot.numpy().astype(np.int64)[bits.numpy() == 0]] = 0
+        return torch.from_numpy(out)
 
     def clear(self):
         self.bits[:] = 0

@@ -45,13 +45,16 @@ def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
         assert c.tolist() == np.bincount(owner, minlength=P).tolist()
         s_np = send.cpu().numpy()   # int32 when the shards fit 2^32 bits (BF_FLAG_ROUTE32)
         s_np = s_np.view(np.uint32).astype(np.uint64) if s_np.dtype == np.int32 else s_np.view(np.uint64)
-        assert (s_np.dtype, send.dtype == torch.int32) == (np.uint64, shards[r].filter.route32)
-        sl = slot.cpu().numpy().astype(np.int64)
-        assert sorted(sl.tolist()) == list(range(n * k))
-        np.testing.assert_array_equal(s_np[sl], local)
+        assert (send.dtype == torch.int32) == shards[r].filter.route32
+        sl = slot.cpu().numpy().astype(np.int64)   # key index of every send entry
+        assert np.bincount(sl, minlength=n).tolist() == [k] * n
         displ = np.concatenate([[0], np.cumsum(c)[:-1]])
-        seg_owner = np.searchsorted(np.cumsum(c), sl, side="right")
-        np.testing.assert_array_equal(seg_owner, owner)
+        key_of = np.arange(n * k) // k
+        for s in range(P):   # owner s's segment holds exactly its (key, local) pairs
+            seg = slice(int(displ[s]), int(displ[s] + c[s]))
+            got = sorted(zip(sl[seg].tolist(), s_np[seg].tolist()))
+            want = sorted(zip(key_of[owner == s].tolist(), local[owner == s].tolist()))
+            assert got == want
         routed.append((send, slot, c, displ, n))
     # exchange: owner s receives every rank's segment s
     for s in range(P):
