@@ -174,6 +174,38 @@ int  bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot,
 int  bf_shard_export(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out);
 int  bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode);
 
+/* ---- the Lua driver's scalable layout (lib/bloomfilter_driver/lua.rb,
+ *      vendor/assets/lua/add.lua + check.lua), device-resident.
+ *
+ *   bf_lua_create        Lua#initialize (lua.rb:14-17): entries = options[:size],
+ *                        precision = options[:error_rate]; no layer exists yet
+ *   bf_lua_insert_many   add.lua, one EVALSHA per key, in batch order: the item goes to
+ *                        layer index(count + 1) and INCRs the count iff it set a new bit
+ *                        (add.lua:6-54); per_key_new[j] = that INCR; *new_layers bit n-1
+ *                        = layer n got a new item (the keys add.lua:52 EXPIREs)
+ *   bf_lua_include_many  check.lua: 0 without a count, else any of layers 1..index(count)
+ *                        holding all of its k_n bits (check.lua:1-61)
+ *   bf_lua_clear         lua.rb:28-30 (KEYS name:* + DEL): layers and count dropped
+ *   bf_lua_get/set_count KEYS[1]:count;  bf_lua_export/import_layer  KEYS[1]:n (SETBIT layout)
+ *   bf_lua_layer_params  add.lua:16-25: bits and k of layer n (host only, no device)
+ *   bf_lua_index         add.lua:13-15 / check.lua:9-11: the layer of a count (host only) */
+typedef struct bf_lua bf_lua;
+int  bf_lua_create(double entries, double precision, const bf_config* cfg /* device only */, bf_lua** out);
+int  bf_lua_destroy(bf_lua* h);
+const char* bf_lua_last_error(const bf_lua* h);   /* h == NULL: last error of bf_lua_create */
+int  bf_lua_insert_many(bf_lua* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                        uint8_t* per_key_new /* nullable */, uint64_t* new_layers /* nullable */);
+int  bf_lua_include_many(bf_lua* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                         uint8_t* out);
+int  bf_lua_clear(bf_lua* h);
+int  bf_lua_get_count(const bf_lua* h, uint64_t* count);
+int  bf_lua_set_count(bf_lua* h, uint64_t count);
+int  bf_lua_layers(const bf_lua* h, uint32_t* nlayers);
+int  bf_lua_export_layer(bf_lua* h, uint32_t layer, uint8_t* buf, uint64_t cap, uint64_t* len_out);
+int  bf_lua_import_layer(bf_lua* h, uint32_t layer, const uint8_t* buf, uint64_t len);
+int  bf_lua_layer_params(double entries, double precision, uint32_t layer, uint64_t* bits, uint32_t* k);
+int  bf_lua_index(double entries, uint64_t count, uint32_t* layer);
+
 /* ---- sizing helpers with the facade's exact semantics (bloomfilter.rb:50-58) */
 int64_t bf_optimal_m(double n, double error_rate);
 int64_t bf_optimal_k(int64_t n, int64_t m_bits);     /* Integer n: floor division, 0 -> 1 */

@@ -7,16 +7,19 @@ name carries a hyphen).  Layout:
 * ``_lib.py``    ctypes binding of that ABI (no CPU fallback)
 * ``bloomfilter.py``  mirror of lib/redis/bloomfilter.rb (facade, sizing, driver lookup)
 * ``drivers/hip.py``  the ``hip`` driver (mirror of lib/bloomfilter_driver/ruby.rb's interface)
+* ``drivers/hip_lua.py``  the ``hip-lua`` driver (the Lua driver's scalable layout, lua.rb)
 * ``keys.py``    Ruby ``to_s`` key marshalling and packing
 * ``fakeredis.py``  in-memory Redis string-command model (no redis-server in this image)
 * ``distributed.py`` multi-GPU layer (replicated / partitioned filters over torch.distributed)
 * ``ruby/``      the Ruby-side drop-in (FFI driver) a maintainer adds to the gem
 """
-from ._lib import ArgumentError, BfHipError, BfHipUnavailable, Filter, version  # noqa: F401
+from ._lib import ArgumentError, BfHipError, BfHipUnavailable, Filter, LuaFilter, version  # noqa: F401
 from .bloomfilter import Bloomfilter, DRIVERS, VERSION, driver_name, register_driver  # noqa: F401
 from .drivers.hip import Hip  # noqa: F401
+from .drivers.hip_lua import HipLua  # noqa: F401
 from .fakeredis import FakeRedis  # noqa: F401
 from . import keys  # noqa: F401
 from . import distributed  # noqa: F401
 
 register_driver(Hip)
+register_driver(HipLua)

@@ -86,6 +86,20 @@ SIGNATURES = {
     "bf_combine_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_shard_export": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_shard_import": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
+    "bf_lua_create": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, ctypes.POINTER(bf_config),
+                                     ctypes.POINTER(_vp)]),
+    "bf_lua_destroy": (ctypes.c_int, [_vp]),
+    "bf_lua_last_error": (ctypes.c_char_p, [_vp]),
+    "bf_lua_insert_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64p]),
+    "bf_lua_include_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "bf_lua_clear": (ctypes.c_int, [_vp]),
+    "bf_lua_get_count": (ctypes.c_int, [_vp, _u64p]),
+    "bf_lua_set_count": (ctypes.c_int, [_vp, _u64]),
+    "bf_lua_layers": (ctypes.c_int, [_vp, _u32p]),
+    "bf_lua_export_layer": (ctypes.c_int, [_vp, _u32, _vp, _u64, _u64p]),
+    "bf_lua_import_layer": (ctypes.c_int, [_vp, _u32, _vp, _u64]),
+    "bf_lua_layer_params": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, _u32, _u64p, _u32p]),
+    "bf_lua_index": (ctypes.c_int, [ctypes.c_double, _u64, _u32p]),
     "bf_optimal_m": (ctypes.c_int64, [ctypes.c_double, ctypes.c_double]),
     "bf_optimal_k": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
 }
@@ -365,3 +379,110 @@ class Filter:
         buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
         _check(self._lib.bf_shard_import(self.handle, _ptr(buf), len(buf) if len(data) else 0, int(mode)),
                self._h)
+
+
+def lua_layer_params(entries, precision, layer: int) -> Tuple[int, int]:
+    """(bits, k) of layer `layer` of the Lua scalable filter (add.lua:16-25)."""
+    b, k = ctypes.c_uint64(), ctypes.c_uint32()
+    rc = load().bf_lua_layer_params(float(entries), float(precision), int(layer), ctypes.byref(b), ctypes.byref(k))
+    if rc:
+        raise ArgumentError("bf_lua_layer_params(%r, %r, %r) failed" % (entries, precision, layer))
+    return int(b.value), int(k.value)
+
+
+def lua_index(entries, count: int) -> int:
+    """The layer a count maps to (add.lua:13-15 / check.lua:9-11)."""
+    li = ctypes.c_uint32()
+    if load().bf_lua_index(float(entries), int(count), ctypes.byref(li)):
+        raise ArgumentError("bf_lua_index(%r, %r) failed" % (entries, count))
+    return int(li.value)
+
+
+def _lua_check(code: int, h=None) -> None:
+    if code == BF_OK:
+        return
+    msg = load().bf_lua_last_error(h).decode(errors="replace")
+    if code in (BF_EINVAL, BF_ERANGE):
+        raise ArgumentError("%s: %s" % (_STATUS.get(code), msg))
+    raise BfHipError(code, msg)
+
+
+class LuaFilter:
+    """The Lua driver's scalable filter on the device (a ``bf_lua*``; see include/bfhip.h)."""
+
+    def __init__(self, entries, precision, device: int = -1):
+        self._lib = load()
+        cfg = bf_config(ctypes.sizeof(bf_config), int(device), 0, 0, 1, 0, 0, 0)
+        h = _vp()
+        _lua_check(self._lib.bf_lua_create(float(entries), float(precision), ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.entries, self.precision = entries, precision
+
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.bf_lua_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        if not self._h:
+            raise ArgumentError("filter is closed")
+        return self._h
+
+    def insert_many(self, keys: np.ndarray, offsets: np.ndarray):
+        """-> (per-key new flags, sorted list of layers that got a new item)."""
+        keys, offsets, n = Filter._keys(keys, offsets)
+        pk = np.zeros(max(n, 1), np.uint8)
+        mask = ctypes.c_uint64(0)
+        _lua_check(self._lib.bf_lua_insert_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(pk),
+                                                ctypes.byref(mask)), self._h)
+        return pk[:n], [i + 1 for i in range(64) if mask.value >> i & 1]
+
+    def include_many(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        keys, offsets, n = Filter._keys(keys, offsets)
+        out = np.zeros(max(n, 1), np.uint8)
+        _lua_check(self._lib.bf_lua_include_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(out)), self._h)
+        return out[:n]
+
+    def clear(self) -> None:
+        _lua_check(self._lib.bf_lua_clear(self.handle), self._h)
+
+    @property
+    def count(self) -> int:
+        c = ctypes.c_uint64()
+        _lua_check(self._lib.bf_lua_get_count(self.handle, ctypes.byref(c)), self._h)
+        return int(c.value)
+
+    @count.setter
+    def count(self, value: int) -> None:
+        _lua_check(self._lib.bf_lua_set_count(self.handle, int(value)), self._h)
+
+    @property
+    def layers(self) -> int:
+        n = ctypes.c_uint32()
+        _lua_check(self._lib.bf_lua_layers(self.handle, ctypes.byref(n)), self._h)
+        return int(n.value)
+
+    def export_layer(self, layer: int) -> bytes:
+        n = ctypes.c_uint64(0)
+        _lua_check(self._lib.bf_lua_export_layer(self.handle, int(layer), None, 0, ctypes.byref(n)), self._h)
+        buf = np.zeros(max(n.value, 1), np.uint8)
+        _lua_check(self._lib.bf_lua_export_layer(self.handle, int(layer), _ptr(buf), len(buf), ctypes.byref(n)),
+                   self._h)
+        return buf[: n.value].tobytes()
+
+    def import_layer(self, layer: int, data: bytes) -> None:
+        buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+        _lua_check(self._lib.bf_lua_import_layer(self.handle, int(layer), _ptr(buf), len(data)), self._h)

@@ -1,0 +1,434 @@
+// bf_lua.hip — the Lua driver's scalable filter on the device
+// (lib/bloomfilter_driver/lua.rb, vendor/assets/lua/add.lua, check.lua).
+//
+// State, as in Redis: a count (KEYS[1]:count) and layers KEYS[1]:1 .. :N, each a
+// SETBIT-layout bitstring of bits_n bits.  Layer n has scale 2^(n-1) * entries,
+// bits_n = floor(-(scale * log(precision * 0.5^n)) / 0.4804530139182) and
+// k_n = floor(0.69314718055995 * bits_n / scale) (add.lua:16-25, check.lua:41-47);
+// probe i = 1 .. k_n is (h[i % 2] + i * h[2 + ((i + i % 2) % 4) / 2]) % bits_n over
+// the same SHA-1 words as the ruby driver (add.lua:30-41) — probe_offset with a
+// 1-based index.  An item goes to layer ceil(log(ceil((entries + count + 1) /
+// entries)) / 0.69314718055995) and bumps the count only if it set a new bit
+// (add.lua:6-17, 43-54); include? checks layers 1 .. index(count) (check.lua).
+//
+// insert_many keeps add.lua's sequential semantics exactly: per layer, the
+// sequential-flag kernels (bf_seq.hip) tell which keys would set a new bit, the
+// batch is cut where the count reaches the layer's capacity, the keys before the
+// cut are applied, and the rest continue on the next layer.
+#include "bfhip.h"
+#include "bf_device.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+using namespace bfdev;
+
+namespace {
+
+constexpr uint32_t kLuaMaxLayers = 64;
+constexpr int kLuaTile = 256;
+constexpr int kLuaStageVec = 16384 / 16;
+
+thread_local std::string g_lua_create_error;
+
+__global__ __launch_bounds__(kLuaTile) void lua_check_kernel(const BfGeom* __restrict__ layers, uint32_t nlayers,
+                                                             const uint8_t* __restrict__ keys16,
+                                                             const uint64_t* __restrict__ offsets, uint64_t bias,
+                                                             uint64_t n, uint8_t* __restrict__ out) {
+    __shared__ uint64_t s_off[kLuaTile + 1];
+    __shared__ uint4 s_stage[kLuaStageVec + kStageSlackVec];
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kLuaTile;
+    const uint32_t cnt = (uint32_t)((n - tile0) < (uint64_t)kLuaTile ? (n - tile0) : kLuaTile);
+    for_key_tile<kLuaTile, kLuaStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage,
+        [&](auto staged, uint32_t lane, const uint32_t* src, uint32_t s, uint32_t L) {
+            uint32_t H[5];
+            sha1_any<decltype(staged)::value>(src, s, L, H);
+            uint32_t found = 0;
+            for (uint32_t li = 0; li < nlayers && !found; ++li) {   // check.lua:38-59
+                const BfGeom g = layers[li];
+                uint32_t ok = 1;
+                for (uint32_t i = 1; i <= g.k && ok; ++i) {
+                    const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i);
+                    ok = (g.bits[o >> 5] >> ((uint32_t)(o ^ 7u) & 31u)) & 1u;
+                }
+                found = ok;
+            }
+            out[tile0 + lane] = (uint8_t)found;
+        });
+}
+
+}  // namespace
+
+struct bf_lua {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    double entries = 0, precision = 0;
+    uint64_t count = 0;
+    std::vector<BfGeom> layers;   // layers[n - 1]: bitset of layer n (allocated on first use)
+    std::vector<uint64_t> layer_bytes;
+    BfGeom* d_layers = nullptr;   // device copy of the layer table for lua_check_kernel
+    void* scratch = nullptr;
+    uint64_t scratch_cap = 0;
+    uint8_t *d_keys = nullptr, *d_out = nullptr, *h_out = nullptr;
+    uint64_t* d_off = nullptr;
+    uint64_t keys_cap = 0, n_cap = 0;
+    unsigned long long* d_last = nullptr;
+    std::string err;
+};
+
+namespace {
+
+int lua_err(bf_lua* h, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf; else g_lua_create_error = buf;
+    return code;
+}
+
+#define LUACHK(h, expr)                                                                            \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return lua_err((h), (e_ == hipErrorOutOfMemory ? BF_ENOMEM : BF_EDEVICE), "%s failed: %s", \
+                           #expr, hipGetErrorString(e_));                                          \
+    } while (0)
+
+struct LuaDeviceGuard {
+    int prev = -1;
+    explicit LuaDeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~LuaDeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// add.lua:13-15 / check.lua:9-11, in IEEE double like Lua 5.1's numbers.
+uint32_t lua_index(double entries, double count) {
+    const double factor = std::ceil((entries + count) / entries);
+    return (uint32_t)std::ceil(std::log(factor) / 0.69314718055995);
+}
+
+// add.lua:16-25 (check.lua:41-47 computes the same values).
+void lua_layer(double entries, double precision, uint32_t n, uint64_t* bits, uint32_t* k) {
+    const double scale = std::pow(2.0, (double)n - 1.0) * entries;
+    const double b = std::floor(-(scale * std::log(precision * std::pow(0.5, (double)n))) / 0.4804530139182);
+    const double kk = std::floor(0.69314718055995 * b / scale);
+    *bits = b > 0 ? (uint64_t)b : 0;
+    *k = kk > 0 ? (uint32_t)kk : 0;
+}
+
+// Largest count whose insert still lands in `layer` (counts c with index(c) == layer).
+uint64_t lua_layer_capacity(double entries, uint32_t layer, uint64_t from) {
+    uint64_t lo = from, step = 1;
+    while (lua_index(entries, (double)(lo + step)) <= layer) {
+        lo += step;
+        step <<= 1;
+    }
+    uint64_t hi = lo + step;   // index(hi) > layer >= index(lo)
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (lua_index(entries, (double)mid) <= layer) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+int ensure_layer(bf_lua* h, uint32_t n) {
+    if (n == 0 || n > kLuaMaxLayers) return lua_err(h, BF_EINVAL, "layer %u outside 1..%u", n, kLuaMaxLayers);
+    while (h->layers.size() < n) {
+        const uint32_t li = (uint32_t)h->layers.size() + 1;
+        uint64_t m;
+        uint32_t k;
+        lua_layer(h->entries, h->precision, li, &m, &k);
+        if (m == 0 || k == 0 || k > BF_MAX_K)
+            return lua_err(h, BF_EINVAL, "layer %u: %llu bits, %u hashes (entries %g, precision %g)", li,
+                           (unsigned long long)m, k, h->entries, h->precision);
+        BfGeom g{};
+        const uint64_t bytes = ((m + 7) / 8 + 255) / 256 * 256;
+        LUACHK(h, hipMalloc((void**)&g.bits, bytes));
+        LUACHK(h, hipMemsetAsync(g.bits, 0, bytes, h->stream));
+        g.m = m;
+        g.inv_m = 1.0 / (double)m;
+        g.k = k;
+        g.nomod = m > (uint64_t)(k + 1) * 0xFFFFFFFFull ? 1u : 0u;   // probes i = 1..k: v <= (k+1)(2^32-1)
+        g.mod_f32 = m >= (1ull << 17) ? 1u : 0u;
+        g.inv_m_f = (float)(1.0 / (double)m);
+        g.shards = 1;
+        g.block_log2 = 20;
+        h->layers.push_back(g);
+        h->layer_bytes.push_back(bytes);
+    }
+    return BF_OK;
+}
+
+int ensure_io(bf_lua* h, uint64_t key_bytes, uint64_t n) {
+    if (key_bytes + 16 > h->keys_cap) {
+        if (h->d_keys) (void)hipFree(h->d_keys);
+        h->d_keys = nullptr;
+        h->keys_cap = std::max<uint64_t>(key_bytes + 16, 1 << 16) * 2;
+        LUACHK(h, hipMalloc((void**)&h->d_keys, h->keys_cap));
+    }
+    if (n + 1 > h->n_cap) {
+        if (h->d_off) (void)hipFree(h->d_off);
+        if (h->d_out) (void)hipFree(h->d_out);
+        if (h->h_out) (void)hipHostFree(h->h_out);
+        h->d_off = nullptr;
+        h->d_out = nullptr;
+        h->h_out = nullptr;
+        h->n_cap = std::max<uint64_t>(n + 1, 1 << 12) * 2;
+        LUACHK(h, hipMalloc((void**)&h->d_off, h->n_cap * 8));
+        LUACHK(h, hipMalloc((void**)&h->d_out, h->n_cap));
+        LUACHK(h, hipHostMalloc((void**)&h->h_out, h->n_cap, hipHostMallocDefault));
+    }
+    return BF_OK;
+}
+
+int ensure_lua_scratch(bf_lua* h, uint64_t bytes) {
+    if (bytes <= h->scratch_cap) return BF_OK;
+    LUACHK(h, hipStreamSynchronize(h->stream));
+    if (h->scratch) (void)hipFree(h->scratch);
+    h->scratch = nullptr;
+    h->scratch_cap = 0;
+    LUACHK(h, hipMalloc(&h->scratch, bytes));
+    h->scratch_cap = bytes;
+    return BF_OK;
+}
+
+// Keys to the device (offsets rebased to 0), 16-byte aligned with slack.
+int stage_keys(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n) {
+    for (uint64_t j = 0; j < n; ++j)
+        if (offsets[j + 1] < offsets[j]) return lua_err(h, BF_EINVAL, "offsets must be non-decreasing (j=%llu)",
+                                                        (unsigned long long)j);
+    const uint64_t base = offsets[0], nbytes = offsets[n] - offsets[0];
+    int rc = ensure_io(h, nbytes, n);
+    if (rc) return rc;
+    std::vector<uint64_t> rebased(n + 1);
+    for (uint64_t j = 0; j <= n; ++j) rebased[j] = offsets[j] - base;
+    if (nbytes) LUACHK(h, hipMemcpyAsync(h->d_keys, keys + base, nbytes, hipMemcpyHostToDevice, h->stream));
+    LUACHK(h, hipMemsetAsync(h->d_keys + nbytes, 0, 16, h->stream));
+    LUACHK(h, hipMemcpyAsync(h->d_off, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, h->stream));
+    LUACHK(h, hipStreamSynchronize(h->stream));   // `rebased` is freed on return
+    return BF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bf_lua_layer_params(double entries, double precision, uint32_t layer, uint64_t* bits, uint32_t* k) {
+    if (!(entries > 0) || !(precision > 0) || layer == 0) return BF_EINVAL;
+    uint64_t b;
+    uint32_t kk;
+    lua_layer(entries, precision, layer, &b, &kk);
+    if (bits) *bits = b;
+    if (k) *k = kk;
+    return BF_OK;
+}
+
+int bf_lua_index(double entries, uint64_t count, uint32_t* layer) {
+    if (!(entries > 0) || !layer) return BF_EINVAL;
+    *layer = lua_index(entries, (double)count);
+    return BF_OK;
+}
+
+int bf_lua_create(double entries, double precision, const bf_config* cfg, bf_lua** out) {
+    if (!out) return lua_err(nullptr, BF_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (!(entries > 0) || !(precision > 0) || !(precision < 1))
+        return lua_err(nullptr, BF_EINVAL, "entries must be > 0 and precision in (0, 1) (got %g, %g)", entries,
+                       precision);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return lua_err(nullptr, BF_EDEVICE, "no HIP device available");
+    int dev = (cfg && cfg->struct_size >= 8) ? cfg->device : -1;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev >= ndev) return lua_err(nullptr, BF_EINVAL, "device %d out of range (%d devices)", dev, ndev);
+    bf_lua* h = new (std::nothrow) bf_lua();
+    if (!h) return lua_err(nullptr, BF_ENOMEM, "host allocation failed");
+    h->device = dev;
+    h->entries = entries;
+    h->precision = precision;
+    LuaDeviceGuard dg(dev);
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&h->d_layers, kLuaMaxLayers * sizeof(BfGeom)) != hipSuccess ||
+        hipMalloc((void**)&h->d_last, 64) != hipSuccess) {
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+        if (h->d_layers) (void)hipFree(h->d_layers);
+        delete h;
+        return lua_err(nullptr, BF_EDEVICE, "stream / table allocation failed");
+    }
+    *out = h;
+    return BF_OK;
+}
+
+int bf_lua_destroy(bf_lua* h) {
+    if (!h) return BF_OK;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        LuaDeviceGuard dg(h->device);
+        (void)hipStreamSynchronize(h->stream);
+        for (BfGeom& g : h->layers) (void)hipFree(g.bits);
+        for (void* p : {(void*)h->d_layers, (void*)h->scratch, (void*)h->d_keys, (void*)h->d_out, (void*)h->d_off,
+                        (void*)h->d_last})
+            if (p) (void)hipFree(p);
+        if (h->h_out) (void)hipHostFree(h->h_out);
+        (void)hipStreamDestroy(h->stream);
+    }
+    delete h;
+    return BF_OK;
+}
+
+const char* bf_lua_last_error(const bf_lua* h) { return h ? h->err.c_str() : g_lua_create_error.c_str(); }
+
+int bf_lua_get_count(const bf_lua* h, uint64_t* count) {
+    if (!h || !count) return BF_EINVAL;
+    *count = h->count;
+    return BF_OK;
+}
+
+int bf_lua_set_count(bf_lua* h, uint64_t count) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->count = count;
+    return BF_OK;
+}
+
+int bf_lua_layers(const bf_lua* h, uint32_t* nlayers) {
+    if (!h || !nlayers) return BF_EINVAL;
+    *nlayers = (uint32_t)h->layers.size();
+    return BF_OK;
+}
+
+int bf_lua_clear(bf_lua* h) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    LUACHK(h, hipStreamSynchronize(h->stream));
+    for (BfGeom& g : h->layers) (void)hipFree(g.bits);
+    h->layers.clear();
+    h->layer_bytes.clear();
+    h->count = 0;
+    return BF_OK;
+}
+
+int bf_lua_insert_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* per_key_new,
+                       uint64_t* new_layers) {
+    if (!h) return BF_EINVAL;
+    if (new_layers) *new_layers = 0;
+    if (n == 0) return BF_OK;
+    if (!offsets || (!keys && offsets[n] != offsets[0])) return lua_err(h, BF_EINVAL, "NULL keys / offsets");
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    int rc = stage_keys(h, keys, offsets, n);
+    if (rc) return rc;
+    uint64_t s = 0;
+    while (s < n) {
+        const uint32_t layer = lua_index(h->entries, (double)(h->count + 1));   // add.lua:6-15
+        if ((rc = ensure_layer(h, layer))) return rc;
+        const BfGeom& g = h->layers[layer - 1];
+        const uint64_t room = lua_layer_capacity(h->entries, layer, h->count + 1) - h->count;   // >= 1
+        const uint64_t cn = std::min<uint64_t>(n - s, bf_seq_chunk_keys(g.k));
+        if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, nullptr)))) return rc;
+        // which keys would set a new bit of this layer, in order (nothing applied yet)
+        LUACHK(h, bf_launch_seq_candidates(g, 1, h->d_keys, h->d_off + s, 0, cn, h->scratch, h->stream));
+        LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, h->d_out, nullptr, h->stream));
+        LUACHK(h, hipMemcpyAsync(h->h_out, h->d_out, cn, hipMemcpyDeviceToHost, h->stream));
+        LUACHK(h, hipStreamSynchronize(h->stream));
+        // cut after the key whose INCR fills the layer (add.lua:48-50); later keys go up a layer
+        uint64_t take = cn, fresh = 0;
+        for (uint64_t j = 0; j < cn; ++j) {
+            fresh += h->h_out[j];
+            if (fresh == room) {
+                take = j + 1;
+                break;
+            }
+        }
+        LUACHK(h, bf_launch_seq_mark(g, 1, cn, take, h->scratch, nullptr, nullptr, h->stream));
+        if (per_key_new) memcpy(per_key_new + s, h->h_out, take);
+        if (fresh && new_layers && layer <= 64) *new_layers |= 1ull << (layer - 1);
+        h->count += fresh;
+        s += take;
+    }
+    LUACHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* out) {
+    if (!h) return BF_EINVAL;
+    if (n == 0) return BF_OK;
+    if (!offsets || !out || (!keys && offsets[n] != offsets[0])) return lua_err(h, BF_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->count == 0) {   // check.lua:3-7
+        memset(out, 0, n);
+        return BF_OK;
+    }
+    LuaDeviceGuard dg(h->device);
+    const uint32_t index = lua_index(h->entries, (double)h->count);   // check.lua:9-11
+    int rc = ensure_layer(h, index);
+    if (rc) return rc;
+    if ((rc = stage_keys(h, keys, offsets, n))) return rc;
+    LUACHK(h, hipMemcpyAsync(h->d_layers, h->layers.data(), index * sizeof(BfGeom), hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(lua_check_kernel, dim3((uint32_t)((n + kLuaTile - 1) / kLuaTile)), dim3(kLuaTile), 0,
+                       h->stream, h->d_layers, index, h->d_keys, h->d_off, (uint64_t)0, n, h->d_out);
+    LUACHK(h, hipGetLastError());
+    LUACHK(h, hipMemcpyAsync(out, h->d_out, n, hipMemcpyDeviceToHost, h->stream));
+    LUACHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+int bf_lua_export_layer(bf_lua* h, uint32_t layer, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+    if (!h || !len_out) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    *len_out = 0;
+    if (layer == 0 || layer > h->layers.size()) return BF_OK;   // a layer never written: absent key
+    LuaDeviceGuard dg(h->device);
+    const BfGeom& g = h->layers[layer - 1];
+    LUACHK(h, hipMemsetAsync(h->d_last, 0, 8, h->stream));
+    LUACHK(h, bf_launch_last_nonzero(g.bits, h->layer_bytes[layer - 1] / 4, h->d_last, h->stream));
+    unsigned long long last = 0;
+    LUACHK(h, hipMemcpyAsync(&last, h->d_last, 8, hipMemcpyDeviceToHost, h->stream));
+    LUACHK(h, hipStreamSynchronize(h->stream));
+    uint64_t len = 0;
+    if (last) {   // trim inside the last nonzero word
+        uint8_t w[4];
+        LUACHK(h, hipMemcpy(w, reinterpret_cast<const uint8_t*>(g.bits) + (last - 1) * 4, 4, hipMemcpyDeviceToHost));
+        len = (last - 1) * 4 + 4;
+        while (len > (last - 1) * 4 && w[len - (last - 1) * 4 - 1] == 0) --len;
+    }
+    *len_out = len;
+    if (!buf) return BF_OK;
+    if (cap < len) return lua_err(h, BF_ERANGE, "buffer of %llu bytes, layer string is %llu", (unsigned long long)cap,
+                                  (unsigned long long)len);
+    if (len) LUACHK(h, hipMemcpy(buf, g.bits, len, hipMemcpyDeviceToHost));
+    return BF_OK;
+}
+
+int bf_lua_import_layer(bf_lua* h, uint32_t layer, const uint8_t* buf, uint64_t len) {
+    if (!h || (len && !buf)) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    int rc = ensure_layer(h, layer);
+    if (rc) return rc;
+    const BfGeom& g = h->layers[layer - 1];
+    const uint64_t full = (g.m + 7) / 8;
+    if (len > full) return lua_err(h, BF_EINVAL, "layer %u string of %llu bytes exceeds %llu", layer,
+                                   (unsigned long long)len, (unsigned long long)full);
+    if (len == full && (g.m & 7) && (buf[len - 1] & (0xFF >> (g.m & 7))))
+        return lua_err(h, BF_EINVAL, "layer %u string sets bits at or beyond %llu", layer, (unsigned long long)g.m);
+    LUACHK(h, hipMemsetAsync(g.bits, 0, h->layer_bytes[layer - 1], h->stream));
+    if (len) LUACHK(h, hipMemcpyAsync(g.bits, buf, len, hipMemcpyHostToDevice, h->stream));
+    LUACHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+}  // extern "C"

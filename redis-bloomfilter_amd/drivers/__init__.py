@@ -1,4 +1,5 @@
 """Driver plugins (the ``Redis::BloomfilterDriver`` namespace)."""
 from .hip import Hip
+from .hip_lua import HipLua
 
-__all__ = ["Hip"]
+__all__ = ["Hip", "HipLua"]

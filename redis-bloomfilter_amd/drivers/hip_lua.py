@@ -1,0 +1,118 @@
+"""``Redis::BloomfilterDriver::HipLua`` — the Lua driver's scalable filter on the GPU.
+
+``driver: 'hip-lua'`` resolves here (``driver_name`` capitalises each dash-separated
+part, bloomfilter.rb:77-79).  It keeps the Redis layout of lib/bloomfilter_driver/lua.rb
+and vendor/assets/lua/add.lua / check.lua, so the Lua driver and this one read each
+other's filters:
+
+* ``KEYS[1]:count`` — the number of items that set a new bit (add.lua:5-11, 48-50);
+* ``KEYS[1]:n``     — layer n's bitstring in SETBIT layout (add.lua:17, 38).
+
+The layers live in HBM (``bf_lua*``, include/bfhip.h).  Attaching (``driver.redis =
+r``) loads the count and every layer key; ``sync='write_through'`` (default) writes
+the layers an insert touched back with SETRANGE and the count with SET, then EXPIREs
+those layers when ``expire`` is given (add.lua:51-53); ``sync='manual'`` leaves Redis
+alone until ``flush()``.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List
+
+import numpy as np
+
+from .. import keys as _keys
+from .._lib import ArgumentError, LuaFilter, lua_index
+
+
+class HipLua:
+    SYNC_MODES = ("write_through", "manual")
+
+    def __init__(self, options: dict):
+        self.options = options
+        entries, precision = options.get("size"), options.get("error_rate")
+        if entries is None or precision is None:
+            raise ArgumentError("options[:size] and options[:error_rate] are required")
+        self.sync_mode = options.get("sync", "write_through")
+        if self.sync_mode not in self.SYNC_MODES:
+            raise ArgumentError("sync must be one of %s" % (self.SYNC_MODES,))
+        # ARGV[1], ARGV[2] reach Lua as strings and are read back as numbers (add.lua:1-2)
+        self.entries, self.precision = float(entries), float(precision)
+        self.filter = LuaFilter(self.entries, self.precision, device=options.get("device", -1))
+        self._redis = None
+
+    @property
+    def redis(self):
+        return self._redis
+
+    @redis.setter
+    def redis(self, r):
+        self._redis = r
+        if r is not None:
+            self.reload()
+
+    @property
+    def key_name(self) -> str:
+        return self.options["key_name"]
+
+    def _layer_key(self, n: int) -> str:
+        return "%s:%d" % (self.key_name, n)
+
+    # -- lua.rb:19-21 (add.lua)
+    def insert(self, data, expire=None):
+        return self.insert_many([data], expire)
+
+    def insert_many(self, keys: Iterable, expire=None) -> np.ndarray:
+        """Insert in order, as one EVALSHA per key would; returns each key's INCR flag."""
+        buf, offs = _keys.pack(keys)
+        pk, touched = self.filter.insert_many(buf, offs)
+        if touched and self._redis is not None and self.sync_mode == "write_through":
+            self._write(touched)
+            if expire:
+                for n in touched:
+                    self._redis.expire(self._layer_key(n), expire)
+        return pk.astype(bool)
+
+    # -- lua.rb:23-26 (check.lua)
+    def include(self, key) -> bool:
+        return bool(self.include_many([key])[0])
+
+    def include_many(self, keys: Iterable) -> np.ndarray:
+        buf, offs = _keys.pack(keys)
+        return self.filter.include_many(buf, offs).astype(bool)
+
+    # -- lua.rb:28-30
+    def clear(self):
+        self.filter.clear()
+        if self._redis is not None:
+            for k in self._redis.keys("%s:*" % self.key_name):
+                self._redis.delete(k)
+
+    # -- Redis sync
+    def _write(self, layers: List[int]) -> None:
+        for n in layers:
+            data = self.filter.export_layer(n)
+            if data:
+                self._redis.setrange(self._layer_key(n), 0, data)
+        self._redis.set("%s:count" % self.key_name, str(self.filter.count))
+
+    def flush(self) -> None:
+        """Write every layer and the count to Redis."""
+        if self._redis is not None:
+            self._write(list(range(1, self.filter.layers + 1)))
+
+    def reload(self) -> None:
+        """Replace the device layers with the Redis keys' values."""
+        if self._redis is None:
+            return
+        self.filter.clear()
+        raw = self._redis.get("%s:count" % self.key_name)
+        count = int(raw) if raw is not None else 0
+        self.filter.count = count
+        if count:
+            for n in range(1, lua_index(self.entries, count) + 1):
+                data = self._redis.get(self._layer_key(n))
+                if data:
+                    self.filter.import_layer(n, bytes(data))
+
+    def close(self):
+        self.filter.close()

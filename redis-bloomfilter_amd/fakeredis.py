@@ -147,6 +147,16 @@ class FakeRedis:
                 return b""
             return bytes(buf[start:end + 1])
 
+    def incr(self, name, amount: int = 1) -> int:
+        """INCR / INCRBY: a missing key counts from 0; the TTL is kept."""
+        k = self._key(name)
+        with self._lock:
+            self.calls.append(("INCR", k))
+            cur = int(self._data[k].decode()) if self._alive(k) else 0
+            cur += int(amount)
+            self._data[k] = bytearray(str(cur).encode())
+            return cur
+
     def strlen(self, name) -> int:
         k = self._key(name)
         with self._lock:

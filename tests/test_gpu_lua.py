@@ -1,0 +1,96 @@
+"""The Lua driver's scalable layout on the GPU against the restated
+scripts (oracle/lua_oracle.py: vendor/assets/lua/add.lua, check.lua) run over
+FakeRedis: the count, every layer's Redis string, each key's INCR flag and every
+include? answer must match exactly.
+"""
+import lua_oracle as L
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def script_run(pkg, keys, entries, precision, key="lbf", r=None):
+    r = r or pkg.FakeRedis()
+    flags = [L.add(r, key, entries, precision, k) for k in keys]
+    return r, np.array(flags, dtype=bool)
+
+
+def layers_of(r, key):
+    out = {}
+    n = 1
+    while r.exists("%s:%d" % (key, n)):
+        out[n] = r.get("%s:%d" % (key, n))
+        n += 1
+    return out
+
+
+@pytest.mark.parametrize("entries,precision,nkeys,span,batches", [
+    (100, 0.01, 900, 700, 1),          # 4 layers, many repeats, one batch
+    (100, 0.01, 900, 700, 7),          # the same keys in uneven batches
+    (1000, 0.02, 5000, 10**9, 3),      # distinct keys, 3 layers
+    (50, 0.2, 2000, 3000, 2),          # tiny filter, low k, dense layers
+    (10_000, 0.001, 100_000, 10**12, 1),   # 4 layers of a bigger filter
+])
+def test_lua_insert_include_match_scripts(pkg, entries, precision, nkeys, span, batches):
+    rng = np.random.default_rng(11)
+    keys = [int(v) for v in rng.integers(0, span, nkeys)]
+    r, want_flags = script_run(pkg, keys, entries, precision)
+    cuts = np.linspace(0, nkeys, batches + 1).astype(int)
+    cuts[1:-1] += rng.integers(-7, 8, batches - 1) if batches > 1 else 0
+    got_flags = []
+    with pkg.LuaFilter(entries, precision) as f:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            buf, offs = pkg.keys.pack(keys[a:b])
+            pk, touched = f.insert_many(buf, offs)
+            got_flags.append(pk.astype(bool))
+        np.testing.assert_array_equal(np.concatenate(got_flags), want_flags)
+        assert f.count == int(r.get("lbf:count"))
+        want_layers = layers_of(r, "lbf")
+        assert f.layers == len(want_layers) and len(want_layers) >= 2
+        for n, s in want_layers.items():
+            assert f.export_layer(n) == s, n
+        probe = keys[: nkeys // 2] + ["fresh-%d" % i for i in range(nkeys // 2)]
+        pb, po = pkg.keys.pack(probe)
+        got = f.include_many(pb, po).astype(bool)
+        want = np.array([L.check(r, "lbf", entries, precision, k) for k in probe])
+        np.testing.assert_array_equal(got, want)
+        assert got[: nkeys // 2].all()
+
+
+def test_hip_lua_driver_write_through_and_interop(pkg):
+    """The driver's Redis keys equal the scripts' after the same inserts (lua.rb layout), a
+    driver attached to the scripts' Redis answers like check.lua, and clear drops name:*."""
+    rng = np.random.default_rng(12)
+    keys = ["w%d" % v for v in rng.integers(0, 400, 500)]
+    mine = pkg.FakeRedis()
+    bf = pkg.Bloomfilter(size=100, error_rate=0.01, key_name="lbf", driver="hip-lua", redis=mine)
+    bf.insert_many(keys[:300])
+    bf.insert_many(keys[300:], 120)
+    r, _ = script_run(pkg, keys, 100, 0.01)
+    assert sorted(mine.keys("lbf:*")) == sorted(r.keys("lbf:*"))
+    for k in r.keys("lbf:*"):
+        assert mine.get(k) == r.get(k), k
+    top = "lbf:%d" % len(layers_of(r, "lbf"))
+    assert mine.ttl(top) > 0                      # add.lua:51-53 EXPIREs the layer written to
+    other = pkg.Bloomfilter(size=100, error_rate=0.01, key_name="lbf", driver="hip-lua", redis=r)
+    probe = keys[:100] + ["nope%d" % i for i in range(200)]
+    np.testing.assert_array_equal(other.include_many(probe),
+                                  [L.check(r, "lbf", 100, 0.01, k) for k in probe])
+    bf.clear()
+    assert mine.keys("lbf:*") == [] and not bf.include("w1")
+
+
+def test_spec_scalable_filter_via_hip_lua(pkg):
+    """spec/redis_bloomfilter_spec.rb:122-128 with driver 'hip-lua'."""
+    bf = pkg.Bloomfilter(size=100, error_rate=0.02, key_name="__test_bf", driver="hip-lua", redis=pkg.FakeRedis())
+    bf.clear()
+    rng = np.random.default_rng(13)
+    visited, errors = set(), 0
+    for _ in range(150):
+        a = int(rng.integers(0, 150))
+        errors += bf.include(a) != (a in visited)
+        visited.add(a)
+        bf.insert(a)
+    assert errors / 150 <= bf.options["error_rate"]
+    bf.clear()
