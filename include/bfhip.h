@@ -128,6 +128,20 @@ int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
  * The choice never changes results; BFHIP_INSERT_BINNED=0/1 forces it. */
 int  bf_insert_plan(const bf_handle* h, uint64_t n, uint32_t* binned, uint64_t* scratch_bytes);
 
+/* ---- incremental Redis sync.  With tracking on, every insert
+ *      (direct, binned and sequential paths) marks the BF_DIRTY_BLOCK_BYTES blocks
+ *      of the Redis string it may have changed; imports mark everything; bf_clear
+ *      forgets it all (the driver DELs the key).  bf_dirty_ranges returns the
+ *      changed byte ranges (offset, length pairs; adjacent blocks coalesced, clipped
+ *      to the string's trimmed length *redis_len, so SETRANGE of each range grows the
+ *      key exactly as the SETBITs would have) and, with clear != 0, forgets them;
+ *      ranges == NULL only counts.  Whole-filter handles only. */
+#define BF_DIRTY_BLOCK_BYTES 65536
+int  bf_track_dirty(bf_handle* h, uint32_t enable);
+int  bf_dirty_ranges(bf_handle* h, uint64_t* ranges /* 2*cap */, uint32_t cap, uint32_t* n_out,
+                     uint64_t* redis_len /* nullable */, uint32_t clear);
+int  bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf);
+
 /* ---- per-kernel timing.  While enabled, every keyed launch (insert / include? /
  *      indexes, host or device API) records HIP events on its stream between its
  *      kernels; bf_profile_read waits for them and returns, per kernel name, the

@@ -13,7 +13,8 @@ name carries a hyphen).  Layout:
 * ``distributed.py`` multi-GPU layer (replicated / partitioned filters over torch.distributed)
 * ``ruby/``      the Ruby-side drop-in (FFI driver) a maintainer adds to the gem
 """
-from ._lib import ArgumentError, BfHipError, BfHipUnavailable, Filter, LuaFilter, version  # noqa: F401
+from ._lib import (ArgumentError, BF_IMPORT_OR, BF_IMPORT_REPLACE, BfHipError, BfHipUnavailable,  # noqa: F401
+                   DIRTY_BLOCK_BYTES, Filter, LuaFilter, version)
 from .bloomfilter import Bloomfilter, DRIVERS, VERSION, driver_name, register_driver  # noqa: F401
 from .drivers.hip import Hip  # noqa: F401
 from .drivers.hip_lua import HipLua  # noqa: F401

@@ -10,7 +10,7 @@ import ctypes
 import os
 import sys
 import threading
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -22,6 +22,7 @@ BF_IMPORT_REPLACE, BF_IMPORT_OR = 0, 1
 BF_FLAG_ROUTE32 = 1
 BF_MAX_K = 64
 PROFILE_NAME_LEN = 64   # BF_PROFILE_NAME_LEN
+DIRTY_BLOCK_BYTES = 65536   # BF_DIRTY_BLOCK_BYTES
 
 _STATUS = {BF_EINVAL: "BF_EINVAL", BF_ENOMEM: "BF_ENOMEM", BF_EDEVICE: "BF_EDEVICE",
            BF_ERCCL: "BF_ERCCL", BF_ERANGE: "BF_ERANGE"}
@@ -75,6 +76,9 @@ SIGNATURES = {
     "bf_indexes_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_device_bits": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), _u64p]),
     "bf_insert_plan": (ctypes.c_int, [_vp, _u64, _u32p, _u64p]),
+    "bf_track_dirty": (ctypes.c_int, [_vp, _u32]),
+    "bf_dirty_ranges": (ctypes.c_int, [_vp, _u64p, _u32, _u32p, _u64p, _u32]),
+    "bf_export_range": (ctypes.c_int, [_vp, _u64, _u64, _vp]),
     "bf_profile": (ctypes.c_int, [_vp, _u32]),
     "bf_profile_read": (ctypes.c_int, [_vp, _vp, _vp, _vp, _u32, _u32p, _u32]),
     "bf_sync": (ctypes.c_int, [_vp]),
@@ -297,6 +301,31 @@ class Filter:
     def import_redis(self, data: bytes, mode: int = BF_IMPORT_REPLACE) -> None:
         buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
         _check(self._lib.bf_import_redis(self.handle, _ptr(buf), len(data), int(mode)), self._h)
+
+    # -- incremental Redis sync
+    def track_dirty(self, enable: bool = True) -> None:
+        """Record which BF_DIRTY_BLOCK_BYTES blocks of the Redis string inserts change."""
+        _check(self._lib.bf_track_dirty(self.handle, 1 if enable else 0), self._h)
+
+    def dirty_ranges(self, clear: bool = True) -> Tuple[List[Tuple[int, int]], int]:
+        """([(byte offset, length), ...], Redis string length) changed since the last clear."""
+        n, rl = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(self._lib.bf_dirty_ranges(self.handle, None, 0, ctypes.byref(n), ctypes.byref(rl), 0), self._h)
+        while True:
+            cap = max(n.value, 1)
+            buf = np.zeros(2 * cap, np.uint64)
+            rc = self._lib.bf_dirty_ranges(self.handle, buf.ctypes.data_as(_u64p), cap, ctypes.byref(n),
+                                           ctypes.byref(rl), 1 if clear else 0)
+            if rc == BF_ERANGE and n.value > cap:   # an insert on another thread grew the set
+                continue
+            _check(rc, self._h)
+            pairs = buf[: 2 * n.value].reshape(-1, 2)
+            return [(int(o), int(l)) for o, l in pairs], int(rl.value)
+
+    def export_range(self, offset: int, length: int) -> bytes:
+        buf = np.zeros(max(int(length), 1), np.uint8)
+        _check(self._lib.bf_export_range(self.handle, int(offset), int(length), _ptr(buf)), self._h)
+        return buf[: int(length)].tobytes()
 
     # -- device-resident API
     def insert_many_dev(self, d_keys: int, d_offsets: int, n: int, d_any_new: int = 0,

@@ -68,6 +68,9 @@ struct bf_handle {
     uint32_t* d_flag = nullptr;
     unsigned long long* d_scan = nullptr;
     uint32_t* h_flag = nullptr;   // pinned
+    // incremental Redis sync (bf_track_dirty): one byte per BF_DIRTY_BLOCK_BYTES of the string
+    uint8_t* d_dirty = nullptr;
+    uint64_t dirty_blocks = 0;
     // per-kernel timing (bf_profile): event sets awaiting harvest, recycled sets, totals
     bool profile = false;
     std::vector<BfMarks> prof_pending, prof_free;
@@ -551,6 +554,7 @@ int bf_destroy(bf_handle* h) {
         if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
         if (h->d_cursor) (void)hipFree(h->d_cursor);
         if (h->d_bin_scratch) (void)hipFree(h->d_bin_scratch);
+        if (h->d_dirty) (void)hipFree(h->d_dirty);
         (void)prof_harvest(h);   // waits for marks recorded on caller streams
         for (BfMarks& mk : h->prof_free)
             for (hipEvent_t e : mk.ev) (void)hipEventDestroy(e);
@@ -606,6 +610,7 @@ int bf_clear(bf_handle* h) {
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
+    if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 0, h->dirty_blocks, h->stream));   // the driver DELs the key
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return BF_OK;
 }
@@ -656,6 +661,7 @@ int import_bytes(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode, 
         if (buf[len - 1] & beyond)
             return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)max_bits);
     }
+    if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 1, h->dirty_blocks, h->stream));
     if (mode == BF_IMPORT_REPLACE) {
         HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -911,6 +917,76 @@ int bf_profile_read(bf_handle* h, char* names, double* total_ms, uint64_t* launc
         if (launches) launches[i] = a.launches;
     }
     if (reset) h->prof_acc.clear();
+    return BF_OK;
+}
+
+int bf_track_dirty(bf_handle* h, uint32_t enable) {
+    if (!h) return BF_EINVAL;
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "dirty tracking needs a whole-filter handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    HIPCHK(h, hipDeviceSynchronize());   // no launch may still use the map
+    if (!enable) {
+        if (h->d_dirty) (void)hipFree(h->d_dirty);
+        h->d_dirty = nullptr;
+        h->dirty_blocks = 0;
+        h->g.dirty = nullptr;
+        return BF_OK;
+    }
+    if (!h->d_dirty) {
+        h->dirty_blocks = (h->dev_bytes + BF_DIRTY_BLOCK_BYTES - 1) / BF_DIRTY_BLOCK_BYTES;
+        HIPCHK(h, hipMalloc((void**)&h->d_dirty, h->dirty_blocks));
+    }
+    HIPCHK(h, hipMemset(h->d_dirty, 0, h->dirty_blocks));
+    h->g.dirty = h->d_dirty;
+    return BF_OK;
+}
+
+int bf_dirty_ranges(bf_handle* h, uint64_t* ranges, uint32_t cap, uint32_t* n_out, uint64_t* redis_len,
+                    uint32_t clear) {
+    if (!h || !n_out) return BF_EINVAL;
+    if (!h->d_dirty) return set_err(h, BF_EINVAL, "dirty tracking is off (bf_track_dirty)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    HIPCHK(h, hipDeviceSynchronize());   // inserts may have run on any stream
+    std::vector<uint8_t> map(h->dirty_blocks);
+    HIPCHK(h, hipMemcpy(map.data(), h->d_dirty, h->dirty_blocks, hipMemcpyDeviceToHost));
+    uint64_t len = 0;
+    int rc = device_trimmed_len(h, &len);
+    if (rc) return rc;
+    if (redis_len) *redis_len = len;
+    // adjacent dirty blocks coalesce; everything is clipped to the string's length, so
+    // SETRANGE grows the key exactly as the SETBITs would have
+    std::vector<uint64_t> out;
+    for (uint64_t b = 0; b < h->dirty_blocks;) {
+        if (!map[b]) { ++b; continue; }
+        uint64_t e = b;
+        while (e < h->dirty_blocks && map[e]) ++e;
+        const uint64_t off = b * BF_DIRTY_BLOCK_BYTES;
+        const uint64_t end = std::min<uint64_t>(e * BF_DIRTY_BLOCK_BYTES, len);
+        if (end > off) { out.push_back(off); out.push_back(end - off); }
+        b = e;
+    }
+    *n_out = (uint32_t)(out.size() / 2);
+    if (ranges) {
+        if (*n_out > cap) return set_err(h, BF_ERANGE, "%u dirty ranges, room for %u", *n_out, cap);
+        memcpy(ranges, out.data(), out.size() * sizeof(uint64_t));
+    }
+    if (clear && (ranges || *n_out == 0)) HIPCHK(h, hipMemset(h->d_dirty, 0, h->dirty_blocks));
+    return BF_OK;
+}
+
+int bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf) {
+    if (!h || (len && !buf)) return BF_EINVAL;
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_export");
+    if (offset > h->dev_bytes || len > h->dev_bytes - offset)
+        return set_err(h, BF_ERANGE, "range [%llu, +%llu) outside the %llu-byte bitset", (unsigned long long)offset,
+                       (unsigned long long)len, (unsigned long long)h->dev_bytes);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    HIPCHK(h, hipDeviceSynchronize());
+    if (len) HIPCHK(h, hipMemcpy(buf, reinterpret_cast<const uint8_t*>(h->g.bits) + offset, len,
+                                 hipMemcpyDeviceToHost));
     return BF_OK;
 }
 

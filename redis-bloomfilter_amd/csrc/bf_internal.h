@@ -22,7 +22,7 @@ struct BfGeom {
                             // insert may have changed the block (bf_track_dirty)
 };
 
-constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = 64 KiB of the Redis string
+constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = BF_DIRTY_BLOCK_BYTES of the string
 
 enum BfOp : int {
     BF_OP_INDEXES      = 0,  // write the k offsets of each key (ruby.rb:41-55)

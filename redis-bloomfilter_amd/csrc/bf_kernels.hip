@@ -91,6 +91,7 @@ __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uin
 #pragma unroll
             for (int c = 0; c < kChunk; ++c) {
                 if (mask[c] && !(v[c] & mask[c])) {
+                    if (g.dirty) g.dirty[w[c] >> (kDirtyShiftBits - 5)] = 1;   // bf_track_dirty
                     if constexpr (OP == BF_OP_INSERT_FLAGS) {
                         const uint32_t old = __hip_atomic_fetch_or(g.bits + w[c], mask[c], __ATOMIC_RELAXED,
                                                                    __HIP_MEMORY_SCOPE_AGENT);

@@ -9,11 +9,13 @@ HBM (one ``bf_handle``); Redis keeps the same bitstring the ruby driver writes:
   imported (a filter written by the ruby driver is readable here) and its TTL
   is mirrored;
 * ``sync='write_through'`` (default): an insert that flips a bit writes the
-  trimmed device string back with SETRANGE (keeps the key's TTL, grows it like
-  SETBIT would), then EXPIREs when ``expire`` is given — ruby.rb:61-62;
+  64 KiB blocks of the string it changed back with SETRANGE (keeps the key's
+  TTL, grows it like SETBIT would), then EXPIREs when ``expire`` is given —
+  ruby.rb:61-62.  The device keeps a dirty-block map (``bf_track_dirty``), so a
+  small batch into a multi-GB filter writes kilobytes, not the whole string;
 * ``sync='manual'``: Redis is only touched by ``clear`` (DEL) and by explicit
-  ``flush()`` / ``reload()``; meant for batch jobs on filters too large for a
-  per-call write-back;
+  ``flush()`` / ``reload()``; ``flush()`` writes what changed since the last
+  one (``flush(full=True)``: the whole string);
 * TTL: the device copy is cleared when the mirrored EXPIRE deadline passes,
   as the Redis key would have vanished (README.md usage, ruby.rb:62).
 
@@ -49,6 +51,7 @@ class Hip:
         self.filter = Filter(m, k, device=options.get("device", -1),
                              batch_keys=options.get("batch_keys", 0),
                              batch_bytes=options.get("batch_bytes", 0))
+        self.filter.track_dirty(True)
         self._redis = None
         self._deadline: Optional[float] = None
 
@@ -113,12 +116,24 @@ class Hip:
             self._redis.delete(self.key_name)
 
     # -- Redis sync
-    def flush(self) -> int:
-        """Write the device filter to Redis (SETRANGE 0: keeps TTL, grows like SETBIT)."""
-        data = self.filter.export_redis()
-        if data and self._redis is not None:
-            self._redis.setrange(self.key_name, 0, data)
-        return len(data)
+    def flush(self, full: bool = False) -> int:
+        """Write the device filter's changes to Redis; returns the bytes sent.
+
+        SETRANGE per changed range keeps the TTL and grows the key like SETBIT would
+        (the ranges are clipped to the trimmed string).  ``full``: the whole string."""
+        ranges, _ = self.filter.dirty_ranges(clear=self._redis is not None)
+        if self._redis is None:
+            return 0
+        if full:
+            data = self.filter.export_redis()
+            if data:
+                self._redis.setrange(self.key_name, 0, data)
+            return len(data)
+        sent = 0
+        for off, n in ranges:
+            self._redis.setrange(self.key_name, off, self.filter.export_range(off, n))
+            sent += n
+        return sent
 
     def reload(self) -> None:
         """Replace the device filter with the Redis key's current value."""
@@ -130,6 +145,7 @@ class Hip:
             self.filter.clear()
             return
         self.filter.import_redis(bytes(data), BF_IMPORT_REPLACE)
+        self.filter.dirty_ranges(clear=True)   # device == Redis now
         ttl = self._redis.ttl(self.key_name) if hasattr(self._redis, "ttl") else -1
         if ttl is not None and ttl > 0:
             self._deadline = self._clock() + ttl

@@ -38,6 +38,7 @@ class FakeRedis:
         self._max = max_string
         self._lock = threading.RLock()
         self.calls: List[Tuple[str, str]] = []   # (command, key) log for tests
+        self.bytes_in = 0                        # payload bytes received by SET/SETRANGE
 
     # -- internals
     def _key(self, name) -> str:
@@ -114,6 +115,7 @@ class FakeRedis:
             raise ResponseError("ERR string exceeds maximum allowed size (proto-max-bulk-len)")
         with self._lock:
             self.calls.append(("SET", k))
+            self.bytes_in += len(v)
             self._data[k] = bytearray(v)
             self._exp.pop(k, None)
             return True
@@ -123,6 +125,7 @@ class FakeRedis:
         v = value.encode() if isinstance(value, str) else bytes(value)
         with self._lock:
             self.calls.append(("SETRANGE", k))
+            self.bytes_in += len(v)
             alive = self._alive(k)
             if not v:
                 return len(self._data[k]) if alive else 0
