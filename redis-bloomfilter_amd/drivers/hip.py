@@ -19,8 +19,16 @@ HBM (one ``bf_handle``); Redis keeps the same bitstring the ruby driver writes:
 * TTL: the device copy is cleared when the mirrored EXPIRE deadline passes,
   as the Redis key would have vanished (README.md usage, ruby.rb:62).
 
+Strings beyond one request: every write is cut into SETRANGE calls of at most
+``chunk_bytes`` (default 8 MiB) and a key longer than that is read back with
+GETRANGE chunks, so a multi-GB filter moves through a server whose
+``proto-max-bulk-len`` admits the whole string without any one huge request
+(stock Redis caps strings at 512 MB and raises for larger offsets, as SETBIT
+would).
+
 Extra options (all optional): ``device`` (HIP ordinal, default current),
-``sync``, ``batch_keys`` / ``batch_bytes`` (host staging chunk sizes).
+``sync``, ``batch_keys`` / ``batch_bytes`` (host staging chunk sizes),
+``chunk_bytes`` (Redis request size).
 """
 from __future__ import annotations
 
@@ -52,6 +60,9 @@ class Hip:
                              batch_keys=options.get("batch_keys", 0),
                              batch_bytes=options.get("batch_bytes", 0))
         self.filter.track_dirty(True)
+        self.chunk_bytes = int(options.get("chunk_bytes", 8 << 20))
+        if self.chunk_bytes <= 0:
+            raise ArgumentError("chunk_bytes must be positive")
         self._redis = None
         self._deadline: Optional[float] = None
 
@@ -121,25 +132,24 @@ class Hip:
 
         SETRANGE per changed range keeps the TTL and grows the key like SETBIT would
         (the ranges are clipped to the trimmed string).  ``full``: the whole string."""
-        ranges, _ = self.filter.dirty_ranges(clear=self._redis is not None)
+        ranges, rlen = self.filter.dirty_ranges(clear=self._redis is not None)
         if self._redis is None:
             return 0
         if full:
-            data = self.filter.export_redis()
-            if data:
-                self._redis.setrange(self.key_name, 0, data)
-            return len(data)
+            ranges = [(0, rlen)] if rlen else []
         sent = 0
         for off, n in ranges:
-            self._redis.setrange(self.key_name, off, self.filter.export_range(off, n))
-            sent += n
+            for c in range(off, off + n, self.chunk_bytes):
+                ln = min(self.chunk_bytes, off + n - c)
+                self._redis.setrange(self.key_name, c, self.filter.export_range(c, ln))
+                sent += ln
         return sent
 
     def reload(self) -> None:
         """Replace the device filter with the Redis key's current value."""
         if self._redis is None:
             return
-        data = self._redis.get(self.key_name)
+        data = self._read_key()
         self._deadline = None
         if data is None:
             self.filter.clear()
@@ -149,6 +159,17 @@ class Hip:
         ttl = self._redis.ttl(self.key_name) if hasattr(self._redis, "ttl") else -1
         if ttl is not None and ttl > 0:
             self._deadline = self._clock() + ttl
+
+    def _read_key(self):
+        """GET, or GETRANGE chunks for a key longer than ``chunk_bytes``."""
+        n = self._redis.strlen(self.key_name) if hasattr(self._redis, "strlen") else 0
+        if n <= self.chunk_bytes:
+            return self._redis.get(self.key_name)
+        buf = bytearray(n)
+        for c in range(0, n, self.chunk_bytes):
+            part = self._redis.getrange(self.key_name, c, min(c + self.chunk_bytes, n) - 1)
+            buf[c:c + len(part)] = part
+        return bytes(buf)
 
     def to_redis_string(self) -> bytes:
         return self.filter.export_redis()

@@ -12,12 +12,16 @@
 # work.  Redis keeps the same bitstring the ruby driver writes (SETBIT layout,
 # MSB-first), so the two drivers read each other's filters:
 #   * attaching (`redis=`) imports an existing key and its TTL;
-#   * sync: :write_through (default) writes the device string back with
-#     SETRANGE after an insert that flipped a bit (SETRANGE keeps the TTL and
-#     grows the string exactly like SETBIT), then EXPIREs iff a bit flipped and
-#     an expire was given (ruby.rb:61-62);
-#   * sync: :manual leaves Redis alone until #flush.
-# Extra options: :device (HIP ordinal), :sync, :batch_keys, :batch_bytes.
+#   * sync: :write_through (default) writes back, with one SETRANGE per range,
+#     the 64 KiB blocks of the string an insert changed (the device's dirty-block
+#     map, bf_track_dirty; SETRANGE keeps the TTL and grows the string exactly
+#     like SETBIT), then EXPIREs iff a bit flipped and an expire was given
+#     (ruby.rb:61-62);
+#   * sync: :manual leaves Redis alone until #flush (changes since the last one).
+# Every write is cut into SETRANGE calls of at most :chunk_bytes (default 8 MiB)
+# and a longer key is read back with GETRANGE chunks, so multi-GB filters move
+# through a server whose proto-max-bulk-len admits them (SURVEY §8 f2).
+# Extra options: :device (HIP ordinal), :sync, :batch_keys, :batch_bytes, :chunk_bytes.
 require 'ffi'
 
 class Redis
@@ -47,6 +51,9 @@ class Redis
       attach_function :bf_clear, [:pointer], :int, blocking: true
       attach_function :bf_export_redis, %i[pointer pointer uint64 pointer], :int, blocking: true
       attach_function :bf_import_redis, %i[pointer pointer uint64 uint32], :int, blocking: true
+      attach_function :bf_track_dirty, %i[pointer uint32], :int, blocking: true
+      attach_function :bf_dirty_ranges, %i[pointer pointer uint32 pointer pointer uint32], :int, blocking: true
+      attach_function :bf_export_range, %i[pointer uint64 uint64 pointer], :int, blocking: true
     end
 
     class Hip
@@ -69,6 +76,9 @@ class Redis
         out = FFI::MemoryPointer.new(:pointer)
         check(HipFFI.bf_create(bits, options[:hashes], cfg, out), nil)
         @handle = FFI::AutoPointer.new(out.read_pointer, HipFFI.method(:bf_destroy))
+        check(HipFFI.bf_track_dirty(@handle, 1))
+        @chunk = options.fetch(:chunk_bytes, 8 << 20)
+        raise ArgumentError, 'chunk_bytes must be positive' unless @chunk.positive?
         @deadline = nil
       end
 
@@ -120,16 +130,45 @@ class Redis
         @redis&.del(@options[:key_name])
       end
 
-      # Device filter -> Redis (SETRANGE 0: keeps the TTL, grows like SETBIT).
-      def flush
-        str = export
-        @redis.setrange(@options[:key_name], 0, str) if @redis && !str.empty?
-        str.bytesize
+      # Device changes -> Redis, one SETRANGE per dirty range (keeps the TTL, grows
+      # like SETBIT); full: true sends the whole string.  Returns the bytes sent.
+      def flush(full: false)
+        ranges = dirty_ranges(clear: !@redis.nil?)
+        return 0 unless @redis
+
+        if full
+          n = export_len
+          ranges = n.positive? ? [[0, n]] : []
+        end
+        ranges.sum do |off, len|
+          (off...(off + len)).step(@chunk).sum do |c|
+            n = [@chunk, off + len - c].min
+            buf = FFI::MemoryPointer.new(:uint8, n)
+            check(HipFFI.bf_export_range(@handle, c, n, buf))
+            @redis.setrange(@options[:key_name], c, buf.read_bytes(n))
+            n
+          end
+        end
+      end
+
+      # [[byte offset, length], ...] changed since the last clear (bf_dirty_ranges).
+      def dirty_ranges(clear: true)
+        n = FFI::MemoryPointer.new(:uint32)
+        loop do
+          check(HipFFI.bf_dirty_ranges(@handle, nil, 0, n, nil, 0))
+          cap = [n.read_uint32, 1].max
+          out = FFI::MemoryPointer.new(:uint64, 2 * cap)
+          rc = HipFFI.bf_dirty_ranges(@handle, out, cap, n, nil, clear ? 1 : 0)
+          next if rc == HipFFI::BF_ERANGE && n.read_uint32 > cap   # grew meanwhile
+
+          check(rc)
+          return out.read_array_of_uint64(2 * n.read_uint32).each_slice(2).to_a
+        end
       end
 
       # Redis -> device filter (replace).
       def reload
-        str = @redis.get(@options[:key_name])
+        str = read_key
         @deadline = nil
         if str.nil?
           check(HipFFI.bf_clear(@handle))
@@ -138,20 +177,34 @@ class Redis
         mem = FFI::MemoryPointer.new(:uint8, [str.bytesize, 1].max)
         mem.put_bytes(0, str)
         check(HipFFI.bf_import_redis(@handle, mem, str.bytesize, HipFFI::BF_IMPORT_REPLACE))
+        dirty_ranges(clear: true)   # device == Redis now
         ttl = @redis.ttl(@options[:key_name])
         @deadline = now + ttl if ttl.positive?
       end
 
       def export
-        len = FFI::MemoryPointer.new(:uint64)
-        check(HipFFI.bf_export_redis(@handle, nil, 0, len))
-        n = len.read_uint64
+        n = export_len
         buf = FFI::MemoryPointer.new(:uint8, [n, 1].max)
         check(HipFFI.bf_export_redis(@handle, buf, n, len))
         buf.read_bytes(n)
       end
 
       private
+
+      def export_len
+        len = FFI::MemoryPointer.new(:uint64)
+        check(HipFFI.bf_export_redis(@handle, nil, 0, len))
+        len.read_uint64
+      end
+
+      # GET, or GETRANGE chunks for a key longer than :chunk_bytes.
+      def read_key
+        key = @options[:key_name]
+        n = @redis.strlen(key)
+        return @redis.get(key) if n <= @chunk
+
+        (0...n).step(@chunk).map { |c| @redis.getrange(key, c, [c + @chunk, n].min - 1) }.join.b
+      end
 
       # `data.to_s` bytes (ruby.rb:42), packed as (bytes, uint64 offsets[n+1]).
       def pack(keys)

@@ -123,6 +123,32 @@ def test_driver_write_through_sends_only_changed_blocks(pkg, oracle):
     assert r.get("big") is None
 
 
+def test_chunked_sync_beyond_512mb(pkg):
+    """A 750 MB filter through a server whose proto-max-bulk-len admits it: writes go out as
+    SETRANGE calls of <= chunk_bytes, a new driver reads the key back with GETRANGE chunks;
+    stock Redis (512 MB cap) refuses the string as it would refuse the SETBITs."""
+    chunk = 64 << 20
+    r = pkg.FakeRedis(max_string=1 << 30)
+    opts = {"size": 626_000_000, "error_rate": 0.01, "key_name": "huge", "redis": r, "driver": "hip",
+            "chunk_bytes": chunk}
+    bf = pkg.Bloomfilter(dict(opts))
+    keys = np.arange(1 << 20, dtype=np.int64) * 7919
+    r.calls.clear()
+    bf.insert_many(keys)
+    s = bf.driver.to_redis_string()
+    assert len(s) > 600 << 20
+    n_set = sum(1 for c, _ in r.calls if c == "SETRANGE")
+    assert n_set >= len(s) // chunk and r.get("huge") == s
+    other = pkg.Bloomfilter(dict(opts))                    # attach: GETRANGE chunks
+    assert sum(1 for c, _ in r.calls if c == "GETRANGE") >= len(s) // chunk
+    assert other.driver.to_redis_string() == s
+    assert other.include_many(keys[:5000]).all()
+    stock = pkg.FakeRedis()
+    small = pkg.Bloomfilter(dict(opts, redis=stock, key_name="huge2"))
+    with pytest.raises(pkg.fakeredis.ResponseError):
+        small.insert_many(keys)
+
+
 def test_manual_sync_flushes_changes_since_last_flush(pkg):
     r = pkg.FakeRedis()
     bf = pkg.Bloomfilter({"size": 10_000_000, "error_rate": 0.01, "key_name": "man", "redis": r,

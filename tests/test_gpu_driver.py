@@ -156,7 +156,8 @@ def test_batched_api_matches_single(pkg):
     assert [bf.include(int(x)) for x in keys[9990:10010]] == inc[9990:10010].tolist()
 
 
-def test_scalable_baseline_row_is_out_of_scope(pkg):
-    """spec:122-128 tests the lua driver's scalable layout: not a hip-driver behaviour."""
+def test_lua_driver_name_is_not_registered(pkg):
+    """spec:122-128's scalable layout runs on the GPU as driver 'hip-lua' (tests/test_gpu_lua.py);
+    'lua' (the EVALSHA driver, lua.rb) stays the reference's own and resolves to nothing here."""
     with pytest.raises(NameError):
         factory(pkg, {"size": 100, "error_rate": 0.02, "key_name": "x"}, driver="lua")
