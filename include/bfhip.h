@@ -80,6 +80,13 @@ typedef struct bf_config {
 /* bf_config.flags */
 #define BF_FLAG_ROUTE32 1u     /* routed owner-local offsets (d_send / d_local) are uint32, halving the
                                   all-to-all bytes; needs every shard's local_bits <= 2^32 (else BF_EINVAL) */
+/* The RubyTest driver's hash engines (lib/bloomfilter_driver/ruby_test.rb:43-61), instead of
+ * the ruby driver's derivation: offset of probe i = MD5 / SHA-1 hexdigest of "#{i}-#{key}"
+ * read as one 128 / 160-bit integer, mod m.  Offsets cover all of [0, m) (no reach cap).
+ * Whole-filter handles only; per_key_new is refused (BF_EINVAL).  crc32 has no flag: the
+ * reference's engine_crc32 raises at its first call (Integer#to_i takes no radix, :52). */
+#define BF_FLAG_ENGINE_MD5  2u
+#define BF_FLAG_ENGINE_SHA1 4u
 
 /* ---- lifecycle */
 int  bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out);

@@ -21,6 +21,7 @@ Reference lines restated (paths relative to the reference repository):
   lib/bloomfilter_driver/ruby.rb:15-17,57-63  insert / set (EXPIRE iff !found && expire)
   lib/bloomfilter_driver/ruby.rb:20-30  include?
   lib/bloomfilter_driver/ruby.rb:33-35  clear (DEL)
+  lib/bloomfilter_driver/ruby_test.rb:43-61  the RubyTest hash engines (py_engine_indexes)
 """
 from __future__ import annotations
 
@@ -90,6 +91,31 @@ def py_indexes(key, m: int, k: int) -> List[int]:
     """ruby.rb:41-55 ``indexes_for`` (pure Python, arbitrary precision like Ruby)."""
     h = py_digest_words(ruby_to_s(key))
     return [(h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) // 2)]) % m for i in range(k)]
+
+
+RFC1321_MD5 = {   # RFC 1321 appendix A.5 test suite
+    "": "d41d8cd98f00b204e9800998ecf8427e",
+    "a": "0cc175b9c0f1b6a831c399e269772661",
+    "abc": "900150983cd24fb0d6963f7d28e17f72",
+    "message digest": "f96b697d7cb7938d525a2f31aaf161d0",
+    "abcdefghijklmnopqrstuvwxyz": "c3fcd3d76192e4007dfb496cca67e13b",
+    "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789": "d174ab98d277d9f5a5611c2c9f419d9f",
+    "1234567890" * 8: "57edf4a22be3c955ac49da2e2107b67a",
+}
+
+
+def py_engine_indexes(key, m: int, k: int, engine: str) -> List[int]:
+    """ruby_test.rb:43-61: ``Digest::<E>.hexdigest("#{i}-#{data}").to_i(16) % bits`` for
+    i in 0...k, ``data`` = ``key.to_s``; crc32 (``:52``) raises, as ``Integer#to_i(16)`` does."""
+    if engine == "crc32":
+        raise ArgumentError_("wrong number of arguments (given 1, expected 0)")
+    f = {"md5": hashlib.md5, "sha1": hashlib.sha1}[engine]
+    data = ruby_to_s(key)
+    return [int(f(b"%d-" % i + data).hexdigest(), 16) % m for i in range(k)]
+
+
+class ArgumentError_(Exception):
+    """Ruby's ArgumentError, raised by the restated engine_crc32."""
 
 
 def reach_bits(m: int, k: int) -> int:

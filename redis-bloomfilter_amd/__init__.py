@@ -14,13 +14,15 @@ name carries a hyphen).  Layout:
 * ``ruby/``      the Ruby-side drop-in (FFI driver) a maintainer adds to the gem
 """
 from ._lib import (ArgumentError, BF_IMPORT_OR, BF_IMPORT_REPLACE, BfHipError, BfHipUnavailable,  # noqa: F401
-                   DIRTY_BLOCK_BYTES, Filter, LuaFilter, version)
+                   BF_FLAG_ENGINE_MD5, BF_FLAG_ENGINE_SHA1, DIRTY_BLOCK_BYTES, Filter, LuaFilter, version)
 from .bloomfilter import Bloomfilter, DRIVERS, VERSION, driver_name, register_driver  # noqa: F401
 from .drivers.hip import Hip  # noqa: F401
 from .drivers.hip_lua import HipLua  # noqa: F401
+from .drivers.hip_test import HipTest  # noqa: F401
 from .fakeredis import FakeRedis  # noqa: F401
 from . import keys  # noqa: F401
 from . import distributed  # noqa: F401
 
 register_driver(Hip)
 register_driver(HipLua)
+register_driver(HipTest)

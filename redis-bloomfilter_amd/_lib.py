@@ -20,6 +20,7 @@ DEFAULT_LIB = os.path.join(PKG_DIR, "lib", "libbfhip.so")
 BF_OK, BF_EINVAL, BF_ENOMEM, BF_EDEVICE, BF_ERCCL, BF_ERANGE = 0, 1, 2, 3, 4, 5
 BF_IMPORT_REPLACE, BF_IMPORT_OR = 0, 1
 BF_FLAG_ROUTE32 = 1
+BF_FLAG_ENGINE_MD5, BF_FLAG_ENGINE_SHA1 = 2, 4   # RubyTest hash engines (ruby_test.rb:43-61)
 BF_MAX_K = 64
 PROFILE_NAME_LEN = 64   # BF_PROFILE_NAME_LEN
 DIRTY_BLOCK_BYTES = 65536   # BF_DIRTY_BLOCK_BYTES

@@ -50,6 +50,7 @@ struct bf_handle {
     uint32_t shards = 1, shard_index = 0, block_log2 = 20;
     uint32_t mem_kind = 0;   // bitset allocation: 0 coarse-grained, 1 uncached, 2 fine-grained
     bool route32 = false;    // BF_FLAG_ROUTE32
+    uint32_t engine = BF_ENGINE_RUBY;   // BF_FLAG_ENGINE_*: the RubyTest hash engines
     uint64_t local_bits = 0;
     // routing scratch (grown on demand)
     uint64_t* d_tmp_local = nullptr;
@@ -194,7 +195,7 @@ int check_keys_args(bf_handle* h, const void* keys, const uint64_t* offsets, uin
 // per probe) clearly exceed one streaming pass over a bitset that lives beyond L2.
 bool use_binned(const bf_handle* h, uint64_t n, bool include, BfBinPlan* plan) {
     const uint32_t mode = include ? h->include_binned_mode : h->binned_mode;
-    if (mode == 0 || h->shards > 1) return false;
+    if (mode == 0 || h->shards > 1 || h->engine != BF_ENGINE_RUBY) return false;
     if (!bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, include, plan)) return false;
     if (mode == 1) return true;
     return h->dev_bytes >= (64ull << 20) &&
@@ -264,6 +265,15 @@ const char* op_kernel_name(BfOp op) {
 // Every keyed launch goes through here: inserts take the binned path when it pays.
 int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, uint64_t bias, uint64_t n,
               uint8_t* out8, uint64_t* out64, uint32_t* flag, hipStream_t s) {
+    if (h->engine != BF_ENGINE_RUBY) {   // RubyTest engines: one fused direct kernel per op
+        if (op == BF_OP_INSERT_FLAGS && out8)
+            return set_err(h, BF_EINVAL, "per_key_new is not available with a RubyTest hash engine");
+        if (op == BF_OP_INSERT_FLAGS) op = BF_OP_INSERT;
+        BfMarks* mk = prof_begin(h, s);
+        HIPCHK(h, bf_launch_engine(h->engine, op, h->g, k16, offs, bias, n, out8, out64, flag, s));
+        bf_mark(mk, s, h->engine == BF_ENGINE_MD5 ? "engine_kernel<MD5>" : "engine_kernel<SHA1>");
+        return BF_OK;
+    }
     if (op == BF_OP_INSERT_FLAGS && out8) {
         // Per-key flags: exact sequential semantics (bf_seq.hip), chunk after chunk in stream order.
         const uint64_t chunk = bf_seq_chunk_keys(h->k);
@@ -465,7 +475,13 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->m = m_bits;
     h->k = k;
     const uint64_t maxval = (uint64_t)k * 0xFFFFFFFFull;      // largest offset ruby.rb:51 can produce
-    h->reach = std::min<uint64_t>(m_bits, maxval + 1);
+    const uint32_t eng = c.flags & (BF_FLAG_ENGINE_MD5 | BF_FLAG_ENGINE_SHA1);
+    if (eng == (BF_FLAG_ENGINE_MD5 | BF_FLAG_ENGINE_SHA1) || (eng && c.shard_count > 1)) {
+        delete h;
+        return set_err(nullptr, BF_EINVAL, "one hash engine per filter, whole-filter handles only");
+    }
+    h->engine = eng == BF_FLAG_ENGINE_MD5 ? BF_ENGINE_MD5 : (eng ? BF_ENGINE_SHA1 : BF_ENGINE_RUBY);
+    h->reach = h->engine != BF_ENGINE_RUBY ? m_bits : std::min<uint64_t>(m_bits, maxval + 1);
     h->shards = c.shard_count > 1 ? c.shard_count : 1;
     h->shard_index = h->shards > 1 ? c.shard_index : 0;
     h->block_log2 = c.shard_block_log2 ? c.shard_block_log2 : 20;

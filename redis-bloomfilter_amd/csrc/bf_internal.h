@@ -41,6 +41,13 @@ hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const
                           uint32_t* any_flag, hipStream_t s,
                           unsigned long long* counts = nullptr /* BF_OP_ROUTE only */);
 
+// RubyTest hash engines (bf_engines.hip, ruby_test.rb:43-61): one lane per (key, probe),
+// offset = digest("#{i}-#{key}") as a big-endian integer mod m.  op: INDEXES, INCLUDE
+// (out8 preset to 1 inside) or INSERT (any_flag nullable).
+enum BfEngine : uint32_t { BF_ENGINE_RUBY = 0, BF_ENGINE_MD5 = 1, BF_ENGINE_SHA1 = 2 };
+hipError_t bf_launch_engine(uint32_t engine, BfOp op, const BfGeom& g, const uint8_t* k16, const uint64_t* offsets,
+                            uint64_t bias, uint64_t n, uint8_t* out8, uint64_t* out64, uint32_t* flag, hipStream_t s);
+
 // Binned insert (bf_binned.hip): plan + launch.  The launch carves every
 // intermediate (probe arrays, run tables, histograms) out of one device
 // scratch buffer of plan.scratch_bytes.

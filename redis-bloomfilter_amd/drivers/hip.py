@@ -58,13 +58,18 @@ class Hip:
         self._clock = options.get("clock", time.monotonic)
         self.filter = Filter(m, k, device=options.get("device", -1),
                              batch_keys=options.get("batch_keys", 0),
-                             batch_bytes=options.get("batch_bytes", 0))
+                             batch_bytes=options.get("batch_bytes", 0),
+                             flags=self._filter_flags())
         self.filter.track_dirty(True)
         self.chunk_bytes = int(options.get("chunk_bytes", 8 << 20))
         if self.chunk_bytes <= 0:
             raise ArgumentError("chunk_bytes must be positive")
         self._redis = None
         self._deadline: Optional[float] = None
+
+    def _filter_flags(self) -> int:
+        """bf_config.flags of the device filter (HipTest picks a hash engine here)."""
+        return 0
 
     # -- attr_accessor :redis (ruby.rb:9); attaching imports the existing key
     @property

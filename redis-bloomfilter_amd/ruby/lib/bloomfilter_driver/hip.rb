@@ -35,6 +35,8 @@ class Redis
       BF_EINVAL = 1
       BF_ERANGE = 5
       BF_IMPORT_REPLACE = 0
+      BF_FLAG_ENGINE_MD5 = 2
+      BF_FLAG_ENGINE_SHA1 = 4
 
       # struct bf_config (include/bfhip.h)
       class Config < FFI::Struct
@@ -73,6 +75,7 @@ class Redis
         cfg[:device] = options.fetch(:device, -1)
         cfg[:batch_keys] = options.fetch(:batch_keys, 0)
         cfg[:batch_bytes] = options.fetch(:batch_bytes, 0)
+        cfg[:flags] = config_flags
         out = FFI::MemoryPointer.new(:pointer)
         check(HipFFI.bf_create(bits, options[:hashes], cfg, out), nil)
         @handle = FFI::AutoPointer.new(out.read_pointer, HipFFI.method(:bf_destroy))
@@ -187,6 +190,13 @@ class Redis
         buf = FFI::MemoryPointer.new(:uint8, [n, 1].max)
         check(HipFFI.bf_export_redis(@handle, buf, n, len))
         buf.read_bytes(n)
+      end
+
+      protected
+
+      # bf_config.flags of the device filter (HipTest picks a hash engine here).
+      def config_flags
+        0
       end
 
       private

@@ -21,7 +21,24 @@ function indexes(buf, m, k) {
   return out;
 }
 
+// lib/bloomfilter_driver/ruby_test.rb:55-61: hexdigest("#{i}-#{data}").to_i(16) % bits
+function engineIndexes(engine, buf, m, k) {
+  const out = [];
+  for (let i = 0; i < k; ++i) {
+    const hex = crypto.createHash(engine).update(Buffer.concat([Buffer.from(i + '-'), buf])).digest('hex');
+    out.push((BigInt('0x' + hex) % BigInt(m)).toString());
+  }
+  return out;
+}
+
 let bad = 0;
+for (const [msg, want] of Object.entries(g.rfc1321_md5)) {
+  if (crypto.createHash('md5').update(Buffer.from(msg, 'latin1')).digest('hex') !== want) bad++;
+}
+for (const v of g.engine_indexes) {
+  const got = engineIndexes(v.engine, Buffer.from(v.key_hex, 'hex'), v.m, v.k);
+  if (got.join(',') !== v.idx.map(String).join(',')) { bad++; console.log('engine mismatch', v.engine, v.key_hex, v.m); }
+}
 for (const [msg, want] of Object.entries(g.fips_sha1)) {
   if (crypto.createHash('sha1').update(Buffer.from(msg, 'latin1')).digest('hex') !== want) bad++;
 }
@@ -45,6 +62,7 @@ for (const s of g.strings) {
   const sha = crypto.createHash('sha1').update(buf).digest('hex');
   if (sha !== s.redis_sha1 || buf.length !== s.redis_len) { bad++; console.log('string mismatch', s.name); }
 }
-console.log(bad === 0 ? 'node crosscheck ok (' + g.indexes.length + ' index vectors, ' + g.strings.length + ' strings)'
+console.log(bad === 0 ? 'node crosscheck ok (' + g.indexes.length + ' index vectors, ' + g.engine_indexes.length +
+                        ' engine vectors, ' + g.strings.length + ' strings)'
                       : 'node crosscheck FAILED: ' + bad);
 process.exit(bad === 0 ? 0 : 1);

@@ -155,3 +155,22 @@ def test_golden_file_is_current():
     out = subprocess.run(["python", os.path.join(HERE, "golden", "make_golden.py"), "--check"],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_rfc1321_md5(golden, O):
+    """The RubyTest engines' MD5 (ruby_test.rb:55-57) is RFC 1321's: its appendix A.5 suite."""
+    assert golden["rfc1321_md5"] == O.RFC1321_MD5
+    for msg, want in O.RFC1321_MD5.items():
+        assert hashlib.md5(msg.encode()).hexdigest() == want
+
+
+def test_golden_engine_indexes(golden, O):
+    """ruby_test.rb:43-61 restated (py_engine_indexes) against the committed vectors."""
+    assert len(golden["engine_indexes"]) == 448
+    for v in golden["engine_indexes"]:
+        got = O.py_engine_indexes(bytes.fromhex(v["key_hex"]), int(v["m"]), v["k"], v["engine"])
+        assert got == [int(x) for x in v["idx"]]
+    # hand-checkable anchor: probe 0 of "asdlol" = int(md5("0-asdlol")) mod m
+    assert O.py_engine_indexes("asdlol", 9585, 1, "md5") == [int(hashlib.md5(b"0-asdlol").hexdigest(), 16) % 9585]
+    with pytest.raises(O.ArgumentError_):
+        O.py_engine_indexes("x", 100, 3, "crc32")
