@@ -38,6 +38,23 @@ class Redis
       BF_FLAG_ENGINE_MD5 = 2
       BF_FLAG_ENGINE_SHA1 = 4
 
+      # `data.to_s` bytes (ruby.rb:42) of every key, packed as (bytes, uint64 offsets[n+1], n).
+      def self.pack(keys)
+        strs = keys.map { |k| k.to_s.b }
+        n = strs.size
+        buf = FFI::MemoryPointer.new(:uint8, [strs.sum(&:bytesize), 1].max)
+        offs = FFI::MemoryPointer.new(:uint64, n + 1)
+        pos = 0
+        offsets = [0]
+        strs.each do |s|
+          buf.put_bytes(pos, s) unless s.empty?
+          pos += s.bytesize
+          offsets << pos
+        end
+        offs.write_array_of_uint64(offsets)
+        [buf, offs, n]
+      end
+
       # struct bf_config (include/bfhip.h)
       class Config < FFI::Struct
         layout :struct_size, :uint32, :device, :int32, :batch_keys, :uint64, :batch_bytes, :uint64,
@@ -218,20 +235,7 @@ class Redis
 
       # `data.to_s` bytes (ruby.rb:42), packed as (bytes, uint64 offsets[n+1]).
       def pack(keys)
-        strs = keys.map { |k| k.to_s.b }
-        n = strs.size
-        total = strs.sum(&:bytesize)
-        buf = FFI::MemoryPointer.new(:uint8, [total, 1].max)
-        offs = FFI::MemoryPointer.new(:uint64, n + 1)
-        pos = 0
-        offsets = [0]
-        strs.each do |s|
-          buf.put_bytes(pos, s) unless s.empty?
-          pos += s.bytesize
-          offsets << pos
-        end
-        offs.write_array_of_uint64(offsets)
-        [buf, offs, n]
+        HipFFI.pack(keys)
       end
 
       def expire_if_due

@@ -31,13 +31,17 @@ def header_arity():
     return out
 
 
+RUBY_DRIVERS = os.path.join(ROOT, "redis-bloomfilter_amd", "ruby", "lib", "bloomfilter_driver")
+
+
 def test_ruby_ffi_binding_matches_header():
-    """redis-bloomfilter_amd/ruby/.../hip.rb attaches only declared functions, with the right arity
+    """redis-bloomfilter_amd/ruby/.../hip*.rb attach only declared functions, with the right arity
     (Ruby is not installed here, so this static check stands in for running it)."""
-    rb = open(os.path.join(ROOT, "redis-bloomfilter_amd", "ruby", "lib", "bloomfilter_driver", "hip.rb")).read()
+    rb = open(os.path.join(RUBY_DRIVERS, "hip.rb")).read()
+    lua_rb = open(os.path.join(RUBY_DRIVERS, "hip_lua.rb")).read()
     arity = header_arity()
-    attached = re.findall(r"attach_function :(bf_\w+),\s*(%i\[[^\]]*\]|\[[^\]]*\])", rb)
-    assert len(attached) >= 9
+    attached = re.findall(r"attach_function :(bf_\w+),\s*(%i\[[^\]]*\]|\[[^\]]*\])", rb + lua_rb)
+    assert len(attached) >= 24
     for name, args in attached:
         assert name in arity, name
         if args.startswith("%i["):
