@@ -120,7 +120,14 @@ uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // early-exit check (1B@1%: 1.82 -> 1.39 ms per 2^24 keys), insert loads the k
 // words and atomics only the unset bits (5.13 -> 3.30 ms).  The environment
 // overrides exist for A/B runs and never change results.
-uint32_t default_first_round(uint32_t k) { return (k + 3) / 4; }
+// include? probe rounds.  A bitset beyond the caches: one word at a time, stopping at the first
+// 0 bit (ruby.rb:23's early exit at every probe), so a non-member costs ~2 line fills instead of
+// ceil(k/4) + a round of the rest — 1B@1 % (k = 6) 1.45 -> 1.32 ms, 100M@0.1 % (k = 10)
+// 2.32 -> 2.01 ms per 2^24 keys (profiles/r01d_ab_rounds_*.json).  A cache-resident bitset is
+// latency-, not fill-bound: ceil(k/4) probes, then the rest at once (1M@1 %: 0.045 vs 0.049 ms).
+constexpr uint64_t kSequentialProbeBytes = 64ull << 20;
+uint32_t default_first_round(uint32_t k, uint64_t bytes) { return bytes > kSequentialProbeBytes ? 1 : (k + 3) / 4; }
+uint32_t default_next_round(uint64_t bytes) { return bytes > kSequentialProbeBytes ? 1 : 0; }
 constexpr uint32_t kDefaultInsertTest = 1;
 constexpr uint32_t kDefaultMemKind = 0;
 constexpr uint32_t kDefaultBinnedMode = 2;     // auto
@@ -546,7 +553,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
     h->g.route32 = h->route32 ? 1u : 0u;
-    h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k));
+    h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k, h->dev_bytes));
+    h->g.next_round = env_u32("BFHIP_INCLUDE_NEXT_ROUND", default_next_round(h->dev_bytes));
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);

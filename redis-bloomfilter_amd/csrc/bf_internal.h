@@ -16,6 +16,7 @@ struct BfGeom {
     uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
     // probe policies (tuning; results are identical for every setting)
     uint32_t  first_round;  // include?: probes loaded before the first early-exit check (0 = all k)
+    uint32_t  next_round;   // include?: probes per later round (0 = all the rest at once)
     uint32_t  insert_test;  // insert: 1 = load the k words first, atomic-OR only the unset bits
     uint32_t  route32;      // BF_FLAG_ROUTE32: routed owner-local offsets are uint32
     uint8_t*  dirty;        // nullable: one byte per 2^kDirtyShiftBits-bit block, set to 1 when an

@@ -67,7 +67,7 @@ __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uin
 #pragma unroll
             for (int c = 0; c < kChunk; ++c) ok &= v[c] >> sh[c];
             i0 = e;
-            rend = k;
+            rend = (g.next_round && i0 + g.next_round < k) ? i0 + g.next_round : k;
             if (!(ok & 1u)) break;
         }
         out8[key] = (uint8_t)(ok & 1u);
