@@ -151,7 +151,8 @@ def prefill_random(f, m: int, k: int, rank: int) -> np.ndarray:
     return host
 
 
-def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto"):
+def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto",
+                overlap: bool = True):
     n, p, batch, prefill = CONFIGS[name]
     B = pkg.Bloomfilter
     m = B.optimal_m(n, p)
@@ -194,8 +195,12 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             out.copy_(pf.include_many_dev(pkb, pko, batch))
 
     for bt in batches[:warmup]:
-        insert(bt)
-        include(bt)
+        if pf is None or not overlap:
+            insert(bt)
+            include(bt)
+        else:
+            (ikb, iko), (pkb, pko) = bt
+            out.copy_(pf.insert_include_dev(ikb, iko, batch, pkb, pko, batch))
     prof = pf.engine.filter if pf is not None else f
     prof.profile(True)      # per-kernel HIP events, recorded on the launch stream inside the timed region
     prof.profile_read(reset=True)
@@ -206,9 +211,14 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     for bt in batches[warmup:]:
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         e[0].record(stream)
-        insert(bt)
-        e[1].record(stream)
-        include(bt)
+        if pf is None or not overlap:
+            insert(bt)
+            e[1].record(stream)
+            include(bt)
+        else:   # partitioned: one overlapped insert + include? step (same results)
+            e[1].record(stream)
+            (ikb, iko), (pkb, pko) = bt
+            out.copy_(pf.insert_include_dev(ikb, iko, batch, pkb, pko, batch))
         e[2].record(stream)
         ev.append(e)
     torch.cuda.synchronize()
@@ -217,6 +227,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     wall = D.max(wall)
     ins_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     inc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    if pf is not None and overlap:   # the step is one overlapped unit: split it evenly for the per-op lines
+        ins_ms = inc_ms = (ins_ms + inc_ms) / 2
     kernels = {name: {"ms": tot / cnt, "launches": cnt} for name, (tot, cnt) in prof.profile_read(reset=True).items()}
     prof.profile(False)
     plan = f.insert_plan(batch) if pf is None else {"binned": False, "scratch_bytes": 0}
@@ -337,12 +349,14 @@ def main():
     ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
     ap.add_argument("--mode", default="auto", choices=["auto", "single", "partitioned"],
                     help="auto: single GPU at N=1, partitioned over the ranks at N>1")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="partitioned: run insert then include? as separate calls (no exchange overlap)")
     args = ap.parse_args()
 
     D = Dist(need_group=(args.mode == "partitioned"))
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
-                                  mode=args.mode)
+                                  mode=args.mode, overlap=not args.no_overlap)
     secondary = {}
     if D.world == 1 and not args.no_secondary:
         for name in ("1m", "100m"):

@@ -60,6 +60,7 @@ struct bf_handle {
     // binned-insert scratch (grown on demand) and policy: 0 never, 1 always, 2 auto
     uint32_t binned_mode = 2;
     uint32_t include_binned_mode = 2;   // the same policy for include?
+    uint32_t shard_test_binned_mode = 2;   // ... and for the owner-side test of routed probes
     uint32_t bin_region_log2 = 19;   // preferred region (LDS image) size of the apply pass
     void* d_bin_scratch = nullptr;   // digests, probe arrays and histograms of one binned launch
     uint64_t bin_scratch_cap = 0;
@@ -552,13 +553,16 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.inv_m_f = (float)(1.0 / (double)m_bits);
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
+    h->g.inv_shards = 1.0 / (double)h->shards;
     h->g.route32 = h->route32 ? 1u : 0u;
     h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k, h->dev_bytes));
     h->g.next_round = env_u32("BFHIP_INCLUDE_NEXT_ROUND", default_next_round(h->dev_bytes));
+    h->g.route_agg = env_u32("BFHIP_ROUTE_AGG", 1);   // P = 1 only: at P = 8 the per-owner loop costs more than the LDS atomics (sim_rank A/B)
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);
     h->include_binned_mode = env_u32("BFHIP_INCLUDE_BINNED", kDefaultIncludeBinnedMode);
+    h->shard_test_binned_mode = env_u32("BFHIP_SHARD_TEST_BINNED", 2);
     *out = h;
     return BF_OK;
 }
@@ -868,6 +872,32 @@ int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     hipStream_t s = pick_stream(h, stream);
+    // Binned like the shard insert: routed probes carry no early exit (all k arrive), so
+    // one streaming pass over the shard beats a random line fill per probe once the
+    // probes outnumber the shard's lines (same cost model and knob shape as the insert).
+    BfBinPlan plan;
+    const uint64_t sub = bf_binned_max_offsets();
+    const uint32_t mode = h->shard_test_binned_mode;
+    const bool binned = mode != 0 &&
+                        bf_binned_plan_offsets(h->dev_bytes, std::min(count, sub), h->bin_region_log2, &plan, true) &&
+                        (mode == 1 || (h->dev_bytes >= (64ull << 20) &&
+                                       (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
+    if (binned) {
+        const size_t esz = h->route32 ? 4 : 8;
+        for (uint64_t c0 = 0; c0 < count; c0 += sub) {
+            const uint64_t cn = std::min(sub, count - c0);
+            if (cn != std::min(count, sub) &&
+                !bf_binned_plan_offsets(h->dev_bytes, cn, h->bin_region_log2, &plan, true))
+                return set_err(h, BF_EINVAL, "binned plan failed for a tail of %llu offsets", (unsigned long long)cn);
+            int rc = ensure_scratch(h, plan.scratch_bytes);
+            if (rc) return rc;
+            BfMarks* mk = prof_begin(h, s);
+            HIPCHK(h, bf_launch_shard_test_binned(h->g, plan, h->dev_bytes,
+                                                  static_cast<const uint8_t*>(d_local) + c0 * esz, h->route32, cn,
+                                                  h->d_bin_scratch, d_bits + c0, s, mk));
+        }
+        return BF_OK;
+    }
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, h->route32, s));
     bf_mark(mk, s, "shard_test");

@@ -209,14 +209,18 @@ void bin_front_keys_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const u
 // Owner side of a partitioned filter: the probes arrive as shard-local offsets
 // (already hashed and routed), so the front pass only sorts them by superbin,
 // 12288 per tile, into the same level-1 layout bin_mid reads.
-template <typename Off>
-__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uint32_t tiles_per_block,
-                              uint32_t sup_log2, uint32_t nsup, uint32_t* __restrict__ level1,
-                              uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt) {
+// KEYS (the binned shard test): each offset carries its input position, so the test pass
+// can write the offset's answer byte.
+template <typename Off, bool KEYS>
+__device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ local, uint64_t count,
+                                                       uint32_t tiles_per_block, uint32_t sup_log2, uint32_t nsup,
+                                                       uint32_t* __restrict__ level1,
+                                                       uint32_t* __restrict__ level1_key,
+                                                       uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt) {
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_sorted[kTileProbes];
+    __shared__ uint32_t s_key[KEYS ? kTileProbes : 1];
     const uint32_t t = threadIdx.x;
     if (t < kMaxSup) {
         s_cnt[t] = 0;
@@ -255,24 +259,51 @@ void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uin
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kSlots; ++q)
-            if (tag[q] != 0xFFFFFFFFu) s_sorted[s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu)] = loc[q];
+            if (tag[q] != 0xFFFFFFFFu) {
+                const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
+                s_sorted[d] = loc[q];
+                if constexpr (KEYS) s_key[d] = (uint32_t)(p0 + (uint32_t)q * kTile + t);
+            }
         __syncthreads();
-        for (uint32_t j = t; j < tp; j += kTile) level1[p0 + j] = s_sorted[j];
+        for (uint32_t j = t; j < tp; j += kTile) {
+            level1[p0 + j] = s_sorted[j];
+            if constexpr (KEYS) level1_key[p0 + j] = s_key[j];
+        }
     }
     if (t < nsup) gcnt[(uint64_t)blockIdx.x * nsup + t] = s_gcnt[t];
 }
 
+template <typename Off>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uint32_t tiles_per_block,
+                              uint32_t sup_log2, uint32_t nsup, uint32_t* __restrict__ level1,
+                              uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt) {
+    bin_front_offsets_body<Off, false>(local, count, tiles_per_block, sup_log2, nsup, level1, nullptr, stab, gcnt);
+}
+
+// 100 KiB of LDS: one workgroup per CU
+template <typename Off>
+__global__ __launch_bounds__(kTile) void bin_front_offsets_keys_kernel(const Off* __restrict__ local, uint64_t count,
+                                                                       uint32_t tiles_per_block, uint32_t sup_log2,
+                                                                       uint32_t nsup, uint32_t* __restrict__ level1,
+                                                                       uint32_t* __restrict__ level1_key,
+                                                                       uint16_t* __restrict__ stab,
+                                                                       uint32_t* __restrict__ gcnt) {
+    bin_front_offsets_body<Off, true>(local, count, tiles_per_block, sup_log2, nsup, level1, level1_key, stab, gcnt);
+}
+
 // gsum[sb][q] = probes of superbin sb in the tiles of front workgroups [64q, 64q + 64).
-// One workgroup per superbin, one wave per group.
+// One workgroup per superbin, one wave per group (kMaxBlocks front workgroups per pass).
 __global__ __launch_bounds__(kMaxBlocks) void bin_group_sum_kernel(const uint32_t* __restrict__ gcnt,
                                                                    uint32_t nblocks, uint32_t nsup, uint32_t nq,
                                                                    uint32_t* __restrict__ gsum) {
-    const uint32_t w = threadIdx.x, sb = blockIdx.x;
-    uint32_t v = w < nblocks ? gcnt[(uint64_t)w * nsup + sb] : 0u;
+    const uint32_t sb = blockIdx.x;
+    for (uint32_t w = threadIdx.x; w < nq * kGroupBlocks; w += kMaxBlocks) {   // wave-uniform bound
+        uint32_t v = w < nblocks ? gcnt[(uint64_t)w * nsup + sb] : 0u;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
-    const uint32_t q = w / kGroupBlocks;
-    if ((w & 63u) == 0 && q < nq) gsum[sb * nq + q] = v;
+        for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+        if ((w & 63u) == 0) gsum[sb * nq + w / kGroupBlocks] = v;
+    }
 }
 
 // base[i]: exclusive prefix of gsum over windows i = (superbin, group); base[N] =
@@ -344,6 +375,29 @@ __device__ __forceinline__ uint32_t run_of(const uint32_t* s_pre, uint32_t nt, u
     return lo;
 }
 
+// Rank of this lane's probe among the tile's probes to `owner`, taken with ONE LDS atomic
+// per (wave, owner) instead of one per probe: with few owners (P <= g.route_agg) every lane
+// of a wave would otherwise hit the same few LDS words (P = 1: all of them).  Loops over the
+// distinct owners present in the wave.  Every lane of the wave must call it.
+__device__ __forceinline__ uint32_t wave_agg_rank(bool live, uint32_t owner, uint32_t* s_cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint64_t pending = __ballot(live);
+    uint32_t rank = 0;
+    while (pending) {   // wave-uniform
+        const int leader = __builtin_ctzll(pending);
+        const uint32_t o = (uint32_t)__shfl((int)owner, leader);
+        const bool mine = live && owner == o;
+        const uint64_t grp = __ballot(mine);
+        uint32_t base = 0;
+        if ((int)lane == leader) base = atomicAdd(s_cnt + o, (uint32_t)__popcll(grp));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (mine) rank = base + (uint32_t)__popcll(grp & below);
+        pending &= ~grp;
+    }
+    return rank;
+}
+
 // Requester side of a partitioned filter (bf_route_dev): hash, then per tile an
 // LDS counting sort of the tile's probes by owner shard (block-cyclic map of
 // include/bfhip.h), written contiguously at the tile's fixed place with the
@@ -351,13 +405,13 @@ __device__ __forceinline__ uint32_t run_of(const uint32_t* s_pre, uint32_t nt, u
 // owner-local offsets need more than 32 bits (their high byte is kept apart);
 // SLOT: each probe carries its key index.
 template <bool WIDE, bool SLOT>
-__global__ __launch_bounds__(kTile) void route_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
-                                                            const uint64_t* __restrict__ offsets, uint64_t bias,
-                                                            uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
-                                                            uint32_t P, uint32_t* __restrict__ lo1,
-                                                            uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1,
-                                                            uint16_t* __restrict__ stab,
-                                                            uint32_t* __restrict__ gcnt) {
+__device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
+                                                 const uint64_t* __restrict__ offsets, uint64_t bias,
+                                                 uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
+                                                 uint32_t P, uint32_t* __restrict__ lo1,
+                                                 uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1,
+                                                 uint16_t* __restrict__ stab,
+                                                 uint32_t* __restrict__ gcnt) {
     __shared__ uint64_t s_off[kTile + 1];
     __shared__ uint4 s_stage[kStageVec + kStageSlackVec];
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
@@ -406,14 +460,19 @@ __global__ __launch_bounds__(kTile) void route_front_kernel(BfGeom g, const uint
             tag[q] = 0xFFFFFFFFu;
             lo[q] = 0;
             hi[q] = 0;
+            uint32_t owner = 0;
             if (live) {
                 const uint4 H = second ? H1 : H0;
-                uint32_t owner;
                 uint64_t local;
                 owner_local(g, probe_offset(g, H.x, H.y, H.z, H.w, i), owner, local);
-                tag[q] = (owner << 16) | atomicAdd(s_cnt + owner, 1u);
                 lo[q] = (uint32_t)local;
                 hi[q] = (uint8_t)(local >> 32);
+            }
+            if (P <= g.route_agg) {   // workgroup-uniform
+                const uint32_t r = wave_agg_rank(live, owner, s_cnt);
+                if (live) tag[q] = (owner << 16) | r;
+            } else if (live) {
+                tag[q] = (owner << 16) | atomicAdd(s_cnt + owner, 1u);
             }
         }
         __syncthreads();
@@ -449,6 +508,24 @@ __global__ __launch_bounds__(kTile) void route_front_kernel(BfGeom g, const uint
     }
     if (t < P) gcnt[(uint64_t)blockIdx.x * P + t] = s_gcnt[t];
 }
+
+#define BF_ROUTE_FRONT_ARGS                                                                                     \
+    BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets, uint64_t bias, uint64_t n, \
+        uint32_t tile_keys, uint32_t tiles_per_block, uint32_t P, uint32_t* __restrict__ lo1,                   \
+        uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1, uint16_t* __restrict__ stab,                     \
+        uint32_t* __restrict__ gcnt
+template <bool WIDE, bool SLOT>
+__global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS) {
+    route_front_body<WIDE, SLOT>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt);
+}
+// 32-bit offsets, no slots (inserts on shards of <= 2^32 bits): 77 KiB of LDS, so two
+// workgroups per CU at 8 waves per SIMD, as bin_front
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void route_front32_kernel(BF_ROUTE_FRONT_ARGS) {
+    route_front_body<false, false>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab,
+                                   gcnt);
+}
+#undef BF_ROUTE_FRONT_ARGS
 
 // One workgroup per 8192-probe block of an (owner, group) window (the grid is an
 // upper bound; spare workgroups exit): the owner's runs from the group's tiles
@@ -900,9 +977,10 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
     return plan_common(bitset_bytes, n, k, k <= kTwoKeys ? 2 * kTile : kTile, pref_region_log2, with_keys, plan);
 }
 
-bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan) {
+bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan,
+                            bool with_keys) {
     if (count == 0 || count > bf_binned_max_offsets()) return false;
-    return plan_common(bitset_bytes, count, 1, kTileProbes, pref_region_log2, false, plan);
+    return plan_common(bitset_bytes, count, 1, kTileProbes, pref_region_log2, with_keys, plan);
 }
 
 namespace {
@@ -956,14 +1034,10 @@ hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, ui
     return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
 }
 
-hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
-                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
-                                    void* scratch, uint8_t* out8, hipStream_t s, BfMarks* mk) {
-    if (n == 0) return hipSuccess;
-    if (!p.with_keys || !out8) return hipErrorInvalidValue;
-    const Carve c = carve(p, scratch);
-    hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, out8, s, mk);
-    if (e != hipSuccess) return e;
+namespace {
+
+hipError_t launch_test(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes, uint8_t* out8,
+                       hipStream_t s, BfMarks* mk) {
     const uint64_t nwords = bitset_bytes / 4;
     if (p.region_log2 == 19)
         hipLaunchKernelGGL((bin_test_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
@@ -975,6 +1049,44 @@ hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_
                            p.rel_log2, out8);
     bf_mark(mk, s, "bin_test");
     return hipGetLastError();
+}
+
+}  // namespace
+
+// Owner side of a partitioned include?: the received offsets sorted by region (their input
+// positions riding along), each region of the shard loaded once into LDS, and every
+// offset's answer byte written (preset to 1, cleared on a 0 bit).
+hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                       const void* local, bool route32, uint64_t count, void* scratch, uint8_t* out8,
+                                       hipStream_t s, BfMarks* mk) {
+    if (count == 0) return hipSuccess;
+    if (!p.with_keys || !out8) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
+    hipError_t e = hipMemsetAsync(out8, 1, count, s);
+    if (e != hipSuccess) return e;
+    if (route32)
+        hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint32_t>, dim3(p.nblocks), dim3(kTile), 0, s,
+                           static_cast<const uint32_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
+                           c.level1_key, c.stab, c.gcnt);
+    else
+        hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
+                           static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
+                           c.level1_key, c.stab, c.gcnt);
+    bf_mark(mk, s, "bin_front_offsets");
+    if ((e = launch_groups_mid(g, p, c, s, mk)) != hipSuccess) return e;
+    return launch_test(g, p, c, bitset_bytes, out8, s, mk);
+}
+
+hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
+                                    void* scratch, uint8_t* out8, hipStream_t s, BfMarks* mk) {
+    if (n == 0) return hipSuccess;
+    if (!p.with_keys || !out8) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, out8, s, mk);
+    if (e != hipSuccess) return e;
+    return launch_test(g, p, c, bitset_bytes, out8, s, mk);
 }
 
 // ---- partitioned filters, requester side ---------------------------------
@@ -1010,9 +1122,14 @@ RouteCarve route_carve(const BfBinPlan& p, bool wide, bool with_slot, void* at0)
 
 }  // namespace
 
+// The route runs one batch in one pass (its send buffer is owner-major over the whole batch),
+// so past kMaxBlocks x kMaxTilesPerBlock tiles it takes more front workgroups, as long as the
+// (owner, group) windows fit the one-workgroup scan.
+constexpr uint32_t kMaxRouteBlocks = 4096;
+constexpr uint32_t kMaxWindows = 2048;
+
 bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kSlots || n == 0 || n > bf_binned_max_keys(k) || shards == 0 || shards > kMaxSup)
-        return false;
+    if (k == 0 || k > (uint32_t)kSlots || n == 0 || shards == 0 || shards > kMaxSup) return false;
     const uint64_t probes = n * k;
     if (probes >= (1ull << 32)) return false;
     BfBinPlan p{};
@@ -1021,8 +1138,11 @@ bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with
     p.tile_probes = p.tile_keys * k;
     p.ntiles = (n + p.tile_keys - 1) / p.tile_keys;
     p.tiles_per_block = (uint32_t)((p.ntiles + kMaxBlocks - 1) / kMaxBlocks);
+    if (p.tiles_per_block > kMaxTilesPerBlock) p.tiles_per_block = kMaxTilesPerBlock;
+    if (p.ntiles > (uint64_t)kMaxRouteBlocks * p.tiles_per_block) return false;
     p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
     p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
+    if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) return false;
     p.probes = probes;
     p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
     p.scratch_bytes = route_carve(p, wide, with_slot, nullptr).bytes;
@@ -1041,9 +1161,11 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     hipLaunchKernelGGL((route_front_kernel<W, S>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, \
                        p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt)
     if (wide) { if (slot) BF_ROUTE_FRONT(true, true); else BF_ROUTE_FRONT(true, false); }
-    else { if (slot) BF_ROUTE_FRONT(false, true); else BF_ROUTE_FRONT(false, false); }
+    else if (slot) BF_ROUTE_FRONT(false, true);
+    else hipLaunchKernelGGL(route_front32_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                            p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);
 #undef BF_ROUTE_FRONT
-    bf_mark(mk, s, "route_front");
+    bf_mark(mk, s, slot ? "route_front_slot" : "route_front");
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
                        p.ngroups, c.gsum);
     hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
@@ -1058,6 +1180,6 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     if (wide) { if (slot) BF_ROUTE_GATHER(true, true); else BF_ROUTE_GATHER(true, false); }
     else { if (slot) BF_ROUTE_GATHER(false, true); else BF_ROUTE_GATHER(false, false); }
 #undef BF_ROUTE_GATHER
-    bf_mark(mk, s, "route_gather");
+    bf_mark(mk, s, slot ? "route_gather_slot" : "route_gather");
     return hipGetLastError();
 }

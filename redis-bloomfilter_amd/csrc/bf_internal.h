@@ -14,9 +14,11 @@ struct BfGeom {
     float     inv_m_f; // (float)(1.0 / m)
     uint32_t  shards;  // partitioned filters: shard count P (1 = whole filter)
     uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
+    double    inv_shards;  // 1.0 / P, for the division-free block -> (owner, local block) map
     // probe policies (tuning; results are identical for every setting)
     uint32_t  first_round;  // include?: probes loaded before the first early-exit check (0 = all k)
     uint32_t  next_round;   // include?: probes per later round (0 = all the rest at once)
+    uint32_t  route_agg;    // route: wave-aggregated owner ranks when P <= route_agg (else LDS atomics)
     uint32_t  insert_test;  // insert: 1 = load the k words first, atomic-OR only the unset bits
     uint32_t  route32;      // BF_FLAG_ROUTE32: routed owner-local offsets are uint32
     uint8_t*  dirty;        // nullable: one byte per 2^kDirtyShiftBits-bit block, set to 1 when an
@@ -93,10 +95,16 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
 // Owner side of a partitioned filter: `count` routed shard-local offsets (uint32
 // when route32, else uint64) ORed into the shard through the same pipeline.
 uint64_t bf_binned_max_offsets();
-bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan);
+bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan,
+                            bool with_keys = false);
 hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                          const void* local, bool route32, uint64_t count, void* scratch,
                                          uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
+// Binned shard test (owner side of a partitioned include?): out8[i] = bit of local[i].
+// Plan with bf_binned_plan_offsets(..., with_keys = true).
+hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                       const void* local, bool route32, uint64_t count, void* scratch, uint8_t* out8,
+                                       hipStream_t s, BfMarks* mk);
 // plan.with_keys must be set; out8 gets the n answers.
 hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                     const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,

@@ -165,6 +165,7 @@ int ensure_layer(bf_lua* h, uint32_t n) {
         g.mod_f32 = m >= (1ull << 17) ? 1u : 0u;
         g.inv_m_f = (float)(1.0 / (double)m);
         g.shards = 1;
+        g.inv_shards = 1.0;
         g.block_log2 = 20;
         h->layers.push_back(g);
         h->layer_bytes.push_back(bytes);

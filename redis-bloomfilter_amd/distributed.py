@@ -160,14 +160,19 @@ class PartitionedFilter:
         self.device = engine.device
 
     # -- exchange helpers
-    def _exchange(self, send: torch.Tensor, counts: torch.Tensor):
+    def _splits(self, counts: torch.Tensor):
+        """Per-owner send counts -> (send splits, receive splits) on the host (one small
+        all-to-all; the host waits for it)."""
         recv_counts = torch.empty_like(counts)
         dist.all_to_all_single(recv_counts, counts, group=self.group)
         cnt = torch.stack([counts, recv_counts]).cpu()
-        send_splits, recv_splits = cnt[0].tolist(), cnt[1].tolist()
+        return cnt[0].tolist(), cnt[1].tolist()
+
+    def _exchange(self, send: torch.Tensor, counts: torch.Tensor, async_op: bool = False):
+        send_splits, recv_splits = self._splits(counts)
         recv = torch.empty(sum(recv_splits), dtype=send.dtype, device=send.device)
-        dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group)
-        return recv, send_splits, recv_splits
+        work = dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group, async_op=async_op)
+        return (recv, send_splits, recv_splits, work) if async_op else (recv, send_splits, recv_splits)
 
     # -- device-resident batch API (keys already in device memory)
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
@@ -183,6 +188,30 @@ class PartitionedFilter:
         dist.all_to_all_single(back, bits, send_splits, recv_splits, group=self.group)
         return self.engine.combine(back, slot, n)
 
+    def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
+                           qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
+        """insert_many_dev(ikb, iko, ni) then include_many_dev(qkb, qko, nq), same results,
+        with the exchanges overlapped with the other batch's kernels:
+
+            route(ins) | a2a(ins) || route(inc) | a2a(inc) || shard_insert | shard_test | a2a(back) | combine
+
+        The collectives run on the process group's own stream (async_op), the kernels on
+        the current stream; every owner still applies all ranks' inserts before it tests
+        (shard_insert precedes shard_test on its stream), so the include? answers see the
+        batch's inserts exactly as in the sequential form."""
+        e = self.engine
+        send_i, _, cnt_i = e.route(ikb, iko, ni, want_slot=False)
+        recv_i, _, _, w_i = self._exchange(send_i, cnt_i, async_op=True)
+        send_q, slot_q, cnt_q = e.route(qkb, qko, nq)            # overlaps a2a(ins)
+        w_i.wait()
+        recv_q, ss_q, rs_q, w_q = self._exchange(send_q, cnt_q, async_op=True)
+        e.shard_insert(recv_i)                                    # overlaps a2a(inc)
+        w_q.wait()
+        bits = e.shard_test(recv_q)
+        back = torch.empty(sum(ss_q), dtype=torch.uint8, device=bits.device)
+        dist.all_to_all_single(back, bits, ss_q, rs_q, group=self.group)
+        return e.combine(back, slot_q, nq)
+
     # -- host API (each rank passes its own keys)
     def insert_many(self, keys: Iterable) -> None:
         kb, ko, n = _device_batch(keys, self.device)
@@ -191,6 +220,12 @@ class PartitionedFilter:
     def include_many(self, keys: Iterable) -> np.ndarray:
         kb, ko, n = _device_batch(keys, self.device)
         return self.include_many_dev(kb, ko, n).cpu().numpy().astype(bool)
+
+    def insert_include(self, insert_keys: Iterable, probe_keys: Iterable) -> np.ndarray:
+        """insert_many(insert_keys) then include_many(probe_keys), exchanges overlapped."""
+        ikb, iko, ni = _device_batch(insert_keys, self.device)
+        qkb, qko, nq = _device_batch(probe_keys, self.device)
+        return self.insert_include_dev(ikb, iko, ni, qkb, qko, nq).cpu().numpy().astype(bool)
 
     def clear(self) -> None:
         self.engine.clear()

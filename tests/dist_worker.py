@@ -48,6 +48,12 @@ def main():
     pf2 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
     pf2.import_redis(s)
     got2 = pf2.include_many(probe)
+    # the overlapped insert + include? step gives the sequential form's shard bytes and answers
+    del pf2   # the 10B case holds 3.5 GB per shard copy
+    pf3 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    got3 = pf3.insert_include(mine, probe)
+    same_shard = bool(np.array_equal(pf3.engine.shard_export(), pf.engine.shard_export()))
+    del pf, pf3
     ok = True
     if rank == 0 or True:
         all_keys = [("r%d-%d" % (r, int(v))) for r in range(P)
@@ -58,7 +64,8 @@ def main():
         want_s = orc.redis_string(bits)
         pb, po = O.pack_keys(probe)
         want = orc.include_many(bits, m, k, pb, po).astype(bool)
-        ok = (s == want_s) and bool((got == want).all()) and bool((got2 == want).all())
+        ok = (s == want_s) and same_shard and bool((got == want).all()) and bool((got2 == want).all()) \
+            and bool((got3 == want).all())
         if not ok:
             print("rank %d MISMATCH: string %s (%d vs %d bytes), include %d diffs" %
                   (rank, s == want_s, len(s), len(want_s), int((got != want).sum())), flush=True)

@@ -25,9 +25,13 @@ def dev_batch(pkg, torch, keys):
 @pytest.mark.parametrize("binned", ["0", "1"])
 @pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20)])
 def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
-    """binned=1 forces the owner-side binned insert (offsets front pass + region apply)."""
+    """binned=1 forces the owner-side binned insert (offsets front pass + region apply) and
+    binned shard test, and takes the wave-aggregated owner ranks in the route; 0 the direct
+    kernels and LDS atomics."""
     import torch
     monkeypatch.setenv("BFHIP_INSERT_BINNED", binned)
+    monkeypatch.setenv("BFHIP_SHARD_TEST_BINNED", binned)
+    monkeypatch.setenv("BFHIP_ROUTE_AGG", "16" if binned == "1" else "0")
     D = pkg.distributed
     dev = torch.device("cuda", 0)
     shards = [D.HipEngine(m, k, P, s, b, dev) for s in range(P)]
@@ -80,6 +84,14 @@ def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
     got = shards[1 % P].combine(back, slot, n).cpu().numpy()
     want = oracle.include_many(bits, m, k, pb, po)
     np.testing.assert_array_equal(got, want)
+    # every owner's answer byte is the bit at that probe's global offset
+    s_np = send.cpu().numpy()
+    s_np = s_np.view(np.uint32).astype(np.uint64) if s_np.dtype == np.int32 else s_np.view(np.uint64)
+    owner_of = np.repeat(np.arange(P), c)
+    lblk, low = s_np >> np.uint64(b), s_np & np.uint64((1 << b) - 1)
+    glob = ((lblk * np.uint64(P) + owner_of.astype(np.uint64)) << np.uint64(b)) | low
+    want_bits = (bits.view(np.uint8)[(glob >> np.uint64(3)).astype(np.int64)] >> (7 - (glob & np.uint64(7))).astype(np.uint8)) & 1
+    np.testing.assert_array_equal(back.cpu().numpy(), want_bits)
     for e in shards:
         e.close()
 
@@ -115,6 +127,11 @@ def test_torch_distributed_world1(pkg, oracle):
             np.testing.assert_array_equal(f.include_many(probe), want)
             assert f.export_redis() == oracle.redis_string(bits)
             f.close()
+        # the overlapped insert + include? step (async RCCL all-to-alls beside the kernels)
+        f = D.PartitionedFilter(m, k, block_log2=16)
+        np.testing.assert_array_equal(f.insert_include(keys, probe), want)
+        assert f.export_redis() == oracle.redis_string(bits)
+        f.close()
     finally:
         dist.destroy_process_group()
 

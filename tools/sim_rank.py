@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Per-rank compute of the partitioned filter at P shards, simulated on ONE GPU.
+
+    python tools/sim_rank.py [--shards 8] [--config nstar] [--steps 5]
+
+Builds shard 0 of a P-way partitioned north-star filter (the largest shard) and runs,
+per step, the kernels one rank runs at world size P: route its 2^24-key insert batch,
+apply a received batch of the same size to its shard, route its include? batch, test
+a received batch, combine.  The received batches are this rank's own routed probes (in
+a balanced run every rank receives about as many as it sends; every owner-local offset
+is valid on shard 0, the largest).  No collective runs: the all-to-all time is not in
+these numbers.  Prints one JSON line with per-kernel means (bf_profile).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import pkgload  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--config", default="nstar", choices=sorted(bench.CONFIGS))
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    pkg = pkgload.load()
+    n_items, err, batch, _ = bench.CONFIGS[args.config]
+    m = pkg.Bloomfilter.optimal_m(n_items, err)
+    k = pkg.Bloomfilter.optimal_k(n_items, m)
+    dev = torch.device("cuda", 0)
+    eng = pkg.distributed.HipEngine(m, k, args.shards, 0, 20, dev)
+    f = eng.filter
+    batches = bench.make_batches(n_items, batch, 0, args.steps + 1, dev)
+    torch.cuda.synchronize()
+
+    def step(b):
+        (ikb, iko), (qkb, qko) = b
+        send, _, _ = eng.route(ikb, iko, batch, want_slot=False)
+        eng.shard_insert(send)
+        send, slot, _ = eng.route(qkb, qko, batch)
+        bits = eng.shard_test(send)
+        return eng.combine(bits, slot, batch)
+
+    step(batches[0])
+    torch.cuda.synchronize()
+    f.profile(True)
+    f.profile_read(reset=True)
+    t0 = time.perf_counter()
+    for b in batches[1:]:
+        step(b)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    prof = f.profile_read(reset=True)
+    out = {"config": args.config, "shards": args.shards, "m": m, "k": k, "batch": batch,
+           "shard_bytes": f.device_bytes, "route32": bool(eng.offset_dtype == torch.int32),
+           "ms_per_step_compute": wall * 1e3,
+           "kernels_ms_per_step": {name: ms / args.steps for name, (ms, _) in prof.items()}}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
