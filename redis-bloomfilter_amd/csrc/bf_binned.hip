@@ -412,13 +412,20 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                                                  uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1,
                                                  uint16_t* __restrict__ stab,
                                                  uint32_t* __restrict__ gcnt) {
-    __shared__ uint64_t s_off[kTile + 1];
-    __shared__ uint4 s_stage[kStageVec + kStageSlackVec];
+    // The key stage (offsets + bytes) is dead once the tile is hashed, so the sorted
+    // tile-relative key indices (u16) reuse it: 76 KiB in all without WIDE, two
+    // workgroups per CU.
+    constexpr uint32_t kOffVec = (8 * (kTile + 1) + 15) / 16;
+    constexpr uint32_t kRawVec = kOffVec + kStageVec + kStageSlackVec;
+    static_assert(kRawVec * 16 >= kTileProbes * 2, "sorted key indices must fit the dead key stage");
+    __shared__ uint4 s_raw[kRawVec];
+    uint64_t* s_off = reinterpret_cast<uint64_t*>(s_raw);
+    uint4* s_stage = s_raw + kOffVec;
+    uint16_t* s_key = reinterpret_cast<uint16_t*>(s_raw);
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_lo[kTileProbes];
     __shared__ uint8_t s_hi[WIDE ? kTileProbes : 1];
-    __shared__ uint32_t s_key[SLOT ? kTileProbes : 1];
     const uint32_t t = threadIdx.x;
     if (t < kMaxSup) {
         s_cnt[t] = 0;
@@ -493,7 +500,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 if constexpr (WIDE) s_hi[d] = hi[q];
                 if constexpr (SLOT) {
                     const bool second = kpl == 2 && q >= (int)kTwoKeys;
-                    s_key[d] = (uint32_t)(key0 + (second ? kTile + t : t));
+                    s_key[d] = (uint16_t)(second ? kTile + t : t);
                 }
             }
         }
@@ -503,8 +510,9 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         for (uint32_t j = t; j < tp; j += kTile) {
             lo1[seg + j] = s_lo[j];
             if constexpr (WIDE) hi1[seg + j] = s_hi[j];
-            if constexpr (SLOT) key1[seg + j] = s_key[j];
+            if constexpr (SLOT) key1[seg + j] = (uint32_t)key0 + s_key[j];
         }
+        if constexpr (SLOT) __syncthreads();   // the next tile's staging overwrites s_key
     }
     if (t < P) gcnt[(uint64_t)blockIdx.x * P + t] = s_gcnt[t];
 }
@@ -518,12 +526,13 @@ template <bool WIDE, bool SLOT>
 __global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS) {
     route_front_body<WIDE, SLOT>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt);
 }
-// 32-bit offsets, no slots (inserts on shards of <= 2^32 bits): 77 KiB of LDS, so two
+// 32-bit offsets (shards of <= 2^32 bits): 76 KiB of LDS with or without slots, so two
 // workgroups per CU at 8 waves per SIMD, as bin_front
+template <bool SLOT>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void route_front32_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<false, false>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab,
-                                   gcnt);
+    route_front_body<false, SLOT>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab,
+                                  gcnt);
 }
 #undef BF_ROUTE_FRONT_ARGS
 
@@ -1161,9 +1170,12 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     hipLaunchKernelGGL((route_front_kernel<W, S>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, \
                        p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt)
     if (wide) { if (slot) BF_ROUTE_FRONT(true, true); else BF_ROUTE_FRONT(true, false); }
-    else if (slot) BF_ROUTE_FRONT(false, true);
-    else hipLaunchKernelGGL(route_front32_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
-                            p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);
+    else if (slot)
+        hipLaunchKernelGGL(route_front32_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                           p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);
+    else
+        hipLaunchKernelGGL(route_front32_kernel<false>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias,
+                           n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);
 #undef BF_ROUTE_FRONT
     bf_mark(mk, s, slot ? "route_front_slot" : "route_front");
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
