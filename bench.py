@@ -52,6 +52,10 @@ CONFIGS = {
     "10k": (10**4, 0.01, 1 << 14, "insert"),
     # hash-bound probe: the 1M@1% (L2-resident) filter driven with 2^24-key batches
     "1m_big": (10**6, 0.01, 1 << 24, "insert"),
+    # BASELINE configs 4 and 5 on one GPU: their reachable prefix (k(2^32-1)+1 bits, 6.98 GB,
+    # ruby.rb:51) fits one MI355X; the 8-GPU layouts are --gpus 8 runs
+    "10b": (10**10, 0.0001, 1 << 24, "random"),
+    "200b": (2 * 10**11, 0.0001, 1 << 24, "random"),
 }
 
 
@@ -139,9 +143,28 @@ def to_host(kb: torch.Tensor, ko: torch.Tensor):
     return kb.cpu().numpy()[: int(offs[-1])], offs
 
 
-def prefill_random(f, m: int, k: int, rank: int) -> np.ndarray:
-    """50 % bit density over the reachable prefix (a full filter holds 1 - e^{-kn/m} ~ 46.5 %)."""
+class _DevBytes:
+    """A torch view of raw device bytes (the filter's bitset) via __cuda_array_interface__."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+def prefill_random(f, m: int, k: int, rank: int, host_copy: bool = True):
+    """50 % bit density over the reachable prefix (a full filter holds 1 - e^{-kn/m} ~ 46.5 %).
+    host_copy=False fills on the device (multi-GB secondary configs) and returns None."""
     nbytes = (f.reach_bits + 7) // 8
+    if not host_copy:
+        ptr, _ = f.device_bits()
+        t = torch.as_tensor(_DevBytes(ptr, nbytes), device="cuda")
+        g = torch.Generator(device=t.device)
+        g.manual_seed(SEED * 7919 + rank)
+        t.random_(0, 256, generator=g)
+        tail = f.reach_bits & 7
+        if tail:
+            t[-1:].bitwise_and_((0xFF << (8 - tail)) & 0xFF)
+        torch.cuda.synchronize()
+        return None
     rng = np.random.default_rng([SEED, 99, rank])
     host = np.frombuffer(rng.bytes(nbytes), dtype=np.uint8).copy()
     tail = f.reach_bits & 7
@@ -166,7 +189,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     if mode == "single":
         f = pkg.Filter(m, k, device=D.local)
         if prefill == "random":
-            host_bits = prefill_random(f, m, k, D.rank)
+            host_bits = prefill_random(f, m, k, D.rank, host_copy=f.device_bytes < (4 << 30))
     else:   # partitioned over the ranks, RCCL all-to-all routing
         pf = pkg.distributed.PartitionedFilter(m, k, block_log2=20, device=dev)
         f = pf.engine.filter
@@ -359,7 +382,7 @@ def main():
                                   mode=args.mode, overlap=not args.no_overlap)
     secondary = {}
     if D.world == 1 and not args.no_secondary:
-        for name in ("1m", "100m"):
+        for name in ("1m", "100m", "10b"):
             if name != args.config:
                 r, _ = time_config(pkg, D, name, max(3, args.steps // 2), 1)
                 secondary[name] = {"keys_per_s": r["keys_per_s"],

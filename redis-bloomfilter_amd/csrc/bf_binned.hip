@@ -45,6 +45,7 @@ constexpr uint32_t kMaxBlocks = 512;          // front workgroups
 constexpr uint32_t kGroupBlocks = 64;         // front workgroups per group (one wave in bin_group_sum)
 constexpr uint32_t kTileProbes = 12288;       // probes per front tile (LDS sort buffer)
 constexpr int kSlots = 12;                    // probes per lane per tile (k <= 12)
+constexpr int kWideSlots = 16;                // ... for 12 < k <= 16 (one key per lane, 1 workgroup per CU)
 constexpr uint32_t kTwoKeys = 6;              // k <= 6: two keys per lane per tile
 constexpr uint32_t kMaxTilesPerBlock = 16;    // <= 1024 tiles per group: one run-table pass in bin_mid
 constexpr uint32_t kBlockProbes = 8192;       // probes per level-2 chunk block (one bin_mid workgroup)
@@ -82,7 +83,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     return r;
 }
 
-template <bool KEYS>
+template <bool KEYS, int SLOTS>
 __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                           const uint64_t* __restrict__ offsets, uint64_t bias,
                                                           uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
@@ -95,8 +96,8 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
     __shared__ uint4 s_stage[kStageVec + kStageSlackVec];
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_sorted[kTileProbes];
-    __shared__ uint32_t s_key[KEYS ? kTileProbes : 1];
+    __shared__ uint32_t s_sorted[kTile * SLOTS];
+    __shared__ uint32_t s_key[KEYS ? kTile * SLOTS : 1];
     const uint32_t t = threadIdx.x;
     if (t < kMaxSup) {
         s_cnt[t] = 0;
@@ -134,9 +135,9 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
             if (live1) out8[key0 + kTile + t] = 1;
         }
         // A: each probe -> (superbin, rank inside the tile's superbin run)
-        uint32_t tag[kSlots], loc[kSlots];
+        uint32_t tag[SLOTS], loc[SLOTS];
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) {
+        for (int q = 0; q < SLOTS; ++q) {
             const bool second = kpl == 2 && q >= (int)kTwoKeys;
             const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
             const bool live = i < k && (second ? live1 : live0);
@@ -163,7 +164,7 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
         __syncthreads();
         // C: counting sort in LDS
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) {
+        for (int q = 0; q < SLOTS; ++q) {
             if (tag[q] != 0xFFFFFFFFu) {
                 const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
                 s_sorted[d] = loc[q];
@@ -192,8 +193,22 @@ void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64
                       uint64_t bias, uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block, uint32_t sup_log2,
                       uint32_t nsup, uint32_t* __restrict__ level1, uint32_t* __restrict__ level1_key,
                       uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint8_t* __restrict__ out8) {
-    bin_front_body<false>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1, level1_key,
-                          stab, gcnt, out8);
+    bin_front_body<false, kSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1,
+                                  level1_key, stab, gcnt, out8);
+}
+
+// 12 < k <= 16: 16 probe slots per lane (64 KiB sort buffer, one workgroup per CU)
+template <bool KEYS>
+__global__ __launch_bounds__(kTile) void bin_front_wide_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+                                                               const uint64_t* __restrict__ offsets, uint64_t bias,
+                                                               uint64_t n, uint32_t tile_keys,
+                                                               uint32_t tiles_per_block, uint32_t sup_log2,
+                                                               uint32_t nsup, uint32_t* __restrict__ level1,
+                                                               uint32_t* __restrict__ level1_key,
+                                                               uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt,
+                                                               uint8_t* __restrict__ out8) {
+    bin_front_body<KEYS, kWideSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1,
+                                     level1_key, stab, gcnt, out8);
 }
 
 // include?: key indices ride along (123 KiB of LDS: one workgroup per CU)
@@ -202,8 +217,8 @@ void bin_front_keys_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const u
                            uint64_t bias, uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block, uint32_t sup_log2,
                            uint32_t nsup, uint32_t* __restrict__ level1, uint32_t* __restrict__ level1_key,
                            uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint8_t* __restrict__ out8) {
-    bin_front_body<true>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1, level1_key,
-                         stab, gcnt, out8);
+    bin_front_body<true, kSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1,
+                                 level1_key, stab, gcnt, out8);
 }
 
 // Owner side of a partitioned filter: the probes arrive as shard-local offsets
@@ -404,7 +419,7 @@ __device__ __forceinline__ uint32_t wave_agg_rank(bool live, uint32_t owner, uin
 // tile's owner run table [owner][tile]; per-workgroup owner totals.  WIDE: the
 // owner-local offsets need more than 32 bits (their high byte is kept apart);
 // SLOT: each probe carries its key index.
-template <bool WIDE, bool SLOT>
+template <bool WIDE, bool SLOT, int SLOTS>
 __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                  const uint64_t* __restrict__ offsets, uint64_t bias,
                                                  uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
@@ -416,16 +431,17 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
     // tile-relative key indices (u16) reuse it: 76 KiB in all without WIDE, two
     // workgroups per CU.
     constexpr uint32_t kOffVec = (8 * (kTile + 1) + 15) / 16;
-    constexpr uint32_t kRawVec = kOffVec + kStageVec + kStageSlackVec;
-    static_assert(kRawVec * 16 >= kTileProbes * 2, "sorted key indices must fit the dead key stage");
+    constexpr uint32_t kStageRaw = kOffVec + kStageVec + kStageSlackVec;
+    constexpr uint32_t kKeyRaw = (kTile * SLOTS * 2 + 15) / 16;
+    constexpr uint32_t kRawVec = SLOT && kKeyRaw > kStageRaw ? kKeyRaw : kStageRaw;
     __shared__ uint4 s_raw[kRawVec];
     uint64_t* s_off = reinterpret_cast<uint64_t*>(s_raw);
     uint4* s_stage = s_raw + kOffVec;
     uint16_t* s_key = reinterpret_cast<uint16_t*>(s_raw);
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_lo[kTileProbes];
-    __shared__ uint8_t s_hi[WIDE ? kTileProbes : 1];
+    __shared__ uint32_t s_lo[kTile * SLOTS];
+    __shared__ uint8_t s_hi[WIDE ? kTile * SLOTS : 1];
     const uint32_t t = threadIdx.x;
     if (t < kMaxSup) {
         s_cnt[t] = 0;
@@ -457,10 +473,10 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         }
         const bool live0 = t < tk;
         const bool live1 = kpl == 2 && kTile + t < tk;
-        uint32_t tag[kSlots], lo[kSlots];
-        uint8_t hi[kSlots];
+        uint32_t tag[SLOTS], lo[SLOTS];
+        uint8_t hi[SLOTS];
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) {
+        for (int q = 0; q < SLOTS; ++q) {
             const bool second = kpl == 2 && q >= (int)kTwoKeys;
             const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
             const bool live = i < k && (second ? live1 : live0);
@@ -493,7 +509,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) {
+        for (int q = 0; q < SLOTS; ++q) {
             if (tag[q] != 0xFFFFFFFFu) {
                 const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
                 s_lo[d] = lo[q];
@@ -522,17 +538,18 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         uint32_t tile_keys, uint32_t tiles_per_block, uint32_t P, uint32_t* __restrict__ lo1,                   \
         uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1, uint16_t* __restrict__ stab,                     \
         uint32_t* __restrict__ gcnt
-template <bool WIDE, bool SLOT>
+template <bool WIDE, bool SLOT, int SLOTS>
 __global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<WIDE, SLOT>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt);
+    route_front_body<WIDE, SLOT, SLOTS>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1,
+                                        stab, gcnt);
 }
 // 32-bit offsets (shards of <= 2^32 bits): 76 KiB of LDS with or without slots, so two
 // workgroups per CU at 8 waves per SIMD, as bin_front
 template <bool SLOT>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void route_front32_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<false, SLOT>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab,
-                                  gcnt);
+    route_front_body<false, SLOT, kSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1,
+                                          stab, gcnt);
 }
 #undef BF_ROUTE_FRONT_ARGS
 
@@ -923,7 +940,16 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
                             const uint64_t* offsets, uint64_t bias, uint64_t n, uint8_t* out8, hipStream_t s,
                             BfMarks* mk) {
     const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
-    if (p.with_keys)
+    if (g.k > (uint32_t)kSlots) {
+        if (p.with_keys)
+            hipLaunchKernelGGL(bin_front_wide_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
+                               bias, n, p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key,
+                               c.stab, c.gcnt, out8);
+        else
+            hipLaunchKernelGGL(bin_front_wide_kernel<false>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
+                               bias, n, p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key,
+                               c.stab, c.gcnt, out8);
+    } else if (p.with_keys)
         hipLaunchKernelGGL(bin_front_keys_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
                            p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
                            out8);
@@ -982,7 +1008,7 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
 
 bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
                     BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kSlots || n == 0 || n > bf_binned_max_keys(k)) return false;
+    if (k == 0 || k > (uint32_t)kWideSlots || n == 0 || n > bf_binned_max_keys(k)) return false;
     return plan_common(bitset_bytes, n, k, k <= kTwoKeys ? 2 * kTile : kTile, pref_region_log2, with_keys, plan);
 }
 
@@ -1138,7 +1164,7 @@ constexpr uint32_t kMaxRouteBlocks = 4096;
 constexpr uint32_t kMaxWindows = 2048;
 
 bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kSlots || n == 0 || shards == 0 || shards > kMaxSup) return false;
+    if (k == 0 || k > (uint32_t)kWideSlots || n == 0 || shards == 0 || shards > kMaxSup) return false;
     const uint64_t probes = n * k;
     if (probes >= (1ull << 32)) return false;
     BfBinPlan p{};
@@ -1166,10 +1192,14 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     hipError_t e;
     if ((e = hipMemsetAsync(counts, 0, (uint64_t)p.nsup * sizeof(unsigned long long), s)) != hipSuccess) return e;
     if (n == 0) return hipSuccess;
-#define BF_ROUTE_FRONT(W, S)                                                                                      \
-    hipLaunchKernelGGL((route_front_kernel<W, S>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, \
-                       p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt)
-    if (wide) { if (slot) BF_ROUTE_FRONT(true, true); else BF_ROUTE_FRONT(true, false); }
+#define BF_ROUTE_FRONT(W, S, SL)                                                                                  \
+    hipLaunchKernelGGL((route_front_kernel<W, S, SL>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, \
+                       n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt)
+    if (g.k > (uint32_t)kSlots) {
+        if (wide) { if (slot) BF_ROUTE_FRONT(true, true, kWideSlots); else BF_ROUTE_FRONT(true, false, kWideSlots); }
+        else { if (slot) BF_ROUTE_FRONT(false, true, kWideSlots); else BF_ROUTE_FRONT(false, false, kWideSlots); }
+    }
+    else if (wide) { if (slot) BF_ROUTE_FRONT(true, true, kSlots); else BF_ROUTE_FRONT(true, false, kSlots); }
     else if (slot)
         hipLaunchKernelGGL(route_front32_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
                            p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);

@@ -304,13 +304,14 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
 
 
 @pytest.mark.parametrize("rl", ["19", "20"])
-@pytest.mark.parametrize("case", ["dup", "tiny", "long", "k12", "nstar"])
+@pytest.mark.parametrize("case", ["dup", "tiny", "long", "k12", "k13", "k16", "nstar"])
 def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     """Forced binned insert and include? on shapes that stress their partition passes: one key repeated
     (every probe in <= k regions, one superbin run per tile holding thousands of probes),
     a few keys over the 1.2 GB north-star filter (a level-2 chunk spanning every superbin:
     the per-probe cursor path), keys past the single-block SHA-1 (multi-block hash in the
-    count pass), k = 12 (the largest k the binned path takes: one key per lane, every probe slot used), and a 200k-key batch on the
+    count pass), k = 12 (every probe slot of the 12-slot front used), k = 13 and 16 (the 16-slot
+    front), and a 200k-key batch on the
     north-star filter; both region sizes (64 KiB / 128 KiB LDS images)."""
     monkeypatch.setenv("BFHIP_INSERT_BINNED", "1")
     monkeypatch.setenv("BFHIP_INCLUDE_BINNED", "1")
@@ -328,6 +329,12 @@ def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     elif case == "k12":
         m, k = 2**32 + 17, 12
         ins = rand_keys(rng, 30_000, 0, 24)
+    elif case == "k13":   # 16 probe slots per lane from here (bin_front_wide_kernel)
+        m, k = 191701167547, 13
+        ins = rand_keys(rng, 30_000, 0, 24)
+    elif case == "k16":
+        m, k = 9585058377, 16
+        ins = rand_keys(rng, 30_000, 0, 70)
     else:
         m, k = 9585058377, 6
         ins = pkg.keys.pack_decimal(rng.integers(0, 10**9, size=200_000))
