@@ -297,7 +297,7 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
     // Binned insert / include?, in sub-batches of at most bf_binned_max_keys keys.
     const bool is_insert = op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS;
     BfBinPlan plan;
-    const uint64_t sub = bf_binned_max_keys(h->k);
+    const uint64_t sub = std::max<uint64_t>(1, bf_binned_max_keys(h->k, h->dev_bytes, h->bin_region_log2));
     if ((is_insert || op == BF_OP_INCLUDE) && use_binned(h, std::min(n, sub), !is_insert, &plan)) {
         for (uint64_t c0 = 0; c0 < n; c0 += sub) {
             const uint64_t cn = std::min(sub, n - c0);
@@ -839,7 +839,7 @@ int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint3
     // Binned when the routed probes' random line fills clearly exceed a streaming pass
     // over the shard (same policy and knob as the whole-filter insert).
     BfBinPlan plan;
-    const uint64_t sub = bf_binned_max_offsets();
+    const uint64_t sub = std::max<uint64_t>(1, bf_binned_max_offsets(h->dev_bytes, h->bin_region_log2));
     const bool binned = h->binned_mode != 0 &&
                         bf_binned_plan_offsets(h->dev_bytes, std::min(count, sub), h->bin_region_log2, &plan) &&
                         (h->binned_mode == 1 || (h->dev_bytes >= (64ull << 20) &&
@@ -876,7 +876,7 @@ int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t
     // one streaming pass over the shard beats a random line fill per probe once the
     // probes outnumber the shard's lines (same cost model and knob shape as the insert).
     BfBinPlan plan;
-    const uint64_t sub = bf_binned_max_offsets();
+    const uint64_t sub = std::max<uint64_t>(1, bf_binned_max_offsets(h->dev_bytes, h->bin_region_log2));
     const uint32_t mode = h->shard_test_binned_mode;
     const bool binned = mode != 0 &&
                         bf_binned_plan_offsets(h->dev_bytes, std::min(count, sub), h->bin_region_log2, &plan, true) &&

@@ -41,7 +41,8 @@ constexpr int kTile = 1024;                   // lanes per workgroup of the fron
 constexpr int kStageVec = 16384 / 16;         // 16 KiB LDS key stage per 1024-key sub-tile
 constexpr uint32_t kMaxSup = 256;             // superbins (8-bit superbin in the sort tags)
 constexpr uint32_t kMaxRel = 8;               // <= 256 regions per superbin
-constexpr uint32_t kMaxBlocks = 512;          // front workgroups
+constexpr uint32_t kMaxBlocks = 512;          // front workgroups before tiles per workgroup grow
+constexpr uint32_t kMaxFrontBlocks = 4096;    // front workgroups once they hold kMaxTilesPerBlock tiles each
 constexpr uint32_t kGroupBlocks = 64;         // front workgroups per group (one wave in bin_group_sum)
 constexpr uint32_t kTileProbes = 12288;       // probes per front tile (LDS sort buffer)
 constexpr int kSlots = 12;                    // probes per lane per tile (k <= 12)
@@ -324,7 +325,10 @@ __global__ __launch_bounds__(kMaxBlocks) void bin_group_sum_kernel(const uint32_
 // base[i]: exclusive prefix of gsum over windows i = (superbin, group); base[N] =
 // all probes.  cb_base[i]: first chunk block of window i (ceil(size / kBlockProbes)
 // blocks each), cb_base[N] = all blocks; cb_window[b] / cb_start[b]: the window
-// and level-2 position of chunk block b.  One workgroup (N <= 2048).
+// and level-2 position of chunk block b.  One workgroup, kScanPer windows per lane
+// (N <= kMaxWindows).
+constexpr uint32_t kScanPer = 4;
+constexpr uint32_t kMaxWindows = 1024 * kScanPer;
 __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __restrict__ gsum, uint32_t N,
                                                               uint32_t* __restrict__ base,
                                                               uint32_t* __restrict__ cb_base,
@@ -332,43 +336,42 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
                                                               uint32_t* __restrict__ cb_start, uint32_t nq,
                                                               unsigned long long* __restrict__ totals) {
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_base[2049], s_cb[2049];
+    __shared__ uint32_t s_base[kMaxWindows + 1], s_cb[kMaxWindows + 1];
     const uint32_t t = threadIdx.x;
-    const uint32_t a = 2 * t < N ? gsum[2 * t] : 0u;
-    const uint32_t b = 2 * t + 1 < N ? gsum[2 * t + 1] : 0u;
-    const uint32_t ca = (a + kBlockProbes - 1) / kBlockProbes, cb = (b + kBlockProbes - 1) / kBlockProbes;
-    uint32_t total, ctotal;
-    const uint32_t ex = block_excl_scan(a + b, s_w, &total);
-    const uint32_t cex = block_excl_scan(ca + cb, s_w, &ctotal);
-    if (2 * t < N) {
-        base[2 * t] = ex;
-        cb_base[2 * t] = cex;
+    uint32_t v[kScanPer], cv[kScanPer], sum = 0, csum = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScanPer; ++e) {   // lane t owns windows [kScanPer t, kScanPer t + kScanPer)
+        const uint32_t w = kScanPer * t + e;
+        v[e] = w < N ? gsum[w] : 0u;
+        cv[e] = (v[e] + kBlockProbes - 1) / kBlockProbes;
+        sum += v[e];
+        csum += cv[e];
     }
-    if (2 * t + 1 < N) {
-        base[2 * t + 1] = ex + a;
-        cb_base[2 * t + 1] = cex + ca;
+    uint32_t total, ctotal;
+    uint32_t ex = block_excl_scan(sum, s_w, &total);
+    uint32_t cex = block_excl_scan(csum, s_w, &ctotal);
+#pragma unroll
+    for (uint32_t e = 0; e < kScanPer; ++e) {
+        const uint32_t w = kScanPer * t + e;
+        if (w < N) {
+            base[w] = ex;
+            cb_base[w] = cex;
+            s_base[w] = ex;
+            s_cb[w] = cex;
+            if (totals && v[e]) atomicAdd(totals + w / nq, (unsigned long long)v[e]);   // per-bucket totals
+        }
+        ex += v[e];
+        cex += cv[e];
     }
     if (t == 0) {
         base[N] = total;
         cb_base[N] = ctotal;
+        s_cb[N] = ctotal;
     }
-    if (totals) {   // per-bucket (superbin / owner) probe totals; zeroed by the caller
-        if (a) atomicAdd(totals + (2 * t) / nq, (unsigned long long)a);
-        if (b) atomicAdd(totals + (2 * t + 1) / nq, (unsigned long long)b);
-    }
+    __syncthreads();
     // every block's window and level-2 start, all lanes over all blocks (a window
     // may hold thousands of blocks): the window is the last one starting at or
     // before the block
-    if (2 * t < N) {
-        s_base[2 * t] = ex;
-        s_cb[2 * t] = cex;
-    }
-    if (2 * t + 1 < N) {
-        s_base[2 * t + 1] = ex + a;
-        s_cb[2 * t + 1] = cex + ca;
-    }
-    if (t == 0) s_cb[N] = ctotal;
-    __syncthreads();
     for (uint32_t blk = t; blk < ctotal; blk += 1024) {
         uint32_t lo = 0, hi = N - 1;
         while (lo < hi) {
@@ -963,11 +966,33 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
 
 }  // namespace
 
-uint64_t bf_binned_max_keys(uint32_t k) {
-    return (uint64_t)kMaxBlocks * kMaxTilesPerBlock * (k <= kTwoKeys ? 2 * kTile : kTile);
+namespace {
+
+// Superbins of a bitset in the region size plan_common picks (0: no plan).
+uint32_t superbins(uint64_t bitset_bytes, uint32_t pref_region_log2);
+
+// Front tiles one pass can take: kMaxTilesPerBlock per workgroup, at most kMaxFrontBlocks
+// workgroups, and (superbin, group) windows within the scan's kMaxWindows.
+uint64_t max_tiles(uint64_t bitset_bytes, uint32_t pref_region_log2) {
+    const uint32_t nsup = superbins(bitset_bytes, pref_region_log2);
+    if (nsup == 0) return 0;
+    const uint64_t groups = kMaxWindows / nsup;
+    const uint64_t blocks = std::min<uint64_t>(kMaxFrontBlocks, groups * kGroupBlocks);
+    return blocks * kMaxTilesPerBlock;
 }
 
-uint64_t bf_binned_max_offsets() { return (uint64_t)kMaxBlocks * kMaxTilesPerBlock * kTileProbes; }
+}  // namespace
+
+uint64_t bf_binned_max_keys(uint32_t k, uint64_t bitset_bytes, uint32_t pref_region_log2) {
+    if (k == 0) return 0;
+    const uint64_t tile_keys = k <= kTwoKeys ? 2 * kTile : kTile;
+    const uint64_t n = max_tiles(bitset_bytes, pref_region_log2) * tile_keys;
+    return std::min<uint64_t>(n, ((1ull << 32) - 1) / k);
+}
+
+uint64_t bf_binned_max_offsets(uint64_t bitset_bytes, uint32_t pref_region_log2) {
+    return std::min<uint64_t>(max_tiles(bitset_bytes, pref_region_log2) * kTileProbes, (1ull << 32) - 1);
+}
 
 namespace {
 
@@ -992,9 +1017,11 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
         p.tile_keys = tile_units;
         p.tile_probes = tile_units * k;
         p.ntiles = (n + tile_units - 1) / tile_units;
-        p.tiles_per_block = (uint32_t)((p.ntiles + kMaxBlocks - 1) / kMaxBlocks);
+        p.tiles_per_block = (uint32_t)std::min<uint64_t>((p.ntiles + kMaxBlocks - 1) / kMaxBlocks, kMaxTilesPerBlock);
+        if (p.ntiles > (uint64_t)kMaxFrontBlocks * p.tiles_per_block) continue;
         p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
         p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
+        if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) continue;
         p.probes = probes;
         p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
         p.scratch_bytes = carve(p, nullptr).bytes;
@@ -1004,17 +1031,22 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
     return false;
 }
 
+uint32_t superbins(uint64_t bitset_bytes, uint32_t pref_region_log2) {
+    BfBinPlan p{};
+    return plan_common(bitset_bytes, 1, 1, 1, pref_region_log2, false, &p) ? p.nsup : 0;
+}
+
 }  // namespace
 
 bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
                     BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kWideSlots || n == 0 || n > bf_binned_max_keys(k)) return false;
+    if (k == 0 || k > (uint32_t)kWideSlots || n == 0) return false;
     return plan_common(bitset_bytes, n, k, k <= kTwoKeys ? 2 * kTile : kTile, pref_region_log2, with_keys, plan);
 }
 
 bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan,
                             bool with_keys) {
-    if (count == 0 || count > bf_binned_max_offsets()) return false;
+    if (count == 0) return false;
     return plan_common(bitset_bytes, count, 1, kTileProbes, pref_region_log2, with_keys, plan);
 }
 
@@ -1160,8 +1192,6 @@ RouteCarve route_carve(const BfBinPlan& p, bool wide, bool with_slot, void* at0)
 // The route runs one batch in one pass (its send buffer is owner-major over the whole batch),
 // so past kMaxBlocks x kMaxTilesPerBlock tiles it takes more front workgroups, as long as the
 // (owner, group) windows fit the one-workgroup scan.
-constexpr uint32_t kMaxRouteBlocks = 4096;
-constexpr uint32_t kMaxWindows = 2048;
 
 bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan) {
     if (k == 0 || k > (uint32_t)kWideSlots || n == 0 || shards == 0 || shards > kMaxSup) return false;
@@ -1174,7 +1204,7 @@ bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with
     p.ntiles = (n + p.tile_keys - 1) / p.tile_keys;
     p.tiles_per_block = (uint32_t)((p.ntiles + kMaxBlocks - 1) / kMaxBlocks);
     if (p.tiles_per_block > kMaxTilesPerBlock) p.tiles_per_block = kMaxTilesPerBlock;
-    if (p.ntiles > (uint64_t)kMaxRouteBlocks * p.tiles_per_block) return false;
+    if (p.ntiles > (uint64_t)kMaxFrontBlocks * p.tiles_per_block) return false;
     p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
     p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
     if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) return false;

@@ -83,9 +83,11 @@ inline void bf_mark(BfMarks* mk, hipStream_t s, const char* name) {
     mk->names[mk->used] = name;
     (void)hipEventRecord(mk->ev[++mk->used], s);
 }
-// Largest batch one binned launch takes (larger batches go in sub-batches).
-uint64_t bf_binned_max_keys(uint32_t k);
-// false: the batch / filter shape is outside the binned path (k > 12, more than
+// Largest batch one binned launch takes on this bitset (larger batches go in
+// sub-batches): up to 4096 front workgroups of 16 tiles, within 4096 (superbin,
+// group) windows of the one-workgroup scan.
+uint64_t bf_binned_max_keys(uint32_t k, uint64_t bitset_bytes, uint32_t pref_region_log2);
+// false: the batch / filter shape is outside the binned path (k > 16, more than
 // bf_binned_max_keys keys, or a bitset beyond 65536 regions of 2^20 bits).
 bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref_region_log2, bool with_keys,
                     BfBinPlan* plan);
@@ -94,7 +96,7 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
                                    void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
 // Owner side of a partitioned filter: `count` routed shard-local offsets (uint32
 // when route32, else uint64) ORed into the shard through the same pipeline.
-uint64_t bf_binned_max_offsets();
+uint64_t bf_binned_max_offsets(uint64_t bitset_bytes, uint32_t pref_region_log2);
 bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan,
                             bool with_keys = false);
 hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
@@ -127,7 +129,7 @@ hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const ui
 // Partitioned filters, requester side, fused (bf_binned.hip): hash + per-tile
 // LDS sort by owner, then an owner-major gather into send[] (uint64 entries when
 // wide, else uint32) and slot[] (key index of each send entry, nullable);
-// counts[s] = probes for owner s.  Needs n <= bf_binned_max_keys(k), k <= 12.
+// counts[s] = probes for owner s.  Needs k <= 16 and P x groups <= 4096 windows.
 bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan);
 hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
                                  const uint64_t* offsets, uint64_t bias, uint64_t n, void* scratch, void* send,
