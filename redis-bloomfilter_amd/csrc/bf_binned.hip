@@ -1002,8 +1002,12 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
     const uint64_t probes = n * k;
     if (probes >= (1ull << 32)) return false;
     const uint64_t bits = bitset_bytes * 8;
-    const uint32_t order[2] = {pref_region_log2 == 20 ? 20u : 19u, pref_region_log2 == 20 ? 19u : 20u};
+    // region (LDS image) sizes tried, the preferred one first: 2^18 (32 KiB, 512 lanes), 2^19, 2^20
+    const uint32_t order[3] = {pref_region_log2 == 20 ? 20u : (pref_region_log2 == 18 ? 18u : 19u),
+                               pref_region_log2 == 20 ? 19u : (pref_region_log2 == 18 ? 19u : 20u),
+                               pref_region_log2 == 18 ? 20u : 0u};
     for (uint32_t rl : order) {
+        if (rl == 0) break;
         const uint64_t nbins = (bits + (1ull << rl) - 1) >> rl;
         uint32_t rel = 0;
         while (((nbins + (1ull << rel) - 1) >> rel) > kMaxSup) ++rel;
@@ -1056,7 +1060,11 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
                         uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
     const uint64_t nwords = bitset_bytes / 4;
     const uint32_t dense = p.probes >= (uint64_t)p.nbins * (1ull << (p.region_log2 - 7)) ? 1u : 0u;
-    if (p.region_log2 == 19)
+    if (p.region_log2 == 18)
+        hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
+                           g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
+                           p.rel_log2, dense, any_flag, g.dirty);
+    else if (p.region_log2 == 19)
         hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
                            any_flag, g.dirty);
@@ -1106,7 +1114,11 @@ namespace {
 hipError_t launch_test(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes, uint8_t* out8,
                        hipStream_t s, BfMarks* mk) {
     const uint64_t nwords = bitset_bytes / 4;
-    if (p.region_log2 == 19)
+    if (p.region_log2 == 18)
+        hipLaunchKernelGGL((bin_test_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
+                           g.bits, nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks,
+                           p.ngroups, p.rel_log2, out8);
+    else if (p.region_log2 == 19)
         hipLaunchKernelGGL((bin_test_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
                            p.rel_log2, out8);

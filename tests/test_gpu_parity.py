@@ -303,7 +303,7 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
         assert f.export_redis() == s
 
 
-@pytest.mark.parametrize("rl", ["19", "20"])
+@pytest.mark.parametrize("rl", ["18", "19", "20"])
 @pytest.mark.parametrize("case", ["dup", "tiny", "long", "k12", "k13", "k16", "nstar"])
 def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     """Forced binned insert and include? on shapes that stress their partition passes: one key repeated
@@ -312,7 +312,7 @@ def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     the per-probe cursor path), keys past the single-block SHA-1 (multi-block hash in the
     count pass), k = 12 (every probe slot of the 12-slot front used), k = 13 and 16 (the 16-slot
     front), and a 200k-key batch on the
-    north-star filter; both region sizes (64 KiB / 128 KiB LDS images)."""
+    north-star filter; every region size (32 / 64 / 128 KiB LDS images)."""
     monkeypatch.setenv("BFHIP_INSERT_BINNED", "1")
     monkeypatch.setenv("BFHIP_INCLUDE_BINNED", "1")
     monkeypatch.setenv("BFHIP_BIN_REGION_LOG2", rl)
