@@ -265,16 +265,30 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     bitset = f.device_bytes
     # algorithmic bytes per launch of each kernel (SURVEY §8 d for the random-access kernels;
     # the binned insert's kernels by the arrays each one must read and write)
+    E = 4 if (pf is None or pf.engine.offset_dtype == torch.int32) else 8   # routed offset bytes
     algo = {
         "bf_keys_kernel<INCLUDE>": batch * (Lmean + 8 + 1 + k * GRANULE),
         "bf_keys_kernel<INSERT>": batch * (Lmean + 8 + 2 * k * GRANULE),
         "bf_keys_kernel<INSERT_FLAGS>": batch * (Lmean + 8 + 2 * k * GRANULE + 1),
         # binned path (bf_binned.hip): keys in, probe arrays written / read once, the bitset
         # streamed once (read + write for insert, read for include?)
-        "bin_front": batch * (Lmean + 8) + P * 4 * (2 if inc_binned else 1) + (batch if inc_binned else 0),
-        "bin_mid": P * 4 * 3 + (P * 4 * 2 if inc_binned else 0),
+        "bin_front": batch * (Lmean + 8) + P * 4,
+        "bin_front_keys": batch * (Lmean + 8) + P * 8 + batch,
+        "bin_mid": P * 4 * 3,
+        "bin_mid_keys": P * 8 * 3,
         "bin_apply": P * 4 + 2 * bitset,
         "bin_test": P * 8 + bitset,
+        # partitioned (P = probes one rank sends, about what it receives): requester route,
+        # owner-side sort of the routed offsets, direct shard ops, combine
+        "route_front": batch * (Lmean + 8) + P * (E if E == 4 else 5),
+        "route_front_slot": batch * (Lmean + 8) + P * ((E if E == 4 else 5) + 4),
+        "route_gather": P * ((E if E == 4 else 5) + E),
+        "route_gather_slot": P * ((E if E == 4 else 5) + E + 8),
+        "bin_front_offsets": P * (E + 4),
+        "bin_front_offsets_keys": P * (E + 8),
+        "shard_insert": P * 2 * GRANULE,
+        "shard_test": P * (GRANULE + 1),
+        "combine": P * 5 + batch,
     }
     for name, kt in kernels.items():
         if name in algo:

@@ -934,7 +934,7 @@ hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c
                            c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
-    bf_mark(mk, s, "bin_mid");
+    bf_mark(mk, s, p.with_keys ? "bin_mid_keys" : "bin_mid");
     return hipGetLastError();
 }
 
@@ -960,7 +960,7 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
         hipLaunchKernelGGL(bin_front_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
                            p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
                            out8);
-    bf_mark(mk, s, "bin_front");
+    bf_mark(mk, s, p.with_keys ? "bin_front_keys" : "bin_front");
     return launch_groups_mid(g, p, c, s, mk);
 }
 
@@ -1152,7 +1152,7 @@ hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint
         hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
                            c.level1_key, c.stab, c.gcnt);
-    bf_mark(mk, s, "bin_front_offsets");
+    bf_mark(mk, s, "bin_front_offsets_keys");
     if ((e = launch_groups_mid(g, p, c, s, mk)) != hipSuccess) return e;
     return launch_test(g, p, c, bitset_bytes, out8, s, mk);
 }
