@@ -282,6 +282,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         # owner-side sort of the routed offsets, direct shard ops, combine
         "route_front": batch * (Lmean + 8) + P * (E if E == 4 else 5),
         "route_front_slot": batch * (Lmean + 8) + P * ((E if E == 4 else 5) + 4),
+        "route_win": batch * (Lmean + 8) + P * E,
+        "route_win_slot": batch * (Lmean + 8) + P * (E + 4),
         "route_gather": P * ((E if E == 4 else 5) + E),
         "route_gather_slot": P * ((E if E == 4 else 5) + E + 8),
         "bin_front_offsets": P * (E + 4),

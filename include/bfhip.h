@@ -184,6 +184,21 @@ int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_of
                   void* d_send /* uint64[n*k], or uint32 with BF_FLAG_ROUTE32 */,
                   uint32_t* d_slot /* nullable, n*k */,
                   uint64_t* d_counts, void* stream);
+/* bf_route_windows_dev   bf_route_dev without its owner-major gather pass: owner s's probes
+ *                        land in a fixed window, d_send[s*window_cap .. s*window_cap +
+ *                        d_counts[s]), in an unspecified order, with d_slot (nullable)
+ *                        alongside; each per-owner window feeds one send of a grouped
+ *                        send/recv exchange.  If some d_counts[s] > window_cap (a skewed
+ *                        batch), that window's contents are undefined: check the counts and
+ *                        fall back to bf_route_dev.  Same limits as bf_route_dev's fused path.
+ * bf_combine_windows_dev bf_combine_dev over that layout: d_bits and d_slot indexed by window
+ *                        entry, the live entries of window s being the first d_counts[s]. */
+int  bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                          void* d_send /* shard_count*window_cap entries */, uint32_t* d_slot /* nullable */,
+                          uint64_t window_cap, uint64_t* d_counts, void* stream);
+int  bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t window_cap,
+                            const uint64_t* d_counts /* device, shard_count */, uint64_t n, uint8_t* d_out,
+                            void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
 int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,

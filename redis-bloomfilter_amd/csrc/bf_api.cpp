@@ -829,6 +829,32 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     return BF_OK;
 }
 
+int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                         void* d_send, uint32_t* d_slot, uint64_t window_cap, uint64_t* d_counts, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
+    if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    const uint64_t probes = n * h->k;
+    if (n && probes / n != h->k) return set_err(h, BF_EINVAL, "n*k overflows");
+    if (probes >= (1ull << 32)) return set_err(h, BF_EINVAL, "n*k must be < 2^32 per call (slot indices are 32-bit)");
+    if (window_cap && (uint64_t)h->shards > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window_cap overflows");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    hipStream_t s = pick_stream(h, stream);
+    BfBinPlan plan;
+    if (n && !bf_route_plan(n, h->k, h->shards, !h->route32, d_slot != nullptr, &plan))
+        return set_err(h, BF_EINVAL, "batch of %llu keys at k=%u over %u shards exceeds one window-route pass",
+                       (unsigned long long)n, h->k, h->shards);
+    if (!n) plan.nsup = h->shards;
+    uint64_t bias = 0;
+    const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_route_windows(h->g, plan, !h->route32, k16, d_offsets, bias, n, d_send, d_slot, window_cap,
+                                      reinterpret_cast<unsigned long long*>(d_counts), s, mk));
+    return BF_OK;
+}
+
 int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
     if (!h) return BF_EINVAL;
     if (count && !d_local) return set_err(h, BF_EINVAL, "d_local is NULL");
@@ -914,6 +940,21 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
     hipStream_t s = pick_stream(h, stream);
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, s));
+    bf_mark(mk, s, "combine");
+    return BF_OK;
+}
+
+int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t window_cap,
+                           const uint64_t* d_counts, uint64_t n, uint8_t* d_out, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (n && (!d_bits || !d_slot || !d_counts || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    hipStream_t s = pick_stream(h, stream);
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_combine_windows(d_bits, d_slot, window_cap, reinterpret_cast<const unsigned long long*>(d_counts),
+                                        h->shards, n, d_out, s));
     bf_mark(mk, s, "combine");
     return BF_OK;
 }

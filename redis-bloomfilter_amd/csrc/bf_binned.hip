@@ -422,14 +422,23 @@ __device__ __forceinline__ uint32_t wave_agg_rank(bool live, uint32_t owner, uin
 // tile's owner run table [owner][tile]; per-workgroup owner totals.  WIDE: the
 // owner-local offsets need more than 32 bits (their high byte is kept apart);
 // SLOT: each probe carries its key index.
-template <bool WIDE, bool SLOT, int SLOTS>
+//
+// WIN (bf_route_windows_dev): no tile-major level 1, group scan or gather pass.  Each tile
+// claims room for its owner-s run in owner s's fixed window of the send buffer with one
+// global atomic per (tile, owner) on wcounts[s], and writes the run straight there
+// (entries [s*wcap, s*wcap + wcounts[s]) in an unspecified order; slots ride along).  A run
+// that would pass wcap is dropped; wcounts[s] still ends at the owner's full total, so
+// the caller sees the overflow and re-routes through the contiguous path.
+template <bool WIDE, bool SLOT, int SLOTS, bool WIN>
 __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                  const uint64_t* __restrict__ offsets, uint64_t bias,
                                                  uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
                                                  uint32_t P, uint32_t* __restrict__ lo1,
                                                  uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1,
                                                  uint16_t* __restrict__ stab,
-                                                 uint32_t* __restrict__ gcnt) {
+                                                 uint32_t* __restrict__ gcnt, uint64_t wcap,
+                                                 unsigned long long* __restrict__ wcounts,
+                                                 void* __restrict__ wsend, uint32_t* __restrict__ wslot) {
     // The key stage (offsets + bytes) is dead once the tile is hashed, so the sorted
     // tile-relative key indices (u16) reuse it: 76 KiB in all without WIDE, two
     // workgroups per CU.
@@ -443,6 +452,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
     uint16_t* s_key = reinterpret_cast<uint16_t*>(s_raw);
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
+    __shared__ unsigned long long s_gbase[WIN ? kMaxSup : 1];
     __shared__ uint32_t s_lo[kTile * SLOTS];
     __shared__ uint8_t s_hi[WIDE ? kTile * SLOTS : 1];
     const uint32_t t = threadIdx.x;
@@ -504,7 +514,15 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         __syncthreads();
         const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
         const uint32_t ex = block_excl_scan(c, s_w, nullptr);
-        if (t <= P) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [owner][tile]
+        if constexpr (WIN) {
+            if (t < P) {   // claim this tile's run in owner t's window (~0 when it would overflow)
+                unsigned long long gb = 0;
+                if (c) gb = atomicAdd(wcounts + t, (unsigned long long)c);
+                s_gbase[t] = (gb + c <= wcap) ? (unsigned long long)t * wcap + gb : ~0ull;
+            }
+        } else {
+            if (t <= P) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [owner][tile]
+        }
         if (t < kMaxSup) {
             s_lbase[t] = ex;
             s_gcnt[t] += c;
@@ -526,34 +544,53 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         __syncthreads();
         const uint64_t seg = key0 * k;
         const uint32_t tp = tk * k;
-        for (uint32_t j = t; j < tp; j += kTile) {
-            lo1[seg + j] = s_lo[j];
-            if constexpr (WIDE) hi1[seg + j] = s_hi[j];
-            if constexpr (SLOT) key1[seg + j] = (uint32_t)key0 + s_key[j];
+        if constexpr (WIN) {
+            for (uint32_t j = t; j < tp; j += kTile) {
+                const uint32_t o = run_of(s_lbase, P, j);
+                const unsigned long long gb = s_gbase[o];   // the run's place in owner o's window
+                if (gb != ~0ull) {
+                    const uint64_t d = gb + (j - s_lbase[o]);
+                    if constexpr (WIDE)
+                        static_cast<uint64_t*>(wsend)[d] = ((uint64_t)s_hi[j] << 32) | s_lo[j];
+                    else
+                        static_cast<uint32_t*>(wsend)[d] = s_lo[j];
+                    if constexpr (SLOT) wslot[d] = (uint32_t)key0 + s_key[j];
+                }
+            }
+            __syncthreads();   // s_gbase and the staged keys are rewritten by the next tile
+        } else {
+            for (uint32_t j = t; j < tp; j += kTile) {
+                lo1[seg + j] = s_lo[j];
+                if constexpr (WIDE) hi1[seg + j] = s_hi[j];
+                if constexpr (SLOT) key1[seg + j] = (uint32_t)key0 + s_key[j];
+            }
+            if constexpr (SLOT) __syncthreads();   // the next tile's staging overwrites s_key
         }
-        if constexpr (SLOT) __syncthreads();   // the next tile's staging overwrites s_key
     }
-    if (t < P) gcnt[(uint64_t)blockIdx.x * P + t] = s_gcnt[t];
+    if constexpr (!WIN)
+        if (t < P) gcnt[(uint64_t)blockIdx.x * P + t] = s_gcnt[t];
 }
 
 #define BF_ROUTE_FRONT_ARGS                                                                                     \
     BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets, uint64_t bias, uint64_t n, \
         uint32_t tile_keys, uint32_t tiles_per_block, uint32_t P, uint32_t* __restrict__ lo1,                   \
         uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1, uint16_t* __restrict__ stab,                     \
-        uint32_t* __restrict__ gcnt
-template <bool WIDE, bool SLOT, int SLOTS>
+        uint32_t* __restrict__ gcnt, uint64_t wcap, unsigned long long* __restrict__ wcounts,                 \
+        void* __restrict__ wsend, uint32_t* __restrict__ wslot
+#define BF_ROUTE_FRONT_PASS \
+    g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt, wcap, wcounts, wsend, wslot
+template <bool WIDE, bool SLOT, int SLOTS, bool WIN>
 __global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<WIDE, SLOT, SLOTS>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1,
-                                        stab, gcnt);
+    route_front_body<WIDE, SLOT, SLOTS, WIN>(BF_ROUTE_FRONT_PASS);
 }
 // 32-bit offsets (shards of <= 2^32 bits): 76 KiB of LDS with or without slots, so two
 // workgroups per CU at 8 waves per SIMD, as bin_front
-template <bool SLOT>
+template <bool SLOT, bool WIN>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void route_front32_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<false, SLOT, kSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1,
-                                          stab, gcnt);
+    route_front_body<false, SLOT, kSlots, WIN>(BF_ROUTE_FRONT_PASS);
 }
+#undef BF_ROUTE_FRONT_PASS
 #undef BF_ROUTE_FRONT_ARGS
 
 // One workgroup per 8192-probe block of an (owner, group) window (the grid is an
@@ -1235,19 +1272,22 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     if ((e = hipMemsetAsync(counts, 0, (uint64_t)p.nsup * sizeof(unsigned long long), s)) != hipSuccess) return e;
     if (n == 0) return hipSuccess;
 #define BF_ROUTE_FRONT(W, S, SL)                                                                                  \
-    hipLaunchKernelGGL((route_front_kernel<W, S, SL>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, \
-                       n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt)
+    hipLaunchKernelGGL((route_front_kernel<W, S, SL, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, \
+                       bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,       \
+                       (uint64_t)0, nullptr, nullptr, nullptr)
     if (g.k > (uint32_t)kSlots) {
         if (wide) { if (slot) BF_ROUTE_FRONT(true, true, kWideSlots); else BF_ROUTE_FRONT(true, false, kWideSlots); }
         else { if (slot) BF_ROUTE_FRONT(false, true, kWideSlots); else BF_ROUTE_FRONT(false, false, kWideSlots); }
     }
     else if (wide) { if (slot) BF_ROUTE_FRONT(true, true, kSlots); else BF_ROUTE_FRONT(true, false, kSlots); }
     else if (slot)
-        hipLaunchKernelGGL(route_front32_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
-                           p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);
+        hipLaunchKernelGGL((route_front32_kernel<true, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
+                           bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,
+                           (uint64_t)0, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL(route_front32_kernel<false>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias,
-                           n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt);
+        hipLaunchKernelGGL((route_front32_kernel<false, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
+                           bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,
+                           (uint64_t)0, nullptr, nullptr, nullptr);
 #undef BF_ROUTE_FRONT
     bf_mark(mk, s, slot ? "route_front_slot" : "route_front");
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
@@ -1265,5 +1305,32 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     else { if (slot) BF_ROUTE_GATHER(false, true); else BF_ROUTE_GATHER(false, false); }
 #undef BF_ROUTE_GATHER
     bf_mark(mk, s, slot ? "route_gather_slot" : "route_gather");
+    return hipGetLastError();
+}
+
+// Window route (bf_route_windows_dev): the front pass alone, each tile's owner runs written
+// straight into fixed per-owner windows of wcap entries (no level 1, group scan or gather).
+hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
+                                   const uint64_t* offsets, uint64_t bias, uint64_t n, void* send, uint32_t* slot,
+                                   uint64_t wcap, unsigned long long* counts, hipStream_t s, BfMarks* mk) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(counts, 0, (uint64_t)p.nsup * sizeof(unsigned long long), s)) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+#define BF_ROUTE_WIN(KERNEL)                                                                                      \
+    hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,      \
+                       p.tiles_per_block, p.nsup, nullptr, nullptr, nullptr, nullptr, nullptr, wcap, counts, send, \
+                       slot)
+    if (g.k > (uint32_t)kSlots) {
+        if (wide) { if (slot) BF_ROUTE_WIN((route_front_kernel<true, true, kWideSlots, true>));
+                    else BF_ROUTE_WIN((route_front_kernel<true, false, kWideSlots, true>)); }
+        else { if (slot) BF_ROUTE_WIN((route_front_kernel<false, true, kWideSlots, true>));
+               else BF_ROUTE_WIN((route_front_kernel<false, false, kWideSlots, true>)); }
+    }
+    else if (wide) { if (slot) BF_ROUTE_WIN((route_front_kernel<true, true, kSlots, true>));
+                     else BF_ROUTE_WIN((route_front_kernel<true, false, kSlots, true>)); }
+    else if (slot) BF_ROUTE_WIN((route_front32_kernel<true, true>));
+    else BF_ROUTE_WIN((route_front32_kernel<false, true>));
+#undef BF_ROUTE_WIN
+    bf_mark(mk, s, slot ? "route_win_slot" : "route_win");
     return hipGetLastError();
 }

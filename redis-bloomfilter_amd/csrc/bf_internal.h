@@ -136,6 +136,19 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
                                  uint32_t* slot, unsigned long long* counts, hipStream_t s,
                                  BfMarks* marks = nullptr);
 
+// Window route (bf_binned.hip): the fused route's front pass writing each tile's owner
+// runs straight into send[s*wcap ..] (and slot[s*wcap ..]) at places claimed with
+// atomics on counts[s]; a run past wcap is dropped (counts[s] > wcap tells the caller).
+hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
+                                   const uint64_t* offsets, uint64_t bias, uint64_t n, void* send, uint32_t* slot,
+                                   uint64_t wcap, unsigned long long* counts, hipStream_t s,
+                                   BfMarks* marks = nullptr);
+// out[j] = AND of bits[p] over the window entries p = s*wcap + i, i < counts[s], s < P,
+// with slot[p] == j.
+hipError_t bf_launch_combine_windows(const uint8_t* bits, const uint32_t* slot, uint64_t wcap,
+                                     const unsigned long long* counts, uint32_t P, uint64_t n, uint8_t* out,
+                                     hipStream_t s);
+
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
 // pairs by owner into send[]; slot[pos] (nullable) = key index (probe / k) of send entry pos.
 // counts[P] must hold the per-owner totals (from BF_OP_ROUTE).

@@ -334,6 +334,21 @@ __global__ __launch_bounds__(256) void combine_kernel(const uint8_t* __restrict_
         if (!bits[p]) out[slot[p]] = 0;
 }
 
+// The same over the window layout of bf_route_windows_dev: window s holds counts[s] live
+// entries at s*wcap; the rest of each window is ignored.
+__global__ __launch_bounds__(256) void combine_windows_kernel(const uint8_t* __restrict__ bits,
+                                                              const uint32_t* __restrict__ slot, uint64_t wcap,
+                                                              const unsigned long long* __restrict__ counts,
+                                                              uint32_t P, uint8_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t s = blockIdx.y;   // one grid row per window
+    const uint64_t live = counts[s] < wcap ? counts[s] : wcap;
+    const uint8_t* wb = bits + s * wcap;
+    const uint32_t* ws = slot + s * wcap;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < live; i += stride)
+        if (!wb[i]) out[ws[i]] = 0;
+}
+
 uint32_t stream_grid(uint64_t nvec) {
     uint64_t g = (nvec + 255) / 256;
     if (g > 2048) g = 2048;   // grid-stride beyond 8 blocks per CU
@@ -419,6 +434,19 @@ hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t
     if (e != hipSuccess) return e;
     const uint64_t total = n * k;
     hipLaunchKernelGGL(combine_kernel, dim3(stream_grid(total)), dim3(256), 0, s, bits, slot, total, out);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_combine_windows(const uint8_t* bits, const uint32_t* slot, uint64_t wcap,
+                                     const unsigned long long* counts, uint32_t P, uint64_t n, uint8_t* out,
+                                     hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(out, 1, n, s);
+    if (e != hipSuccess) return e;
+    if (wcap == 0) return hipSuccess;
+    uint32_t gx = stream_grid(wcap) / P;
+    hipLaunchKernelGGL(combine_windows_kernel, dim3(gx ? gx : 1u, P), dim3(256), 0, s, bits, slot, wcap, counts, P,
+                       out);
     return hipGetLastError();
 }
 

@@ -7,8 +7,8 @@ Two layouts (SURVEY §8 e):
     over the P ranks (block = 2^block_log2 bits, owner = block % P), so a
     filter larger than one GPU's HBM (the 200B-key config) fits, and the
     probe-dense low offsets (h0 < 2^32, ruby.rb:51) spread over every GPU.
-    insert:   route (hash -> owner-local offsets grouped by owner) ->
-              all_to_all(counts) -> all_to_all(offsets) -> owner atomic-OR
+    insert:   route (hash -> owner-local offsets, one send window per owner) ->
+              all_to_all(counts) -> all_to_all(offsets) -> owner OR
     include?: route -> all_to_all(offsets) -> owner bit test ->
               reverse all_to_all(1 byte per probe) -> requester AND per key
     Each rank brings its own key batch (weak scaling); the only data-path
@@ -20,8 +20,11 @@ Two layouts (SURVEY §8 e):
     rank's inserts and the replicas stay byte-identical.
 
 The per-rank compute goes through an *engine* with four primitives (route,
-shard_insert, shard_test, combine); ``HipEngine`` is libbfhip.so's
-``bf_route_dev`` / ``bf_shard_*_dev`` / ``bf_combine_dev``.  The CPU tests
+shard_insert, shard_test, combine) plus the window forms of route and combine;
+``HipEngine`` is libbfhip.so's ``bf_route[_windows]_dev`` / ``bf_shard_*_dev`` /
+``bf_combine[_windows]_dev``.  The all-to-alls are grouped sends/receives
+(``batch_isend_irecv``: one RCCL group of ncclSend/ncclRecv), so each owner's
+segment can sit in its own window of the send buffer.  The CPU tests
 substitute a numpy engine to exercise this module's exchange logic over gloo.
 """
 from __future__ import annotations
@@ -109,6 +112,24 @@ class HipEngine:
                               slot.data_ptr() if want_slot else 0, counts.data_ptr(), stream=self._stream())
         return send, slot, counts
 
+    def route_windows(self, kb: torch.Tensor, ko: torch.Tensor, n: int, cap: int, want_slot: bool = True):
+        """route() without the owner-major gather: owner s's probes are send[s*cap : s*cap +
+        counts[s]] in an unspecified order (slot alongside); counts[s] > cap = overflow."""
+        send = torch.empty(self.P * cap, dtype=self.offset_dtype, device=self.device)
+        slot = torch.empty(self.P * cap, dtype=torch.int32, device=self.device) if want_slot else None
+        counts = torch.empty(self.P, dtype=torch.int64, device=self.device)
+        self.filter.route_windows_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
+                                      slot.data_ptr() if want_slot else 0, cap, counts.data_ptr(),
+                                      stream=self._stream())
+        return send, slot, counts
+
+    def combine_windows(self, bits: torch.Tensor, slot: torch.Tensor, counts: torch.Tensor, cap: int,
+                        n: int) -> torch.Tensor:
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self.filter.combine_windows_dev(bits.data_ptr(), slot.data_ptr(), cap, counts.data_ptr(), n, out.data_ptr(),
+                                        stream=self._stream())
+        return out
+
     def shard_insert(self, local: torch.Tensor) -> None:
         self.filter.shard_insert_dev(local.data_ptr(), local.numel(), stream=self._stream())
 
@@ -144,10 +165,20 @@ def _device_batch(keys, device) -> Tuple[torch.Tensor, torch.Tensor, int]:
     return kb, ko, len(offs) - 1
 
 
-class PartitionedFilter:
-    """A filter block-cyclically partitioned over the ranks of a process group."""
+def _prefix(counts) -> List[int]:
+    return np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64).tolist() if len(counts) else []
 
-    def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None):
+
+class PartitionedFilter:
+    """A filter block-cyclically partitioned over the ranks of a process group.
+
+    windows=True (default): the route writes each owner's probes straight into a fixed
+    window of the send buffer (bf_route_windows_dev) and the windows go out as one group of
+    sends/receives, so no pass regroups them owner-major; a batch that overflows a window
+    takes the contiguous bf_route_dev path instead (same exchange, same answers)."""
+
+    def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None,
+                 windows: bool = True):
         self.group = group
         self.P = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -158,6 +189,8 @@ class PartitionedFilter:
             engine = HipEngine(self.m, self.k, self.P, self.rank, self.block_log2, device)
         self.engine = engine
         self.device = engine.device
+        self.windows = windows
+        self.window_overflows = 0
 
     # -- exchange helpers
     def _splits(self, counts: torch.Tensor):
@@ -168,49 +201,105 @@ class PartitionedFilter:
         cnt = torch.stack([counts, recv_counts]).cpu()
         return cnt[0].tolist(), cnt[1].tolist()
 
-    def _exchange(self, send: torch.Tensor, counts: torch.Tensor, async_op: bool = False):
-        send_splits, recv_splits = self._splits(counts)
-        recv = torch.empty(sum(recv_splits), dtype=send.dtype, device=send.device)
-        work = dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group, async_op=async_op)
-        return (recv, send_splits, recv_splits, work) if async_op else (recv, send_splits, recv_splits)
+    def _cap(self, n: int) -> int:
+        """Window size per owner for a batch of n keys: the block-cyclic map spreads probes
+        evenly, so 1/P of them plus 12.5 % and a small-batch slack; a skewed batch
+        (e.g. one key repeated) overflows and takes the contiguous route."""
+        probes = n * self.k
+        return min(probes, probes // self.P + probes // (8 * self.P) + 4096)
+
+    def _route(self, kb, ko, n: int, want_slot: bool):
+        """Probes grouped by owner: (send, slot, counts, displs, splits) where owner s's
+        entries are send[displs[s] : displs[s] + splits[0][s]]; splits = (send, receive)
+        counts, already exchanged (the host waits for that small all-to-all)."""
+        e = self.engine
+        if self.windows and hasattr(e, "route_windows"):
+            cap = self._cap(n)
+            send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
+            splits = self._splits(counts)
+            if max(splits[0]) <= cap:
+                return send, slot, counts, [s * cap for s in range(self.P)], splits, cap
+            # A window past cap holds undefined entries: re-route contiguously.  Each rank
+            # decides alone and needs no second count exchange (the per-owner totals are the
+            # same), and the grouped send/recv below serves both layouts.
+            self.window_overflows += 1
+            send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
+        else:
+            send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
+            splits = self._splits(counts)
+        return send, slot, counts, _prefix(splits[0]), splits, None
+
+    def _p2p(self, send: torch.Tensor, sdispl, ssplit, recv: torch.Tensor, rdispl, rsplit):
+        """Grouped send/recv: send[sdispl[s] : +ssplit[s]] to rank s, recv[rdispl[s] :
+        +rsplit[s]] from rank s (an all-to-all whose segments need not be contiguous; one
+        RCCL group of ncclSend/ncclRecv on the process group's stream).  The self segment
+        is a device copy on the current stream.  Returns the works to wait on."""
+        ops = []
+        for peer in range(self.P):
+            sv = send[sdispl[peer]: sdispl[peer] + ssplit[peer]]
+            rv = recv[rdispl[peer]: rdispl[peer] + rsplit[peer]]
+            if peer == self.rank:
+                if ssplit[peer]:
+                    rv.copy_(sv)
+                continue
+            g = peer if self.group is None else dist.get_global_rank(self.group, peer)
+            if ssplit[peer]:
+                ops.append(dist.P2POp(dist.isend, sv, g, self.group))
+            if rsplit[peer]:
+                ops.append(dist.P2POp(dist.irecv, rv, g, self.group))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def _exchange(self, kb, ko, n: int, want_slot: bool):
+        """route, then the offsets to their owners (async): returns (recv, route, works)."""
+        rt = self._route(kb, ko, n, want_slot)
+        send, _, _, displs, (ss, rs), _ = rt
+        recv = torch.empty(sum(rs), dtype=send.dtype, device=send.device)
+        works = self._p2p(send, displs, ss, recv, _prefix(rs), rs)
+        return recv, rt, works
+
+    def _answer(self, bits: torch.Tensor, rt, n: int) -> torch.Tensor:
+        """Owner answers (one byte per received probe) back to the requesters, then AND per key."""
+        send, slot, counts, displs, (ss, rs), cap = rt
+        back = torch.empty(self.P * cap if cap is not None else sum(ss), dtype=torch.uint8, device=bits.device)
+        for w in self._p2p(bits, _prefix(rs), rs, back, displs, ss):
+            w.wait()
+        if cap is not None:
+            return self.engine.combine_windows(back, slot, counts, cap, n)
+        return self.engine.combine(back, slot, n)
 
     # -- device-resident batch API (keys already in device memory)
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
-        send, _, counts = self.engine.route(kb, ko, n, want_slot=False)
-        recv, _, _ = self._exchange(send, counts)
+        recv, _, works = self._exchange(kb, ko, n, want_slot=False)
+        for w in works:
+            w.wait()
         self.engine.shard_insert(recv)
 
     def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
-        send, slot, counts = self.engine.route(kb, ko, n)
-        recv, send_splits, recv_splits = self._exchange(send, counts)
-        bits = self.engine.shard_test(recv)
-        back = torch.empty(sum(send_splits), dtype=torch.uint8, device=bits.device)
-        dist.all_to_all_single(back, bits, send_splits, recv_splits, group=self.group)
-        return self.engine.combine(back, slot, n)
+        recv, rt, works = self._exchange(kb, ko, n, want_slot=True)
+        for w in works:
+            w.wait()
+        return self._answer(self.engine.shard_test(recv), rt, n)
 
     def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
                            qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
         """insert_many_dev(ikb, iko, ni) then include_many_dev(qkb, qko, nq), same results,
         with the exchanges overlapped with the other batch's kernels:
 
-            route(ins) | a2a(ins) || route(inc) | a2a(inc) || shard_insert | shard_test | a2a(back) | combine
+            route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test | send(back) | combine
 
-        The collectives run on the process group's own stream (async_op), the kernels on
-        the current stream; every owner still applies all ranks' inserts before it tests
+        The sends/receives run on the process group's own stream, the kernels on the
+        current stream; every owner still applies all ranks' inserts before it tests
         (shard_insert precedes shard_test on its stream), so the include? answers see the
         batch's inserts exactly as in the sequential form."""
         e = self.engine
-        send_i, _, cnt_i = e.route(ikb, iko, ni, want_slot=False)
-        recv_i, _, _, w_i = self._exchange(send_i, cnt_i, async_op=True)
-        send_q, slot_q, cnt_q = e.route(qkb, qko, nq)            # overlaps a2a(ins)
-        w_i.wait()
-        recv_q, ss_q, rs_q, w_q = self._exchange(send_q, cnt_q, async_op=True)
-        e.shard_insert(recv_i)                                    # overlaps a2a(inc)
-        w_q.wait()
-        bits = e.shard_test(recv_q)
-        back = torch.empty(sum(ss_q), dtype=torch.uint8, device=bits.device)
-        dist.all_to_all_single(back, bits, ss_q, rs_q, group=self.group)
-        return e.combine(back, slot_q, nq)
+        recv_i, _, w_i = self._exchange(ikb, iko, ni, want_slot=False)
+        recv_q, rt_q, w_q = self._exchange(qkb, qko, nq, want_slot=True)   # route(inc) overlaps send(ins)
+        for w in w_i:
+            w.wait()
+        e.shard_insert(recv_i)                                              # overlaps send(inc)
+        for w in w_q:
+            w.wait()
+        return self._answer(e.shard_test(recv_q), rt_q, nq)
 
     # -- host API (each rank passes its own keys)
     def insert_many(self, keys: Iterable) -> None:

@@ -7,6 +7,7 @@ infrastructure), since this container has no GPU.  Rank 0 checks the
 assembled Redis string and every include? answer against a single-filter
 oracle run over all ranks' keys.
 """
+import hashlib
 import json
 import os
 import sys
@@ -53,7 +54,20 @@ def main():
     pf3 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
     got3 = pf3.insert_include(mine, probe)
     same_shard = bool(np.array_equal(pf3.engine.shard_export(), pf.engine.shard_export()))
+    shard_sha = hashlib.sha1(pf.engine.shard_export().tobytes()).hexdigest()
     del pf, pf3
+    # the same step through the contiguous route (windows off), and with every window
+    # overflowing (each rank falls back to the contiguous route after the count exchange)
+    got45 = []
+    for kw, cap in (({"windows": False}, None), ({}, 3)):
+        pf4 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc), **kw)
+        if cap is not None:
+            pf4._cap = lambda n, c=cap: c
+        got45.append(pf4.insert_include(mine, probe))
+        same_shard = same_shard and hashlib.sha1(pf4.engine.shard_export().tobytes()).hexdigest() == shard_sha
+        if cap is not None:
+            same_shard = same_shard and pf4.window_overflows == 2
+        del pf4
     ok = True
     if rank == 0 or True:
         all_keys = [("r%d-%d" % (r, int(v))) for r in range(P)
@@ -65,7 +79,7 @@ def main():
         pb, po = O.pack_keys(probe)
         want = orc.include_many(bits, m, k, pb, po).astype(bool)
         ok = (s == want_s) and same_shard and bool((got == want).all()) and bool((got2 == want).all()) \
-            and bool((got3 == want).all())
+            and bool((got3 == want).all()) and all(bool((g == want).all()) for g in got45)
         if not ok:
             print("rank %d MISMATCH: string %s (%d vs %d bytes), include %d diffs" %
                   (rank, s == want_s, len(s), len(want_s), int((got != want).sum())), flush=True)

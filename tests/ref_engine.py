@@ -33,6 +33,28 @@ class NumpyEngine:
         return (torch.from_numpy(local[order].view(np.int64).copy()), torch.from_numpy(slot) if want_slot else None,
                 torch.from_numpy(counts))
 
+    def route_windows(self, kb, ko, n, cap, want_slot=True):
+        """route() in the window layout; each window's entries shuffled, since the HIP
+        route leaves their order unspecified (the exchange must not depend on it)."""
+        send, slot, counts = self.route(kb, ko, n, want_slot=True)
+        c = counts.numpy()
+        wsend = np.zeros(self.P * cap, np.int64)
+        wslot = np.full(self.P * cap, -1, np.int32)
+        rng = np.random.default_rng(int(c.sum()) + 7)
+        at = 0
+        for s in range(self.P):
+            live = min(int(c[s]), cap)
+            perm = at + rng.permutation(int(c[s]))[:live]
+            wsend[s * cap: s * cap + live] = send.numpy()[perm]
+            wslot[s * cap: s * cap + live] = slot.numpy()[perm]
+            at += int(c[s])
+        return torch.from_numpy(wsend), torch.from_numpy(wslot) if want_slot else None, counts
+
+    def combine_windows(self, bits, slot, counts, cap, n):
+        c = counts.numpy()
+        live = np.concatenate([np.arange(s * cap, s * cap + min(int(c[s]), cap)) for s in range(self.P)])
+        return self.combine(bits[torch.from_numpy(live)], slot[torch.from_numpy(live)], n)
+
     def shard_insert(self, local):
         lo = local.numpy().view(np.uint64)
         assert (lo < np.uint64(self.local_bits)).all(), "owner-local offset outside the shard"

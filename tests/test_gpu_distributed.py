@@ -96,6 +96,59 @@ def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
         e.close()
 
 
+@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20),
+                                     (9585058377, 6, 2, 20)])
+def test_route_windows(pkg, oracle, m, k, P, b):
+    """bf_route_windows_dev: window s holds exactly owner s's (key, local offset) pairs
+    (the multiset bf_route_dev puts in segment s); bf_combine_windows_dev over the window
+    layout equals the AND; a window smaller than its owner's probes shows in the counts.
+    (9585058377, 6, 2): shards past 2^32 bits, so 64-bit routed offsets."""
+    import torch
+    D = pkg.distributed
+    dev = torch.device("cuda", 0)
+    e = D.HipEngine(m, k, P, 0, b, dev)
+    rng = np.random.default_rng(17)
+    keys = ["w%d" % int(v) for v in rng.integers(0, 10**12, 30000)]
+    kb, ko, n, buf, offs = dev_batch(pkg, torch, keys)
+    idx = oracle.indexes_many(buf, offs, m, k).reshape(-1)
+    owner, local = D.block_owner_local(idx, P, b)
+    want_c = np.bincount(owner, minlength=P)
+    key_of = np.arange(n * k) // k
+    cap = int(want_c.max()) + 37
+    send, slot, counts = e.route_windows(kb, ko, n, cap)
+    torch.cuda.synchronize()
+    assert counts.cpu().numpy().tolist() == want_c.tolist()
+    s_np = send.cpu().numpy()
+    s_np = s_np.view(np.uint32).astype(np.uint64) if s_np.dtype == np.int32 else s_np.view(np.uint64)
+    sl = slot.cpu().numpy().astype(np.int64)
+    for s in range(P):
+        w = slice(s * cap, s * cap + int(want_c[s]))
+        got = sorted(zip(sl[w].tolist(), s_np[w].tolist()))
+        assert got == sorted(zip(key_of[owner == s].tolist(), local[owner == s].tolist()))
+    # combine over windows: answer bytes from a known bitset, dead window tails poisoned with 0
+    bits = oracle.new_bitset(m, k)
+    ib, io = pkg.keys.pack(keys[: n // 2])
+    oracle.insert_many(bits, m, k, ib, io)
+    ans = np.zeros(P * cap, np.uint8)
+    for s in range(P):
+        lo = s_np[s * cap: s * cap + int(want_c[s])]
+        blk, low = lo >> np.uint64(b), lo & np.uint64((1 << b) - 1)
+        glob = ((blk * np.uint64(P) + np.uint64(s)) << np.uint64(b)) | low
+        ans[s * cap: s * cap + int(want_c[s])] = \
+            (bits.view(np.uint8)[(glob >> np.uint64(3)).astype(np.int64)] >> (7 - (glob & np.uint64(7))).astype(np.uint8)) & 1
+    got = e.combine_windows(torch.from_numpy(ans).to(dev), slot, counts, cap, n).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.include_many(bits, m, k, buf, offs))
+    assert got[: n // 2].all()
+    # too-small windows: the counts still report every owner's full total
+    small = int(want_c.min()) // 2
+    _, _, c2 = e.route_windows(kb, ko, n, small, want_slot=False)
+    assert c2.cpu().numpy().tolist() == want_c.tolist()
+    # an empty batch zeroes the counts
+    _, _, c3 = e.route_windows(kb, ko, 0, 16)
+    assert c3.cpu().numpy().tolist() == [0] * P
+    e.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -127,11 +180,16 @@ def test_torch_distributed_world1(pkg, oracle):
             np.testing.assert_array_equal(f.include_many(probe), want)
             assert f.export_redis() == oracle.redis_string(bits)
             f.close()
-        # the overlapped insert + include? step (async RCCL all-to-alls beside the kernels)
-        f = D.PartitionedFilter(m, k, block_log2=16)
-        np.testing.assert_array_equal(f.insert_include(keys, probe), want)
-        assert f.export_redis() == oracle.redis_string(bits)
-        f.close()
+        # the overlapped insert + include? step (async RCCL sends beside the kernels), through
+        # the window route, the contiguous route, and the overflow fallback
+        for kw, cap in (({}, None), ({"windows": False}, None), ({}, 5)):
+            f = D.PartitionedFilter(m, k, block_log2=16, **kw)
+            if cap is not None:
+                f._cap = lambda n, c=cap: c
+            np.testing.assert_array_equal(f.insert_include(keys, probe), want)
+            assert f.export_redis() == oracle.redis_string(bits)
+            assert f.window_overflows == (2 if cap is not None else 0)
+            f.close()
     finally:
         dist.destroy_process_group()
 
