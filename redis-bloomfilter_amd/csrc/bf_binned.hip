@@ -236,7 +236,7 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_sorted[kTileProbes];
-    __shared__ uint32_t s_key[KEYS ? kTileProbes : 1];
+    __shared__ uint16_t s_key[KEYS ? kTileProbes : 1];   // tile-relative input positions (< 2^14)
     const uint32_t t = threadIdx.x;
     if (t < kMaxSup) {
         s_cnt[t] = 0;
@@ -278,12 +278,12 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
             if (tag[q] != 0xFFFFFFFFu) {
                 const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
                 s_sorted[d] = loc[q];
-                if constexpr (KEYS) s_key[d] = (uint32_t)(p0 + (uint32_t)q * kTile + t);
+                if constexpr (KEYS) s_key[d] = (uint16_t)((uint32_t)q * kTile + t);
             }
         __syncthreads();
         for (uint32_t j = t; j < tp; j += kTile) {
             level1[p0 + j] = s_sorted[j];
-            if constexpr (KEYS) level1_key[p0 + j] = s_key[j];
+            if constexpr (KEYS) level1_key[p0 + j] = (uint32_t)p0 + s_key[j];
         }
     }
     if (t < nsup) gcnt[(uint64_t)blockIdx.x * nsup + t] = s_gcnt[t];
@@ -297,9 +297,10 @@ void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uin
     bin_front_offsets_body<Off, false>(local, count, tiles_per_block, sup_log2, nsup, level1, nullptr, stab, gcnt);
 }
 
-// 100 KiB of LDS: one workgroup per CU
+// 76 KiB of LDS (u16 positions): two workgroups per CU at 8 waves per SIMD, as the plain pass
 template <typename Off>
-__global__ __launch_bounds__(kTile) void bin_front_offsets_keys_kernel(const Off* __restrict__ local, uint64_t count,
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void bin_front_offsets_keys_kernel(const Off* __restrict__ local, uint64_t count,
                                                                        uint32_t tiles_per_block, uint32_t sup_log2,
                                                                        uint32_t nsup, uint32_t* __restrict__ level1,
                                                                        uint32_t* __restrict__ level1_key,
@@ -657,7 +658,7 @@ __global__ __launch_bounds__(kTile) void route_gather_kernel(const uint32_t* __r
 // share of them.  The run table is built once; each block's loads are issued
 // while the previous block is sorted and written.
 template <bool KEYS>
-__global__ __launch_bounds__(kTile) void bin_mid_kernel(const uint32_t* __restrict__ level1,
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void bin_mid_kernel(const uint32_t* __restrict__ level1,
                                                         const uint32_t* __restrict__ level1_key,
                                                         const uint16_t* __restrict__ stab, uint64_t ntiles,
                                                         uint32_t tile_probes, uint32_t tiles_per_group,
