@@ -886,6 +886,11 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     }
 }
 
+// BF_TEST_NT: the probe streams and the region are read non-temporally, so that the
+// scattered answer bytes keep their lines in the caches.
+#ifndef BF_TEST_NT
+#define BF_TEST_NT 1
+#endif
 // include?: the region in LDS; a probe on a 0 bit clears its key's answer.
 template <uint32_t RLOG2, uint32_t LANES>
 __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restrict__ bits, uint64_t nwords,
@@ -903,8 +908,18 @@ __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restr
     const uint32_t t = threadIdx.x;
     const uint64_t v0 = (uint64_t)blockIdx.x * kVec;
     const uint64_t nvec = nwords / 4;
+#if BF_TEST_NT
+    typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
+    const nt_u32x4* gn = reinterpret_cast<const nt_u32x4*>(bits);
+    for (uint32_t v = t; v < kVec; v += LANES) {
+        nt_u32x4 x = {0u, 0u, 0u, 0u};
+        if (v0 + v < nvec) x = __builtin_nontemporal_load(gn + v0 + v);
+        s_bits4[v] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+#else
     const uint4* gv = reinterpret_cast<const uint4*>(bits);
     for (uint32_t v = t; v < kVec; v += LANES) s_bits4[v] = v0 + v < nvec ? gv[v0 + v] : make_uint4(0, 0, 0, 0);
+#endif
     __syncthreads();
     for_region_probes<kLoads>(cb_base, cb_start, tabs, max_chunks, blockIdx.x, nq, rel_log2, s_pre, s_gst, s_w,
         [&](const uint32_t* idx) {
@@ -914,8 +929,13 @@ __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restr
                 l[c] = 0xFFFFFFFFu;
                 key[c] = 0;
                 if (idx[c] != 0xFFFFFFFFu) {
+#if BF_TEST_NT
+                    l[c] = __builtin_nontemporal_load(level2 + idx[c]);
+                    key[c] = __builtin_nontemporal_load(level2_key + idx[c]);
+#else
                     l[c] = level2[idx[c]];
                     key[c] = level2_key[idx[c]];
+#endif
                 }
             }
 #pragma unroll
