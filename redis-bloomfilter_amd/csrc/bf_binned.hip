@@ -454,6 +454,12 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ unsigned long long s_gbase[WIN ? kMaxSup : 1];
+    __shared__ uint32_t s_obase[WIN ? kMaxSup : 1];
+    // WIN: ~128 sort buckets however few the owners, so that the LDS rank atomics do not
+    // all land on P words (the owner's buckets stay consecutive: one run per owner)
+    uint32_t sub_log2 = 0;
+    if constexpr (WIN)
+        while ((P << (sub_log2 + 1)) <= 128u) ++sub_log2;
     __shared__ uint32_t s_lo[kTile * SLOTS];
     __shared__ uint8_t s_hi[WIDE ? kTile * SLOTS : 1];
     const uint32_t t = threadIdx.x;
@@ -505,7 +511,12 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 lo[q] = (uint32_t)local;
                 hi[q] = (uint8_t)(local >> 32);
             }
-            if (P <= g.route_agg) {   // workgroup-uniform
+            if constexpr (WIN) {   // bucket = (owner, low offset bits): 2^sub_log2 LDS counters per owner
+                if (live) {
+                    const uint32_t bkt = (owner << sub_log2) | (lo[q] & ((1u << sub_log2) - 1u));
+                    tag[q] = (bkt << 16) | atomicAdd(s_cnt + bkt, 1u);
+                }
+            } else if (P <= g.route_agg) {   // workgroup-uniform
                 const uint32_t r = wave_agg_rank(live, owner, s_cnt);
                 if (live) tag[q] = (owner << 16) | r;
             } else if (live) {
@@ -515,21 +526,24 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         __syncthreads();
         const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
         const uint32_t ex = block_excl_scan(c, s_w, nullptr);
-        if constexpr (WIN) {
-            if (t < P) {   // claim this tile's run in owner t's window (~0 when it would overflow)
-                unsigned long long gb = 0;
-                if (c) gb = atomicAdd(wcounts + t, (unsigned long long)c);
-                s_gbase[t] = (gb + c <= wcap) ? (unsigned long long)t * wcap + gb : ~0ull;
-            }
-        } else {
+        if constexpr (!WIN)
             if (t <= P) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [owner][tile]
-        }
         if (t < kMaxSup) {
             s_lbase[t] = ex;
             s_gcnt[t] += c;
             s_cnt[t] = 0;
         }
         __syncthreads();
+        if constexpr (WIN) {
+            if (t < P) {   // claim this tile's owner-t run (its buckets, consecutive) in owner t's window
+                const uint32_t hi_b = (t + 1) << sub_log2;   // == kMaxSup only for the last of 256 owners
+                const uint32_t ob = s_lbase[t << sub_log2], oc = (hi_b < kMaxSup ? s_lbase[hi_b] : tk * k) - ob;
+                unsigned long long gb = 0;
+                if (oc) gb = atomicAdd(wcounts + t, (unsigned long long)oc);
+                s_gbase[t] = (gb + oc <= wcap) ? (unsigned long long)t * wcap + gb : ~0ull;   // ~0: overflow
+                s_obase[t] = ob;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < SLOTS; ++q) {
             if (tag[q] != 0xFFFFFFFFu) {
@@ -547,10 +561,10 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         const uint32_t tp = tk * k;
         if constexpr (WIN) {
             for (uint32_t j = t; j < tp; j += kTile) {
-                const uint32_t o = run_of(s_lbase, P, j);
+                const uint32_t o = run_of(s_obase, P, j);
                 const unsigned long long gb = s_gbase[o];   // the run's place in owner o's window
                 if (gb != ~0ull) {
-                    const uint64_t d = gb + (j - s_lbase[o]);
+                    const uint64_t d = gb + (j - s_obase[o]);
                     if constexpr (WIDE)
                         static_cast<uint64_t*>(wsend)[d] = ((uint64_t)s_hi[j] << 32) | s_lo[j];
                     else
