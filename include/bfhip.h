@@ -242,6 +242,13 @@ int  bf_lua_import_layer(bf_lua* h, uint32_t layer, const uint8_t* buf, uint64_t
 int  bf_lua_layer_params(double entries, double precision, uint32_t layer, uint64_t* bits, uint32_t* k);
 int  bf_lua_index(double entries, uint64_t count, uint32_t* layer);
 
+/* ---- one key's k offsets without a filter (Ruby#indexes_for, ruby.rb:41-55): computed
+ *      by the same device kernel as bf_indexes_many, on the calling thread's current
+ *      HIP device; out holds k uint64.  m = 0 or k = 0: BF_EINVAL (the reference raises
+ *      ZeroDivisionError at ruby.rb:51).  Not a hot path: it allocates per call.
+ *      Errors read back through bf_last_error(NULL). */
+int  bf_indexes(const uint8_t* key, uint64_t len, uint64_t m_bits, uint32_t k, uint64_t* out);
+
 /* ---- sizing helpers with the facade's exact semantics (bloomfilter.rb:50-58) */
 int64_t bf_optimal_m(double n, double error_rate);
 int64_t bf_optimal_k(int64_t n, int64_t m_bits);     /* Integer n: floor division, 0 -> 1 */

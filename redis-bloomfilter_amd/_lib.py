@@ -69,6 +69,7 @@ SIGNATURES = {
     "bf_insert_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u8p, _vp]),
     "bf_include_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
     "bf_indexes_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "bf_indexes": (ctypes.c_int, [_vp, _u64, _u64, _u32, _vp]),
     "bf_clear": (ctypes.c_int, [_vp]),
     "bf_export_redis": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_import_redis": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
@@ -171,6 +172,15 @@ def optimal_m(n, error_rate) -> int:
 
 def optimal_k(n: int, m: int) -> int:
     return int(load().bf_optimal_k(int(n), int(m)))
+
+
+def indexes(key: bytes, m: int, k: int) -> List[int]:
+    """One key's k offsets (Ruby#indexes_for, ruby.rb:41-55) through bf_indexes: the device
+    kernel on the current GPU, no filter needed."""
+    buf = np.frombuffer(bytes(key), np.uint8) if len(key) else np.zeros(1, np.uint8)
+    out = np.zeros(max(int(k), 1), np.uint64)
+    _check(load().bf_indexes(_ptr(buf), len(key), int(m), int(k), _ptr(out)))
+    return [int(x) for x in out[: int(k)]]
 
 
 def _ptr(a: Optional[np.ndarray]):

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <vector>
 
 #define BFHIP_VERSION_STR "bfhip 0.1.0 (gfx950; redis-bloomfilter 1.1.2 ruby-driver layout)"
 
@@ -440,6 +441,37 @@ const char* bf_version(void) { return BFHIP_VERSION_STR; }
 
 const char* bf_last_error(const bf_handle* h) {
     return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int bf_indexes(const uint8_t* key, uint64_t len, uint64_t m_bits, uint32_t k, uint64_t* out) {
+    if (m_bits == 0 || k == 0) return set_err(nullptr, BF_EINVAL, "m and k must be positive (ruby.rb:51 divides by m)");
+    if (k > BF_MAX_K) return set_err(nullptr, BF_EINVAL, "k must be in [1, %u], got %u", BF_MAX_K, k);
+    if (!out || (len && !key)) return set_err(nullptr, BF_EINVAL, "NULL pointer");
+    BfGeom g{};
+    g.m = m_bits;
+    g.inv_m = 1.0 / (double)m_bits;
+    g.k = k;
+    g.nomod = (m_bits > (uint64_t)k * 0xFFFFFFFFull) ? 1u : 0u;
+    g.mod_f32 = (m_bits >= (1ull << 17)) ? 1u : 0u;
+    g.inv_m_f = (float)(1.0 / (double)m_bits);
+    g.shards = 1;
+    g.inv_shards = 1.0;
+    const uint64_t kb = round_up(len + 16, 16);
+    uint8_t* d = nullptr;   // key bytes (16-B slack), offsets[2], k offsets
+    if (hipMalloc(&d, kb + 16 + 8ull * k) != hipSuccess) return set_err(nullptr, BF_ENOMEM, "hipMalloc failed");
+    std::vector<uint8_t> host(kb + 16, 0);
+    if (len) memcpy(host.data(), key, len);
+    const uint64_t offs[2] = {0, len};
+    memcpy(host.data() + kb, offs, 16);
+    uint64_t* d_out = reinterpret_cast<uint64_t*>(d + kb + 16);
+    hipError_t e = hipMemcpy(d, host.data(), kb + 16, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = bf_launch_keys(BF_OP_INDEXES, g, d, reinterpret_cast<const uint64_t*>(d + kb), 0, 1, nullptr, d_out, nullptr,
+                           nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, 8ull * k, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(nullptr, BF_EDEVICE, "bf_indexes: %s", hipGetErrorString(e));
+    return BF_OK;
 }
 
 int64_t bf_optimal_m(double n, double p) {

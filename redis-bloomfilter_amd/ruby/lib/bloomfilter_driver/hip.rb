@@ -73,6 +73,7 @@ class Redis
       attach_function :bf_track_dirty, %i[pointer uint32], :int, blocking: true
       attach_function :bf_dirty_ranges, %i[pointer pointer uint32 pointer pointer uint32], :int, blocking: true
       attach_function :bf_export_range, %i[pointer uint64 uint64 pointer], :int, blocking: true
+      attach_function :bf_indexes, %i[pointer uint64 uint64 uint32 pointer], :int, blocking: true
     end
 
     class Hip
@@ -210,6 +211,16 @@ class Redis
       end
 
       protected
+
+      # Ruby#indexes_for (ruby.rb:41-55): the k offsets of one key, from the device kernel.
+      def indexes_for(data)
+        s = data.to_s.b
+        key = FFI::MemoryPointer.new(:uint8, [s.bytesize, 1].max)
+        key.put_bytes(0, s)
+        out = FFI::MemoryPointer.new(:uint64, @options[:hashes])
+        check(HipFFI.bf_indexes(key, s.bytesize, @options[:bits], @options[:hashes], out), nil)
+        out.read_array_of_uint64(@options[:hashes])
+      end
 
       # bf_config.flags of the device filter (HipTest picks a hash engine here).
       def config_flags

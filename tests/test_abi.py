@@ -91,6 +91,13 @@ def test_invalid_arguments_without_gpu(pkg):
         pkg.Filter(100, 0)
     with pytest.raises(pkg.ArgumentError, match="k must be"):
         pkg.Filter(100, 65)
+    # bf_indexes (one key, no filter): m = 0 is the reference's ZeroDivisionError (ruby.rb:51)
+    with pytest.raises(pkg.ArgumentError, match="m and k must be positive"):
+        pkg._lib.indexes(b"asdlol", 0, 6)
+    with pytest.raises(pkg.ArgumentError, match="m and k must be positive"):
+        pkg._lib.indexes(b"asdlol", 9585, 0)
+    with pytest.raises(pkg.ArgumentError, match="k must be in"):
+        pkg._lib.indexes(b"asdlol", 9585, 65)
 
 
 def test_null_handle_is_einval(pkg):

@@ -70,6 +70,16 @@ def test_indexes_match_oracle(pkg, oracle, m, k):
             np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("m,k", [(9585, 6), (2**32 + 17, 10), (191701167547, 13), (2**40 + 3, 64)])
+def test_single_key_indexes_no_filter(pkg, oracle, m, k):
+    """bf_indexes (handle-free, one key): the same device kernel, no bitset allocated —
+    so the 10B / 2^40-bit regimes cost nothing here."""
+    for key in ["asdlol", "", "a" * 55, "b" * 56, "d" * 119, "héllo wörld ✓", "42"]:
+        b, o = pkg.keys.pack([key])
+        want = oracle.indexes_many(b, o, m, k).reshape(-1).tolist()
+        assert pkg._lib.indexes(bytes(b), m, k) == want
+
+
 def test_known_answers(pkg):
     """SURVEY §7 known answers (Python hashlib + Node crypto restatements)."""
     cases = {("asdlol", 9585, 6): [5260, 6438, 144, 8807, 5008, 5791],
