@@ -184,21 +184,32 @@ int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_of
                   void* d_send /* uint64[n*k], or uint32 with BF_FLAG_ROUTE32 */,
                   uint32_t* d_slot /* nullable, n*k */,
                   uint64_t* d_counts, void* stream);
-/* bf_route_windows_dev   bf_route_dev without its owner-major gather pass: owner s's probes
- *                        land in a fixed window, d_send[s*window_cap .. s*window_cap +
- *                        d_counts[s]), in an unspecified order, with d_slot (nullable)
- *                        alongside; each per-owner window feeds one send of a grouped
- *                        send/recv exchange.  If some d_counts[s] > window_cap (a skewed
- *                        batch), that window's contents are undefined: check the counts and
- *                        fall back to bf_route_dev.  Same limits as bf_route_dev's fused path.
+/* bf_route_window_split  nh = the 2^32-bit sub-ranges of the largest shard (1 when every
+ *                        shard fits 2^32 bits): the window route keeps nwin = shard_count*nh
+ *                        windows, window w = s*nh + hi holding owner s's probes whose local
+ *                        offset is (hi << 32) | entry.
+ * bf_route_windows_dev   bf_route_dev without its owner-major gather pass: window w's
+ *                        probes land in d_send[w*window_cap .. w*window_cap + d_counts[w])
+ *                        as uint32, in an unspecified order, with d_slot (nullable)
+ *                        alongside; each window feeds one send of a grouped send/recv
+ *                        exchange.  d_counts holds nwin uint64.  If some d_counts[w] >
+ *                        window_cap (a skewed batch), that window's contents are undefined:
+ *                        route again with window_cap = n*k, which always fits.
+ * bf_shard_insert_hi_dev / bf_shard_test_hi_dev   the owner ops on the uint32 entries of
+ *                        sub-range hi (local offset = (hi << 32) | entry).
  * bf_combine_windows_dev bf_combine_dev over that layout: d_bits and d_slot indexed by window
- *                        entry, the live entries of window s being the first d_counts[s]. */
+ *                        entry, the live entries of window w being the first d_counts[w]. */
+int  bf_route_window_split(const bf_handle* h, uint32_t* nh);
 int  bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
-                          void* d_send /* shard_count*window_cap entries */, uint32_t* d_slot /* nullable */,
-                          uint64_t window_cap, uint64_t* d_counts, void* stream);
+                          uint32_t* d_send /* nwin*window_cap entries */, uint32_t* d_slot /* nullable */,
+                          uint64_t window_cap, uint64_t* d_counts /* nwin */, void* stream);
+int  bf_shard_insert_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count, uint32_t hi,
+                            uint32_t* d_any_new /* nullable */, void* stream);
+int  bf_shard_test_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count, uint32_t hi, uint8_t* d_bits,
+                          void* stream);
 int  bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t window_cap,
-                            const uint64_t* d_counts /* device, shard_count */, uint64_t n, uint8_t* d_out,
-                            void* stream);
+                            uint32_t nwin, const uint64_t* d_counts /* device, nwin */, uint64_t n,
+                            uint8_t* d_out, void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
 int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,

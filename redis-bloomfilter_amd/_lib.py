@@ -90,8 +90,11 @@ SIGNATURES = {
     "bf_shard_insert_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
     "bf_shard_test_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
     "bf_combine_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_route_window_split": (ctypes.c_int, [_vp, _u32p]),
     "bf_route_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp]),
-    "bf_combine_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "bf_shard_insert_hi_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
+    "bf_shard_test_hi_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
+    "bf_combine_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp]),
     "bf_shard_export": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_shard_import": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
     "bf_lua_create": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, ctypes.POINTER(bf_config),
@@ -405,10 +408,23 @@ class Filter:
         _check(self._lib.bf_route_windows_dev(self.handle, d_keys, d_offsets, int(n), d_send, d_slot or None,
                                               int(window_cap), d_counts, self._s(stream)), self._h)
 
-    def combine_windows_dev(self, d_bits: int, d_slot: int, window_cap: int, d_counts: int, n: int, d_out: int,
-                            stream=None) -> None:
-        _check(self._lib.bf_combine_windows_dev(self.handle, d_bits, d_slot, int(window_cap), d_counts, int(n),
-                                                d_out, self._s(stream)), self._h)
+    def route_window_split(self) -> int:
+        nh = ctypes.c_uint32()
+        _check(self._lib.bf_route_window_split(self.handle, ctypes.byref(nh)), self._h)
+        return int(nh.value)
+
+    def shard_insert_hi_dev(self, d_local32: int, count: int, hi: int, d_any_new: int = 0, stream=None) -> None:
+        _check(self._lib.bf_shard_insert_hi_dev(self.handle, d_local32, int(count), int(hi), d_any_new or None,
+                                                self._s(stream)), self._h)
+
+    def shard_test_hi_dev(self, d_local32: int, count: int, hi: int, d_bits: int, stream=None) -> None:
+        _check(self._lib.bf_shard_test_hi_dev(self.handle, d_local32, int(count), int(hi), d_bits, self._s(stream)),
+               self._h)
+
+    def combine_windows_dev(self, d_bits: int, d_slot: int, window_cap: int, nwin: int, d_counts: int, n: int,
+                            d_out: int, stream=None) -> None:
+        _check(self._lib.bf_combine_windows_dev(self.handle, d_bits, d_slot, int(window_cap), int(nwin), d_counts,
+                                                int(n), d_out, self._s(stream)), self._h)
 
     def shard_insert_dev(self, d_local: int, count: int, d_any_new: int = 0, stream=None) -> None:
         _check(self._lib.bf_shard_insert_dev(self.handle, d_local, int(count), d_any_new or None,

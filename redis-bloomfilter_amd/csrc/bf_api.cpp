@@ -861,33 +861,50 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     return BF_OK;
 }
 
+int bf_route_window_split(const bf_handle* h, uint32_t* nh) {
+    if (!h || !nh) return BF_EINVAL;
+    // the largest shard (index 0) holds ceil(nblocks / P) blocks
+    const uint64_t nblocks = (h->reach + (1ull << h->block_log2) - 1) >> h->block_log2;
+    const uint64_t bits0 = h->shards == 1 ? h->reach : ((nblocks + h->shards - 1) / h->shards) << h->block_log2;
+    *nh = (uint32_t)((bits0 + 0xFFFFFFFFull) >> 32);
+    if (*nh == 0) *nh = 1;
+    return BF_OK;
+}
+
 int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
-                         void* d_send, uint32_t* d_slot, uint64_t window_cap, uint64_t* d_counts, void* stream) {
+                         uint32_t* d_send, uint32_t* d_slot, uint64_t window_cap, uint64_t* d_counts, void* stream) {
     if (!h) return BF_EINVAL;
     if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
     if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
     const uint64_t probes = n * h->k;
     if (n && probes / n != h->k) return set_err(h, BF_EINVAL, "n*k overflows");
     if (probes >= (1ull << 32)) return set_err(h, BF_EINVAL, "n*k must be < 2^32 per call (slot indices are 32-bit)");
-    if (window_cap && (uint64_t)h->shards > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window_cap overflows");
+    uint32_t nh = 1;
+    bf_route_window_split(h, &nh);
+    const uint32_t nwin = h->shards * nh;
+    if (nwin > 256) return set_err(h, BF_EINVAL, "%u shards x %u sub-ranges exceed 256 windows", h->shards, nh);
+    if (window_cap && (uint64_t)nwin > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window_cap overflows");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     hipStream_t s = pick_stream(h, stream);
     BfBinPlan plan;
-    if (n && !bf_route_plan(n, h->k, h->shards, !h->route32, d_slot != nullptr, &plan))
-        return set_err(h, BF_EINVAL, "batch of %llu keys at k=%u over %u shards exceeds one window-route pass",
-                       (unsigned long long)n, h->k, h->shards);
-    if (!n) plan.nsup = h->shards;
+    if (n && !bf_route_plan(n, h->k, nwin, false, d_slot != nullptr, &plan))
+        return set_err(h, BF_EINVAL, "batch of %llu keys at k=%u over %u windows exceeds one window-route pass",
+                       (unsigned long long)n, h->k, nwin);
+    if (!n) plan.nsup = nwin;
     uint64_t bias = 0;
     const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_route_windows(h->g, plan, !h->route32, k16, d_offsets, bias, n, d_send, d_slot, window_cap,
+    HIPCHK(h, bf_launch_route_windows(h->g, plan, nh, k16, d_offsets, bias, n, d_send, d_slot, window_cap,
                                       reinterpret_cast<unsigned long long*>(d_counts), s, mk));
     return BF_OK;
 }
 
-int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
+namespace {
+// Owner-side OR of `count` routed local offsets: uint32 entries when u32 (+ bias), else uint64.
+int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint32_t* d_any_new,
+                      void* stream) {
     if (!h) return BF_EINVAL;
     if (count && !d_local) return set_err(h, BF_EINVAL, "d_local is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -903,7 +920,7 @@ int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint3
                         (h->binned_mode == 1 || (h->dev_bytes >= (64ull << 20) &&
                                                  (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
     if (binned) {
-        const size_t esz = h->route32 ? 4 : 8;
+        const size_t esz = u32 ? 4 : 8;
         for (uint64_t c0 = 0; c0 < count; c0 += sub) {
             const uint64_t cn = std::min(sub, count - c0);
             if (cn != std::min(count, sub) && !bf_binned_plan_offsets(h->dev_bytes, cn, h->bin_region_log2, &plan))
@@ -912,18 +929,33 @@ int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint3
             if (rc) return rc;
             BfMarks* mk = prof_begin(h, s);
             HIPCHK(h, bf_launch_shard_insert_binned(h->g, plan, h->dev_bytes,
-                                                    static_cast<const uint8_t*>(d_local) + c0 * esz, h->route32, cn,
-                                                    h->d_bin_scratch, d_any_new, s, mk));
+                                                    static_cast<const uint8_t*>(d_local) + c0 * esz, u32, cn,
+                                                    h->d_bin_scratch, d_any_new, s, mk, bias));
         }
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, h->route32, s));
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, u32, s, bias));
     bf_mark(mk, s, "shard_insert");
     return BF_OK;
 }
+}  // namespace
 
-int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
+int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
+    if (!h) return BF_EINVAL;
+    return shard_insert_impl(h, d_local, h->route32, 0, count, d_any_new, stream);
+}
+
+int bf_shard_insert_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count, uint32_t hi, uint32_t* d_any_new,
+                           void* stream) {
+    if (!h) return BF_EINVAL;
+    if (((uint64_t)hi << 32) >= h->local_bits) return set_err(h, BF_EINVAL, "hi=%u is past the shard", hi);
+    return shard_insert_impl(h, d_local32, true, (uint64_t)hi << 32, count, d_any_new, stream);
+}
+
+namespace {
+int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint8_t* d_bits,
+                    void* stream) {
     if (!h) return BF_EINVAL;
     if (count && (!d_local || !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -941,7 +973,7 @@ int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t
                         (mode == 1 || (h->dev_bytes >= (64ull << 20) &&
                                        (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
     if (binned) {
-        const size_t esz = h->route32 ? 4 : 8;
+        const size_t esz = u32 ? 4 : 8;
         for (uint64_t c0 = 0; c0 < count; c0 += sub) {
             const uint64_t cn = std::min(sub, count - c0);
             if (cn != std::min(count, sub) &&
@@ -951,15 +983,28 @@ int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t
             if (rc) return rc;
             BfMarks* mk = prof_begin(h, s);
             HIPCHK(h, bf_launch_shard_test_binned(h->g, plan, h->dev_bytes,
-                                                  static_cast<const uint8_t*>(d_local) + c0 * esz, h->route32, cn,
-                                                  h->d_bin_scratch, d_bits + c0, s, mk));
+                                                  static_cast<const uint8_t*>(d_local) + c0 * esz, u32, cn,
+                                                  h->d_bin_scratch, d_bits + c0, s, mk, bias));
         }
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, h->route32, s));
+    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, u32, s, bias));
     bf_mark(mk, s, "shard_test");
     return BF_OK;
+}
+}  // namespace
+
+int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
+    if (!h) return BF_EINVAL;
+    return shard_test_impl(h, d_local, h->route32, 0, count, d_bits, stream);
+}
+
+int bf_shard_test_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count, uint32_t hi, uint8_t* d_bits,
+                         void* stream) {
+    if (!h) return BF_EINVAL;
+    if (((uint64_t)hi << 32) >= h->local_bits) return set_err(h, BF_EINVAL, "hi=%u is past the shard", hi);
+    return shard_test_impl(h, d_local32, true, (uint64_t)hi << 32, count, d_bits, stream);
 }
 
 int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t n, uint8_t* d_out,
@@ -977,7 +1022,7 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
 }
 
 int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t window_cap,
-                           const uint64_t* d_counts, uint64_t n, uint8_t* d_out, void* stream) {
+                           uint32_t nwin, const uint64_t* d_counts, uint64_t n, uint8_t* d_out, void* stream) {
     if (!h) return BF_EINVAL;
     if (n && (!d_bits || !d_slot || !d_counts || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -986,7 +1031,7 @@ int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* 
     hipStream_t s = pick_stream(h, stream);
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows(d_bits, d_slot, window_cap, reinterpret_cast<const unsigned long long*>(d_counts),
-                                        h->shards, n, d_out, s));
+                                        nwin, n, d_out, s));
     bf_mark(mk, s, "combine");
     return BF_OK;
 }

@@ -232,7 +232,8 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
                                                        uint32_t tiles_per_block, uint32_t sup_log2, uint32_t nsup,
                                                        uint32_t* __restrict__ level1,
                                                        uint32_t* __restrict__ level1_key,
-                                                       uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt) {
+                                                       uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt,
+                                                       uint64_t bias) {
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_sorted[kTileProbes];
@@ -257,7 +258,7 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
             tag[q] = 0xFFFFFFFFu;
             loc[q] = 0;
             if (j < tp) {
-                const uint64_t o = (uint64_t)local[p0 + j];
+                const uint64_t o = (uint64_t)local[p0 + j] + bias;
                 const uint32_t sb = (uint32_t)(o >> sup_log2);
                 tag[q] = (sb << 16) | atomicAdd(s_cnt + sb, 1u);
                 loc[q] = (uint32_t)(o & smask);
@@ -293,8 +294,9 @@ template <typename Off>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uint32_t tiles_per_block,
                               uint32_t sup_log2, uint32_t nsup, uint32_t* __restrict__ level1,
-                              uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt) {
-    bin_front_offsets_body<Off, false>(local, count, tiles_per_block, sup_log2, nsup, level1, nullptr, stab, gcnt);
+                              uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint64_t bias) {
+    bin_front_offsets_body<Off, false>(local, count, tiles_per_block, sup_log2, nsup, level1, nullptr, stab, gcnt,
+                                       bias);
 }
 
 // 76 KiB of LDS (u16 positions): two workgroups per CU at 8 waves per SIMD, as the plain pass
@@ -305,8 +307,9 @@ void bin_front_offsets_keys_kernel(const Off* __restrict__ local, uint64_t count
                                                                        uint32_t nsup, uint32_t* __restrict__ level1,
                                                                        uint32_t* __restrict__ level1_key,
                                                                        uint16_t* __restrict__ stab,
-                                                                       uint32_t* __restrict__ gcnt) {
-    bin_front_offsets_body<Off, true>(local, count, tiles_per_block, sup_log2, nsup, level1, level1_key, stab, gcnt);
+                                                                       uint32_t* __restrict__ gcnt, uint64_t bias) {
+    bin_front_offsets_body<Off, true>(local, count, tiles_per_block, sup_log2, nsup, level1, level1_key, stab, gcnt,
+                                      bias);
 }
 
 // gsum[sb][q] = probes of superbin sb in the tiles of front workgroups [64q, 64q + 64).
@@ -439,7 +442,8 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                                                  uint16_t* __restrict__ stab,
                                                  uint32_t* __restrict__ gcnt, uint64_t wcap,
                                                  unsigned long long* __restrict__ wcounts,
-                                                 void* __restrict__ wsend, uint32_t* __restrict__ wslot) {
+                                                 void* __restrict__ wsend, uint32_t* __restrict__ wslot,
+                                                 uint32_t nh) {
     // The key stage (offsets + bytes) is dead once the tile is hashed, so the sorted
     // tile-relative key indices (u16) reuse it: 76 KiB in all without WIDE, two
     // workgroups per CU.
@@ -511,9 +515,10 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 lo[q] = (uint32_t)local;
                 hi[q] = (uint8_t)(local >> 32);
             }
-            if constexpr (WIN) {   // bucket = (owner, low offset bits): 2^sub_log2 LDS counters per owner
+            if constexpr (WIN) {   // bucket = (window, low offset bits): 2^sub_log2 LDS counters per window
                 if (live) {
-                    const uint32_t bkt = (owner << sub_log2) | (lo[q] & ((1u << sub_log2) - 1u));
+                    const uint32_t win = owner * nh + hi[q];   // window = (owner, 2^32-bit sub-range)
+                    const uint32_t bkt = (win << sub_log2) | (lo[q] & ((1u << sub_log2) - 1u));
                     tag[q] = (bkt << 16) | atomicAdd(s_cnt + bkt, 1u);
                 }
             } else if (P <= g.route_agg) {   // workgroup-uniform
@@ -565,10 +570,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 const unsigned long long gb = s_gbase[o];   // the run's place in owner o's window
                 if (gb != ~0ull) {
                     const uint64_t d = gb + (j - s_obase[o]);
-                    if constexpr (WIDE)
-                        static_cast<uint64_t*>(wsend)[d] = ((uint64_t)s_hi[j] << 32) | s_lo[j];
-                    else
-                        static_cast<uint32_t*>(wsend)[d] = s_lo[j];
+                    static_cast<uint32_t*>(wsend)[d] = s_lo[j];   // the window implies the high bits
                     if constexpr (SLOT) wslot[d] = (uint32_t)key0 + s_key[j];
                 }
             }
@@ -591,9 +593,9 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         uint32_t tile_keys, uint32_t tiles_per_block, uint32_t P, uint32_t* __restrict__ lo1,                   \
         uint8_t* __restrict__ hi1, uint32_t* __restrict__ key1, uint16_t* __restrict__ stab,                     \
         uint32_t* __restrict__ gcnt, uint64_t wcap, unsigned long long* __restrict__ wcounts,                 \
-        void* __restrict__ wsend, uint32_t* __restrict__ wslot
+        void* __restrict__ wsend, uint32_t* __restrict__ wslot, uint32_t nh
 #define BF_ROUTE_FRONT_PASS \
-    g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt, wcap, wcounts, wsend, wslot
+    g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt, wcap, wcounts, wsend, wslot, nh
 template <bool WIDE, bool SLOT, int SLOTS, bool WIN>
 __global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS) {
     route_front_body<WIDE, SLOT, SLOTS, WIN>(BF_ROUTE_FRONT_PASS);
@@ -1163,18 +1165,18 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
 
 hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                          const void* local, bool route32, uint64_t count, void* scratch,
-                                         uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
+                                         uint32_t* any_flag, hipStream_t s, BfMarks* mk, uint64_t bias) {
     if (count == 0) return hipSuccess;
     const Carve c = carve(p, scratch);
     const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
     if (route32)
         hipLaunchKernelGGL(bin_front_offsets_kernel<uint32_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint32_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.stab, c.gcnt);
+                           c.stab, c.gcnt, bias);
     else
         hipLaunchKernelGGL(bin_front_offsets_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.stab, c.gcnt);
+                           c.stab, c.gcnt, bias);
     bf_mark(mk, s, "bin_front_offsets");
     hipError_t e = launch_groups_mid(g, p, c, s, mk);
     if (e != hipSuccess) return e;
@@ -1209,7 +1211,7 @@ hipError_t launch_test(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint
 // offset's answer byte written (preset to 1, cleared on a 0 bit).
 hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const void* local, bool route32, uint64_t count, void* scratch, uint8_t* out8,
-                                       hipStream_t s, BfMarks* mk) {
+                                       hipStream_t s, BfMarks* mk, uint64_t bias) {
     if (count == 0) return hipSuccess;
     if (!p.with_keys || !out8) return hipErrorInvalidValue;
     const Carve c = carve(p, scratch);
@@ -1219,11 +1221,11 @@ hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint
     if (route32)
         hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint32_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint32_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.level1_key, c.stab, c.gcnt);
+                           c.level1_key, c.stab, c.gcnt, bias);
     else
         hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.level1_key, c.stab, c.gcnt);
+                           c.level1_key, c.stab, c.gcnt, bias);
     bf_mark(mk, s, "bin_front_offsets_keys");
     if ((e = launch_groups_mid(g, p, c, s, mk)) != hipSuccess) return e;
     return launch_test(g, p, c, bitset_bytes, out8, s, mk);
@@ -1309,7 +1311,7 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
 #define BF_ROUTE_FRONT(W, S, SL)                                                                                  \
     hipLaunchKernelGGL((route_front_kernel<W, S, SL, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, \
                        bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,       \
-                       (uint64_t)0, nullptr, nullptr, nullptr)
+                       (uint64_t)0, nullptr, nullptr, nullptr, 1u)
     if (g.k > (uint32_t)kSlots) {
         if (wide) { if (slot) BF_ROUTE_FRONT(true, true, kWideSlots); else BF_ROUTE_FRONT(true, false, kWideSlots); }
         else { if (slot) BF_ROUTE_FRONT(false, true, kWideSlots); else BF_ROUTE_FRONT(false, false, kWideSlots); }
@@ -1318,11 +1320,11 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     else if (slot)
         hipLaunchKernelGGL((route_front32_kernel<true, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
                            bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,
-                           (uint64_t)0, nullptr, nullptr, nullptr);
+                           (uint64_t)0, nullptr, nullptr, nullptr, 1u);
     else
         hipLaunchKernelGGL((route_front32_kernel<false, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
                            bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,
-                           (uint64_t)0, nullptr, nullptr, nullptr);
+                           (uint64_t)0, nullptr, nullptr, nullptr, 1u);
 #undef BF_ROUTE_FRONT
     bf_mark(mk, s, slot ? "route_front_slot" : "route_front");
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
@@ -1343,9 +1345,11 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     return hipGetLastError();
 }
 
-// Window route (bf_route_windows_dev): the front pass alone, each tile's owner runs written
-// straight into fixed per-owner windows of wcap entries (no level 1, group scan or gather).
-hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
+// Window route (bf_route_windows_dev): the front pass alone, each tile's runs written
+// straight into fixed windows of wcap uint32 entries, window = owner * nh + (local >> 32)
+// (nh = 1 when every shard fits 2^32 bits), with no level 1, group scan or gather.
+// p comes from bf_route_plan over shards * nh buckets.
+hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const uint8_t* keys16,
                                    const uint64_t* offsets, uint64_t bias, uint64_t n, void* send, uint32_t* slot,
                                    uint64_t wcap, unsigned long long* counts, hipStream_t s, BfMarks* mk) {
     hipError_t e;
@@ -1354,15 +1358,11 @@ hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, bool wid
 #define BF_ROUTE_WIN(KERNEL)                                                                                      \
     hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,      \
                        p.tiles_per_block, p.nsup, nullptr, nullptr, nullptr, nullptr, nullptr, wcap, counts, send, \
-                       slot)
+                       slot, nh)
     if (g.k > (uint32_t)kSlots) {
-        if (wide) { if (slot) BF_ROUTE_WIN((route_front_kernel<true, true, kWideSlots, true>));
-                    else BF_ROUTE_WIN((route_front_kernel<true, false, kWideSlots, true>)); }
-        else { if (slot) BF_ROUTE_WIN((route_front_kernel<false, true, kWideSlots, true>));
-               else BF_ROUTE_WIN((route_front_kernel<false, false, kWideSlots, true>)); }
+        if (slot) BF_ROUTE_WIN((route_front_kernel<false, true, kWideSlots, true>));
+        else BF_ROUTE_WIN((route_front_kernel<false, false, kWideSlots, true>));
     }
-    else if (wide) { if (slot) BF_ROUTE_WIN((route_front_kernel<true, true, kSlots, true>));
-                     else BF_ROUTE_WIN((route_front_kernel<true, false, kSlots, true>)); }
     else if (slot) BF_ROUTE_WIN((route_front32_kernel<true, true>));
     else BF_ROUTE_WIN((route_front32_kernel<false, true>));
 #undef BF_ROUTE_WIN

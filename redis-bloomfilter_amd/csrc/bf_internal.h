@@ -101,12 +101,13 @@ bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref
                             bool with_keys = false);
 hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                          const void* local, bool route32, uint64_t count, void* scratch,
-                                         uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
+                                         uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr,
+                                         uint64_t bias = 0);
 // Binned shard test (owner side of a partitioned include?): out8[i] = bit of local[i].
 // Plan with bf_binned_plan_offsets(..., with_keys = true).
 hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const void* local, bool route32, uint64_t count, void* scratch, uint8_t* out8,
-                                       hipStream_t s, BfMarks* mk);
+                                       hipStream_t s, BfMarks* mk, uint64_t bias = 0);
 // plan.with_keys must be set; out8 gets the n answers.
 hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                     const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
@@ -139,7 +140,7 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
 // Window route (bf_binned.hip): the fused route's front pass writing each tile's owner
 // runs straight into send[s*wcap ..] (and slot[s*wcap ..]) at places claimed with
 // atomics on counts[s]; a run past wcap is dropped (counts[s] > wcap tells the caller).
-hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, bool wide, const uint8_t* keys16,
+hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const uint8_t* keys16,
                                    const uint64_t* offsets, uint64_t bias, uint64_t n, void* send, uint32_t* slot,
                                    uint64_t wcap, unsigned long long* counts, hipStream_t s,
                                    BfMarks* marks = nullptr);
@@ -157,10 +158,11 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
                                    uint32_t P, uint32_t k, const unsigned long long* counts,
                                    unsigned long long* cursor, void* send, uint32_t* slot,
                                    bool route32, hipStream_t s);
+// bias: added to every local offset (the 2^32-bit sub-range of a split window route)
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count,
-                                  uint32_t* any_flag, bool route32, hipStream_t s);
+                                  uint32_t* any_flag, bool route32, hipStream_t s, uint64_t bias = 0);
 hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count,
-                                uint8_t* out, bool route32, hipStream_t s);
+                                uint8_t* out, bool route32, hipStream_t s, uint64_t bias = 0);
 // out[j] = AND of bits[p] over the n*k send entries p with slot[p] == j.
 hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k,
                              uint8_t* out, hipStream_t s);

@@ -259,7 +259,8 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const Off* __restric
 template <bool FLAGS, typename Off>
 __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
                                                            const Off* __restrict__ local,
-                                                           uint64_t count, uint32_t* __restrict__ any_flag) {
+                                                           uint64_t count, uint32_t* __restrict__ any_flag,
+                                                           uint64_t bias) {
     // Test-then-set as in the direct insert: 4 probes per lane in flight, an atomic
     // only for bits still 0 (a 1 seen here is final within the launch).
     constexpr int U = 4;
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
             const uint64_t p = p0 + u * stride;
             mask[u] = 0; v[u] = 0; w[u] = 0;
             if (p < count) {
-                const uint64_t o = local[p];
+                const uint64_t o = (uint64_t)local[p] + bias;
                 w[u] = o >> 5;
                 mask[u] = 1u << ((uint32_t)(o ^ 7u) & 31u);
                 v[u] = bits[w[u]];
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
 template <typename Off>
 __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits,
                                                          const Off* __restrict__ local, uint64_t count,
-                                                         uint8_t* __restrict__ out) {
+                                                         uint8_t* __restrict__ out, uint64_t bias) {
     constexpr int U = 4;   // 4 independent probe loads per lane in flight
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < count; p0 += U * stride) {
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restr
             const uint64_t p = p0 + u * stride;
             v[u] = 0; sh[u] = 0;
             if (p < count) {
-                const uint64_t o = local[p];
+                const uint64_t o = (uint64_t)local[p] + bias;
                 sh[u] = (uint32_t)(o ^ 7u) & 31u;
                 v[u] = bits[o >> 5];
             }
@@ -399,31 +400,34 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
 }
 
 template <typename Off>
-static void launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag, hipStream_t s) {
+static void launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag, uint64_t bias,
+                                hipStream_t s) {
     const Off* l = static_cast<const Off*>(local);
     if (any_flag)
-        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count, any_flag);
+        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count,
+                           any_flag, bias);
     else
-        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count, any_flag);
+        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count,
+                           any_flag, bias);
 }
 
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag,
-                                  bool route32, hipStream_t s) {
+                                  bool route32, hipStream_t s, uint64_t bias) {
     if (count == 0) return hipSuccess;
-    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, s);
-    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, s);
+    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, bias, s);
+    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, bias, s);
     return hipGetLastError();
 }
 
 hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count, uint8_t* out,
-                                bool route32, hipStream_t s) {
+                                bool route32, hipStream_t s, uint64_t bias) {
     if (count == 0) return hipSuccess;
     if (route32)
         hipLaunchKernelGGL(shard_test_kernel<uint32_t>, dim3(stream_grid(count)), dim3(256), 0, s, bits,
-                           static_cast<const uint32_t*>(local), count, out);
+                           static_cast<const uint32_t*>(local), count, out, bias);
     else
         hipLaunchKernelGGL(shard_test_kernel<uint64_t>, dim3(stream_grid(count)), dim3(256), 0, s, bits,
-                           static_cast<const uint64_t*>(local), count, out);
+                           static_cast<const uint64_t*>(local), count, out, bias);
     return hipGetLastError();
 }
 

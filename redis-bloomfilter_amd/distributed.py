@@ -98,6 +98,7 @@ class HipEngine:
                              flags=BF_FLAG_ROUTE32 if route32 else 0)
         self.k, self.P = k, P
         self.offset_dtype = torch.int32 if route32 else torch.int64
+        self.nh = self.filter.route_window_split()   # 2^32-bit sub-ranges per window-routed owner
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -113,11 +114,13 @@ class HipEngine:
         return send, slot, counts
 
     def route_windows(self, kb: torch.Tensor, ko: torch.Tensor, n: int, cap: int, want_slot: bool = True):
-        """route() without the owner-major gather: owner s's probes are send[s*cap : s*cap +
-        counts[s]] in an unspecified order (slot alongside); counts[s] > cap = overflow."""
-        send = torch.empty(self.P * cap, dtype=self.offset_dtype, device=self.device)
-        slot = torch.empty(self.P * cap, dtype=torch.int32, device=self.device) if want_slot else None
-        counts = torch.empty(self.P, dtype=torch.int64, device=self.device)
+        """route() without the owner-major gather: window w = owner * nh + hi holds that owner's
+        probes with local offset (hi << 32) | entry, as uint32, in send[w*cap : w*cap +
+        counts[w]] in an unspecified order (slot alongside); counts[w] > cap = overflow."""
+        nwin = self.P * self.nh
+        send = torch.empty(nwin * cap, dtype=torch.int32, device=self.device)
+        slot = torch.empty(nwin * cap, dtype=torch.int32, device=self.device) if want_slot else None
+        counts = torch.empty(nwin, dtype=torch.int64, device=self.device)
         self.filter.route_windows_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
                                       slot.data_ptr() if want_slot else 0, cap, counts.data_ptr(),
                                       stream=self._stream())
@@ -126,9 +129,15 @@ class HipEngine:
     def combine_windows(self, bits: torch.Tensor, slot: torch.Tensor, counts: torch.Tensor, cap: int,
                         n: int) -> torch.Tensor:
         out = torch.empty(n, dtype=torch.uint8, device=self.device)
-        self.filter.combine_windows_dev(bits.data_ptr(), slot.data_ptr(), cap, counts.data_ptr(), n, out.data_ptr(),
-                                        stream=self._stream())
+        self.filter.combine_windows_dev(bits.data_ptr(), slot.data_ptr(), cap, counts.numel(), counts.data_ptr(), n,
+                                        out.data_ptr(), stream=self._stream())
         return out
+
+    def shard_insert_hi(self, local32: torch.Tensor, hi: int) -> None:
+        self.filter.shard_insert_hi_dev(local32.data_ptr(), local32.numel(), hi, stream=self._stream())
+
+    def shard_test_hi(self, local32: torch.Tensor, hi: int, out: torch.Tensor) -> None:
+        self.filter.shard_test_hi_dev(local32.data_ptr(), local32.numel(), hi, out.data_ptr(), stream=self._stream())
 
     def shard_insert(self, local: torch.Tensor) -> None:
         self.filter.shard_insert_dev(local.data_ptr(), local.numel(), stream=self._stream())
@@ -202,83 +211,117 @@ class PartitionedFilter:
         return cnt[0].tolist(), cnt[1].tolist()
 
     def _cap(self, n: int) -> int:
-        """Window size per owner for a batch of n keys: the block-cyclic map spreads probes
-        evenly, so 1/P of them plus 12.5 % and a small-batch slack; a skewed batch
-        (e.g. one key repeated) overflows and takes the contiguous route."""
+        """Window size for a batch of n keys: the block-cyclic map spreads probes evenly, so
+        1/P of them plus 12.5 % and a small-batch slack (a sub-range window of a split owner
+        gets the owner's whole share); a skewed batch (e.g. one key repeated) overflows and
+        is routed again with cap = n*k."""
         probes = n * self.k
         return min(probes, probes // self.P + probes // (8 * self.P) + 4096)
 
-    def _route(self, kb, ko, n: int, want_slot: bool):
-        """Probes grouped by owner: (send, slot, counts, displs, splits) where owner s's
-        entries are send[displs[s] : displs[s] + splits[0][s]]; splits = (send, receive)
-        counts, already exchanged (the host waits for that small all-to-all)."""
-        e = self.engine
+    def _route(self, kb, ko, n: int, want_slot: bool) -> dict:
+        """Route a batch and exchange its counts (the host waits for that small all-to-all).
+        Returns the send buffer, slots, device counts and the segment lists of the exchange:
+        ``sseg`` = [(peer, offset, count)] to send, ``rseg`` = [(peer, offset, count)] to
+        receive, both in the order the two sides agree on, plus ``hruns`` = [(hi, start, end)]
+        of the receive buffer for the owner ops (window route: one run per 2^32-bit sub-range)."""
+        e, P = self.engine, self.P
         if self.windows and hasattr(e, "route_windows"):
+            nh = e.nh
             cap = self._cap(n)
             send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
-            splits = self._splits(counts)
-            if max(splits[0]) <= cap:
-                return send, slot, counts, [s * cap for s in range(self.P)], splits, cap
-            # A window past cap holds undefined entries: re-route contiguously.  Each rank
-            # decides alone and needs no second count exchange (the per-owner totals are the
-            # same), and the grouped send/recv below serves both layouts.
-            self.window_overflows += 1
-            send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
-        else:
-            send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
-            splits = self._splits(counts)
-        return send, slot, counts, _prefix(splits[0]), splits, None
+            sc, rc = self._splits(counts)   # rc[s*nh + h]: source s's probes for my sub-range h
+            if max(sc) > cap:
+                # A window past cap holds undefined entries: route again into windows that
+                # always fit.  Each rank decides alone and the counts are the same, so the
+                # exchange below does not change shape.
+                self.window_overflows += 1
+                cap = max(n * self.k, 1)
+                send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
+            sseg = [(o, (o * nh + h) * cap, sc[o * nh + h]) for o in range(P) for h in range(nh)]
+            rseg, hruns, at = [None] * (P * nh), [], 0
+            for h in range(nh):   # receive buffer: sub-range major, then source
+                h0 = at
+                for src in range(P):
+                    rseg[src * nh + h] = (src, at, rc[src * nh + h])
+                    at += rc[src * nh + h]
+                hruns.append((h, h0, at))
+            return dict(send=send, slot=slot, counts=counts, cap=cap, sseg=sseg, rseg=rseg, hruns=hruns, total=at)
+        send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
+        sc, rc = self._splits(counts)
+        sd, rd = _prefix(sc), _prefix(rc)
+        return dict(send=send, slot=slot, counts=counts, cap=None,
+                    sseg=[(o, sd[o], sc[o]) for o in range(P)], rseg=[(o, rd[o], rc[o]) for o in range(P)],
+                    hruns=None, total=sum(rc))
 
-    def _p2p(self, send: torch.Tensor, sdispl, ssplit, recv: torch.Tensor, rdispl, rsplit):
-        """Grouped send/recv: send[sdispl[s] : +ssplit[s]] to rank s, recv[rdispl[s] :
-        +rsplit[s]] from rank s (an all-to-all whose segments need not be contiguous; one
-        RCCL group of ncclSend/ncclRecv on the process group's stream).  The self segment
-        is a device copy on the current stream.  Returns the works to wait on."""
+    def _p2p(self, send: torch.Tensor, sseg, recv: torch.Tensor, rseg):
+        """Grouped send/recv: each (peer, offset, count) of sseg goes to that peer, each of
+        rseg comes from it (an all-to-all whose segments need not be contiguous; one RCCL
+        group of ncclSend/ncclRecv on the process group's stream; messages between two
+        ranks match in list order).  The self segments are device copies on the current
+        stream.  Returns the works to wait on."""
         ops = []
-        for peer in range(self.P):
-            sv = send[sdispl[peer]: sdispl[peer] + ssplit[peer]]
-            rv = recv[rdispl[peer]: rdispl[peer] + rsplit[peer]]
-            if peer == self.rank:
-                if ssplit[peer]:
-                    rv.copy_(sv)
-                continue
-            g = peer if self.group is None else dist.get_global_rank(self.group, peer)
-            if ssplit[peer]:
-                ops.append(dist.P2POp(dist.isend, sv, g, self.group))
-            if rsplit[peer]:
-                ops.append(dist.P2POp(dist.irecv, rv, g, self.group))
+        mine_s = [(o, c) for p_, o, c in sseg if p_ == self.rank]
+        mine_r = [(o, c) for p_, o, c in rseg if p_ == self.rank]
+        for (so, c), (ro, _) in zip(mine_s, mine_r):
+            if c:
+                recv[ro: ro + c].copy_(send[so: so + c])
+        for peer, off, c in sseg:
+            if peer != self.rank and c:
+                g = peer if self.group is None else dist.get_global_rank(self.group, peer)
+                ops.append(dist.P2POp(dist.isend, send[off: off + c], g, self.group))
+        for peer, off, c in rseg:
+            if peer != self.rank and c:
+                g = peer if self.group is None else dist.get_global_rank(self.group, peer)
+                ops.append(dist.P2POp(dist.irecv, recv[off: off + c], g, self.group))
         return dist.batch_isend_irecv(ops) if ops else []
 
     def _exchange(self, kb, ko, n: int, want_slot: bool):
         """route, then the offsets to their owners (async): returns (recv, route, works)."""
         rt = self._route(kb, ko, n, want_slot)
-        send, _, _, displs, (ss, rs), _ = rt
-        recv = torch.empty(sum(rs), dtype=send.dtype, device=send.device)
-        works = self._p2p(send, displs, ss, recv, _prefix(rs), rs)
+        recv = torch.empty(rt["total"], dtype=rt["send"].dtype, device=rt["send"].device)
+        works = self._p2p(rt["send"], rt["sseg"], recv, rt["rseg"])
         return recv, rt, works
 
-    def _answer(self, bits: torch.Tensor, rt, n: int) -> torch.Tensor:
+    def _shard_insert(self, recv: torch.Tensor, rt: dict) -> None:
+        if rt["hruns"] is None:
+            self.engine.shard_insert(recv)
+            return
+        for h, a, b in rt["hruns"]:
+            if b > a:
+                self.engine.shard_insert_hi(recv[a:b], h)
+
+    def _shard_test(self, recv: torch.Tensor, rt: dict) -> torch.Tensor:
+        if rt["hruns"] is None:
+            return self.engine.shard_test(recv)
+        bits = torch.empty(recv.numel(), dtype=torch.uint8, device=recv.device)
+        for h, a, b in rt["hruns"]:
+            if b > a:
+                self.engine.shard_test_hi(recv[a:b], h, bits[a:b])
+        return bits
+
+    def _answer(self, bits: torch.Tensor, rt: dict, n: int) -> torch.Tensor:
         """Owner answers (one byte per received probe) back to the requesters, then AND per key."""
-        send, slot, counts, displs, (ss, rs), cap = rt
-        back = torch.empty(self.P * cap if cap is not None else sum(ss), dtype=torch.uint8, device=bits.device)
-        for w in self._p2p(bits, _prefix(rs), rs, back, displs, ss):
+        cap = rt["cap"]
+        size = rt["send"].numel() if cap is not None else sum(c for _, _, c in rt["sseg"])
+        back = torch.empty(size, dtype=torch.uint8, device=bits.device)
+        for w in self._p2p(bits, rt["rseg"], back, rt["sseg"]):
             w.wait()
         if cap is not None:
-            return self.engine.combine_windows(back, slot, counts, cap, n)
-        return self.engine.combine(back, slot, n)
+            return self.engine.combine_windows(back, rt["slot"], rt["counts"], cap, n)
+        return self.engine.combine(back, rt["slot"], n)
 
     # -- device-resident batch API (keys already in device memory)
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
-        recv, _, works = self._exchange(kb, ko, n, want_slot=False)
+        recv, rt, works = self._exchange(kb, ko, n, want_slot=False)
         for w in works:
             w.wait()
-        self.engine.shard_insert(recv)
+        self._shard_insert(recv, rt)
 
     def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
         recv, rt, works = self._exchange(kb, ko, n, want_slot=True)
         for w in works:
             w.wait()
-        return self._answer(self.engine.shard_test(recv), rt, n)
+        return self._answer(self._shard_test(recv, rt), rt, n)
 
     def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
                            qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
@@ -291,15 +334,14 @@ class PartitionedFilter:
         current stream; every owner still applies all ranks' inserts before it tests
         (shard_insert precedes shard_test on its stream), so the include? answers see the
         batch's inserts exactly as in the sequential form."""
-        e = self.engine
-        recv_i, _, w_i = self._exchange(ikb, iko, ni, want_slot=False)
+        recv_i, rt_i, w_i = self._exchange(ikb, iko, ni, want_slot=False)
         recv_q, rt_q, w_q = self._exchange(qkb, qko, nq, want_slot=True)   # route(inc) overlaps send(ins)
         for w in w_i:
             w.wait()
-        e.shard_insert(recv_i)                                              # overlaps send(inc)
+        self._shard_insert(recv_i, rt_i)                                    # overlaps send(inc)
         for w in w_q:
             w.wait()
-        return self._answer(e.shard_test(recv_q), rt_q, nq)
+        return self._answer(self._shard_test(recv_q, rt_q), rt_q, nq)
 
     # -- host API (each rank passes its own keys)
     def insert_many(self, keys: Iterable) -> None:

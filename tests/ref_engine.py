@@ -20,6 +20,7 @@ class NumpyEngine:
         self.m, self.k, self.P, self.b, self.orc = m, k, P, block_log2, orc
         reach = min(m, k * 0xFFFFFFFF + 1)
         self.local_bits = D.shard_local_bits(reach, P, rank, block_log2)
+        self.nh = max(1, -(-D.shard_local_bits(reach, P, 0, block_log2) // (1 << 32)))   # bf_route_window_split
         self.bits = np.zeros((self.local_bits + 7) // 8, np.uint8)
 
     def route(self, kb, ko, n, want_slot=True):
@@ -34,26 +35,41 @@ class NumpyEngine:
                 torch.from_numpy(counts))
 
     def route_windows(self, kb, ko, n, cap, want_slot=True):
-        """route() in the window layout; each window's entries shuffled, since the HIP
-        route leaves their order unspecified (the exchange must not depend on it)."""
-        send, slot, counts = self.route(kb, ko, n, want_slot=True)
-        c = counts.numpy()
-        wsend = np.zeros(self.P * cap, np.int64)
-        wslot = np.full(self.P * cap, -1, np.int32)
-        rng = np.random.default_rng(int(c.sum()) + 7)
-        at = 0
-        for s in range(self.P):
-            live = min(int(c[s]), cap)
-            perm = at + rng.permutation(int(c[s]))[:live]
-            wsend[s * cap: s * cap + live] = send.numpy()[perm]
-            wslot[s * cap: s * cap + live] = slot.numpy()[perm]
-            at += int(c[s])
-        return torch.from_numpy(wsend), torch.from_numpy(wslot) if want_slot else None, counts
+        """route() in the window layout (window = owner * nh + local >> 32, uint32 entries);
+        each window's entries shuffled, since the HIP route leaves their order unspecified
+        (the exchange must not depend on it)."""
+        buf = kb.numpy()
+        offs = ko.numpy().view(np.uint64)
+        idx = self.orc.indexes_many(buf, offs, self.m, self.k).reshape(-1)
+        owner, local = D.block_owner_local(idx, self.P, self.b)
+        win = owner.astype(np.int64) * self.nh + (local >> np.uint64(32)).astype(np.int64)
+        nwin = self.P * self.nh
+        counts = np.bincount(win, minlength=nwin).astype(np.int64)
+        wsend = np.zeros(nwin * cap, np.int32)
+        wslot = np.full(nwin * cap, -1, np.int32)
+        key_of = (np.arange(n * self.k, dtype=np.int64) // self.k).astype(np.int32)
+        rng = np.random.default_rng(int(counts.sum()) + 7)
+        for w in range(nwin):
+            sel = np.flatnonzero(win == w)
+            sel = rng.permutation(sel)[: min(len(sel), cap)]
+            wsend[w * cap: w * cap + len(sel)] = (local[sel] & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+            wslot[w * cap: w * cap + len(sel)] = key_of[sel]
+        return torch.from_numpy(wsend), torch.from_numpy(wslot) if want_slot else None, torch.from_numpy(counts)
 
     def combine_windows(self, bits, slot, counts, cap, n):
         c = counts.numpy()
-        live = np.concatenate([np.arange(s * cap, s * cap + min(int(c[s]), cap)) for s in range(self.P)])
+        live = np.concatenate([np.arange(w * cap, w * cap + min(int(c[w]), cap)) for w in range(len(c))])
         return self.combine(bits[torch.from_numpy(live)], slot[torch.from_numpy(live)], n)
+
+    def _hi(self, local32, hi):
+        lo = local32.numpy().view(np.uint32).astype(np.uint64) | (np.uint64(hi) << np.uint64(32))
+        return torch.from_numpy(lo.view(np.int64))
+
+    def shard_insert_hi(self, local32, hi):
+        self.shard_insert(self._hi(local32, hi))
+
+    def shard_test_hi(self, local32, hi, out):
+        out.copy_(self.shard_test(self._hi(local32, hi)))
 
     def shard_insert(self, local):
         lo = local.numpy().view(np.uint64)

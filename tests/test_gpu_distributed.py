@@ -97,55 +97,75 @@ def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
 
 
 @pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20),
-                                     (9585058377, 6, 2, 20)])
+                                     (9585058377, 6, 2, 20), (191701167547, 13, 1, 20)])
 def test_route_windows(pkg, oracle, m, k, P, b):
-    """bf_route_windows_dev: window s holds exactly owner s's (key, local offset) pairs
-    (the multiset bf_route_dev puts in segment s); bf_combine_windows_dev over the window
-    layout equals the AND; a window smaller than its owner's probes shows in the counts.
-    (9585058377, 6, 2): shards past 2^32 bits, so 64-bit routed offsets."""
+    """bf_route_windows_dev: window w = s*nh + hi holds exactly owner s's (key, local offset)
+    pairs with local >> 32 == hi, as uint32 (the multiset bf_route_dev puts in segment s, split
+    by sub-range); the owner's hi ops see (hi << 32) | entry; bf_combine_windows_dev over the
+    window layout equals the AND; a window smaller than its probes shows in the counts.
+    (9585058377, 6, 2) and the 10B cases: shards past 2^32 bits, so nh > 1."""
     import torch
     D = pkg.distributed
     dev = torch.device("cuda", 0)
     e = D.HipEngine(m, k, P, 0, b, dev)
+    nh = e.nh
+    want_nh = max(1, -(-D.shard_local_bits(min(m, k * 0xFFFFFFFF + 1), P, 0, b) // (1 << 32)))
+    assert nh == want_nh
+    nwin = P * nh
     rng = np.random.default_rng(17)
     keys = ["w%d" % int(v) for v in rng.integers(0, 10**12, 30000)]
     kb, ko, n, buf, offs = dev_batch(pkg, torch, keys)
     idx = oracle.indexes_many(buf, offs, m, k).reshape(-1)
     owner, local = D.block_owner_local(idx, P, b)
-    want_c = np.bincount(owner, minlength=P)
+    win = owner.astype(np.int64) * nh + (local >> np.uint64(32)).astype(np.int64)
+    want_c = np.bincount(win, minlength=nwin)
     key_of = np.arange(n * k) // k
     cap = int(want_c.max()) + 37
     send, slot, counts = e.route_windows(kb, ko, n, cap)
     torch.cuda.synchronize()
+    assert send.dtype == torch.int32
     assert counts.cpu().numpy().tolist() == want_c.tolist()
-    s_np = send.cpu().numpy()
-    s_np = s_np.view(np.uint32).astype(np.uint64) if s_np.dtype == np.int32 else s_np.view(np.uint64)
+    s_np = send.cpu().numpy().view(np.uint32).astype(np.uint64)
     sl = slot.cpu().numpy().astype(np.int64)
-    for s in range(P):
-        w = slice(s * cap, s * cap + int(want_c[s]))
-        got = sorted(zip(sl[w].tolist(), s_np[w].tolist()))
-        assert got == sorted(zip(key_of[owner == s].tolist(), local[owner == s].tolist()))
-    # combine over windows: answer bytes from a known bitset, dead window tails poisoned with 0
+    for w in range(nwin):
+        ws = slice(w * cap, w * cap + int(want_c[w]))
+        got = sorted(zip(sl[ws].tolist(), (s_np[ws] | np.uint64((w % nh) << 32)).tolist()))
+        assert got == sorted(zip(key_of[win == w].tolist(), local[win == w].tolist()))
+    # owner-side hi ops: shard 0 inserts its windows, then answers every probe of them
+    ins = [(h, send[h * cap: h * cap + int(want_c[h])]) for h in range(nh)]
+    for h, run in ins:
+        e.shard_insert_hi(run, h)
+    for h, run in ins:
+        bits_h = torch.empty(run.numel(), dtype=torch.uint8, device=dev)
+        e.shard_test_hi(run, h, bits_h)
+        assert bool(bits_h.all())
+    shard = e.shard_export()
+    lo = local[owner == 0]
+    want_shard = np.zeros_like(shard)
+    np.bitwise_or.at(want_shard, (lo >> np.uint64(3)).astype(np.int64), (np.uint64(0x80) >> (lo & np.uint64(7))).astype(np.uint8))
+    np.testing.assert_array_equal(shard, want_shard)
+    # combine over windows: answer bytes from a known bitset
     bits = oracle.new_bitset(m, k)
     ib, io = pkg.keys.pack(keys[: n // 2])
     oracle.insert_many(bits, m, k, ib, io)
-    ans = np.zeros(P * cap, np.uint8)
-    for s in range(P):
-        lo = s_np[s * cap: s * cap + int(want_c[s])]
-        blk, low = lo >> np.uint64(b), lo & np.uint64((1 << b) - 1)
-        glob = ((blk * np.uint64(P) + np.uint64(s)) << np.uint64(b)) | low
-        ans[s * cap: s * cap + int(want_c[s])] = \
+    ans = np.zeros(nwin * cap, np.uint8)
+    for w in range(nwin):
+        s_, h = divmod(w, nh)
+        lw = s_np[w * cap: w * cap + int(want_c[w])] | np.uint64(h << 32)
+        blk, low = lw >> np.uint64(b), lw & np.uint64((1 << b) - 1)
+        glob = ((blk * np.uint64(P) + np.uint64(s_)) << np.uint64(b)) | low
+        ans[w * cap: w * cap + int(want_c[w])] = \
             (bits.view(np.uint8)[(glob >> np.uint64(3)).astype(np.int64)] >> (7 - (glob & np.uint64(7))).astype(np.uint8)) & 1
     got = e.combine_windows(torch.from_numpy(ans).to(dev), slot, counts, cap, n).cpu().numpy()
     np.testing.assert_array_equal(got, oracle.include_many(bits, m, k, buf, offs))
     assert got[: n // 2].all()
-    # too-small windows: the counts still report every owner's full total
-    small = int(want_c.min()) // 2
+    # too-small windows: the counts still report every window's full total
+    small = max(1, int(want_c[want_c > 0].min()) // 2)
     _, _, c2 = e.route_windows(kb, ko, n, small, want_slot=False)
     assert c2.cpu().numpy().tolist() == want_c.tolist()
     # an empty batch zeroes the counts
     _, _, c3 = e.route_windows(kb, ko, 0, 16)
-    assert c3.cpu().numpy().tolist() == [0] * P
+    assert c3.cpu().numpy().tolist() == [0] * nwin
     e.close()
 
 
@@ -189,6 +209,19 @@ def test_torch_distributed_world1(pkg, oracle):
             np.testing.assert_array_equal(f.insert_include(keys, probe), want)
             assert f.export_redis() == oracle.redis_string(bits)
             assert f.window_overflows == (2 if cap is not None else 0)
+            f.close()
+        # a shard past 2^32 bits (the north-star filter, 1.2 GB, in one shard): the window
+        # route splits it into nh = 3 sub-range windows of uint32 entries
+        m, k = 9585058377, 6
+        bits = oracle.new_bitset(m, k)
+        oracle.insert_many(bits, m, k, ib, io)
+        want = oracle.include_many(bits, m, k, pb, po).astype(bool)
+        for kw in ({}, {"windows": False}):
+            f = D.PartitionedFilter(m, k, block_log2=20, **kw)
+            assert f.engine.nh == 3
+            np.testing.assert_array_equal(f.insert_include(keys, probe), want)
+            shard = f.engine.shard_export()
+            assert np.array_equal(shard[: len(bits.view(np.uint8))], bits.view(np.uint8)[: len(shard)])
             f.close()
     finally:
         dist.destroy_process_group()

@@ -48,22 +48,34 @@ def main():
     P = args.shards
     cap = batch * k // P + batch * k // (8 * P) + 4096
 
-    def received(send, counts):   # the windows' live entries, contiguous (what the receive delivers)
+    nh = eng.nh   # 2^32-bit sub-range windows per owner (1 when the shard fits 2^32 bits)
+
+    def received(send, counts):
+        """Stand-in for the receive: every window's live entries, grouped by sub-range h
+        (what the grouped send/recv delivers when every source routed this batch)."""
         c = counts.cpu().tolist()
-        return torch.cat([send[s * cap: s * cap + c[s]] for s in range(P)])
+        runs = []
+        for h in range(nh):
+            parts = [send[(s * nh + h) * cap: (s * nh + h) * cap + c[s * nh + h]] for s in range(P)]
+            runs.append((h, torch.cat(parts)))
+        return runs
 
     def step_windows(b):
         (ikb, iko), (qkb, qko) = b
         send, _, counts = eng.route_windows(ikb, iko, batch, cap, want_slot=False)
-        eng.shard_insert(received(send, counts))
+        for h, run in received(send, counts):
+            eng.shard_insert_hi(run, h)
         send, slot, counts = eng.route_windows(qkb, qko, batch, cap)
-        bits = eng.shard_test(received(send, counts))
-        back = torch.empty(P * cap, dtype=torch.uint8, device=dev)
+        back = torch.empty(P * nh * cap, dtype=torch.uint8, device=dev)
         c = counts.cpu().tolist()
-        at = 0
-        for s in range(P):
-            back[s * cap: s * cap + c[s]] = bits[at: at + c[s]]
-            at += c[s]
+        for h, run in received(send, counts):
+            bits = torch.empty(run.numel(), dtype=torch.uint8, device=dev)
+            eng.shard_test_hi(run, h, bits)
+            at = 0
+            for s in range(P):
+                w = s * nh + h
+                back[w * cap: w * cap + c[w]] = bits[at: at + c[w]]
+                at += c[w]
         return eng.combine_windows(back, slot, counts, cap, batch)
 
     def step(b):
