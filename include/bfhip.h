@@ -210,6 +210,18 @@ int  bf_shard_test_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t coun
 int  bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t window_cap,
                             uint32_t nwin, const uint64_t* d_counts /* device, nwin */, uint64_t n,
                             uint8_t* d_out, void* stream);
+/* The return trip of a window-routed include? at one bit per probe:
+ * bf_pack_segments_dev           owner: segment q of d_seg (device, nseg triples of uint64:
+ *                                source offset, count, destination byte offset) packs the answer
+ *                                bytes d_bits[src .. src + count) LSB-first into ceil(count/8)
+ *                                bytes at d_packed[dst]; max_count >= every count.
+ * bf_combine_windows_packed_dev  requester: bf_combine_windows_dev with window w's answers
+ *                                as bits at d_packed + w*ceil(window_cap/8). */
+int  bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_seg, uint32_t nseg,
+                          uint64_t max_count, uint8_t* d_packed, void* stream);
+int  bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint32_t* d_slot,
+                                   uint64_t window_cap, uint32_t nwin, const uint64_t* d_counts, uint64_t n,
+                                   uint8_t* d_out, void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
 int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,

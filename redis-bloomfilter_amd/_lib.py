@@ -95,6 +95,8 @@ SIGNATURES = {
     "bf_shard_insert_hi_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
     "bf_shard_test_hi_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
     "bf_combine_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp]),
+    "bf_pack_segments_dev": (ctypes.c_int, [_vp, _vp, _vp, _u32, _u64, _vp, _vp]),
+    "bf_combine_windows_packed_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp]),
     "bf_shard_export": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_shard_import": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
     "bf_lua_create": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, ctypes.POINTER(bf_config),
@@ -412,6 +414,16 @@ class Filter:
         nh = ctypes.c_uint32()
         _check(self._lib.bf_route_window_split(self.handle, ctypes.byref(nh)), self._h)
         return int(nh.value)
+
+    def pack_segments_dev(self, d_bits: int, d_seg: int, nseg: int, max_count: int, d_packed: int,
+                          stream=None) -> None:
+        _check(self._lib.bf_pack_segments_dev(self.handle, d_bits, d_seg, int(nseg), int(max_count), d_packed,
+                                              self._s(stream)), self._h)
+
+    def combine_windows_packed_dev(self, d_packed: int, d_slot: int, window_cap: int, nwin: int, d_counts: int,
+                                   n: int, d_out: int, stream=None) -> None:
+        _check(self._lib.bf_combine_windows_packed_dev(self.handle, d_packed, d_slot, int(window_cap), int(nwin),
+                                                       d_counts, int(n), d_out, self._s(stream)), self._h)
 
     def shard_insert_hi_dev(self, d_local32: int, count: int, hi: int, d_any_new: int = 0, stream=None) -> None:
         _check(self._lib.bf_shard_insert_hi_dev(self.handle, d_local32, int(count), int(hi), d_any_new or None,

@@ -1036,6 +1036,38 @@ int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* 
     return BF_OK;
 }
 
+int bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_seg, uint32_t nseg,
+                         uint64_t max_count, uint8_t* d_packed, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (nseg && (!d_bits || !d_seg || !d_packed)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (nseg > 65535) return set_err(h, BF_EINVAL, "at most 65535 segments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    hipStream_t s = pick_stream(h, stream);
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_pack_segments(d_bits, reinterpret_cast<const unsigned long long*>(d_seg), nseg, max_count,
+                                      d_packed, s));
+    bf_mark(mk, s, "pack_answers");
+    return BF_OK;
+}
+
+int bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint32_t* d_slot, uint64_t window_cap,
+                                  uint32_t nwin, const uint64_t* d_counts, uint64_t n, uint8_t* d_out, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (n && (!d_packed || !d_slot || !d_counts || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    hipStream_t s = pick_stream(h, stream);
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_combine_windows_packed(d_packed, d_slot, window_cap,
+                                               reinterpret_cast<const unsigned long long*>(d_counts), nwin, n, d_out,
+                                               s));
+    bf_mark(mk, s, "combine");
+    return BF_OK;
+}
+
 int bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                        uint32_t* d_any_new, uint8_t* d_per_key_new, void* stream) {
     const BfOp op = (d_any_new || d_per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;

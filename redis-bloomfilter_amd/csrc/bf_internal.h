@@ -150,6 +150,15 @@ hipError_t bf_launch_combine_windows(const uint8_t* bits, const uint32_t* slot, 
                                      const unsigned long long* counts, uint32_t P, uint64_t n, uint8_t* out,
                                      hipStream_t s);
 
+// Answer bytes -> LSB-first bits per segment (seg: nseg triples src, count, dst byte);
+// max_count bounds the counts (grid size).  And the windowed combine over such bits
+// (window s at packed + s * ceil(wcap / 8)).
+hipError_t bf_launch_pack_segments(const uint8_t* bits, const unsigned long long* seg, uint32_t nseg,
+                                   uint64_t max_count, uint8_t* packed, hipStream_t s);
+hipError_t bf_launch_combine_windows_packed(const uint8_t* packed, const uint32_t* slot, uint64_t wcap,
+                                            const unsigned long long* counts, uint32_t P, uint64_t n, uint8_t* out,
+                                            hipStream_t s);
+
 // Partitioned filters.  cursor[P]: scratch.  Groups `total` (owner, local) probe
 // pairs by owner into send[]; slot[pos] (nullable) = key index (probe / k) of send entry pos.
 // counts[P] must hold the per-owner totals (from BF_OP_ROUTE).

@@ -350,6 +350,40 @@ __global__ __launch_bounds__(256) void combine_windows_kernel(const uint8_t* __r
         if (!wb[i]) out[ws[i]] = 0;
 }
 
+// Answer bytes -> bits for the return trip of a partitioned include?: segment q =
+// (src offset, count, dst byte offset) packs bits[src .. src + count) LSB-first into
+// ceil(count / 8) bytes at packed[dst].  One grid row per segment.
+__global__ __launch_bounds__(256) void pack_segments_kernel(const uint8_t* __restrict__ bits,
+                                                            const unsigned long long* __restrict__ seg,
+                                                            uint8_t* __restrict__ packed) {
+    const unsigned long long src = seg[3 * blockIdx.y], cnt = seg[3 * blockIdx.y + 1], dst = seg[3 * blockIdx.y + 2];
+    const uint64_t nbytes = (cnt + 7) / 8;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nbytes; b += stride) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            if (b * 8 + i < cnt) v |= (uint32_t)(bits[src + b * 8 + i] & 1u) << i;
+        packed[dst + b] = (uint8_t)v;
+    }
+}
+
+// combine_windows_kernel over packed answers: window s's entry i is bit (i & 7) of
+// packed[s * wcap8 + i / 8].
+__global__ __launch_bounds__(256) void combine_windows_packed_kernel(const uint8_t* __restrict__ packed,
+                                                                     const uint32_t* __restrict__ slot, uint64_t wcap,
+                                                                     uint64_t wcap8,
+                                                                     const unsigned long long* __restrict__ counts,
+                                                                     uint8_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t s = blockIdx.y;
+    const uint64_t live = counts[s] < wcap ? counts[s] : wcap;
+    const uint8_t* wb = packed + s * wcap8;
+    const uint32_t* ws = slot + s * wcap;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < live; i += stride)
+        if (!((wb[i >> 3] >> (i & 7)) & 1u)) out[ws[i]] = 0;
+}
+
 uint32_t stream_grid(uint64_t nvec) {
     uint64_t g = (nvec + 255) / 256;
     if (g > 2048) g = 2048;   // grid-stride beyond 8 blocks per CU
@@ -451,6 +485,27 @@ hipError_t bf_launch_combine_windows(const uint8_t* bits, const uint32_t* slot, 
     uint32_t gx = stream_grid(wcap) / P;
     hipLaunchKernelGGL(combine_windows_kernel, dim3(gx ? gx : 1u, P), dim3(256), 0, s, bits, slot, wcap, counts, P,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_pack_segments(const uint8_t* bits, const unsigned long long* seg, uint32_t nseg,
+                                   uint64_t max_count, uint8_t* packed, hipStream_t s) {
+    if (nseg == 0 || max_count == 0) return hipSuccess;
+    uint32_t gx = stream_grid((max_count + 7) / 8) / nseg;
+    hipLaunchKernelGGL(pack_segments_kernel, dim3(gx ? gx : 1u, nseg), dim3(256), 0, s, bits, seg, packed);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_combine_windows_packed(const uint8_t* packed, const uint32_t* slot, uint64_t wcap,
+                                            const unsigned long long* counts, uint32_t P, uint64_t n, uint8_t* out,
+                                            hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(out, 1, n, s);
+    if (e != hipSuccess) return e;
+    if (wcap == 0) return hipSuccess;
+    uint32_t gx = stream_grid(wcap) / P;
+    hipLaunchKernelGGL(combine_windows_packed_kernel, dim3(gx ? gx : 1u, P), dim3(256), 0, s, packed, slot, wcap,
+                       (wcap + 7) / 8, counts, out);
     return hipGetLastError();
 }
 

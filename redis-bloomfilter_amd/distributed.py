@@ -133,6 +133,20 @@ class HipEngine:
                                         out.data_ptr(), stream=self._stream())
         return out
 
+    def pack_answers(self, bits: torch.Tensor, seg: torch.Tensor, max_count: int, total: int) -> torch.Tensor:
+        """Answer bytes -> bits per segment (seg: [nseg, 3] int64 src, count, dst byte)."""
+        packed = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+        self.filter.pack_segments_dev(bits.data_ptr(), seg.data_ptr(), seg.shape[0], max_count, packed.data_ptr(),
+                                      stream=self._stream())
+        return packed
+
+    def combine_windows_packed(self, packed: torch.Tensor, slot: torch.Tensor, counts: torch.Tensor, cap: int,
+                               n: int) -> torch.Tensor:
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self.filter.combine_windows_packed_dev(packed.data_ptr(), slot.data_ptr(), cap, counts.numel(),
+                                               counts.data_ptr(), n, out.data_ptr(), stream=self._stream())
+        return out
+
     def shard_insert_hi(self, local32: torch.Tensor, hi: int) -> None:
         self.filter.shard_insert_hi_dev(local32.data_ptr(), local32.numel(), hi, stream=self._stream())
 
@@ -187,7 +201,7 @@ class PartitionedFilter:
     takes the contiguous bf_route_dev path instead (same exchange, same answers)."""
 
     def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None,
-                 windows: bool = True):
+                 windows: bool = True, pack_answers: bool = True):
         self.group = group
         self.P = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -199,6 +213,7 @@ class PartitionedFilter:
         self.engine = engine
         self.device = engine.device
         self.windows = windows
+        self.pack_answers = pack_answers   # window route: include? answers return as bits
         self.window_overflows = 0
 
     # -- exchange helpers
@@ -245,7 +260,19 @@ class PartitionedFilter:
                     rseg[src * nh + h] = (src, at, rc[src * nh + h])
                     at += rc[src * nh + h]
                 hruns.append((h, h0, at))
-            return dict(send=send, slot=slot, counts=counts, cap=cap, sseg=sseg, rseg=rseg, hruns=hruns, total=at)
+            rt = dict(send=send, slot=slot, counts=counts, cap=cap, sseg=sseg, rseg=rseg, hruns=hruns, total=at)
+            if want_slot and self.pack_answers and hasattr(e, "pack_answers"):
+                # the answers return as bits: segment (src, h) packs to ceil(count / 8) bytes,
+                # window w lands at w * ceil(cap / 8) on the requester
+                cap8 = (cap + 7) // 8
+                pk = [(c + 7) // 8 for _, _, c in rseg]
+                pd = _prefix(pk)
+                rt["pseg"] = torch.tensor([[off, c, d] for (_, off, c), d in zip(rseg, pd)],
+                                          dtype=torch.int64).to(self.device)
+                rt["pk_send"] = [(src, d, k_) for (src, _, _), d, k_ in zip(rseg, pd, pk)]
+                rt["pk_recv"] = [(o, (off // cap) * cap8, (c + 7) // 8) for o, off, c in sseg]
+                rt["pk_total"], rt["pk_max"], rt["cap8"] = sum(pk), max(c for _, _, c in rseg), cap8
+            return rt
         send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
         sc, rc = self._splits(counts)
         sd, rd = _prefix(sc), _prefix(rc)
@@ -302,6 +329,12 @@ class PartitionedFilter:
     def _answer(self, bits: torch.Tensor, rt: dict, n: int) -> torch.Tensor:
         """Owner answers (one byte per received probe) back to the requesters, then AND per key."""
         cap = rt["cap"]
+        if "pseg" in rt:   # one bit per probe on the way back
+            packed = self.engine.pack_answers(bits, rt["pseg"], rt["pk_max"], rt["pk_total"])
+            back = torch.empty(max(rt["counts"].numel() * rt["cap8"], 1), dtype=torch.uint8, device=bits.device)
+            for w in self._p2p(packed, rt["pk_send"], back, rt["pk_recv"]):
+                w.wait()
+            return self.engine.combine_windows_packed(back, rt["slot"], rt["counts"], cap, n)
         size = rt["send"].numel() if cap is not None else sum(c for _, _, c in rt["sseg"])
         back = torch.empty(size, dtype=torch.uint8, device=bits.device)
         for w in self._p2p(bits, rt["rseg"], back, rt["sseg"]):

@@ -59,7 +59,7 @@ def main():
     # the same step through the contiguous route (windows off), and with every window
     # overflowing (each rank falls back to the contiguous route after the count exchange)
     got45 = []
-    for kw, cap in (({"windows": False}, None), ({}, 3)):
+    for kw, cap in (({"windows": False}, None), ({}, 3), ({"pack_answers": False}, None)):
         pf4 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc), **kw)
         if cap is not None:
             pf4._cap = lambda n, c=cap: c

@@ -61,6 +61,24 @@ class NumpyEngine:
         live = np.concatenate([np.arange(w * cap, w * cap + min(int(c[w]), cap)) for w in range(len(c))])
         return self.combine(bits[torch.from_numpy(live)], slot[torch.from_numpy(live)], n)
 
+    def pack_answers(self, bits, seg, max_count, total):
+        out = np.zeros(max(total, 1), np.uint8)
+        b = bits.numpy()
+        for src, cnt, dst in seg.numpy().tolist():
+            pk = np.packbits(b[src: src + cnt] & 1, bitorder="little")
+            out[dst: dst + len(pk)] = pk
+        return torch.from_numpy(out)
+
+    def combine_windows_packed(self, packed, slot, counts, cap, n):
+        cap8 = (cap + 7) // 8
+        p = packed.numpy()
+        c = counts.numpy()
+        bits = np.ones(len(c) * cap, np.uint8)
+        for w in range(len(c)):
+            live = min(int(c[w]), cap)
+            bits[w * cap: w * cap + live] = np.unpackbits(p[w * cap8: (w + 1) * cap8], bitorder="little")[:live]
+        return self.combine_windows(torch.from_numpy(bits), slot, counts, cap, n)
+
     def _hi(self, local32, hi):
         lo = local32.numpy().view(np.uint32).astype(np.uint64) | (np.uint64(hi) << np.uint64(32))
         return torch.from_numpy(lo.view(np.int64))

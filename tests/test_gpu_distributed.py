@@ -169,6 +169,39 @@ def test_route_windows(pkg, oracle, m, k, P, b):
     e.close()
 
 
+def test_pack_segments_and_packed_combine(pkg):
+    """bf_pack_segments_dev at odd offsets and counts (LSB-first, ceil(count/8) bytes each),
+    and bf_combine_windows_packed_dev equal to the byte-per-probe windowed combine."""
+    import torch
+    D = pkg.distributed
+    dev = torch.device("cuda", 0)
+    e = D.HipEngine(95851, 6, 3, 0, 10, dev)
+    rng = np.random.default_rng(3)
+    bits = rng.integers(0, 2, 100_003).astype(np.uint8)
+    segs = [(0, 0), (0, 1), (5, 13), (100, 8), (1001, 40_000), (41_001, 59_002)]
+    pk = [(c + 7) // 8 for _, c in segs]
+    dst = np.concatenate([[0], np.cumsum(pk)[:-1]]).tolist()
+    seg = torch.tensor([[o, c, d] for (o, c), d in zip(segs, dst)], dtype=torch.int64).to(dev)
+    got = e.pack_answers(torch.from_numpy(bits).to(dev), seg, max(c for _, c in segs), sum(pk)).cpu().numpy()
+    for (o, c), d, k_ in zip(segs, dst, pk):
+        np.testing.assert_array_equal(got[d: d + k_], np.packbits(bits[o: o + c], bitorder="little"))
+    # packed combine == byte combine over 4 windows
+    cap, nwin, n = 1000, 4, 700
+    counts = np.array([0, 999, 1000, 537], np.int64)
+    slot = rng.integers(0, n, nwin * cap).astype(np.int32)
+    ans = rng.integers(0, 2, nwin * cap).astype(np.uint8) | (rng.random(nwin * cap) < 0.9).astype(np.uint8)
+    cap8 = (cap + 7) // 8
+    packed = np.concatenate([np.packbits(ans[w * cap: (w + 1) * cap], bitorder="little")[:cap8] for w in range(nwin)])
+    t = lambda a: torch.from_numpy(a).to(dev)
+    ct = t(counts)
+    e.P = nwin   # the combine takes the window count from counts
+    want = e.combine_windows(t(ans), t(slot), ct, cap, n).cpu().numpy()
+    got = e.combine_windows_packed(t(packed), t(slot), ct, cap, n).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    assert (want == 0).any() and (want == 1).any()
+    e.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -202,7 +235,7 @@ def test_torch_distributed_world1(pkg, oracle):
             f.close()
         # the overlapped insert + include? step (async RCCL sends beside the kernels), through
         # the window route, the contiguous route, and the overflow fallback
-        for kw, cap in (({}, None), ({"windows": False}, None), ({}, 5)):
+        for kw, cap in (({}, None), ({"windows": False}, None), ({}, 5), ({"pack_answers": False}, None)):
             f = D.PartitionedFilter(m, k, block_log2=16, **kw)
             if cap is not None:
                 f._cap = lambda n, c=cap: c
