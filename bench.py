@@ -174,6 +174,18 @@ def prefill_random(f, m: int, k: int, rank: int, host_copy: bool = True):
     return host
 
 
+def auto_mode(world: int, m: int, k: int) -> str:
+    """single at N = 1; replicated at N = 2 for a filter that fits one GPU, where one xGMI
+    link carries the whole exchange: the replicated step moves ~10 B per key once (key bytes +
+    a length byte) against ~24 B per key out and back for the partitioned one, and its extra
+    compute (each replica hashes both batches) is what the partitioned owner-side sort costs
+    anyway; partitioned from N = 4 on, where the replicas' N-fold insert work loses."""
+    if world == 1:
+        return "single"
+    reach_bytes = (min(m, k * 0xFFFFFFFF + 1) + 7) // 8
+    return "replicated" if world == 2 and reach_bytes <= (64 << 30) else "partitioned"
+
+
 def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto",
                 overlap: bool = True):
     n, p, batch, prefill = CONFIGS[name]
@@ -185,8 +197,14 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     pf = None
     host_bits = None
     if mode == "auto":
-        mode = "single" if D.world == 1 else "partitioned"
-    if mode == "single":
+        mode = auto_mode(D.world, m, k)
+    rf = None
+    if mode == "replicated":   # every rank a whole replica: include? local, inserts all-gathered
+        rf = pkg.distributed.ReplicatedFilter(m, k, device=dev)
+        f = rf.filter
+        if prefill == "random":   # identical replicas: the same bits on every rank
+            prefill_random(f, m, k, 0, host_copy=f.device_bytes < (4 << 30))
+    elif mode == "single":
         f = pkg.Filter(m, k, device=D.local)
         if prefill == "random":
             host_bits = prefill_random(f, m, k, D.rank, host_copy=f.device_bytes < (4 << 30))
@@ -205,14 +223,18 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
 
     def insert(bt):
         ikb, iko = bt[0]
-        if pf is None:
+        if rf is not None:
+            rf.insert_many_dev(ikb, iko, batch)
+        elif pf is None:
             f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, stream=sp)
         else:
             pf.insert_many_dev(ikb, iko, batch)
 
     def include(bt):
         pkb, pko = bt[1]
-        if pf is None:
+        if rf is not None:
+            out.copy_(rf.include_many_dev(pkb, pko, batch))
+        elif pf is None:
             f.include_many_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), stream=sp)
         else:
             out.copy_(pf.include_many_dev(pkb, pko, batch))
@@ -329,6 +351,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         pf.close()
     else:
         f.close()
+    res["mode"] = mode
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
@@ -386,13 +409,13 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
-    ap.add_argument("--mode", default="auto", choices=["auto", "single", "partitioned"],
-                    help="auto: single GPU at N=1, partitioned over the ranks at N>1")
+    ap.add_argument("--mode", default="auto", choices=["auto", "single", "partitioned", "replicated"],
+                    help="auto: single GPU at N=1, replicated at N=2 (filter fits one GPU), partitioned from N=4")
     ap.add_argument("--no-overlap", action="store_true",
                     help="partitioned: run insert then include? as separate calls (no exchange overlap)")
     args = ap.parse_args()
 
-    D = Dist(need_group=(args.mode == "partitioned"))
+    D = Dist(need_group=(args.mode in ("partitioned", "replicated")))
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
                                   mode=args.mode, overlap=not args.no_overlap)
@@ -438,9 +461,11 @@ def main():
                                "include_many? per step (50%% members)" % (args.config, n, p, main_res["m"],
                                                                           main_res["k"], batch, batch),
                    "global_batch": 2 * batch * D.world,
-                   "parallelism": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key batches "
-                                  "routed to owner GPUs by RCCL all-to-all)" % D.world
-                   if (D.world > 1 or args.mode == "partitioned") else "single GPU"},
+                   "parallelism": {"partitioned": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key "
+                                                  "batches routed to owner GPUs, grouped RCCL send/recv)" % D.world,
+                                   "replicated": "replicated x%d (include? local; insert batches all-gathered "
+                                                 "over RCCL, every replica applies every batch)" % D.world,
+                                   "single": "single GPU"}[main_res["mode"]]},
         "roofline": {"bound": "hbm", "kernel": dom_name,
                      "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK if achieved else None,

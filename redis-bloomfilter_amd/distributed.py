@@ -16,8 +16,9 @@ Two layouts (SURVEY §8 e):
 
 ``ReplicatedFilter`` — every rank holds the whole filter (read-mostly
     filters that fit one GPU).  include? is purely local (no collective);
-    insert all-gathers the packed key batches so every replica applies every
-    rank's inserts and the replicas stay byte-identical.
+    insert all-gathers the key bytes and key lengths (one byte per key while
+    keys fit 255 bytes) beside the rank's own insert, then applies the other
+    ranks' batches as one insert, so the replicas stay byte-identical.
 
 The per-rank compute goes through an *engine* with four primitives (route,
 shard_insert, shard_test, combine) plus the window forms of route and combine;
@@ -408,6 +409,25 @@ class PartitionedFilter:
         self.engine.close()
 
 
+def merge_gathered(gk: torch.Tensor, gl: torch.Tensor, sizes, max_b: int, max_n: int, skip: int):
+    """The all-gathered batches (rank r's key bytes at gk[r*max_b ..], its key lengths at
+    gl[r*max_n ..]; sizes[r] = (bytes, keys, max length)) except rank `skip`'s, as ONE packed
+    batch: (key bytes + 16 B slack, int64 offsets[n+1], n)."""
+    parts_b, parts_l = [], []
+    for r, (nb, cnt, _) in enumerate(sizes):
+        if r == skip or cnt == 0:
+            continue
+        parts_b.append(gk[r * max_b: r * max_b + nb])
+        parts_l.append(gl[r * max_n: r * max_n + cnt])
+    n = sum(int(x.numel()) for x in parts_l)
+    if n == 0:
+        return None, None, 0
+    kb = torch.cat(parts_b + [torch.zeros(16, dtype=torch.uint8, device=gk.device)])
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=gk.device)
+    torch.cumsum(torch.cat(parts_l).to(torch.int64), 0, out=offs[1:])
+    return kb, offs, n
+
+
 class ReplicatedFilter:
     """Every rank holds the whole filter; include? is local, insert is all-gathered."""
 
@@ -422,22 +442,39 @@ class ReplicatedFilter:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
-        sizes = torch.tensor([kb.numel(), n], dtype=torch.int64, device=self.device)
-        all_sizes = [torch.empty_like(sizes) for _ in range(self.P)]
-        dist.all_gather(all_sizes, sizes, group=self.group)
-        all_sizes = torch.stack(all_sizes).cpu().tolist()
-        max_b = max(s[0] for s in all_sizes)
-        max_n = max(s[1] for s in all_sizes)
+        """Every rank's batch reaches every replica: the key bytes and one length per key
+        (uint8 while every key fits 255 bytes, else int32) are all-gathered while this
+        rank's own batch is inserted, then the other ranks' batches go in as ONE insert
+        (one binned pass over the bitset).  OR is order-free, so the replicas end
+        byte-identical to one filter that took the batches in any order."""
+        z = torch.zeros(1, dtype=torch.int64, device=self.device)
+        lens = (ko[1: n + 1] - ko[:n]) if n else z[:0]
+        # (bytes, keys, longest key, first offset): one small all-gather, one host wait
+        sizes = torch.cat([ko[n: n + 1] - ko[0:1], z + n, lens.max().view(1) if n else z, ko[0:1]])
+        all_sizes = torch.empty(self.P * 4, dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(all_sizes, sizes, group=self.group)
+        all_sizes = all_sizes.view(self.P, 4).cpu().tolist()
+        nbytes, _, _, ko0 = all_sizes[dist.get_rank(self.group)]
+        all_sizes = [sz[:3] for sz in all_sizes]
+        max_b = max(max(sz[0] for sz in all_sizes), 1)
+        max_n = max(max(sz[1] for sz in all_sizes), 1)
+        ldt = torch.uint8 if max(sz[2] for sz in all_sizes) <= 255 else torch.int32
         kb_p = torch.zeros(max_b, dtype=torch.uint8, device=self.device)
-        kb_p[: kb.numel()] = kb
-        ko_p = torch.zeros(max_n + 1, dtype=torch.int64, device=self.device)
-        ko_p[: n + 1] = ko[: n + 1]
-        gk = [torch.empty_like(kb_p) for _ in range(self.P)]
-        go = [torch.empty_like(ko_p) for _ in range(self.P)]
-        dist.all_gather(gk, kb_p, group=self.group)
-        dist.all_gather(go, ko_p, group=self.group)
-        for (nbytes, cnt), k_t, o_t in zip(all_sizes, gk, go):
-            self.filter.insert_many_dev(k_t.data_ptr(), o_t.data_ptr(), cnt, stream=self._stream())
+        if nbytes:
+            kb_p[:nbytes] = kb[ko0: ko0 + nbytes]
+        ln_p = torch.zeros(max_n, dtype=ldt, device=self.device)
+        ln_p[:n] = lens.to(ldt)
+        gk = torch.empty(self.P * max_b, dtype=torch.uint8, device=self.device)
+        gl = torch.empty(self.P * max_n, dtype=ldt, device=self.device)
+        w1 = dist.all_gather_into_tensor(gk, kb_p, group=self.group, async_op=True)
+        w2 = dist.all_gather_into_tensor(gl, ln_p, group=self.group, async_op=True)
+        if n:   # own batch, beside the gather
+            self.filter.insert_many_dev(kb.data_ptr(), ko.data_ptr(), n, stream=self._stream())
+        w1.wait()
+        w2.wait()
+        ob, oo, on = merge_gathered(gk, gl, all_sizes, max_b, max_n, skip=dist.get_rank(self.group))
+        if on:
+            self.filter.insert_many_dev(ob.data_ptr(), oo.data_ptr(), on, stream=self._stream())
 
     def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
         out = torch.empty(n, dtype=torch.uint8, device=self.device)

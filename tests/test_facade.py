@@ -143,3 +143,29 @@ def test_fakeredis_ttl(pkg):
     assert r.ttl("j") == -1
     assert r.delete("j", "nope") == 1
     assert r.keys("*") == []
+
+
+def test_replicated_merge_gathered(pkg):
+    """distributed.merge_gathered: the all-gathered batches minus this rank's, as one packed
+    batch whose keys are exactly the other ranks' keys in rank order (CPU tensors)."""
+    import torch
+    D = pkg.distributed
+    batches = [["a", "bb", ""], [], ["ccc", "d" * 300], ["x"]]
+    max_b = max(max(sum(len(k) for k in b) for b in batches), 1)
+    max_n = max(len(b) for b in batches)
+    gk = torch.zeros(len(batches) * max_b, dtype=torch.uint8)
+    gl = torch.zeros(len(batches) * max_n, dtype=torch.int32)
+    sizes = []
+    for r, b in enumerate(batches):
+        raw = "".join(b).encode()
+        gk[r * max_b: r * max_b + len(raw)] = torch.tensor(list(raw), dtype=torch.uint8)
+        gl[r * max_n: r * max_n + len(b)] = torch.tensor([len(k) for k in b], dtype=torch.int32)
+        sizes.append((len(raw), len(b), max([len(k) for k in b], default=0)))
+    for skip in range(len(batches)):
+        kb, ko, n = D.merge_gathered(gk, gl, sizes, max_b, max_n, skip)
+        want = [k for r, b in enumerate(batches) if r != skip for k in b]
+        assert n == len(want)
+        o = ko.tolist()
+        got = [bytes(kb[o[j]: o[j + 1]].tolist()).decode() for j in range(n)]
+        assert got == want
+        assert kb.numel() == o[-1] + 16
