@@ -24,6 +24,21 @@ namespace {
 
 using namespace bfdev;
 
+// include? probe load policy (A/B knob, build-time): 0 plain, 1 non-temporal,
+// 2 relaxed agent-scope load (L1 bypass).  Random 4 B probes never hit L1.
+#ifndef BF_PROBE_LOAD
+#define BF_PROBE_LOAD 0
+#endif
+__device__ __forceinline__ uint32_t probe_load(const uint32_t* p) {
+#if BF_PROBE_LOAD == 1
+    return __builtin_nontemporal_load(p);
+#elif BF_PROBE_LOAD == 2
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    return *p;
+#endif
+}
+
 template <int OP, bool STAGED>
 __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uint32_t s, uint32_t L,
                                        uint64_t key, uint8_t* __restrict__ out8,
@@ -61,7 +76,7 @@ __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uin
                 if (i0 + c < e) {
                     const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + c);
                     sh[c] = (uint32_t)(o ^ 7u) & 31u;
-                    v[c] = g.bits[o >> 5];
+                    v[c] = probe_load(g.bits + (o >> 5));
                 }
             }
 #pragma unroll
