@@ -1,8 +1,11 @@
 #!/bin/bash
-# Build include? probe-load A/B variants of libbfhip.so (on the CPU host, before gpurun):
-#   ab_libs/pl<N>/libbfhip.so with -DBF_PROBE_LOAD=<N>; select one with BFHIP_LIB=...
+# Build A/B variants of libbfhip.so (on the CPU host, before gpurun):
+#   ab_libs/<name>/libbfhip.so built with the given -D flags; select one with BFHIP_LIB=...
 set -e
 cd "$(dirname "$0")/.."
-for v in 1 2; do
-    make -s -j8 -C redis-bloomfilter_amd/csrc OUTDIR=$PWD/ab_libs/pl$v EXTRA=-DBF_PROBE_LOAD=$v
+# Variants: NAME=FLAGS pairs, e.g. bash tools/build_ab_libs.sh pl1=-DBF_PROBE_LOAD=1 short0=-DBF_SHA1_SHORT=0
+for nv in "${@:-pl1=-DBF_PROBE_LOAD=1 pl2=-DBF_PROBE_LOAD=2}"; do
+    for pair in $nv; do
+        make -s -j8 -C redis-bloomfilter_amd/csrc OUTDIR=$PWD/ab_libs/${pair%%=*} EXTRA="${pair#*=}"
+    done
 done
