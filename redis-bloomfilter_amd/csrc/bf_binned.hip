@@ -834,6 +834,29 @@ __device__ __forceinline__ void for_region_probes(const uint32_t* __restrict__ c
     }
 }
 
+// bin_apply region access policy (A/B knob, build-time): 0 plain, 1 non-temporal loads and stores,
+// 2 non-temporal loads only, 3 non-temporal stores only.
+#ifndef BF_APPLY_NT
+#define BF_APPLY_NT 3
+#endif
+typedef uint32_t apply_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 apply_load(const uint4* p) {
+#if BF_APPLY_NT == 1 || BF_APPLY_NT == 2
+    const apply_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const apply_u32x4*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void apply_store(uint4* p, uint4 v) {
+#if BF_APPLY_NT == 1 || BF_APPLY_NT == 3
+    const apply_u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<apply_u32x4*>(p));
+#else
+    *p = v;
+#endif
+}
+
 template <uint32_t RLOG2, uint32_t LANES>
 __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
                                                           const uint32_t* __restrict__ level2,
@@ -863,7 +886,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     for (uint32_t c = 0; c < kPer; ++c) {
         const uint32_t v = c * LANES + t;
         old[c] = make_uint4(0, 0, 0, 0);
-        if (dense && v0 + v < nvec) old[c] = gv[v0 + v];
+        if (dense && v0 + v < nvec) old[c] = apply_load(gv + v0 + v);
     }
     for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
@@ -881,7 +904,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     for (uint32_t c = 0; c < kPer; ++c) {   // sparse: every touched vector's load issues before any store
         const uint32_t v = c * LANES + t;
         msk[c] = s_mask4[v];
-        if (!dense && v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) old[c] = gv[v0 + v];
+        if (!dense && v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) old[c] = apply_load(gv + v0 + v);
     }
     uint32_t fresh = 0;
 #pragma unroll
@@ -891,7 +914,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
             const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
                                 (msk[c].w & ~old[c].w);
             fresh |= fr;
-            gv[v0 + v] = make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z, old[c].w | msk[c].w);
+            apply_store(gv + v0 + v, make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z, old[c].w | msk[c].w));
             if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
         }
     }
