@@ -36,6 +36,19 @@
 using namespace bfdev;
 
 namespace {
+// Level-1 / level-2 staging stores (A/B knob, build-time bit mask): bit 0 non-temporal
+// level-1 stores (bin_front), bit 1 non-temporal level-2 stores (bin_mid).
+#ifndef BF_STAGE_NT
+#define BF_STAGE_NT 3
+#endif
+template <int BIT>
+__device__ __forceinline__ void stage_store(uint32_t* p, uint32_t v) {
+    if constexpr ((BF_STAGE_NT & BIT) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+}  // namespace
+
+namespace {
 
 constexpr int kTile = 1024;                   // lanes per workgroup of the front / mid passes
 constexpr int kStageVec = 16384 / 16;         // 16 KiB LDS key stage per 1024-key sub-tile
@@ -180,7 +193,7 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
         const uint64_t seg = key0 * k;
         const uint32_t tp = tk * k;
         for (uint32_t j = t; j < tp; j += kTile) {
-            level1[seg + j] = s_sorted[j];
+            stage_store<1>(level1 + seg + j, s_sorted[j]);
             if constexpr (KEYS) level1_key[seg + j] = s_key[j];
         }
         // the next tile's first LDS writes (staging, then s_sorted) follow barriers
@@ -770,7 +783,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         __syncthreads();
         const uint32_t out0 = wbase + f0;
         for (uint32_t j = t; j < f1 - f0; j += kTile) {
-            level2[out0 + j] = s_sorted[j];
+            stage_store<2>(level2 + out0 + j, s_sorted[j]);
             if constexpr (KEYS) level2_key[out0 + j] = s_key[j];
         }
         if (c + 1 < c_hi) {
