@@ -325,7 +325,12 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         "insert": {"op_ms": ins_ms, "keys_per_s": batch / (ins_ms / 1e3),
                    "path": "binned" if plan["binned"] else "direct",
                    "algo_bytes_per_key": (Lmean + 8 + 2 * bitset / batch) if plan["binned"]
-                   else (Lmean + 8 + 2 * k * GRANULE)},
+                   else (Lmean + 8 + 2 * k * GRANULE),
+                   # SURVEY §8(d)'s random-access model (L + 8 + 2kG) beside the streaming one
+                   # the binned path is bound by (L + 8 + 2 * bitset / batch): the fraction of
+                   # 8 TB/s each model gives the op's keys/s
+                   "frac_random_model": batch / (ins_ms / 1e3) * (Lmean + 8 + 2 * k * GRANULE) / HBM_PEAK,
+                   "frac_streaming_model": batch / (ins_ms / 1e3) * (Lmean + 8 + 2 * bitset / batch) / HBM_PEAK},
         "include": {"op_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
                     "path": "binned" if inc_binned else "direct",
                     "algo_bytes_per_key": (Lmean + 8 + 1 + bitset / batch) if inc_binned
@@ -337,15 +342,24 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     ib, io = to_host(*batches[0][0])
     pb, po = to_host(*batches[0][1])
     if want_host and pf is None:
-        # PCIe-inclusive rate of the host-pointer entry points (H2D keys + D2H answers).
+        # PCIe-inclusive rate of the host-pointer entry points (pageable numpy keys + uint64
+        # offsets in, answers out), after one warm-up call that sizes the pinned staging.
         torch.cuda.synchronize()
-        t = time.perf_counter()
         f.insert_many(ib, io)
-        t_ins = time.perf_counter() - t
-        t = time.perf_counter()
         f.include_many(pb, po)
-        t_inc = time.perf_counter() - t
-        res["host_api"] = {"insert_keys_per_s": batch / t_ins, "include_keys_per_s": batch / t_inc}
+        reps = 3
+        t = time.perf_counter()
+        for _ in range(reps):
+            f.insert_many(ib, io)
+        t_ins = (time.perf_counter() - t) / reps
+        t = time.perf_counter()
+        for _ in range(reps):
+            f.include_many(pb, po)
+        t_inc = (time.perf_counter() - t) / reps
+        res["host_api"] = {"insert_keys_per_s": batch / t_ins, "include_keys_per_s": batch / t_inc,
+                           "pcie_bytes_per_key": float(io[-1]) / batch + 4,
+                           "host_threads": int(os.environ.get("BFHIP_HOST_THREADS", "0")) or
+                           min(16, usable_cores())}
     del batches
     if pf is not None:
         pf.close()
@@ -355,33 +369,80 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
-def cpu_baseline(data, budget_s: float = 10.0):
-    """Oracle (C restatement, OpenMP) on the host cores, bounded sample of the same workload:
-    the first step's insert and include? batches, in 2^20-key chunks, passed over again
-    until ~budget_s of CPU work is done."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O   # the checker, here the timed CPU baseline ("port")
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def usable_cores() -> int:
+    """CPUs this process can keep busy: its affinity mask, capped by the cgroup CPU quota
+    (a gpurun box exposes all 256 CPUs of the host in the mask but grants one GPU's share,
+    16, through cpu.max) and by OMP_NUM_THREADS when set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def _time_oracle(orc, data, threads: int, budget_s: float):
+    """Keys/s of the oracle's insert + include? over the first step's batches (2^20-key
+    chunks, passed over again until ~budget_s of work is done) on `threads` OpenMP threads."""
     ib, io, pb, po, host_bits, m, k = data
-    orc = O.COracle()
-    threads = max(1, min(16, os.cpu_count() or 1))
     bits = host_bits.copy() if host_bits is not None else orc.new_bitset(m, k)
     done = 0
-    t0 = time.perf_counter()
     n_total = len(io) - 1
-    chunk = 1 << 20
+    chunk = 1 << 20 if threads > 1 else 1 << 17
     i = 0
+    t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         j = min(i + chunk, n_total)
-        sub_o = io[i:j + 1]
-        orc.insert_many_omp(bits, m, k, ib, sub_o, threads)
-        sub_p = po[i:j + 1]
-        orc.include_many_omp(bits, m, k, pb, sub_p, threads)
+        orc.insert_many_omp(bits, m, k, ib, io[i:j + 1], threads)
+        orc.include_many_omp(bits, m, k, pb, po[i:j + 1], threads)
         done += 2 * (j - i)
         i = j if j < n_total else 0
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "keys/s", "cores": threads, "kind": "port",
+    return done / dt, done, dt
+
+
+def cpu_baseline(data, budget_s: float = 10.0):
+    """The oracle (oracle/bf_oracle.c: the same SHA-1, offsets and byte-order bitset, OpenMP)
+    on the host, on a bounded sample of the same workload: all the cores this process may
+    use (usable_cores(): a gpurun box grants one GPU 16 of its host's cores) and one core.  The
+    reference's own drivers need ruby + redis-server, probed here and recorded."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O   # the checker, here the timed CPU baseline ("port")
+    orc = O.COracle()
+    cores = usable_cores()
+    v_all, d_all, t_all = _time_oracle(orc, data, cores, budget_s)
+    v_one, d_one, t_one = _time_oracle(orc, data, 1, budget_s)
+    import shutil
+    tools = {t: shutil.which(t) for t in ("ruby", "redis-server", "lua")}
+    n_total = len(data[1]) - 1
+    return {"value": v_all, "unit": "keys/s", "cores": cores, "kind": "port",
+            "single_core": {"value": v_one, "cores": 1,
+                            "sample": "%d insert + %d include? keys, %.1f s" % (d_one // 2, d_one // 2, t_one)},
+            "cpu_model": cpu_model(), "machine_cpus": os.cpu_count(),
             "sample": "%d insert + %d include? keys (the first step's %d-key batches, repeated) on the same "
-                      "prefilled filter, oracle/bf_oracle.c with OpenMP, %.1f s" % (done // 2, done // 2, n_total, dt)}
+                      "prefilled filter, oracle/bf_oracle.c with OpenMP on %d threads, %.1f s"
+                      % (d_all // 2, d_all // 2, n_total, cores, t_all),
+            "reference_drivers": {"tools": tools, "timed": all(tools[t] for t in ("ruby", "redis-server")),
+                                  "note": "the reference ruby/lua drivers (bf_100_000_flat.rb shape) need ruby + "
+                                          "redis-server; absent on this box, so only their published "
+                                          "README.md:80-95 numbers are quoted"}}
 
 
 def load_traffic(workload: str, kernel: str):

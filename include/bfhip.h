@@ -6,7 +6,11 @@
  * returns an int status (BF_OK = 0).  No exceptions cross the ABI.  The
  * library owns device memory and streams; the caller owns every buffer it
  * passes (read/written during the call only).  Calls on one handle are
- * serialised by an internal mutex; different handles are independent.
+ * serialised by an internal mutex, and so is their device work, across
+ * streams too: a call whose launches go to a different stream than the
+ * previous call's waits (on the device, hipStreamWaitEvent) for that call's
+ * last launch, because the launches share the bitset and the handle's
+ * scratch.  Different handles are independent.
  *
  * Reference interface each entry point replaces (paths relative to the
  * reference repository kontera-technologies/redis-bloomfilter @ 1.1.2):
@@ -119,7 +123,10 @@ int  bf_clear(bf_handle* h);
 int  bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out);
 int  bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode);
 
-/* ---- device-resident API (device pointers; async on `stream`) */
+/* ---- device-resident API (device pointers; async on `stream`).
+ *      Key bytes: the kernels read d_key_bytes in aligned 16-byte vectors, so the buffer
+ *      must stay readable up to 16 bytes past d_key_bytes + d_offsets[n] (pad the
+ *      allocation by 16 bytes; the host-pointer API does this in its staging copy). */
 int  bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets,
                         uint64_t n, uint32_t* d_any_new /* nullable: OR-ed with 1 when a bit flips */,
                         uint8_t* d_per_key_new /* nullable */, void* stream);
@@ -272,7 +279,10 @@ int  bf_lua_index(double entries, uint64_t count, uint32_t* layer);
  *      Errors read back through bf_last_error(NULL). */
 int  bf_indexes(const uint8_t* key, uint64_t len, uint64_t m_bits, uint32_t k, uint64_t* out);
 
-/* ---- sizing helpers with the facade's exact semantics (bloomfilter.rb:50-58) */
+/* ---- sizing helpers with the facade's exact semantics (bloomfilter.rb:50-58).
+ *      bf_optimal_m returns BF_OPTIMAL_M_INVALID when the result is not a finite int64
+ *      (error_rate 0 -> Infinity: the reference raises FloatDomainError at Float#round). */
+#define BF_OPTIMAL_M_INVALID INT64_MIN
 int64_t bf_optimal_m(double n, double error_rate);
 int64_t bf_optimal_k(int64_t n, int64_t m_bits);     /* Integer n: floor division, 0 -> 1 */
 

@@ -64,7 +64,7 @@ def add(redis, key: str, entries, precision, data, expire=None) -> bool:
             found = False
     if not found:                                                      # :48-54
         redis.incr(countkey)
-        if expire:
+        if expire is not None and expire is not False:   # tonumber(ARGV[4]) (add.lua:4): 0 is truthy in Lua
             redis.expire(lkey, expire)
     return not found
 

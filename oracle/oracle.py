@@ -183,7 +183,7 @@ class RubyDriverRestatement:
         changed = [self.redis.setbit(name, i, 1)
                    for i in py_indexes(key, self.options["bits"], self.options["hashes"])]
         found = 0 not in changed
-        if not found and expire:
+        if not found and expire is not None and expire is not False:   # Ruby truthiness: 0 expires
             self.redis.expire(name, expire)
 
 

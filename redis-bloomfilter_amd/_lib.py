@@ -171,8 +171,14 @@ def version() -> str:
     return load().bf_version().decode()
 
 
+BF_OPTIMAL_M_INVALID = -(1 << 63)
+
+
 def optimal_m(n, error_rate) -> int:
-    return int(load().bf_optimal_m(float(n), float(error_rate)))
+    m = int(load().bf_optimal_m(float(n), float(error_rate)))
+    if m == BF_OPTIMAL_M_INVALID:   # Infinity/NaN: Float#round raises FloatDomainError in Ruby
+        raise FloatingPointError("FloatDomainError: optimal_m(%r, %r) is not finite" % (n, error_rate))
+    return m
 
 
 def optimal_k(n: int, m: int) -> int:

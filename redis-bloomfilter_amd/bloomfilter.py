@@ -120,8 +120,13 @@ class Bloomfilter:
         return h
 
     # bloomfilter.rb:61-73 (+ the batched delegators the hip driver adds)
+    def _expire(self, expire):
+        """``expire || @options[:default_expire]`` (bloomfilter.rb:62): only nil and false fall
+        back to the default — 0 is truthy in Ruby and is passed on (EXPIRE key 0 deletes it)."""
+        return self.options["default_expire"] if expire is None or expire is False else expire
+
     def insert(self, data, expire=None):
-        return self.driver.insert(data, expire or self.options["default_expire"])
+        return self.driver.insert(data, self._expire(expire))
 
     def include(self, key) -> bool:
         return self.driver.include(key)
@@ -132,7 +137,7 @@ class Bloomfilter:
         return self.driver.clear()
 
     def insert_many(self, keys, expire=None):
-        expire = expire or self.options["default_expire"]
+        expire = self._expire(expire)
         if hasattr(self.driver, "insert_many"):
             return self.driver.insert_many(keys, expire)
         for k in keys:   # looping fallback for drivers without a batch path

@@ -6,15 +6,20 @@
 #include "bfhip.h"
 #include "bf_internal.h"
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
-#include <vector>
 #include <vector>
 
 #define BFHIP_VERSION_STR "bfhip 0.1.0 (gfx950; redis-bloomfilter 1.1.2 ruby-driver layout)"
@@ -23,20 +28,111 @@ namespace {
 
 thread_local std::string g_create_error;
 
+// A fork-join pool for the host side of the host-pointer calls: the offsets scan and the
+// staging copies into pinned memory are memory-bandwidth work that one core cannot feed
+// to PCIe (r01: 4-5e8 keys/s behind a single memcpy thread).  Workers start on first use;
+// the calling thread takes parts too.
+class HostPool {
+public:
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    void start(unsigned n) {
+        if (!th_.empty() || n <= 1) return;
+        for (unsigned i = 1; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    // fn(p) for every p < parts; returns when all are done.
+    void run(unsigned parts, const std::function<void(unsigned)>& fn) {
+        if (parts <= 1 || th_.empty()) {
+            for (unsigned p = 0; p < parts; ++p) fn(p);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            parts_ = parts;
+            next_.store(0);
+            active_ = (unsigned)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return active_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void work() {
+        for (unsigned p; (p = next_.fetch_add(1)) < parts_;) (*fn_)(p);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            lk.unlock();
+            work();
+            lk.lock();
+            if (--active_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* fn_ = nullptr;
+    unsigned parts_ = 0, active_ = 0;
+    std::atomic<unsigned> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Host threads for the staging work: BFHIP_HOST_THREADS, else the CPUs this process may run
+// on (its affinity mask, capped by the cgroup CPU quota), at most 16 — past that the copies
+// saturate host memory bandwidth.
+unsigned host_threads() {
+    if (const char* v = getenv("BFHIP_HOST_THREADS"))
+        if (*v) return std::max(1u, (unsigned)strtoul(v, nullptr, 10));
+    cpu_set_t set;
+    unsigned n = 1;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = (unsigned)CPU_COUNT(&set);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long long period = 0;
+        if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period)
+            n = std::min<unsigned>(n, (unsigned)std::max(1ull, (strtoull(q, nullptr, 10) + period - 1) / period));
+        fclose(f);
+    }
+    return std::max(1u, std::min(16u, n));
+}
+
+// One staging slot of the host-pointer pipeline: pinned host + device buffers for a chunk's
+// key bytes, its uint32 relative offsets (widened on the device) and its per-key results.
 struct Slot {
-    uint8_t*  h_keys = nullptr;   // pinned
-    uint64_t* h_off = nullptr;    // pinned, cap_keys + 1
-    uint8_t*  h_out = nullptr;    // pinned, cap_keys (per-key bytes) or cap_keys*k*8 (indexes)
+    uint8_t*  h_keys = nullptr;    // pinned, cap_bytes + 16
+    uint32_t* h_off = nullptr;     // pinned, cap_keys + 1
+    uint8_t*  h_out = nullptr;     // pinned, out_cap
     uint8_t*  d_keys = nullptr;
+    uint32_t* d_off32 = nullptr;
     uint64_t* d_off = nullptr;
     uint8_t*  d_out = nullptr;
-    uint64_t  cap_bytes = 0;
-    hipEvent_t done = nullptr;
+    uint64_t  cap_bytes = 0, cap_keys = 0, out_cap = 0;
+    hipEvent_t h2d = nullptr;      // the chunk's inputs are on the device (copy stream)
+    hipEvent_t done = nullptr;     // the chunk's kernels and result copy are done (compute stream)
     // pending result copy-out
     bool      busy = false;
     uint8_t*  user_out = nullptr;
     uint64_t  out_bytes = 0;
 };
+constexpr int kSlots = 3;   // host staging of chunk c+2 || H2D of c+1 || kernels of c
 
 }  // namespace
 
@@ -65,9 +161,11 @@ struct bf_handle {
     uint32_t bin_region_log2 = 19;   // preferred region (LDS image) size of the apply pass
     void* d_bin_scratch = nullptr;   // digests, probe arrays and histograms of one binned launch
     uint64_t bin_scratch_cap = 0;
-    uint64_t cap_keys = 0, cap_bytes = 0;
-    Slot slot[2];
+    uint64_t cap_keys = 0, cap_bytes = 0;   // chunk limits of the host-pointer calls (bf_config)
+    Slot slot[kSlots];
     bool staging_ready = false;
+    hipStream_t copy_stream = nullptr;      // H2D of the host-pointer pipeline
+    HostPool pool;
     uint32_t* d_flag = nullptr;
     unsigned long long* d_scan = nullptr;
     uint32_t* h_flag = nullptr;   // pinned
@@ -79,10 +177,36 @@ struct bf_handle {
     std::vector<BfMarks> prof_pending, prof_free;
     struct ProfAcc { std::string name; double ms; uint64_t launches; };
     std::vector<ProfAcc> prof_acc;
+    // cross-stream ordering (StreamOrder): the event after the handle's last device work
+    hipEvent_t order_ev = nullptr;
+    hipStream_t order_stream = nullptr;
+    bool order_valid = false;
     std::string err;
 };
 
 namespace {
+
+// Orders one handle's device work across streams.  Every entry point that touches the
+// bitset or the handle's scratch (the binned / sequential arenas, staging, routing
+// scratch) holds one of these around its launches: work arriving on a different stream
+// than the previous call's first waits for that call's last launch (hipStreamWaitEvent,
+// no host sync), so *_dev calls on two streams never race on the shared scratch or on
+// bin_apply's plain region stores.  Calls on one stream pay only an event record.
+struct StreamOrder {
+    bf_handle* h;
+    hipStream_t s;
+    StreamOrder(bf_handle* h_, hipStream_t s_) : h(h_), s(s_) {
+        if (h->order_valid && h->order_stream != s) (void)hipStreamWaitEvent(s, h->order_ev, 0);
+    }
+    ~StreamOrder() {
+        if (h->order_ev && hipEventRecord(h->order_ev, s) == hipSuccess) {
+            h->order_valid = true;
+            h->order_stream = s;
+        }
+    }
+    StreamOrder(const StreamOrder&) = delete;
+    StreamOrder& operator=(const StreamOrder&) = delete;
+};
 
 int set_err(bf_handle* h, int code, const char* fmt, ...) {
     char buf[512];
@@ -149,33 +273,55 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 int free_staging(bf_handle* h) {
     for (Slot& s : h->slot) {
         if (s.done) (void)hipEventSynchronize(s.done);
+        if (s.h2d) (void)hipEventSynchronize(s.h2d);
         if (s.h_keys) (void)hipHostFree(s.h_keys);
         if (s.h_off) (void)hipHostFree(s.h_off);
         if (s.h_out) (void)hipHostFree(s.h_out);
         if (s.d_keys) (void)hipFree(s.d_keys);
+        if (s.d_off32) (void)hipFree(s.d_off32);
         if (s.d_off) (void)hipFree(s.d_off);
         if (s.d_out) (void)hipFree(s.d_out);
         if (s.done) (void)hipEventDestroy(s.done);
+        if (s.h2d) (void)hipEventDestroy(s.h2d);
         s = Slot{};
     }
     h->staging_ready = false;
     return BF_OK;
 }
 
-int ensure_staging(bf_handle* h, uint64_t need_bytes) {
-    if (h->staging_ready && h->slot[0].cap_bytes >= need_bytes) return BF_OK;
+uint64_t pow2_at_least(uint64_t x, uint64_t lo) {
+    uint64_t p = lo;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Staging sized to the call (powers of two, grown on demand, never past the bf_config chunk
+// limits except for one key longer than batch_bytes): a one-key Ruby `insert` pins kilobytes,
+// not the full chunk size.
+int ensure_staging(bf_handle* h, uint64_t keys, uint64_t bytes, uint64_t out_bytes) {
+    const uint64_t want_keys = pow2_at_least(std::min(keys, h->cap_keys), 1024);
+    const uint64_t want_bytes = pow2_at_least(bytes, 1ull << 16);
+    const uint64_t want_out = pow2_at_least(out_bytes, 1024);
+    const Slot& cur = h->slot[0];
+    if (h->staging_ready && cur.cap_keys >= want_keys && cur.cap_bytes >= want_bytes && cur.out_cap >= want_out)
+        return BF_OK;
+    const uint64_t ck = std::max(want_keys, cur.cap_keys), cb = std::max(want_bytes, cur.cap_bytes),
+                   co = std::max(want_out, cur.out_cap);
     free_staging(h);
-    const uint64_t cap_bytes = round_up(std::max(h->cap_bytes, need_bytes), 4096) + 64;
-    const uint64_t outb = h->cap_keys;   // 1 byte per key; indexes use fewer keys per chunk
+    if (!h->copy_stream) HIPCHK(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
     for (Slot& s : h->slot) {
-        HIPCHK(h, hipHostMalloc((void**)&s.h_keys, cap_bytes, hipHostMallocDefault));
-        HIPCHK(h, hipHostMalloc((void**)&s.h_off, (h->cap_keys + 1) * sizeof(uint64_t), hipHostMallocDefault));
-        HIPCHK(h, hipHostMalloc((void**)&s.h_out, outb, hipHostMallocDefault));
-        HIPCHK(h, hipMalloc((void**)&s.d_keys, cap_bytes));
-        HIPCHK(h, hipMalloc((void**)&s.d_off, (h->cap_keys + 1) * sizeof(uint64_t)));
-        HIPCHK(h, hipMalloc((void**)&s.d_out, outb));
+        HIPCHK(h, hipHostMalloc((void**)&s.h_keys, cb + 16, hipHostMallocDefault));
+        HIPCHK(h, hipHostMalloc((void**)&s.h_off, (ck + 1) * sizeof(uint32_t), hipHostMallocDefault));
+        HIPCHK(h, hipHostMalloc((void**)&s.h_out, co, hipHostMallocDefault));
+        HIPCHK(h, hipMalloc((void**)&s.d_keys, cb + 16));
+        HIPCHK(h, hipMalloc((void**)&s.d_off32, (ck + 1) * sizeof(uint32_t)));
+        HIPCHK(h, hipMalloc((void**)&s.d_off, (ck + 1) * sizeof(uint64_t)));
+        HIPCHK(h, hipMalloc((void**)&s.d_out, co));
+        HIPCHK(h, hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming));
         HIPCHK(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-        s.cap_bytes = cap_bytes - 64;
+        s.cap_keys = ck;
+        s.cap_bytes = cb;
+        s.out_cap = co;
     }
     h->staging_ready = true;
     return BF_OK;
@@ -191,6 +337,11 @@ int retire_slot(bf_handle* h, Slot& s) {
     s.out_bytes = 0;
     return BF_OK;
 }
+
+constexpr uint64_t kParallelKeys = 1ull << 15;   // smaller calls stay on the calling thread
+
+// Splits [0, n) into `parts` near-equal ranges.
+inline uint64_t part_lo(uint64_t n, unsigned parts, unsigned p) { return n * p / parts; }
 
 int check_keys_args(bf_handle* h, const void* keys, const uint64_t* offsets, uint64_t n) {
     if (!h) return BF_EINVAL;
@@ -322,42 +473,75 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
     return BF_OK;
 }
 
-// Host-pointer driver: chunk, stage, launch, copy results back.
+// Host-pointer driver: chunk, stage, launch, copy results back, as a 3-slot pipeline over
+// two streams.  For chunk c: the host (a thread pool) copies its key bytes and its offsets,
+// as uint32 relative to the chunk's first key, into the slot's pinned buffers; the copy
+// stream moves them to the device; the compute stream waits for that (event), widens the
+// offsets and runs the op, then copies the per-key results back.  So the host staging of
+// chunk c+2, the H2D of chunk c+1 and the kernels of chunk c overlap, and every key costs
+// L + 4 bytes over PCIe.  The offsets are scanned once up front (non-decreasing, and the
+// longest key, which sizes the staging), in parallel.
 int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets, uint64_t n,
              uint8_t* out8, uint64_t* out64, uint8_t* any_new) {
     int rc = check_keys_args(h, keys, offsets, n);
     if (rc) return rc;
     if (op != BF_OP_INDEXES && h->shards > 1)
         return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter: use bf_route_dev");
-    for (uint64_t j = 0; j < n; ++j)
-        if (offsets[j + 1] < offsets[j]) return set_err(h, BF_EINVAL, "offsets must be non-decreasing (j=%llu)", (unsigned long long)j);
     if (any_new) *any_new = 0;
     if (n == 0) return BF_OK;
 
-    // Largest single key decides the minimum stage size.
+    const bool par = n >= kParallelKeys;
+    if (par) h->pool.start(host_threads());
+    const unsigned parts = par ? h->pool.size() * 4 : 1;
+    std::vector<uint64_t> part_max(parts, 0), part_bad(parts, UINT64_MAX);
+    h->pool.run(parts, [&](unsigned p) {
+        const uint64_t lo = part_lo(n, parts, p), hi = part_lo(n, parts, p + 1);
+        uint64_t mx = 0;
+        for (uint64_t j = lo; j < hi; ++j) {
+            const uint64_t a = offsets[j], b = offsets[j + 1];
+            if (b < a) {
+                part_bad[p] = j;
+                return;
+            }
+            mx = std::max(mx, b - a);
+        }
+        part_max[p] = mx;
+    });
     uint64_t maxkey = 0;
-    for (uint64_t j = 0; j < n; ++j) maxkey = std::max(maxkey, offsets[j + 1] - offsets[j]);
-    rc = ensure_staging(h, maxkey);
+    for (unsigned p = 0; p < parts; ++p) {
+        if (part_bad[p] != UINT64_MAX)
+            return set_err(h, BF_EINVAL, "offsets must be non-decreasing (j=%llu)", (unsigned long long)part_bad[p]);
+        maxkey = std::max(maxkey, part_max[p]);
+    }
+    if (maxkey >= (1ull << 31))
+        return set_err(h, BF_EINVAL, "a key of %llu bytes: host-pointer calls take keys below 2 GiB",
+                       (unsigned long long)maxkey);
+
+    const uint64_t out_per_key = op == BF_OP_INDEXES ? (uint64_t)h->k * 8 : 1;
+    // Chunks of n/8 keys (at least 2^20, at most batch_keys): enough chunks that the
+    // pipeline's fill and drain (one chunk's staging, one chunk's kernels) stay small.
+    const uint64_t cap_keys = op == BF_OP_INDEXES ? std::max<uint64_t>(1, h->cap_keys / (h->k * 8)) : h->cap_keys;
+    const uint64_t chunk_keys = std::min(n, std::min(cap_keys, std::max<uint64_t>(n / 8, 1ull << 20)));
+    const uint64_t total = offsets[n] - offsets[0];
+    rc = ensure_staging(h, chunk_keys, std::max(std::min(total, h->cap_bytes), maxkey), chunk_keys * out_per_key);
     if (rc) return rc;
 
-    uint64_t keys_per_chunk = h->cap_keys;
-    if (op == BF_OP_INDEXES) keys_per_chunk = std::max<uint64_t>(1, h->cap_keys / ((uint64_t)h->k * 8));
     const bool want_flag = (op == BF_OP_INSERT_FLAGS) && any_new;
     if (want_flag) HIPCHK(h, hipMemsetAsync(h->d_flag, 0, sizeof(uint32_t), h->stream));
 
     uint64_t i = 0;
     int c = 0;
     while (i < n) {
-        Slot& s = h->slot[c & 1];
+        Slot& s = h->slot[c % kSlots];
         rc = retire_slot(h, s);
         if (rc) return rc;
-        // chunk [i, j): at most keys_per_chunk keys and s.cap_bytes bytes
-        uint64_t jmax = std::min(n, i + keys_per_chunk);
+        // chunk [i, j): at most chunk_keys keys and s.cap_bytes bytes
+        const uint64_t jmax = std::min(n, i + std::min(chunk_keys, s.cap_keys));
         const uint64_t base = offsets[i];
         uint64_t j;
         if (offsets[jmax] - base <= s.cap_bytes) {
             j = jmax;
-        } else {  // binary search the last j with offsets[j] - base <= cap
+        } else {   // binary search the last j with offsets[j] - base <= cap (maxkey <= cap: j > i)
             uint64_t lo = i + 1, hi = jmax;
             while (lo < hi) {
                 const uint64_t mid = (lo + hi + 1) / 2;
@@ -367,15 +551,23 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
         }
         const uint64_t cn = j - i;
         const uint64_t nbytes = offsets[j] - base;
-        if (nbytes) memcpy(s.h_keys, keys + base, nbytes);
+        const unsigned cparts = (par && cn >= kParallelKeys) ? h->pool.size() * 2 : 1;
+        h->pool.run(cparts, [&](unsigned p) {
+            const uint64_t blo = part_lo(nbytes, cparts, p), bhi = part_lo(nbytes, cparts, p + 1);
+            if (bhi > blo) memcpy(s.h_keys + blo, keys + base + blo, bhi - blo);
+            const uint64_t tlo = part_lo(cn + 1, cparts, p), thi = part_lo(cn + 1, cparts, p + 1);
+            for (uint64_t t = tlo; t < thi; ++t) s.h_off[t] = (uint32_t)(offsets[i + t] - base);
+        });
         memset(s.h_keys + nbytes, 0, 16);
-        memcpy(s.h_off, offsets + i, (cn + 1) * sizeof(uint64_t));
-        HIPCHK(h, hipMemcpyAsync(s.d_keys, s.h_keys, round_up(nbytes + 1, 16), hipMemcpyHostToDevice, h->stream));
-        HIPCHK(h, hipMemcpyAsync(s.d_off, s.h_off, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(s.d_keys, s.h_keys, round_up(nbytes + 1, 16), hipMemcpyHostToDevice, h->copy_stream));
+        HIPCHK(h, hipMemcpyAsync(s.d_off32, s.h_off, (cn + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                 h->copy_stream));
+        HIPCHK(h, hipEventRecord(s.h2d, h->copy_stream));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, s.h2d, 0));
+        HIPCHK(h, bf_launch_widen_offsets(s.d_off32, s.d_off, cn + 1, h->stream));
         uint8_t* d_out8 = (op == BF_OP_INCLUDE || (op == BF_OP_INSERT_FLAGS && out8)) ? s.d_out : nullptr;
         uint64_t* d_out64 = (op == BF_OP_INDEXES) ? reinterpret_cast<uint64_t*>(s.d_out) : nullptr;
-        rc = launch_op(h, op, s.d_keys, s.d_off, (uint64_t)0 - base, cn, d_out8, d_out64,
-                       want_flag ? h->d_flag : nullptr, h->stream);
+        rc = launch_op(h, op, s.d_keys, s.d_off, 0, cn, d_out8, d_out64, want_flag ? h->d_flag : nullptr, h->stream);
         if (rc) return rc;
         s.out_bytes = 0;
         s.user_out = nullptr;
@@ -429,7 +621,8 @@ int run_dev(bf_handle* h, BfOp op, const uint8_t* d_keys, const uint64_t* d_offs
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     uint64_t bias = 0;
     const uint8_t* k16 = align_keys(d_keys, &bias);
-    return launch_op(h, op, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, pick_stream(h, stream));
+    StreamOrder so(h, pick_stream(h, stream));
+    return launch_op(h, op, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, so.s);
 }
 
 }  // namespace
@@ -476,8 +669,11 @@ int bf_indexes(const uint8_t* key, uint64_t len, uint64_t m_bits, uint32_t k, ui
 
 int64_t bf_optimal_m(double n, double p) {
     // lib/redis/bloomfilter.rb:50-52 — left-to-right IEEE double, Float#round (half away from zero).
-    const double v = (-1.0 * n) * std::log(p) / std::pow(std::log(2.0), 2.0);
-    return (int64_t)std::round(v);
+    // A non-finite or out-of-range result (error_rate 0 gives Infinity, where the reference
+    // raises FloatDomainError) returns BF_OPTIMAL_M_INVALID instead of an undefined cast.
+    const double v = std::round((-1.0 * n) * std::log(p) / std::pow(std::log(2.0), 2.0));
+    if (!std::isfinite(v) || v >= 9223372036854775808.0 || v < -9223372036854775808.0) return BF_OPTIMAL_M_INVALID;
+    return (int64_t)v;
 }
 
 int64_t bf_optimal_k(int64_t n, int64_t m) {
@@ -550,6 +746,10 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     }
     h->cap_keys = c.batch_keys ? c.batch_keys : (1ull << 22);
     h->cap_bytes = c.batch_bytes ? c.batch_bytes : (64ull << 20);
+    if (h->cap_bytes > (1ull << 31) || h->cap_keys > (1ull << 31)) {   // uint32 relative offsets per chunk
+        delete h;
+        return set_err(nullptr, BF_EINVAL, "batch_keys and batch_bytes must be <= 2^31");
+    }
 
     DeviceGuard dg(dev);
     auto fail = [&](int code, const char* what, hipError_t e) {
@@ -558,6 +758,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
         if (h->d_flag) (void)hipFree(h->d_flag);
         if (h->d_scan) (void)hipFree(h->d_scan);
         if (h->h_flag) (void)hipHostFree(h->h_flag);
+        if (h->order_ev) (void)hipEventDestroy(h->order_ev);
         if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
         return code;
@@ -565,6 +766,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     if (!dg.ok) return fail(BF_EDEVICE, "hipSetDevice", hipErrorInvalidDevice);
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(BF_EDEVICE, "hipStreamCreate", e);
+    if ((e = hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming)) != hipSuccess) return fail(BF_EDEVICE, "hipEventCreate", e);
     // Bitset memory kind (A/B knob): 0 coarse-grained hipMalloc, 1 uncached (MTYPE UC),
     // 2 fine-grained.
     h->mem_kind = env_u32("BFHIP_BITS_MEM", kDefaultMemKind);
@@ -604,6 +806,7 @@ int bf_destroy(bf_handle* h) {
     {
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceGuard dg(h->device);
+        if (h->order_valid) (void)hipEventSynchronize(h->order_ev);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         free_staging(h);
         if (h->g.bits) (void)hipFree(h->g.bits);
@@ -618,6 +821,8 @@ int bf_destroy(bf_handle* h) {
         (void)prof_harvest(h);   // waits for marks recorded on caller streams
         for (BfMarks& mk : h->prof_free)
             for (hipEvent_t e : mk.ev) (void)hipEventDestroy(e);
+        if (h->order_ev) (void)hipEventDestroy(h->order_ev);
+        if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -640,6 +845,7 @@ int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offse
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     const BfOp op = (any_new || per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
+    StreamOrder so(h, h->stream);
     int rc = run_host(h, op, key_bytes, offsets, n, per_key_new, nullptr, any_new);
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -652,6 +858,7 @@ int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, h->stream);
     return run_host(h, BF_OP_INCLUDE, key_bytes, offsets, n, out, nullptr, nullptr);
 }
 
@@ -661,6 +868,7 @@ int bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, h->stream);
     return run_host(h, BF_OP_INDEXES, key_bytes, offsets, n, nullptr, out, nullptr);
 }
 
@@ -669,6 +877,7 @@ int bf_clear(bf_handle* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, h->stream);
     HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
     if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 0, h->dirty_blocks, h->stream));   // the driver DELs the key
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -689,6 +898,7 @@ namespace {
 
 // Trimmed length of the first `max_bytes` bytes of the device bitset (Redis STRLEN after SETBITs).
 int device_trimmed_len(bf_handle* h, uint64_t* len_out) {
+    StreamOrder so(h, h->stream);
     HIPCHK(h, hipMemsetAsync(h->d_scan, 0, sizeof(unsigned long long), h->stream));
     HIPCHK(h, bf_launch_last_nonzero(h->g.bits, h->dev_bytes / 4, h->d_scan, h->stream));
     unsigned long long last = 0;
@@ -721,6 +931,7 @@ int import_bytes(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode, 
         if (buf[len - 1] & beyond)
             return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)max_bits);
     }
+    StreamOrder so(h, h->stream);
     if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 1, h->dirty_blocks, h->stream));
     if (mode == BF_IMPORT_REPLACE) {
         HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
@@ -806,6 +1017,7 @@ int bf_shard_export(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out)
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    if (h->order_valid) HIPCHK(h, hipEventSynchronize(h->order_ev));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (len) HIPCHK(h, hipMemcpy(buf, h->g.bits, len, hipMemcpyDeviceToHost));
     return BF_OK;
@@ -830,7 +1042,8 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
     BfBinPlan plan;
     if (h->binned_mode != 0 && bf_route_plan(n, h->k, h->shards, !h->route32, d_slot != nullptr, &plan)) {
@@ -887,7 +1100,8 @@ int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     BfBinPlan plan;
     if (n && !bf_route_plan(n, h->k, nwin, false, d_slot != nullptr, &plan))
         return set_err(h, BF_EINVAL, "batch of %llu keys at k=%u over %u windows exceeds one window-route pass",
@@ -910,7 +1124,8 @@ int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     // Binned when the routed probes' random line fills clearly exceed a streaming pass
     // over the shard (same policy and knob as the whole-filter insert).
     BfBinPlan plan;
@@ -961,7 +1176,8 @@ int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, 
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     // Binned like the shard insert: routed probes carry no early exit (all k arrive), so
     // one streaming pass over the shard beats a random line fill per probe once the
     // probes outnumber the shard's lines (same cost model and knob shape as the insert).
@@ -1014,7 +1230,8 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, s));
     bf_mark(mk, s, "combine");
@@ -1028,7 +1245,8 @@ int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* 
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows(d_bits, d_slot, window_cap, reinterpret_cast<const unsigned long long*>(d_counts),
                                         nwin, n, d_out, s));
@@ -1044,7 +1262,8 @@ int bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_pack_segments(d_bits, reinterpret_cast<const unsigned long long*>(d_seg), nseg, max_count,
                                       d_packed, s));
@@ -1059,7 +1278,8 @@ int bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const u
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
-    hipStream_t s = pick_stream(h, stream);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows_packed(d_packed, d_slot, window_cap,
                                                reinterpret_cast<const unsigned long long*>(d_counts), nwin, n, d_out,

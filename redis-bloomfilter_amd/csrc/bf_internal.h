@@ -183,3 +183,6 @@ hipError_t bf_launch_last_nonzero(const uint32_t* words, uint64_t nwords,
 
 // dst[i] |= src[i] for i < nwords (nwords multiple of 4, both 16-byte aligned).
 hipError_t bf_launch_or(uint32_t* dst, const uint32_t* src, uint64_t nwords, hipStream_t s);
+
+// out[i] = in[i] (uint32 -> uint64), i < count: the host-pointer calls' relative offsets.
+hipError_t bf_launch_widen_offsets(const uint32_t* in, uint64_t* out, uint64_t count, hipStream_t s);

@@ -399,6 +399,15 @@ __global__ __launch_bounds__(256) void combine_windows_packed_kernel(const uint8
         if (!((wb[i >> 3] >> (i & 7)) & 1u)) out[ws[i]] = 0;
 }
 
+// Host-pointer calls ship each chunk's offsets as uint32 relative to the chunk's first key
+// (4 B per key over PCIe instead of 8); the kernels take uint64.
+__global__ __launch_bounds__(256) void widen_offsets_kernel(const uint32_t* __restrict__ in,
+                                                            uint64_t* __restrict__ out, uint64_t count) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride)
+        out[i] = in[i];
+}
+
 uint32_t stream_grid(uint64_t nvec) {
     uint64_t g = (nvec + 255) / 256;
     if (g > 2048) g = 2048;   // grid-stride beyond 8 blocks per CU
@@ -538,5 +547,11 @@ hipError_t bf_launch_or(uint32_t* dst, const uint32_t* src, uint64_t nwords, hip
     if (nvec == 0) return hipSuccess;
     hipLaunchKernelGGL(or_kernel, dim3(stream_grid(nvec)), dim3(256), 0, s,
                        reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), nvec);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_widen_offsets(const uint32_t* in, uint64_t* out, uint64_t count, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(widen_offsets_kernel, dim3(stream_grid(count)), dim3(256), 0, s, in, out, count);
     return hipGetLastError();
 }

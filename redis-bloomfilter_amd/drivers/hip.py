@@ -86,14 +86,21 @@ class Hip:
     def key_name(self) -> str:
         return self.options["key_name"]
 
-    # -- TTL mirror
+    # -- TTL mirror.  The local deadline is taken on our clock BEFORE the EXPIRE / PTTL
+    # request, so it never falls after the server's; when it passes, the device copy is
+    # cleared and (write-through) the key is DELeted, so device and Redis agree from then
+    # on instead of drifting apart by the TTL's rounding (the key was due to vanish
+    # within one round trip anyway).
     def _expired(self) -> None:
         if self._deadline is not None and self._clock() >= self._deadline:
             self._deadline = None
             self.filter.clear()
+            if self._redis is not None and self.sync_mode == "write_through":
+                self._redis.delete(self.key_name)
 
     def _arm(self, expire) -> None:
-        self._deadline = self._clock() + float(expire)
+        t0 = self._clock()
+        self._deadline = t0 + float(expire)
         if self._redis is not None and self.sync_mode == "write_through":
             self._redis.expire(self.key_name, expire)
 
@@ -105,12 +112,14 @@ class Hip:
         """Insert a batch; returns True iff some bit flipped (the ruby driver's !found)."""
         self._expired()
         buf, offs = _keys.pack(keys)
-        want = bool(expire) or (self._redis is not None and self.sync_mode == "write_through")
+        # ruby.rb:62 `if !found && expire`: any expire but nil/false counts, 0 included
+        armed = expire is not None and expire is not False
+        want = armed or (self._redis is not None and self.sync_mode == "write_through")
         any_new, _ = self.filter.insert_many(buf, offs, any_new=want)
         if any_new:
             if self._redis is not None and self.sync_mode == "write_through":
                 self.flush()
-            if expire:
+            if armed:
                 self._arm(expire)
         return bool(any_new) if want else None
 
@@ -161,9 +170,15 @@ class Hip:
             return
         self.filter.import_redis(bytes(data), BF_IMPORT_REPLACE)
         self.filter.dirty_ranges(clear=True)   # device == Redis now
-        ttl = self._redis.ttl(self.key_name) if hasattr(self._redis, "ttl") else -1
+        t0 = self._clock()
+        if hasattr(self._redis, "pttl"):   # milliseconds: no whole-second rounding
+            ttl = self._redis.pttl(self.key_name)
+            ttl = ttl / 1000.0 if ttl is not None and ttl > 0 else -1
+        else:
+            ttl = self._redis.ttl(self.key_name) if hasattr(self._redis, "ttl") else -1
+            ttl = ttl - 1 if ttl is not None and ttl > 0 else -1   # TTL rounds up
         if ttl is not None and ttl > 0:
-            self._deadline = self._clock() + ttl
+            self._deadline = t0 + ttl
 
     def _read_key(self):
         """GET, or GETRANGE chunks for a key longer than ``chunk_bytes``."""

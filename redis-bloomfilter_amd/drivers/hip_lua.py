@@ -16,7 +16,8 @@ alone until ``flush()``.
 """
 from __future__ import annotations
 
-from typing import Iterable, List
+import time
+from typing import Dict, Iterable, List
 
 import numpy as np
 
@@ -39,6 +40,10 @@ class HipLua:
         self.entries, self.precision = float(entries), float(precision)
         self.filter = LuaFilter(self.entries, self.precision, device=options.get("device", -1))
         self._redis = None
+        # TTL mirror per layer key (add.lua:51-53 EXPIREs the layer an item went into): the
+        # deadline is taken before the EXPIRE request, so it never falls after the server's
+        self._clock = options.get("clock", time.monotonic)
+        self._deadlines: Dict[int, float] = {}
 
     @property
     def redis(self):
@@ -61,14 +66,28 @@ class HipLua:
     def insert(self, data, expire=None):
         return self.insert_many([data], expire)
 
+    def _expired(self) -> None:
+        """Layers whose mirrored TTL passed are gone in Redis: empty them on the device too
+        (the count key has no TTL and stays, as in Redis)."""
+        now = self._clock()
+        for n in [n for n, t in self._deadlines.items() if now >= t]:
+            del self._deadlines[n]
+            self.filter.import_layer(n, b"")
+            if self._redis is not None and self.sync_mode == "write_through":
+                self._redis.delete(self._layer_key(n))
+
     def insert_many(self, keys: Iterable, expire=None) -> np.ndarray:
         """Insert in order, as one EVALSHA per key would; returns each key's INCR flag."""
+        self._expired()
         buf, offs = _keys.pack(keys)
         pk, touched = self.filter.insert_many(buf, offs)
         if touched and self._redis is not None and self.sync_mode == "write_through":
             self._write(touched)
-            if expire:
-                for n in touched:
+        if touched and expire is not None and expire is not False:   # add.lua:51 tonumber(ARGV[4]): 0 is truthy
+            t0 = self._clock()
+            for n in touched:
+                self._deadlines[n] = t0 + float(expire)
+                if self._redis is not None and self.sync_mode == "write_through":
                     self._redis.expire(self._layer_key(n), expire)
         return pk.astype(bool)
 
@@ -77,12 +96,14 @@ class HipLua:
         return bool(self.include_many([key])[0])
 
     def include_many(self, keys: Iterable) -> np.ndarray:
+        self._expired()
         buf, offs = _keys.pack(keys)
         return self.filter.include_many(buf, offs).astype(bool)
 
     # -- lua.rb:28-30
     def clear(self):
         self.filter.clear()
+        self._deadlines.clear()
         if self._redis is not None:
             for k in self._redis.keys("%s:*" % self.key_name):
                 self._redis.delete(k)
@@ -105,14 +126,19 @@ class HipLua:
         if self._redis is None:
             return
         self.filter.clear()
+        self._deadlines.clear()
         raw = self._redis.get("%s:count" % self.key_name)
         count = int(raw) if raw is not None else 0
         self.filter.count = count
         if count:
             for n in range(1, lua_index(self.entries, count) + 1):
+                t0 = self._clock()
+                pttl = self._redis.pttl(self._layer_key(n)) if hasattr(self._redis, "pttl") else -1
                 data = self._redis.get(self._layer_key(n))
                 if data:
                     self.filter.import_layer(n, bytes(data))
+                    if pttl is not None and pttl > 0:
+                        self._deadlines[n] = t0 + pttl / 1000.0
 
     def close(self):
         self.filter.close()

@@ -209,6 +209,16 @@ class FakeRedis:
                 return -1
             return int(math.ceil(exp - self._clock() - 1e-9))
 
+    def pttl(self, name) -> int:
+        k = self._key(name)
+        with self._lock:
+            if not self._alive(k):
+                return -2
+            exp = self._exp.get(k)
+            if exp is None:
+                return -1
+            return int(math.ceil((exp - self._clock()) * 1000 - 1e-6))
+
     def persist(self, name) -> bool:
         k = self._key(name)
         with self._lock:

@@ -124,7 +124,7 @@ class Redis
         if changed
           flush if @redis && @sync == :write_through
           if expire
-            @deadline = now + expire
+            @deadline = now + expire   # taken before EXPIRE: never after the server's deadline
             @redis.expire(@options[:key_name], expire) if @redis && @sync == :write_through
           end
         end
@@ -199,15 +199,18 @@ class Redis
         mem.put_bytes(0, str)
         check(HipFFI.bf_import_redis(@handle, mem, str.bytesize, HipFFI::BF_IMPORT_REPLACE))
         dirty_ranges(clear: true)   # device == Redis now
-        ttl = @redis.ttl(@options[:key_name])
-        @deadline = now + ttl if ttl.positive?
+        t0 = now
+        pttl = @redis.pttl(@options[:key_name])   # milliseconds: no whole-second rounding
+        @deadline = t0 + pttl / 1000.0 if pttl.positive?
       end
 
+      # The Redis string of the device filter (GET key_name after the same SETBITs).
       def export
         n = export_len
         buf = FFI::MemoryPointer.new(:uint8, [n, 1].max)
+        len = FFI::MemoryPointer.new(:uint64)
         check(HipFFI.bf_export_redis(@handle, buf, n, len))
-        buf.read_bytes(n)
+        buf.read_bytes(len.read_uint64)
       end
 
       protected
@@ -249,11 +252,14 @@ class Redis
         HipFFI.pack(keys)
       end
 
+      # The mirrored TTL passed: drop the device copy and (write-through) the key, so device
+      # and Redis agree from here on (the key was due to vanish within a round trip anyway).
       def expire_if_due
         return unless @deadline && now >= @deadline
 
         @deadline = nil
         check(HipFFI.bf_clear(@handle))
+        @redis.del(@options[:key_name]) if @redis && @sync == :write_through
       end
 
       def now

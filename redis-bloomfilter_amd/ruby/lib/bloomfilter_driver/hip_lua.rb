@@ -50,6 +50,7 @@ class Redis
         out = FFI::MemoryPointer.new(:pointer)
         check(HipLuaFFI.bf_lua_create(@entries, @precision, cfg, out), nil)
         @handle = FFI::AutoPointer.new(out.read_pointer, HipLuaFFI.method(:bf_lua_destroy))
+        @deadlines = {}   # layer => monotonic deadline of its mirrored TTL (add.lua:51-53)
       end
 
       def redis=(redis)
@@ -63,14 +64,19 @@ class Redis
       end
 
       def insert_many(keys, expire = nil)
+        expire_if_due
         buf, offs, n = HipFFI.pack(keys)
         flags = FFI::MemoryPointer.new(:uint8, [n, 1].max)
         mask = FFI::MemoryPointer.new(:uint64)
         check(HipLuaFFI.bf_lua_insert_many(@handle, buf, offs, n, flags, mask))
         touched = (0...64).select { |i| mask.read_uint64[i] == 1 }.map { |i| i + 1 }
-        if !touched.empty? && @redis && @sync == :write_through
-          write(touched)
-          touched.each { |l| @redis.expire(layer_key(l), expire) } if expire
+        write(touched) if !touched.empty? && @redis && @sync == :write_through
+        if !touched.empty? && expire
+          t0 = now   # before EXPIRE: never after the server's deadline
+          touched.each do |l|
+            @deadlines[l] = t0 + expire
+            @redis.expire(layer_key(l), expire) if @redis && @sync == :write_through
+          end
         end
         flags.read_array_of_uint8(n).map { |b| b == 1 }
       end
@@ -81,6 +87,7 @@ class Redis
       end
 
       def include_many?(keys)
+        expire_if_due
         buf, offs, n = HipFFI.pack(keys)
         out = FFI::MemoryPointer.new(:uint8, [n, 1].max)
         check(HipLuaFFI.bf_lua_include_many(@handle, buf, offs, n, out))
@@ -90,6 +97,7 @@ class Redis
       # lua.rb:28-30
       def clear
         check(HipLuaFFI.bf_lua_clear(@handle))
+        @deadlines.clear
         @redis&.keys("#{@options[:key_name]}:*")&.each { |k| @redis.del(k) }
       end
 
@@ -101,6 +109,7 @@ class Redis
       # Redis -> device layers and count (replace).
       def reload
         check(HipLuaFFI.bf_lua_clear(@handle))
+        @deadlines.clear
         count = @redis.get("#{@options[:key_name]}:count").to_i
         check(HipLuaFFI.bf_lua_set_count(@handle, count))
         return if count.zero?
@@ -108,16 +117,34 @@ class Redis
         idx = FFI::MemoryPointer.new(:uint32)
         check(HipLuaFFI.bf_lua_index(@entries, count, idx))
         (1..idx.read_uint32).each do |l|
+          t0 = now
+          pttl = @redis.pttl(layer_key(l))
           str = @redis.get(layer_key(l))
           next if str.nil? || str.empty?
 
           mem = FFI::MemoryPointer.new(:uint8, str.bytesize)
           mem.put_bytes(0, str)
           check(HipLuaFFI.bf_lua_import_layer(@handle, l, mem, str.bytesize))
+          @deadlines[l] = t0 + pttl / 1000.0 if pttl.positive?
         end
       end
 
       private
+
+      # Layers whose mirrored TTL passed are gone in Redis: empty them on the device too
+      # (the count key has no TTL and stays, as in Redis).
+      def expire_if_due
+        t = now
+        @deadlines.select { |_, d| t >= d }.each_key do |l|
+          @deadlines.delete(l)
+          check(HipLuaFFI.bf_lua_import_layer(@handle, l, nil, 0))
+          @redis.del(layer_key(l)) if @redis && @sync == :write_through
+        end
+      end
+
+      def now
+        Process.clock_gettime(Process::CLOCK_MONOTONIC)
+      end
 
       def layer_key(layer)
         "#{@options[:key_name]}:#{layer}"

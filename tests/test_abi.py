@@ -57,6 +57,89 @@ def test_ruby_ffi_binding_matches_header():
     assert layout == fields
 
 
+def _ruby_methods(src):
+    """(name, params, body lines with their line numbers) of every `def` in a Ruby file,
+    a method ending at the first `end` indented like its `def`."""
+    lines = src.splitlines()
+    out = []
+    i = 0
+    while i < len(lines):
+        m = re.match(r"^(\s*)def (?:self\.)?(\w+[?!=]?)\s*(?:\((.*)\))?\s*$", lines[i])
+        if not m:
+            i += 1
+            continue
+        indent, name, params = m.group(1), m.group(2), m.group(3) or ""
+        j = i + 1
+        while j < len(lines) and not re.match(r"^%send\b" % re.escape(indent), lines[j]):
+            j += 1
+        out.append((name, params, [(n + 1, lines[n]) for n in range(i + 1, j)]))
+        i = j + 1
+    return out
+
+
+def _split_args(s):
+    """Top-level comma split of an argument list."""
+    depth, cur, args = 0, "", []
+    for ch in s:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        if ch == "," and depth == 0:
+            args.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        args.append(cur.strip())
+    return args
+
+
+def _ffi_calls(line):
+    """(function, [args]) of every HipFFI / HipLuaFFI call on a line (balanced parentheses)."""
+    for m in re.finditer(r"\bHip(?:Lua)?FFI\.(bf_\w+)\(", line):
+        depth, k = 1, m.end()
+        while k < len(line) and depth:
+            depth += {"(": 1, ")": -1}.get(line[k], 0)
+            k += 1
+        yield m.group(1), _split_args(line[m.end():k - 1])
+
+
+def test_ruby_ffi_calls_are_well_formed():
+    """Every FFI call in the Ruby drivers passes as many arguments as the C prototype takes, and
+    every local it names is bound before the call in the same method (a parameter, an earlier
+    assignment or block parameter) or is a method of the drivers — Ruby is absent here, so this
+    static check stands in for running them (it catches e.g. an unbound `len`, a NameError)."""
+    arity = header_arity()
+    srcs = {fn: open(os.path.join(RUBY_DRIVERS, fn)).read() for fn in ("hip.rb", "hip_lua.rb", "hip_test.rb")}
+    methods = {name for src in srcs.values() for name, _, _ in _ruby_methods(src)}
+    literals = {"nil", "true", "false", "self"}
+    ncalls = 0
+    for fn, src in srcs.items():
+        for name, params, body in _ruby_methods(src):
+            bound = {p.strip().lstrip("*&").split("=")[0].split(":")[0].strip() for p in params.split(",") if p.strip()}
+            for lineno, line in body:
+                code = line.split(" #")[0]
+                for fname, args in _ffi_calls(code):
+                    ncalls += 1
+                    where = "%s:%d %s" % (fn, lineno, fname)
+                    assert fname in arity, where
+                    assert len(args) == arity[fname], (where, args)
+                    for a in args:
+                        root = re.match(r"^[a-z_]\w*", a)
+                        if not root or root.group(0) in literals:
+                            continue   # literal, constant, @ivar or expression on one of them
+                        assert root.group(0) in bound or root.group(0) in methods, \
+                            "%s: '%s' is not bound in %s" % (where, root.group(0), name)
+                # assignments (incl. `a, b = ...`) and block parameters bind for later lines
+                lhs = re.match(r"^\s*([a-z_][\w\s,]*?)\s*(?:\|\|)?=(?!=|~)", code)
+                if lhs:
+                    bound |= {v.strip() for v in lhs.group(1).split(",")}
+                for blk in re.findall(r"\|([^|]+)\|", code):
+                    bound |= {v.strip() for v in blk.split(",")}
+    assert ncalls >= 25
+
+
 def test_library_exports_every_symbol(pkg):
     lib = pkg._lib.load()
     for name in declared_functions():
@@ -81,6 +164,15 @@ def test_sizing_helpers_match_facade(pkg, oracle):
         m = pkg._lib.optimal_m(n, p)
         assert m == oracle.optimal_m(n, p) == pkg.Bloomfilter.optimal_m(n, p)
         assert pkg._lib.optimal_k(n, m) == oracle.optimal_k(n, m) == pkg.Bloomfilter.optimal_k(n, m)
+
+
+def test_optimal_m_non_finite_is_an_error(pkg):
+    """error_rate 0 -> Infinity: the reference raises FloatDomainError (Float#round); the ABI
+    returns BF_OPTIMAL_M_INVALID instead of casting Infinity to int64."""
+    assert pkg._lib.load().bf_optimal_m(100.0, 0.0) == pkg._lib.BF_OPTIMAL_M_INVALID
+    assert pkg._lib.load().bf_optimal_m(float("nan"), 0.01) == pkg._lib.BF_OPTIMAL_M_INVALID
+    with pytest.raises(FloatingPointError):
+        pkg._lib.optimal_m(100, 0.0)
 
 
 def test_invalid_arguments_without_gpu(pkg):

@@ -169,3 +169,43 @@ def test_replicated_merge_gathered(pkg):
         got = [bytes(kb[o[j]: o[j + 1]].tolist()).decode() for j in range(n)]
         assert got == want
         assert kb.numel() == o[-1] + 16
+
+
+class RecordingDriver(FakeRubyDriver):
+    def insert(self, data, expire):
+        self.last_expire = expire
+
+
+def test_expire_keeps_ruby_truthiness(pkg, registry):
+    """bloomfilter.rb:62 `expire || @options[:default_expire]`: nil and false take the default,
+    0 is truthy in Ruby and is passed on (ruby.rb:62 then EXPIREs with 0, deleting the key)."""
+    pkg.register_driver(RecordingDriver, "Recording")
+    bf = pkg.Bloomfilter(size=100, error_rate=0.01, driver="recording", default_expire=60)
+    for given, want in [(None, 60), (False, 60), (0, 0), (5, 5)]:
+        bf.insert("x", given)
+        assert bf.driver.last_expire == want, given
+
+
+def test_fakeredis_pttl_and_expire_zero(pkg):
+    now = [0.0]
+    r = pkg.FakeRedis(clock=lambda: now[0])
+    r.setbit("k", 3, 1)
+    assert r.pttl("k") == -1 and r.pttl("missing") == -2
+    r.expire("k", 2)
+    now[0] = 0.25
+    assert r.pttl("k") == 1750 and r.ttl("k") == 2
+    assert r.expire("k", 0) is True and r.exists("k") == 0   # EXPIRE 0 deletes, like Redis
+
+
+def test_oracle_restatements_expire_zero(pkg, O):
+    """The ruby.rb / add.lua restatements EXPIRE on 0 (Ruby and Lua truthiness)."""
+    import lua_oracle
+    r = pkg.FakeRedis()
+    ruby = O.RubyDriverRestatement({"bits": 9585, "hashes": 6, "key_name": "bf", "redis": r})
+    ruby.insert("asdlol", 0)
+    assert r.exists("bf") == 0 and ruby.include("asdlol") is False
+    ruby.insert("asdlol")
+    assert r.exists("bf") == 1 and r.ttl("bf") == -1 and ruby.include("asdlol") is True
+    lua_oracle.add(r, "lb", 1000, 0.01, "asdlol", 0)
+    assert r.exists("lb:1") == 0 and r.get("lb:count") == b"1"
+    assert lua_oracle.check(r, "lb", 1000, 0.01, "asdlol") is False

@@ -23,7 +23,8 @@ def dev_batch(pkg, torch, keys):
 
 
 @pytest.mark.parametrize("binned", ["0", "1"])
-@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20)])
+@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20),
+                                     (3834023350947, 13, 8, 20)])   # 200B@0.01 % over 8 GPUs (BASELINE configs[4])
 def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
     """binned=1 forces the owner-side binned insert (offsets front pass + region apply) and
     binned shard test, and takes the wave-aggregated owner ranks in the route; 0 the direct
@@ -97,7 +98,8 @@ def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
 
 
 @pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20),
-                                     (9585058377, 6, 2, 20), (191701167547, 13, 1, 20)])
+                                     (9585058377, 6, 2, 20), (191701167547, 13, 1, 20),
+                                     (3834023350947, 13, 8, 20)])   # 200B at P = 8: nh = 2
 def test_route_windows(pkg, oracle, m, k, P, b):
     """bf_route_windows_dev: window w = s*nh + hi holds exactly owner s's (key, local offset)
     pairs with local >> 32 == hi, as uint32 (the multiset bf_route_dev puts in segment s, split
@@ -111,6 +113,8 @@ def test_route_windows(pkg, oracle, m, k, P, b):
     nh = e.nh
     want_nh = max(1, -(-D.shard_local_bits(min(m, k * 0xFFFFFFFF + 1), P, 0, b) // (1 << 32)))
     assert nh == want_nh
+    if m == 3834023350947:
+        assert nh == 2
     nwin = P * nh
     rng = np.random.default_rng(17)
     keys = ["w%d" % int(v) for v in rng.integers(0, 10**12, 30000)]

@@ -50,6 +50,7 @@ REGIMES = [
     (9585058377, 6),               # 1B@1% (north star)
     (13 * 0xFFFFFFFF + 1, 13),     # m == reach (largest m still reduced)
     (191701167547, 13),            # 10B@0.01%: m > k*(2^32-1), modulo skipped
+    (3834023350947, 13),           # 200B@0.01% (BASELINE configs[4]): modulo skipped, same reach
     (2**40 + 3, 64),               # k = BF_MAX_K
     # float32-quotient modulo boundaries (m >= 2^17) and the float64 path below it
     (2**17 - 1, 13), (2**17, 13), (2**17 + 1, 64), (2**32 - 1, 13), (2**32, 6), (2**32 + 1, 64),
@@ -352,3 +353,28 @@ def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     extra = rand_keys(rng, 5_000, 0, 24)
     probe = (np.concatenate([ib, extra[0]]), np.concatenate([io, extra[1][1:] + io[-1]]))
     _insert_include_roundtrip(pkg, oracle, m, k, ins, probe)
+
+
+@pytest.mark.parametrize("binned", ["0", "1"])
+def test_config_200b(pkg, oracle, monkeypatch, binned):
+    """BASELINE configs[4]'s filter, 200B keys @ 0.01 %: m = 3,834,023,350,947, k = 13.  m is far
+    beyond k*(2^32-1), so ruby.rb:51's modulo never reduces and the offsets stay below
+    k*(2^32-1)+1: the device holds that 6.98 GB reachable prefix (1.46 % of m).  Offsets,
+    the Redis string (length + sha1) and include? answers against the oracle, through the
+    direct and the binned insert."""
+    monkeypatch.setenv("BFHIP_INSERT_BINNED", binned)
+    m = pkg.Bloomfilter.optimal_m(2 * 10**11, 0.0001)
+    k = pkg.Bloomfilter.optimal_k(2 * 10**11, m)
+    assert (m, k) == (3834023350947, 13)
+    rng = np.random.default_rng(RNG_SEED + 11)
+    ins = pkg.keys.pack_decimal(rng.integers(0, 2 * 10**11, size=4000))
+    probe = pkg.keys.pack_decimal(rng.integers(0, 2 * 10**11, size=4000))
+    ib, io = ins
+    pb, po = probe
+    probe = (np.concatenate([ib, pb]), np.concatenate([io, po[1:] + io[-1]]))
+    with pkg.Filter(m, k) as f:
+        assert f.reach_bits == k * 0xFFFFFFFF + 1
+        np.testing.assert_array_equal(f.indexes_many(ib, io), oracle.indexes_many(ib, io, m, k))
+    s, inc = _insert_include_roundtrip(pkg, oracle, m, k, ins, probe)
+    assert inc[:4000].all()
+    assert len(s) * 8 <= k * 0xFFFFFFFF + 1

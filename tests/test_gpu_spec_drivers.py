@@ -62,3 +62,35 @@ def test_should_add_ttl_when_requested(pkg, driver):   # spec:114-118 (the lua l
     bf = factory(pkg, {"size": 100, "error_rate": 0.01, "key_name": "__test_bf_%s" % driver}, driver, r)
     bf.insert("asdlolol", 120)
     assert r.ttl("__test_bf_%s%s" % (driver, ":1" if driver == "hip-lua" else "")) > 0
+
+
+@pytest.mark.parametrize("driver", DRIVERS)
+def test_insert_with_expire_zero(pkg, driver):
+    """insert(x, 0): 0 is truthy in Ruby (bloomfilter.rb:62, ruby.rb:62) and in Lua
+    (tonumber(ARGV[4]), add.lua:4, 51), so the reference EXPIREs the key with 0 and Redis
+    deletes it; include? then reads a missing key -> false.  A later insert without expire
+    rebuilds the key with no TTL.  Checked against the restatements on their own FakeRedis."""
+    import lua_oracle
+    import oracle as O
+    r, r_ref = pkg.FakeRedis(), pkg.FakeRedis()
+    name = "__test_bf_exp0_%s" % driver
+    bf = factory(pkg, {"size": 1000, "error_rate": 0.01, "key_name": name}, driver, r)
+    key = name + (":1" if driver == "hip-lua" else "")
+    bf.insert("asdlolol", 0)
+    assert r.exists(key) == 0
+    assert bf.include("asdlolol") is False
+    if driver == "hip":
+        ref = O.RubyDriverRestatement({"bits": bf.options["bits"], "hashes": bf.options["hashes"],
+                                       "key_name": name, "redis": r_ref})
+        ref.insert("asdlolol", 0)
+        assert ref.include("asdlolol") is False and r_ref.exists(name) == 0
+    elif driver == "hip-lua":
+        lua_oracle.add(r_ref, name, 1000, 0.01, "asdlolol", 0)
+        assert lua_oracle.check(r_ref, name, 1000, 0.01, "asdlolol") is False
+        assert r.get(name + ":count") == r_ref.get(name + ":count") == b"1"   # the count has no TTL
+    bf.insert("asdlolol")
+    assert bf.include("asdlolol") is True
+    assert r.exists(key) == 1 and r.ttl(key) == -1
+    if driver == "hip":
+        ref.insert("asdlolol")
+        assert r.get(name) == r_ref.get(name)

@@ -1,17 +1,26 @@
 #!/bin/bash
-# PMC passes over the bench's north-star workload (run on the GPU box from the
-# repo root).  One rocprofv3 run per counter group (gfx950: <= 4 TCC counters
-# per pass), kernel trace kept separate; outputs under gpurun_out/pmc_<tag>/.
-# Summarise with: python tools/pmc_summary.py gpurun_out/pmc_* > profiles/...
+# PMC passes over one bench workload (run on the GPU box from the repo root):
+#   bash tools/pmc_passes.sh [config] [tag] [passes...]
+# One rocprofv3 run per counter group (gfx950: <= 4 TCC, <= 8 SQ, <= 2 GRBM counters per
+# pass), kernel trace kept separate; outputs under gpurun_out/pmc_<tag>_<pass>/.
+# Summarise with: python tools/pmc_summary.py gpurun_out/pmc_<tag>_* --workload <config>
 export TMPDIR=/tmp
-CMD="python bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api"
-run() {   # tag, counters...
-    local tag=$1; shift
-    timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_${tag} -o run -- $CMD \
-        > gpurun_out/pmc_${tag}.log 2>&1
+CONFIG=${1:-nstar}
+TAG=${2:-$CONFIG}
+if [ $# -gt 2 ]; then shift 2; PASSES="$*"; else PASSES="rd wr dram valu"; fi
+run() {   # pass, counters...
+    local pass=$1; shift
+    timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_${TAG}_${pass} -o run -- \
+        python bench.py --config $CONFIG --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api \
+        > gpurun_out/pmc_${TAG}_${pass}.log 2>&1
 }
-run rd   TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_64B_sum &&
-run wr   TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_128B_sum &&
-run dram TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum &&
-run fs   FETCH_SIZE &&
-run ws   WRITE_SIZE
+for p in $PASSES; do
+    case $p in
+        rd)   run rd   TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_64B_sum ;;
+        wr)   run wr   TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_128B_sum ;;
+        dram) run dram TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum ;;
+        valu) run valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT ;;
+        fs)   run fs   FETCH_SIZE ;;
+        ws)   run ws   WRITE_SIZE ;;
+    esac || exit $?
+done

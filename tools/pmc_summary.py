@@ -24,6 +24,7 @@ KERNELS = {
     "bf_keys_kernel<INSERT>": re.compile(r"bf_keys_kernel<2>"),
     "bf_keys_kernel<INSERT_FLAGS>": re.compile(r"bf_keys_kernel<3>"),
     "bin_front": re.compile(r"bin_front_kernel"),
+    "bin_front_wide": re.compile(r"bin_front_wide_kernel"),
     "bin_mid": re.compile(r"bin_mid_kernel"),
     "bin_apply": re.compile(r"bin_apply_kernel"),
     "bin_test": re.compile(r"bin_test_kernel"),
@@ -69,6 +70,15 @@ def derive(c):
         out["FETCH_SIZE_bytes"] = g("FETCH_SIZE") * 1024
     if g("WRITE_SIZE") is not None:
         out["WRITE_SIZE_bytes"] = g("WRITE_SIZE") * 1024
+    # VALU (the hash-bound kernels): SQ_ACTIVE_INST_VALU counts quad-cycles (MI355X_MICROARCH.md
+    # per-instruction table), summed over every SIMD; GRBM_GUI_ACTIVE is summed over the 8 XCDs,
+    # so the kernel's cycles are GRBM_GUI_ACTIVE / 8.  valu_busy = the fraction of the 1024
+    # SIMDs' cycles spent issuing VALU instructions.
+    av, gui = g("SQ_ACTIVE_INST_VALU"), g("GRBM_GUI_ACTIVE")
+    if av is not None and gui:
+        out["valu_busy"] = av * 4 / (1024 * gui / 8)
+    if g("SQ_INSTS_VALU") is not None and g("SQ_BUSY_CYCLES") is not None:
+        out["valu_insts_per_busy_cycle"] = g("SQ_INSTS_VALU") / max(g("SQ_BUSY_CYCLES"), 1)
     tot = sum(out.get(k) or 0 for k in ("read_bytes", "write_bytes"))
     out["hbm_bytes"] = tot if tot else None
     return out
@@ -91,6 +101,8 @@ def main():
         d["profiled_ms_mean"] = sum(dur[name]) / len(dur[name]) if dur[name] else None
         d["keys_per_launch"] = args.batch
         d["hbm_bytes_per_launch"] = d.get("hbm_bytes")
+        if d.get("SQ_INSTS_VALU") is not None:   # one lane per key: wave instructions x 64 / keys
+            d["valu_lane_insts_per_key"] = d["SQ_INSTS_VALU"] * 64 / args.batch
         if d.get("hbm_bytes"):
             d["hbm_bytes_per_key"] = d["hbm_bytes"] / args.batch
             if d.get("profiled_ms_mean"):
