@@ -174,14 +174,22 @@ def prefill_random(f, m: int, k: int, rank: int, host_copy: bool = True):
     return host
 
 
-def auto_mode(world: int, m: int, k: int) -> str:
-    """single at N = 1; replicated at N = 2 for a filter that fits one GPU, where one xGMI
-    link carries the whole exchange: the replicated step moves ~10 B per key once (key bytes +
-    a length byte) against ~24 B per key out and back for the partitioned one, and its extra
-    compute (each replica hashes both batches) is what the partitioned owner-side sort costs
-    anyway; partitioned from N = 4 on, where the replicas' N-fold insert work loses."""
+def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
+    """single at N = 1.  BASELINE's own layouts for its multi-GPU configs: 10b (configs[3],
+    "10B keys replicated on 8 GPUs, key batches sharded") replicated, 200b (configs[4])
+    partitioned.  Otherwise replicated at N = 2 for a filter that fits one GPU, where one
+    xGMI link carries the whole exchange: the replicated step moves ~10 B per key once (key
+    bytes + a length byte) against ~24 B per key out and back for the partitioned one, and
+    its extra compute (each replica hashes both batches) is what the partitioned owner-side
+    sort costs anyway; partitioned from N = 4 on, where the replicas' N-fold insert work
+    loses (a replicated 1.2 GB filter cannot take the OR-reduce form either: 2.4 GB of
+    bitset on the wire per step against ~1.3 GB of gathered keys)."""
     if world == 1:
         return "single"
+    if config == "10b":
+        return "replicated"
+    if config == "200b":
+        return "partitioned"
     reach_bytes = (min(m, k * 0xFFFFFFFF + 1) + 7) // 8
     return "replicated" if world == 2 and reach_bytes <= (64 << 30) else "partitioned"
 
@@ -197,7 +205,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     pf = None
     host_bits = None
     if mode == "auto":
-        mode = auto_mode(D.world, m, k)
+        mode = auto_mode(D.world, m, k, name)
     rf = None
     if mode == "replicated":   # every rank a whole replica: include? local, inserts all-gathered
         rf = pkg.distributed.ReplicatedFilter(m, k, device=dev)
@@ -366,6 +374,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     else:
         f.close()
     res["mode"] = mode
+    if rf is not None:
+        res["replicated_insert_mode"] = rf.last_insert_mode
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
@@ -525,7 +535,9 @@ def main():
                    "parallelism": {"partitioned": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key "
                                                   "batches routed to owner GPUs, grouped RCCL send/recv)" % D.world,
                                    "replicated": "replicated x%d (include? local; insert batches all-gathered "
-                                                 "over RCCL, every replica applies every batch)" % D.world,
+                                                 "over RCCL and every replica applies every batch, or own batch + "
+                                                 "OR-all-reduce of the bitset when that moves fewer bytes: %s)"
+                                                 % (D.world, main_res.get("replicated_insert_mode")),
                                    "single": "single GPU"}[main_res["mode"]]},
         "roofline": {"bound": "hbm", "kernel": dom_name,
                      "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,

@@ -57,6 +57,11 @@ extern "C" {
 #define BF_ERANGE   5   /* output buffer too small (bf_export_redis) / string outside the reachable range */
 
 #define BF_MAX_K    64u /* hashes supported per key */
+#define BF_MAX_DEVICES 16 /* devices of one multi-device handle */
+
+/* ---- multi-device handles (bf_config.mode) */
+#define BF_MODE_REPLICATED  0u  /* every device holds the whole filter; include? batches split over them */
+#define BF_MODE_PARTITIONED 1u  /* the reachable prefix block-cyclically split; probes routed to owners */
 
 /* ---- import modes */
 #define BF_IMPORT_REPLACE 0u  /* like SET key value            */
@@ -79,6 +84,25 @@ typedef struct bf_config {
     uint32_t shard_index;      /* this handle's shard, < shard_count                       */
     uint32_t shard_block_log2; /* ownership block size, 3..40 (0 => 20: 128 KiB blocks)    */
     uint32_t flags;            /* BF_FLAG_* */
+    /* Multi-device handles (one process, several GPUs; the Ruby driver's `devices:` and
+     * `mode:` options, SURVEY §8 b).  device_count > 0 makes a handle over
+     * devices[0 .. device_count) (`device` is then ignored; a device may repeat):
+     *   BF_MODE_REPLICATED   every device holds the whole filter.  Inserts go to every
+     *                        device (in parallel, one host thread each), include? batches
+     *                        are split over the devices.  Export reads device 0.
+     *   BF_MODE_PARTITIONED  the reachable prefix is split block-cyclically over the devices
+     *                        (shard_block_log2, as for one-handle-per-GPU shards).  Each
+     *                        device hashes its part of a batch into per-owner windows
+     *                        (bf_route_windows_dev), the windows travel to their owners by
+     *                        peer copies over xGMI (hipMemcpyPeerAsync), the owners apply
+     *                        or test them, and include? answers travel back the same way.
+     * The host-pointer API, export / import (the owner shards' blocks interleaved), clear,
+     * dirty tracking and bf_export_range work on both; per_key_new needs BF_MODE_REPLICATED;
+     * the device-resident (*_dev, bf_device_bits, bf_stream) and shard entry points return
+     * BF_EINVAL on a multi-device handle.  shard_count / shard_index must be 0 / 1. */
+    uint32_t device_count;
+    uint32_t mode;             /* BF_MODE_* */
+    int32_t  devices[BF_MAX_DEVICES];
 } bf_config;
 
 /* bf_config.flags */

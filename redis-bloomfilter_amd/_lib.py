@@ -45,11 +45,17 @@ class ArgumentError(ValueError):
     """Mirror of Ruby's ArgumentError (raised where the reference raises it)."""
 
 
+BF_MAX_DEVICES = 16
+BF_MODE_REPLICATED, BF_MODE_PARTITIONED = 0, 1
+
+
 class bf_config(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("batch_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
                 ("shard_count", ctypes.c_uint32), ("shard_index", ctypes.c_uint32),
-                ("shard_block_log2", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("shard_block_log2", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("device_count", ctypes.c_uint32), ("mode", ctypes.c_uint32),
+                ("devices", ctypes.c_int32 * BF_MAX_DEVICES)]
 
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -221,10 +227,24 @@ class Filter:
 
     def __init__(self, m_bits: int, k: int, device: int = -1, batch_keys: int = 0,
                  batch_bytes: int = 0, shard_count: int = 1, shard_index: int = 0,
-                 shard_block_log2: int = 0, flags: int = 0):
+                 shard_block_log2: int = 0, flags: int = 0, devices=None, mode: str = "replicated"):
+        """devices: a list of HIP ordinals -> one multi-device handle over them (bf_config
+        device_count / devices / mode; ``mode`` "replicated" or "partitioned")."""
         self._lib = load()
         cfg = bf_config(ctypes.sizeof(bf_config), int(device), int(batch_keys), int(batch_bytes),
                         int(shard_count), int(shard_index), int(shard_block_log2), int(flags))
+        if devices is not None:
+            devices = [int(d) for d in devices]
+            if not 0 < len(devices) <= BF_MAX_DEVICES:
+                raise ArgumentError("devices must list 1..%d ordinals" % BF_MAX_DEVICES)
+            if mode not in ("replicated", "partitioned"):
+                raise ArgumentError("mode must be 'replicated' or 'partitioned'")
+            cfg.device_count = len(devices)
+            cfg.mode = BF_MODE_PARTITIONED if mode == "partitioned" else BF_MODE_REPLICATED
+            for i, d in enumerate(devices):
+                cfg.devices[i] = d
+        self.devices = devices
+        self.mode = mode if devices is not None else None
         self.route32 = bool(flags & BF_FLAG_ROUTE32)
         h = _vp()
         rc = self._lib.bf_create(int(m_bits), int(k), ctypes.byref(cfg), ctypes.byref(h))

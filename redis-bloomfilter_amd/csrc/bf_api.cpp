@@ -5,6 +5,7 @@
 // packing chunk c+1 on the host overlaps the device work of chunk c.
 #include "bfhip.h"
 #include "bf_internal.h"
+#include "bf_multi.h"
 
 #include <sched.h>
 
@@ -181,6 +182,7 @@ struct bf_handle {
     hipEvent_t order_ev = nullptr;
     hipStream_t order_stream = nullptr;
     bool order_valid = false;
+    BfMulti* multi = nullptr;   // a multi-device handle (bf_config.device_count > 0): bf_multi.cpp
     std::string err;
 };
 
@@ -633,6 +635,7 @@ extern "C" {
 const char* bf_version(void) { return BFHIP_VERSION_STR; }
 
 const char* bf_last_error(const bf_handle* h) {
+    if (h && h->multi) return bfm_last_error(h->multi);
     return h ? h->err.c_str() : g_create_error.c_str();
 }
 
@@ -697,6 +700,22 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
         memcpy(&c, cfg, std::min<size_t>(sizeof c, cfg->struct_size));
     } else {
         c.device = -1;
+    }
+    if (c.device_count > 0) {   // one handle over several devices (bf_multi.cpp)
+        BfMulti* mh = nullptr;
+        std::string err;
+        const int rc = bfm_create(m_bits, k, c, &mh, &err);
+        if (rc) return set_err(nullptr, rc, "%s", err.c_str());
+        bf_handle* h = new (std::nothrow) bf_handle();
+        if (!h) {
+            bfm_destroy(mh);
+            return set_err(nullptr, BF_ENOMEM, "host allocation failed");
+        }
+        h->multi = mh;
+        h->m = m_bits;
+        h->k = k;
+        *out = h;
+        return BF_OK;
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -803,6 +822,11 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
 
 int bf_destroy(bf_handle* h) {
     if (!h) return BF_OK;
+    if (h->multi) {
+        bfm_destroy(h->multi);
+        delete h;
+        return BF_OK;
+    }
     {
         std::lock_guard<std::mutex> lk(h->mu);
         DeviceGuard dg(h->device);
@@ -830,6 +854,7 @@ int bf_destroy(bf_handle* h) {
 }
 
 int bf_info(const bf_handle* h, uint64_t* m_bits, uint32_t* k, uint64_t* reach_bits, uint64_t* device_bytes) {
+    if (h && h->multi) return bfm_info(h->multi, m_bits, k, reach_bits, device_bytes);
     if (!h) return BF_EINVAL;
     if (m_bits) *m_bits = h->m;
     if (k) *k = h->k;
@@ -840,6 +865,7 @@ int bf_info(const bf_handle* h, uint64_t* m_bits, uint32_t* k, uint64_t* reach_b
 
 int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                    uint8_t* any_new, uint8_t* per_key_new) {
+    if (h && h->multi) return bfm_insert_many(h->multi, key_bytes, offsets, n, any_new, per_key_new);
     if (!h) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -853,6 +879,7 @@ int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offse
 }
 
 int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n, uint8_t* out) {
+    if (h && h->multi) return bfm_include_many(h->multi, key_bytes, offsets, n, out);
     if (!h) return BF_EINVAL;
     if (n && !out) return set_err(h, BF_EINVAL, "out is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -863,6 +890,7 @@ int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
 }
 
 int bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n, uint64_t* out) {
+    if (h && h->multi) return bfm_indexes_many(h->multi, key_bytes, offsets, n, out);
     if (!h) return BF_EINVAL;
     if (n && !out) return set_err(h, BF_EINVAL, "out is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -873,6 +901,7 @@ int bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
 }
 
 int bf_clear(bf_handle* h) {
+    if (h && h->multi) return bfm_clear(h->multi);
     if (!h) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -885,6 +914,7 @@ int bf_clear(bf_handle* h) {
 }
 
 int bf_sync(bf_handle* h) {
+    if (h && h->multi) return bfm_sync(h->multi);
     if (!h) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -974,6 +1004,7 @@ int ensure_route_scratch(bf_handle* h, uint64_t probes) {
 extern "C" {
 
 int bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+    if (h && h->multi) return len_out ? bfm_export_redis(h->multi, buf, cap, len_out) : BF_EINVAL;
     if (!h || !len_out) return BF_EINVAL;
     if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_export and interleave blocks");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -990,6 +1021,7 @@ int bf_export_redis(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out)
 }
 
 int bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode) {
+    if (h && h->multi) return bfm_import_redis(h->multi, buf, len, mode);
     if (!h) return BF_EINVAL;
     if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_import");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1000,6 +1032,7 @@ int bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mod
 
 int bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_index, uint32_t* block_log2,
                   uint64_t* local_bits) {
+    if (h && h->multi) return bfm_shard_info(h->multi, shard_count, shard_index, block_log2, local_bits);
     if (!h) return BF_EINVAL;
     if (shard_count) *shard_count = h->shards;
     if (shard_index) *shard_index = h->shard_index;
@@ -1009,6 +1042,7 @@ int bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_ind
 }
 
 int bf_shard_export(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h || !len_out) return BF_EINVAL;
     const uint64_t len = (h->local_bits + 7) / 8;
     *len_out = len;
@@ -1024,6 +1058,7 @@ int bf_shard_export(bf_handle* h, uint8_t* buf, uint64_t cap, uint64_t* len_out)
 }
 
 int bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -1033,6 +1068,7 @@ int bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mod
 
 int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                  void* d_send, uint32_t* d_slot, uint64_t* d_counts, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
     if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
@@ -1075,6 +1111,7 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
 }
 
 int bf_route_window_split(const bf_handle* h, uint32_t* nh) {
+    if (h && h->multi) return BF_EINVAL;
     if (!h || !nh) return BF_EINVAL;
     // the largest shard (index 0) holds ceil(nblocks / P) blocks
     const uint64_t nblocks = (h->reach + (1ull << h->block_log2) - 1) >> h->block_log2;
@@ -1086,6 +1123,7 @@ int bf_route_window_split(const bf_handle* h, uint32_t* nh) {
 
 int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                          uint32_t* d_send, uint32_t* d_slot, uint64_t window_cap, uint64_t* d_counts, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (!d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
     if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
@@ -1150,19 +1188,21 @@ int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, u32, s, bias));
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, u32, s, bias, h->g.dirty));
     bf_mark(mk, s, "shard_insert");
     return BF_OK;
 }
 }  // namespace
 
 int bf_shard_insert_dev(bf_handle* h, const void* d_local, uint64_t count, uint32_t* d_any_new, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     return shard_insert_impl(h, d_local, h->route32, 0, count, d_any_new, stream);
 }
 
 int bf_shard_insert_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count, uint32_t hi, uint32_t* d_any_new,
                            void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (((uint64_t)hi << 32) >= h->local_bits) return set_err(h, BF_EINVAL, "hi=%u is past the shard", hi);
     return shard_insert_impl(h, d_local32, true, (uint64_t)hi << 32, count, d_any_new, stream);
@@ -1212,12 +1252,14 @@ int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, 
 }  // namespace
 
 int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     return shard_test_impl(h, d_local, h->route32, 0, count, d_bits, stream);
 }
 
 int bf_shard_test_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count, uint32_t hi, uint8_t* d_bits,
                          void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (((uint64_t)hi << 32) >= h->local_bits) return set_err(h, BF_EINVAL, "hi=%u is past the shard", hi);
     return shard_test_impl(h, d_local32, true, (uint64_t)hi << 32, count, d_bits, stream);
@@ -1225,6 +1267,7 @@ int bf_shard_test_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t count
 
 int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t n, uint8_t* d_out,
                    void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (n && (!d_bits || !d_slot || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1240,6 +1283,7 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
 
 int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, uint64_t window_cap,
                            uint32_t nwin, const uint64_t* d_counts, uint64_t n, uint8_t* d_out, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (n && (!d_bits || !d_slot || !d_counts || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1256,6 +1300,7 @@ int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* 
 
 int bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_seg, uint32_t nseg,
                          uint64_t max_count, uint8_t* d_packed, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (nseg && (!d_bits || !d_seg || !d_packed)) return set_err(h, BF_EINVAL, "NULL device pointer");
     if (nseg > 65535) return set_err(h, BF_EINVAL, "at most 65535 segments");
@@ -1273,6 +1318,7 @@ int bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_
 
 int bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint32_t* d_slot, uint64_t window_cap,
                                   uint32_t nwin, const uint64_t* d_counts, uint64_t n, uint8_t* d_out, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (n && (!d_packed || !d_slot || !d_counts || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1290,27 +1336,32 @@ int bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const u
 
 int bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                        uint32_t* d_any_new, uint8_t* d_per_key_new, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     const BfOp op = (d_any_new || d_per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
     return run_dev(h, op, d_key_bytes, d_offsets, n, d_per_key_new, nullptr, d_any_new, stream);
 }
 
 int bf_include_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                         uint8_t* d_out, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     return run_dev(h, BF_OP_INCLUDE, d_key_bytes, d_offsets, n, d_out, nullptr, nullptr, stream);
 }
 
 int bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                         uint64_t* d_out, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     return run_dev(h, BF_OP_INDEXES, d_key_bytes, d_offsets, n, nullptr, d_out, nullptr, stream);
 }
 
 int bf_stream(bf_handle* h, void** stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h || !stream) return BF_EINVAL;
     *stream = reinterpret_cast<void*>(h->stream);
     return BF_OK;
 }
 
 int bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (d_bits) *d_bits = h->g.bits;
     if (device_bytes) *device_bytes = h->dev_bytes;
@@ -1318,6 +1369,7 @@ int bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes) {
 }
 
 int bf_profile(bf_handle* h, uint32_t enable) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -1328,6 +1380,7 @@ int bf_profile(bf_handle* h, uint32_t enable) {
 
 int bf_profile_read(bf_handle* h, char* names, double* total_ms, uint64_t* launches, uint32_t cap,
                     uint32_t* n_out, uint32_t reset) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h || !n_out) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -1345,8 +1398,15 @@ int bf_profile_read(bf_handle* h, char* names, double* total_ms, uint64_t* launc
 }
 
 int bf_track_dirty(bf_handle* h, uint32_t enable) {
+    if (h && h->multi) return bfm_track_dirty(h->multi, enable);
     if (!h) return BF_EINVAL;
     if (h->shards > 1) return set_err(h, BF_EINVAL, "dirty tracking needs a whole-filter handle");
+    return bfi_track_dirty(h, enable);
+}
+
+}  // extern "C"
+
+int bfi_track_dirty(bf_handle* h, uint32_t enable) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     HIPCHK(h, hipDeviceSynchronize());   // no launch may still use the map
@@ -1366,8 +1426,55 @@ int bf_track_dirty(bf_handle* h, uint32_t enable) {
     return BF_OK;
 }
 
+// The changed byte ranges of the handle's own bytes (whole filter: the Redis string; shard:
+// its local bytes), clipped to their trimmed length; clear forgets them.
+int bfi_dirty_local(bf_handle* h, std::vector<uint64_t>* out, bool clear) {
+    if (!h->d_dirty) return set_err(h, BF_EINVAL, "dirty tracking is off (bf_track_dirty)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    HIPCHK(h, hipDeviceSynchronize());   // inserts may have run on any stream
+    std::vector<uint8_t> map(h->dirty_blocks);
+    HIPCHK(h, hipMemcpy(map.data(), h->d_dirty, h->dirty_blocks, hipMemcpyDeviceToHost));
+    uint64_t len = 0;
+    int rc = device_trimmed_len(h, &len);
+    if (rc) return rc;
+    out->clear();
+    for (uint64_t b = 0; b < h->dirty_blocks;) {
+        if (!map[b]) { ++b; continue; }
+        uint64_t e = b;
+        while (e < h->dirty_blocks && map[e]) ++e;
+        const uint64_t off = b * BF_DIRTY_BLOCK_BYTES;
+        const uint64_t end = std::min<uint64_t>(e * BF_DIRTY_BLOCK_BYTES, len);
+        if (end > off) { out->push_back(off); out->push_back(end - off); }
+        b = e;
+    }
+    if (clear) HIPCHK(h, hipMemset(h->d_dirty, 0, h->dirty_blocks));
+    return BF_OK;
+}
+
+int bfi_trimmed_len(bf_handle* h, uint64_t* len) {
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    return device_trimmed_len(h, len);
+}
+
+int bfi_export_local(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf) {
+    if (offset > h->dev_bytes || len > h->dev_bytes - offset)
+        return set_err(h, BF_ERANGE, "range [%llu, +%llu) outside the %llu-byte bitset", (unsigned long long)offset,
+                       (unsigned long long)len, (unsigned long long)h->dev_bytes);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (h->order_valid) HIPCHK(h, hipEventSynchronize(h->order_ev));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (len) HIPCHK(h, hipMemcpy(buf, reinterpret_cast<const uint8_t*>(h->g.bits) + offset, len, hipMemcpyDeviceToHost));
+    return BF_OK;
+}
+
+extern "C" {
+
 int bf_dirty_ranges(bf_handle* h, uint64_t* ranges, uint32_t cap, uint32_t* n_out, uint64_t* redis_len,
                     uint32_t clear) {
+    if (h && h->multi) return n_out ? bfm_dirty_ranges(h->multi, ranges, cap, n_out, redis_len, clear) : BF_EINVAL;
     if (!h || !n_out) return BF_EINVAL;
     if (!h->d_dirty) return set_err(h, BF_EINVAL, "dirty tracking is off (bf_track_dirty)");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1401,6 +1508,7 @@ int bf_dirty_ranges(bf_handle* h, uint64_t* ranges, uint32_t cap, uint32_t* n_ou
 }
 
 int bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf) {
+    if (h && h->multi) return (len && !buf) ? BF_EINVAL : bfm_export_range(h->multi, offset, len, buf);
     if (!h || (len && !buf)) return BF_EINVAL;
     if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_export");
     if (offset > h->dev_bytes || len > h->dev_bytes - offset)
@@ -1415,6 +1523,7 @@ int bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf) {
 }
 
 int bf_insert_plan(const bf_handle* h, uint64_t n, uint32_t* binned, uint64_t* scratch_bytes) {
+    if (h && h->multi) return bfm_insert_plan(h->multi, n, binned, scratch_bytes);
     if (!h) return BF_EINVAL;
     BfBinPlan plan{};
     const bool b = n > 0 && use_binned(h, n, false, &plan);

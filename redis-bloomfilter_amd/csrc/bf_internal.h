@@ -168,8 +168,10 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
                                    unsigned long long* cursor, void* send, uint32_t* slot,
                                    bool route32, hipStream_t s);
 // bias: added to every local offset (the 2^32-bit sub-range of a split window route)
+// dirty (nullable): the shard's bf_track_dirty map
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count,
-                                  uint32_t* any_flag, bool route32, hipStream_t s, uint64_t bias = 0);
+                                  uint32_t* any_flag, bool route32, hipStream_t s, uint64_t bias = 0,
+                                  uint8_t* dirty = nullptr);
 hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count,
                                 uint8_t* out, bool route32, hipStream_t s, uint64_t bias = 0);
 // out[j] = AND of bits[p] over the n*k send entries p with slot[p] == j.

@@ -275,7 +275,7 @@ template <bool FLAGS, typename Off>
 __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
                                                            const Off* __restrict__ local,
                                                            uint64_t count, uint32_t* __restrict__ any_flag,
-                                                           uint64_t bias) {
+                                                           uint64_t bias, uint8_t* __restrict__ dirty) {
     // Test-then-set as in the direct insert: 4 probes per lane in flight, an atomic
     // only for bits still 0 (a 1 seen here is final within the launch).
     constexpr int U = 4;
@@ -298,6 +298,7 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (mask[u] && !(v[u] & mask[u])) {
+                if (dirty) dirty[w[u] >> (kDirtyShiftBits - 5)] = 1;   // bf_track_dirty (shards of a multi-device handle)
                 if constexpr (FLAGS) {
                     const uint32_t old = __hip_atomic_fetch_or(bits + w[u], mask[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     isnew |= (old & mask[u]) ? 0u : 1u;
@@ -459,21 +460,21 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
 
 template <typename Off>
 static void launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag, uint64_t bias,
-                                hipStream_t s) {
+                                uint8_t* dirty, hipStream_t s) {
     const Off* l = static_cast<const Off*>(local);
     if (any_flag)
         hipLaunchKernelGGL((shard_insert_kernel<true, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count,
-                           any_flag, bias);
+                           any_flag, bias, dirty);
     else
         hipLaunchKernelGGL((shard_insert_kernel<false, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count,
-                           any_flag, bias);
+                           any_flag, bias, dirty);
 }
 
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag,
-                                  bool route32, hipStream_t s, uint64_t bias) {
+                                  bool route32, hipStream_t s, uint64_t bias, uint8_t* dirty) {
     if (count == 0) return hipSuccess;
-    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, bias, s);
-    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, bias, s);
+    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, bias, dirty, s);
+    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, bias, dirty, s);
     return hipGetLastError();
 }
 

@@ -174,12 +174,55 @@ class HipEngine:
         torch.cuda.current_stream(self.device).synchronize()
         return self.filter.shard_export()
 
+    def shard_tensor(self) -> torch.Tensor:
+        """The shard's local bytes as a device tensor VIEW of the bitset (no copy): what the
+        export gather sends over RCCL."""
+        return device_bytes_view(self.filter, (self.filter.local_bits + 7) // 8)
+
     def shard_import(self, local: np.ndarray) -> None:
         torch.cuda.current_stream(self.device).synchronize()
         self.filter.shard_import(local[: (self.filter.local_bits + 7) // 8].tobytes())
 
     def close(self):
         self.filter.close()
+
+
+class _DevBytes:
+    """Raw device bytes exposed to torch through __cuda_array_interface__."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+def device_bytes_view(f: Filter, nbytes: Optional[int] = None) -> torch.Tensor:
+    """A uint8 torch tensor aliasing a filter's device bitset (Redis byte order)."""
+    ptr, total = f.device_bits()
+    dev = torch.device("cuda", f.device if f.device >= 0 else torch.cuda.current_device())
+    return torch.as_tensor(_DevBytes(ptr, total if nbytes is None else min(nbytes, total)), device=dev)
+
+
+def or_allreduce_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place bitwise OR of a uint8 tensor over the group.  RCCL has no bitwise-OR
+    reduction (ncclRedOp_t: sum / prod / max / min / avg), so it is built as SURVEY §8(e)
+    (ii) says: all_to_all (rank r receives every rank's r-th chunk) -> local OR ->
+    all_gather of the OR-ed chunks; each rank moves 2 (P-1)/P of the tensor, like a ring
+    all-reduce."""
+    P = dist.get_world_size(group)
+    if P == 1 or t.numel() == 0:
+        return t
+    n = t.numel()
+    per = -(-n // (P * 16)) * 16                  # chunks of whole 16-B vectors
+    buf = torch.zeros(P * per, dtype=torch.uint8, device=t.device)
+    buf[:n] = t
+    recv = torch.empty_like(buf)
+    dist.all_to_all_single(recv, buf, group=group)
+    parts = recv.view(P, per // 8, 8).view(torch.int64).view(P, per // 8)
+    acc = parts[0].clone()
+    for r in range(1, P):
+        acc.bitwise_or_(parts[r])
+    dist.all_gather_into_tensor(buf, acc.view(torch.uint8).view(-1), group=group)
+    t.copy_(buf[:n])
+    return t
 
 
 def _device_batch(keys, device) -> Tuple[torch.Tensor, torch.Tensor, int]:
@@ -234,25 +277,41 @@ class PartitionedFilter:
         probes = n * self.k
         return min(probes, probes // self.P + probes // (8 * self.P) + 4096)
 
-    def _route(self, kb, ko, n: int, want_slot: bool) -> dict:
-        """Route a batch and exchange its counts (the host waits for that small all-to-all).
-        Returns the send buffer, slots, device counts and the segment lists of the exchange:
-        ``sseg`` = [(peer, offset, count)] to send, ``rseg`` = [(peer, offset, count)] to
-        receive, both in the order the two sides agree on, plus ``hruns`` = [(hi, start, end)]
-        of the receive buffer for the owner ops (window route: one run per 2^32-bit sub-range)."""
-        e, P = self.engine, self.P
+    def _route_start(self, kb, ko, n: int, want_slot: bool) -> dict:
+        """Enqueue a batch's route and the all-to-all of its counts; nothing waits here, so
+        the next batch's route can be enqueued before the host needs these counts."""
+        e = self.engine
         if self.windows and hasattr(e, "route_windows"):
-            nh = e.nh
             cap = self._cap(n)
             send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
-            sc, rc = self._splits(counts)   # rc[s*nh + h]: source s's probes for my sub-range h
+        else:
+            cap = None
+            send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
+        recv_counts = torch.empty_like(counts)
+        work = dist.all_to_all_single(recv_counts, counts, group=self.group, async_op=True)
+        return dict(kb=kb, ko=ko, n=n, want_slot=want_slot, send=send, slot=slot, counts=counts,
+                    recv_counts=recv_counts, work=work, cap=cap)
+
+    def _route_finish(self, st: dict) -> dict:
+        """Wait for the counts (host) and build the exchange: the send buffer, slots, device
+        counts and the segment lists ``sseg`` = [(peer, offset, count)] to send and ``rseg`` =
+        [(peer, offset, count)] to receive, in the order the two sides agree on, plus ``hruns``
+        = [(hi, start, end)] of the receive buffer for the owner ops (window route: one run
+        per 2^32-bit sub-range)."""
+        e, P, n, want_slot = self.engine, self.P, st["n"], st["want_slot"]
+        st["work"].wait()
+        cnt = torch.stack([st["counts"], st["recv_counts"]]).cpu()
+        sc, rc = cnt[0].tolist(), cnt[1].tolist()
+        send, slot, counts, cap = st["send"], st["slot"], st["counts"], st["cap"]
+        if cap is not None:
+            nh = e.nh
             if max(sc) > cap:
                 # A window past cap holds undefined entries: route again into windows that
                 # always fit.  Each rank decides alone and the counts are the same, so the
                 # exchange below does not change shape.
                 self.window_overflows += 1
                 cap = max(n * self.k, 1)
-                send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
+                send, slot, counts = e.route_windows(st["kb"], st["ko"], n, cap, want_slot=want_slot)
             sseg = [(o, (o * nh + h) * cap, sc[o * nh + h]) for o in range(P) for h in range(nh)]
             rseg, hruns, at = [None] * (P * nh), [], 0
             for h in range(nh):   # receive buffer: sub-range major, then source
@@ -274,12 +333,13 @@ class PartitionedFilter:
                 rt["pk_recv"] = [(o, (off // cap) * cap8, (c + 7) // 8) for o, off, c in sseg]
                 rt["pk_total"], rt["pk_max"], rt["cap8"] = sum(pk), max(c for _, _, c in rseg), cap8
             return rt
-        send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
-        sc, rc = self._splits(counts)
         sd, rd = _prefix(sc), _prefix(rc)
         return dict(send=send, slot=slot, counts=counts, cap=None,
                     sseg=[(o, sd[o], sc[o]) for o in range(P)], rseg=[(o, rd[o], rc[o]) for o in range(P)],
                     hruns=None, total=sum(rc))
+
+    def _route(self, kb, ko, n: int, want_slot: bool) -> dict:
+        return self._route_finish(self._route_start(kb, ko, n, want_slot))
 
     def _p2p(self, send: torch.Tensor, sseg, recv: torch.Tensor, rseg):
         """Grouped send/recv: each (peer, offset, count) of sseg goes to that peer, each of
@@ -305,7 +365,9 @@ class PartitionedFilter:
 
     def _exchange(self, kb, ko, n: int, want_slot: bool):
         """route, then the offsets to their owners (async): returns (recv, route, works)."""
-        rt = self._route(kb, ko, n, want_slot)
+        return self._send_routed(self._route(kb, ko, n, want_slot))
+
+    def _send_routed(self, rt: dict):
         recv = torch.empty(rt["total"], dtype=rt["send"].dtype, device=rt["send"].device)
         works = self._p2p(rt["send"], rt["sseg"], recv, rt["rseg"])
         return recv, rt, works
@@ -368,8 +430,12 @@ class PartitionedFilter:
         current stream; every owner still applies all ranks' inserts before it tests
         (shard_insert precedes shard_test on its stream), so the include? answers see the
         batch's inserts exactly as in the sequential form."""
-        recv_i, rt_i, w_i = self._exchange(ikb, iko, ni, want_slot=False)
-        recv_q, rt_q, w_q = self._exchange(qkb, qko, nq, want_slot=True)   # route(inc) overlaps send(ins)
+        # both routes are enqueued before the host waits for the first batch's counts, so the
+        # device goes straight on to route(inc) while the host builds send(ins)
+        st_i = self._route_start(ikb, iko, ni, want_slot=False)
+        st_q = self._route_start(qkb, qko, nq, want_slot=True)
+        recv_i, rt_i, w_i = self._send_routed(self._route_finish(st_i))
+        recv_q, rt_q, w_q = self._send_routed(self._route_finish(st_q))   # send(inc) overlaps shard_insert
         for w in w_i:
             w.wait()
         self._shard_insert(recv_i, rt_i)                                    # overlaps send(inc)
@@ -396,11 +462,82 @@ class PartitionedFilter:
         self.engine.clear()
 
     # -- Redis string (collective: every rank must call)
-    def export_redis(self) -> bytes:
+    def _shard_tensor(self) -> torch.Tensor:
+        if hasattr(self.engine, "shard_tensor"):
+            return self.engine.shard_tensor()
+        return torch.from_numpy(self.engine.shard_export())
+
+    def export_redis(self, dst: int = 0) -> Optional[bytes]:
+        """The trimmed Redis string, assembled on rank ``dst`` (None on the others).  The
+        shards travel one at a time into one preallocated buffer of the largest shard's size
+        (device memory under RCCL), so no rank but ``dst`` ever holds more than its own shard
+        and ``dst`` holds the string once, on the host."""
+        mine = self._shard_tensor()
+        bb = (1 << self.block_log2) // 8
+        nblocks = (self.reach_bits + (1 << self.block_log2) - 1) >> self.block_log2
+        if self.rank != dst:
+            if mine.numel():
+                dist.send(mine, dist.get_global_rank(self.group, dst) if self.group is not None else dst,
+                          group=self.group)
+            return None
+        out = np.zeros(nblocks * bb, dtype=np.uint8)
+        view = out.reshape(nblocks, bb)
+        big = (shard_local_bits(self.reach_bits, self.P, 0, self.block_log2) + 7) // 8
+        buf = torch.empty(big, dtype=torch.uint8, device=mine.device)
+        for s_ in range(self.P):
+            cnt = len(range(s_, nblocks, self.P))
+            if cnt == 0:
+                continue
+            nb = (shard_local_bits(self.reach_bits, self.P, s_, self.block_log2) + 7) // 8
+            if s_ == self.rank:
+                part = mine[:nb]
+            else:
+                dist.recv(buf[:nb], dist.get_global_rank(self.group, s_) if self.group is not None else s_,
+                          group=self.group)
+                part = buf[:nb]
+            host = part.cpu().numpy()
+            if len(host) < cnt * bb:   # a whole-filter handle (P == 1) stops at the reachable prefix
+                host = np.concatenate([host, np.zeros(cnt * bb - len(host), np.uint8)])
+            view[s_::self.P] = host[: cnt * bb].reshape(cnt, bb)
+        out = out[: (self.reach_bits + 7) // 8]
+        nz = np.flatnonzero(out)
+        return out[: nz[-1] + 1].tobytes() if len(nz) else b""
+
+    def write_redis(self, redis, key: str, chunk_bytes: int = 8 << 20, replace: bool = True) -> int:
+        """Write the filter to ``key`` with every rank sending its own blocks (SETRANGE at the
+        block's place in the string), so nothing is gathered anywhere.  Collective.  The
+        string's length is the global last nonzero byte + 1 (one all-reduce): every write is
+        clipped to it, all-zero blocks are skipped, and the block holding that last byte
+        grows the key to exactly the length the SETBITs would have.
+        ``replace``: rank 0 DELs the key first (a barrier orders it before the writes).
+        Returns the bytes this rank sent."""
         local = self.engine.shard_export()
-        parts: List[Optional[np.ndarray]] = [None] * self.P
-        dist.all_gather_object(parts, local, group=self.group)
-        return interleave_shards(parts, self.reach_bits, self.block_log2)
+        bb = (1 << self.block_log2) // 8
+        nz = np.flatnonzero(local)
+        last = -1
+        if len(nz):   # the local byte -> its place in the string
+            lb = int(nz[-1])
+            last = ((lb // bb) * self.P + self.rank) * bb + lb % bb
+        t = torch.tensor([last], dtype=torch.int64, device=self._shard_tensor().device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        length = int(t.item()) + 1
+        if replace and self.rank == 0:
+            redis.delete(key)
+        dist.barrier(group=self.group)
+        sent = 0
+        for j in range(len(local) // bb + (1 if len(local) % bb else 0)):
+            off = (j * self.P + self.rank) * bb
+            if off >= length:
+                break
+            blk = local[j * bb: (j + 1) * bb][: length - off]
+            if not blk.any():
+                continue
+            for c in range(0, len(blk), chunk_bytes):
+                part = blk[c: c + chunk_bytes]
+                redis.setrange(key, off + c, part.tobytes())
+                sent += len(part)
+        dist.barrier(group=self.group)
+        return sent
 
     def import_redis(self, data: bytes) -> None:
         self.engine.shard_import(split_shard(data, self.P, self.rank, self.reach_bits, self.block_log2))
@@ -429,24 +566,43 @@ def merge_gathered(gk: torch.Tensor, gl: torch.Tensor, sizes, max_b: int, max_n:
 
 
 class ReplicatedFilter:
-    """Every rank holds the whole filter; include? is local, insert is all-gathered."""
+    """Every rank holds the whole filter; include? is local.  An insert reaches every replica
+    one of two ways (SURVEY §8 e):
 
-    def __init__(self, m: int, k: int, group=None, device=None):
+    * ``"gather"`` (i): the key batches are all-gathered and every replica inserts all of
+      them — about L + 1 bytes per key on the wire, but the insert work grows with P;
+    * ``"or"`` (ii): every replica inserts only its own batch, then the bitsets are
+      OR-all-reduced (``or_allreduce_``) — 2 (P-1)/P of the bitset on the wire per rank,
+      the insert work stays flat.
+
+    ``insert_mode="auto"`` takes (ii) when the bitset is small next to the gathered batches
+    (2 * bitset bytes < all ranks' key bytes + lengths), e.g. the 1M@1 % filter (1.2 MB)
+    against 2^24-key batches, and (i) otherwise, e.g. the north-star filter (1.2 GB)."""
+
+    MODES = ("auto", "gather", "or")
+
+    def __init__(self, m: int, k: int, group=None, device=None, insert_mode: str = "auto"):
+        if insert_mode not in self.MODES:
+            raise ArgumentError("insert_mode must be one of %s" % (self.MODES,))
         self.group = group
         self.P = dist.get_world_size(group)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.filter = Filter(m, k, device=self.device.index)
         self.k = k
+        self.insert_mode = insert_mode
+        self.last_insert_mode = None
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
-        """Every rank's batch reaches every replica: the key bytes and one length per key
-        (uint8 while every key fits 255 bytes, else int32) are all-gathered while this
-        rank's own batch is inserted, then the other ranks' batches go in as ONE insert
-        (one binned pass over the bitset).  OR is order-free, so the replicas end
-        byte-identical to one filter that took the batches in any order."""
+        """Every rank's batch reaches every replica; OR is order-free, so the replicas end
+        byte-identical to one filter that took the batches in any order.
+
+        gather: the key bytes and one length per key (uint8 while every key fits 255 bytes,
+        else int32) are all-gathered while this rank's own batch is inserted, then the
+        other ranks' batches go in as ONE insert (one binned pass over the bitset).
+        or: this rank's batch, then the bitset OR-all-reduced."""
         z = torch.zeros(1, dtype=torch.int64, device=self.device)
         lens = (ko[1: n + 1] - ko[:n]) if n else z[:0]
         # (bytes, keys, longest key, first offset): one small all-gather, one host wait
@@ -456,6 +612,17 @@ class ReplicatedFilter:
         all_sizes = all_sizes.view(self.P, 4).cpu().tolist()
         nbytes, _, _, ko0 = all_sizes[dist.get_rank(self.group)]
         all_sizes = [sz[:3] for sz in all_sizes]
+        mode = self.insert_mode
+        if mode == "auto":
+            wide = max(sz[2] for sz in all_sizes) > 255
+            gather_bytes = sum(sz[0] + sz[1] * (4 if wide else 1) for sz in all_sizes)
+            mode = "or" if 2 * self.filter.device_bytes < gather_bytes else "gather"
+        self.last_insert_mode = mode
+        if mode == "or":
+            if n:
+                self.filter.insert_many_dev(kb.data_ptr(), ko.data_ptr(), n, stream=self._stream())
+            or_allreduce_(device_bytes_view(self.filter), self.group)
+            return
         max_b = max(max(sz[0] for sz in all_sizes), 1)
         max_n = max(max(sz[1] for sz in all_sizes), 1)
         ldt = torch.uint8 if max(sz[2] for sz in all_sizes) <= 255 else torch.int32

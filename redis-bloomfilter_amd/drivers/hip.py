@@ -27,8 +27,10 @@ GETRANGE chunks, so a multi-GB filter moves through a server whose
 would).
 
 Extra options (all optional): ``device`` (HIP ordinal, default current),
-``sync``, ``batch_keys`` / ``batch_bytes`` (host staging chunk sizes),
-``chunk_bytes`` (Redis request size).
+``devices`` (a list of ordinals, or a count: one filter over several GPUs) with
+``mode`` ``'replicated'`` (default) or ``'partitioned'`` (include/bfhip.h,
+bf_config.devices), ``sync``, ``batch_keys`` / ``batch_bytes`` (host staging chunk
+sizes), ``chunk_bytes`` (Redis request size).
 """
 from __future__ import annotations
 
@@ -56,10 +58,14 @@ class Hip:
         if self.sync_mode not in self.SYNC_MODES:
             raise ArgumentError("sync must be one of %s" % (self.SYNC_MODES,))
         self._clock = options.get("clock", time.monotonic)
+        devices = options.get("devices")
+        if isinstance(devices, int):   # `devices: 8` -> the first 8 GPUs
+            devices = list(range(devices))
         self.filter = Filter(m, k, device=options.get("device", -1),
                              batch_keys=options.get("batch_keys", 0),
                              batch_bytes=options.get("batch_bytes", 0),
-                             flags=self._filter_flags())
+                             flags=self._filter_flags(),
+                             devices=devices, mode=str(options.get("mode", "replicated")))
         self.filter.track_dirty(True)
         self.chunk_bytes = int(options.get("chunk_bytes", 8 << 20))
         if self.chunk_bytes <= 0:

@@ -21,7 +21,8 @@
 # Every write is cut into SETRANGE calls of at most :chunk_bytes (default 8 MiB)
 # and a longer key is read back with GETRANGE chunks, so multi-GB filters move
 # through a server whose proto-max-bulk-len admits them (SURVEY §8 f2).
-# Extra options: :device (HIP ordinal), :sync, :batch_keys, :batch_bytes, :chunk_bytes.
+# Extra options: :device (HIP ordinal), :devices (ordinals or a count) + :mode (:replicated or
+# :partitioned) for one filter over several GPUs, :sync, :batch_keys, :batch_bytes, :chunk_bytes.
 require 'ffi'
 
 class Redis
@@ -55,10 +56,15 @@ class Redis
         [buf, offs, n]
       end
 
+      BF_MAX_DEVICES = 16
+      BF_MODE_REPLICATED = 0
+      BF_MODE_PARTITIONED = 1
+
       # struct bf_config (include/bfhip.h)
       class Config < FFI::Struct
         layout :struct_size, :uint32, :device, :int32, :batch_keys, :uint64, :batch_bytes, :uint64,
-               :shard_count, :uint32, :shard_index, :uint32, :shard_block_log2, :uint32, :flags, :uint32
+               :shard_count, :uint32, :shard_index, :uint32, :shard_block_log2, :uint32, :flags, :uint32,
+               :device_count, :uint32, :mode, :uint32, :devices, [:int32, BF_MAX_DEVICES]
       end
 
       attach_function :bf_version, [], :string
@@ -94,6 +100,7 @@ class Redis
         cfg[:batch_keys] = options.fetch(:batch_keys, 0)
         cfg[:batch_bytes] = options.fetch(:batch_bytes, 0)
         cfg[:flags] = config_flags
+        configure_devices(cfg, options)
         out = FFI::MemoryPointer.new(:pointer)
         check(HipFFI.bf_create(bits, options[:hashes], cfg, out), nil)
         @handle = FFI::AutoPointer.new(out.read_pointer, HipFFI.method(:bf_destroy))
@@ -228,6 +235,25 @@ class Redis
       # bf_config.flags of the device filter (HipTest picks a hash engine here).
       def config_flags
         0
+      end
+
+      # `devices: [0, 1, ...]` (or a count) and `mode: :replicated | :partitioned`: one filter
+      # over several GPUs from this process (bf_config.device_count / devices / mode).
+      def configure_devices(cfg, options)
+        devices = options[:devices]
+        return if devices.nil?
+
+        devices = (0...devices).to_a if devices.is_a?(Integer)
+        unless devices.is_a?(Array) && !devices.empty? && devices.size <= HipFFI::BF_MAX_DEVICES
+          raise ArgumentError, "devices must list 1..#{HipFFI::BF_MAX_DEVICES} GPU ordinals"
+        end
+
+        mode = (options[:mode] || :replicated).to_sym
+        raise ArgumentError, 'mode must be :replicated or :partitioned' unless %i[replicated partitioned].include?(mode)
+
+        cfg[:device_count] = devices.size
+        cfg[:mode] = mode == :partitioned ? HipFFI::BF_MODE_PARTITIONED : HipFFI::BF_MODE_REPLICATED
+        devices.each_with_index { |d, i| cfg[:devices][i] = d }
       end
 
       private

@@ -30,10 +30,32 @@ from redis_bloomfilter_amd import distributed as D  # noqa: E402
 from ref_engine import NumpyEngine  # noqa: E402
 
 
+def or_allreduce_case(rank, P):
+    """distributed.or_allreduce_ against the OR of every rank's tensor, for sizes that do
+    not divide into P 16-byte chunks."""
+    ok = True
+    for n in (1, 15, 1000, 4099):
+        mine = torch.from_numpy(np.random.default_rng([n, rank]).integers(0, 256, n, dtype=np.uint8))
+        t = mine.clone()
+        D.or_allreduce_(t)
+        want = np.zeros(n, np.uint8)
+        for r in range(P):
+            want |= np.random.default_rng([n, r]).integers(0, 256, n, dtype=np.uint8)
+        ok = ok and bool((t.numpy() == want).all())
+    return ok
+
+
 def main():
     dist.init_process_group("gloo")
     rank, P = dist.get_rank(), dist.get_world_size()
     cfg = json.loads(os.environ["BF_DIST_CFG"])
+    if cfg.get("case") == "or_allreduce":
+        flag = torch.tensor([1 if or_allreduce_case(rank, P) else 0])
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            print("DIST_RESULT", "ok" if flag.item() == 1 else "fail", flush=True)
+        dist.destroy_process_group()
+        sys.exit(0 if flag.item() == 1 else 1)
     m, k, b = cfg["m"], cfg["k"], cfg["block_log2"]
     orc = O.COracle()
     pf = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
@@ -44,7 +66,32 @@ def main():
              for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, cfg["n"])]
     probe += ["fresh-%d-%d" % (rank, i) for i in range(cfg["n"])]
     got = pf.include_many(probe)
-    s = pf.export_redis()
+    # the single-filter oracle over every rank's keys (each rank computes it)
+    all_keys = [("r%d-%d" % (r, int(v))) for r in range(P)
+                for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, cfg["n"])]
+    ib, io = O.pack_keys(all_keys)
+    bits = orc.new_bitset(m, k)
+    orc.insert_many(bits, m, k, ib, io)
+    want_s = orc.redis_string(bits)
+    del bits
+    s = pf.export_redis()                    # assembled on rank 0 only
+    export_ok = (s == want_s) if rank == 0 else (s is None)
+    write_ok = True
+    if pf.reach_bits <= (1 << 31):
+        # per-rank SETRANGE of each rank's own blocks into "Redis" (here one FakeRedis per
+        # process, merged below by OR, since each rank only writes its own blocks)
+        r = pkg.FakeRedis(max_string=1 << 40)
+        if rank == 0:
+            r.set("bf", b"stale")            # replace: rank 0 DELs first (the shared key)
+        pf.write_redis(r, "bf", chunk_bytes=4096)
+        parts = [None] * P
+        dist.all_gather_object(parts, r.get("bf") or b"")
+        width = max(len(x) for x in parts)
+        merged = np.zeros(width, np.uint8)
+        for x in parts:
+            merged[: len(x)] |= np.frombuffer(x, np.uint8)
+        write_ok = merged.tobytes() == want_s and width == len(want_s)
+    s = want_s if rank != 0 else s
     # round trip: a fresh partitioned filter loaded from the string answers identically
     pf2 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
     pf2.import_redis(s)
@@ -70,19 +117,15 @@ def main():
         del pf4
     ok = True
     if rank == 0 or True:
-        all_keys = [("r%d-%d" % (r, int(v))) for r in range(P)
-                    for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, cfg["n"])]
-        ib, io = O.pack_keys(all_keys)
         bits = orc.new_bitset(m, k)
         orc.insert_many(bits, m, k, ib, io)
-        want_s = orc.redis_string(bits)
         pb, po = O.pack_keys(probe)
         want = orc.include_many(bits, m, k, pb, po).astype(bool)
-        ok = (s == want_s) and same_shard and bool((got == want).all()) and bool((got2 == want).all()) \
-            and bool((got3 == want).all()) and all(bool((g == want).all()) for g in got45)
+        ok = export_ok and same_shard and write_ok and bool((got == want).all()) \
+            and bool((got2 == want).all()) and bool((got3 == want).all()) and all(bool((g == want).all()) for g in got45)
         if not ok:
-            print("rank %d MISMATCH: string %s (%d vs %d bytes), include %d diffs" %
-                  (rank, s == want_s, len(s), len(want_s), int((got != want).sum())), flush=True)
+            print("rank %d MISMATCH: export %s, write_redis %s, include %d diffs" %
+                  (rank, export_ok, write_ok, int((got != want).sum())), flush=True)
     flag = torch.tensor([1 if ok else 0])
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if rank == 0:

@@ -52,9 +52,11 @@ def test_ruby_ffi_binding_matches_header():
         assert n == arity[name], (name, n, arity[name])
     # the FFI struct layout lists bf_config's fields in order
     cfg = re.search(r"typedef struct bf_config \{(.*?)\} bf_config;", open(HEADER).read(), re.S).group(1)
-    fields = re.findall(r"\b(?:uint32_t|int32_t|uint64_t)\s+(\w+);", cfg)
-    layout = re.findall(r":(\w+), :(?:u?int\d+)", re.search(r"layout (.*?)\n\s*end", rb, re.S).group(1))
+    cfg = re.sub(r"/\*.*?\*/", "", cfg, flags=re.S)
+    fields = re.findall(r"\b(?:uint32_t|int32_t|uint64_t)\s+(\w+)(?:\[\w+\])?;", cfg)
+    layout = re.findall(r":(\w+), (?::u?int\d+|\[:u?int\d+, \w+\])", re.search(r"layout (.*?)\n\s*end", rb, re.S).group(1))
     assert layout == fields
+    assert "devices" in fields
 
 
 def _ruby_methods(src):

@@ -44,6 +44,21 @@ def test_partitioned_gloo(world, m, k, block_log2):
     assert "DIST_RESULT ok" in out.stdout
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_or_allreduce_gloo(world):
+    """The replicated filter's OR-all-reduce (all_to_all + local OR + all_gather)."""
+    env = dict(os.environ)
+    env["BF_DIST_CFG"] = json.dumps({"case": "or_allreduce"})
+    env["BFHIP_STANDALONE"] = "1"
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(HERE, "dist_worker.py")]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
 def test_ownership_map_properties(pkg):
     D = pkg.distributed if hasattr(pkg, "distributed") else __import__("redis_bloomfilter_amd.distributed",
                                                                        fromlist=["x"])

@@ -231,11 +231,17 @@ def test_torch_distributed_world1(pkg, oracle):
         bits = oracle.new_bitset(m, k)
         oracle.insert_many(bits, m, k, ib, io)
         want = oracle.include_many(bits, m, k, pb, po).astype(bool)
-        for cls, kw in ((D.PartitionedFilter, {"block_log2": 16}), (D.ReplicatedFilter, {})):
+        for cls, kw in ((D.PartitionedFilter, {"block_log2": 16}), (D.ReplicatedFilter, {}),
+                        (D.ReplicatedFilter, {"insert_mode": "or"})):
             f = cls(m, k, **kw)
             f.insert_many(keys)
             np.testing.assert_array_equal(f.include_many(probe), want)
             assert f.export_redis() == oracle.redis_string(bits)
+            if cls is D.PartitionedFilter:   # per-rank SETRANGE of the rank's blocks
+                r = pkg.FakeRedis()
+                r.set("bf", b"stale")
+                f.write_redis(r, "bf", chunk_bytes=1 << 14)
+                assert r.get("bf") == oracle.redis_string(bits)
             f.close()
         # the overlapped insert + include? step (async RCCL sends beside the kernels), through
         # the window route, the contiguous route, and the overflow fallback
