@@ -195,7 +195,7 @@ def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
 
 
 def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto",
-                overlap: bool = True):
+                overlap: bool = True, pipeline: bool = False):
     n, p, batch, prefill = CONFIGS[name]
     B = pkg.Bloomfilter
     m = B.optimal_m(n, p)
@@ -228,10 +228,25 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     out = torch.empty(batch, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream   # 0 = the null stream torch uses by default
+    pipeline = pipeline and mode == "single"
+    if pipeline:
+        # Pipelined steps (include/bfhip.h, bf_include_hash_dev): step i inserts batch i from
+        # its SHA-1 words (bf_insert_digests_dev: no hash pass), then answers include? batch i
+        # while hashing insert batch i+1 in the same kernel — the include? waits on its probes'
+        # memory latency and the hashing fills its idle VALUs.  Same work per step (one hash of
+        # each key, one insert of 2^24 keys, one include? of 2^24 keys after it) and the same
+        # answers (tests/test_gpu_digests.py::test_pipelined_steps_equal_plain_steps); the
+        # last step hashes batch 0's keys again so that every step does the same work.
+        digs = [torch.empty((batch, 4), dtype=torch.int32, device=dev) for _ in range(2)]
+        ikb0, iko0 = batches[0][0]
+        f.hash_many_dev(ikb0.data_ptr(), iko0.data_ptr(), batch, digs[0].data_ptr(), stream=sp)
+        step_no = [0]
 
     def insert(bt):
         ikb, iko = bt[0]
-        if rf is not None:
+        if pipeline:
+            f.insert_digests_dev(digs[step_no[0] % 2].data_ptr(), batch, stream=sp)
+        elif rf is not None:
             rf.insert_many_dev(ikb, iko, batch)
         elif pf is None:
             f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, stream=sp)
@@ -240,7 +255,13 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
 
     def include(bt):
         pkb, pko = bt[1]
-        if rf is not None:
+        if pipeline:
+            i = step_no[0]
+            nkb, nko = batches[(i + 1) % len(batches)][0]
+            f.include_hash_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), nkb.data_ptr(), nko.data_ptr(),
+                               batch, digs[(i + 1) % 2].data_ptr(), stream=sp)
+            step_no[0] = i + 1
+        elif rf is not None:
             out.copy_(rf.include_many_dev(pkb, pko, batch))
         elif pf is None:
             f.include_many_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), stream=sp)
@@ -303,6 +324,10 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         # binned path (bf_binned.hip): keys in, probe arrays written / read once, the bitset
         # streamed once (read + write for insert, read for include?)
         "bin_front": batch * (Lmean + 8) + P * 4,
+        # pipelined steps: the front pass reads 16 B of SHA-1 words per key; the include?
+        # kernel also reads the next batch's keys and writes their words
+        "bin_front_digest": batch * 16 + P * 4,
+        "include_hash_kernel": batch * (Lmean + 8 + 1 + k * GRANULE) + batch * (Lmean + 8 + 16),
         "bin_front_keys": batch * (Lmean + 8) + P * 8 + batch,
         "bin_mid": P * 4 * 3,
         "bin_mid_keys": P * 8 * 3,
@@ -327,7 +352,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             kt["algo_bytes"] = algo[name]
             kt["GBps"] = algo[name] / (kt["ms"] / 1e3) / 1e9
     res = {
-        "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3),
+        "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3), "pipelined": pipeline,
         "wall_s": wall, "steps": steps,
         "keys_per_s": 2 * batch * D.world * steps / wall,
         "insert": {"op_ms": ins_ms, "keys_per_s": batch / (ins_ms / 1e3),
@@ -484,12 +509,15 @@ def main():
                     help="auto: single GPU at N=1, replicated at N=2 (filter fits one GPU), partitioned from N=4")
     ap.add_argument("--no-overlap", action="store_true",
                     help="partitioned: run insert then include? as separate calls (no exchange overlap)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="single GPU: 1 = pipelined steps (next insert batch hashed inside the include? "
+                         "kernel, inserted from its SHA-1 words), 0 = plain insert_many + include_many")
     args = ap.parse_args()
 
     D = Dist(need_group=(args.mode in ("partitioned", "replicated")))
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
-                                  mode=args.mode, overlap=not args.no_overlap)
+                                  mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline))
     secondary = {}
     if D.world == 1 and not args.no_secondary:
         for name in ("1m", "100m", "10b"):
@@ -542,7 +570,13 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom_name,
                      "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK if achieved else None,
-                     "traffic": traffic, "algo_bytes": dom.get("algo_bytes"), "keys_per_launch": batch,
+                     "traffic": traffic,
+                     # the PMC-measured fabric bytes per launch over the same launch time: what
+                     # the kernel actually moves (128 B line fills; SURVEY's 64 B granule model
+                     # undercounts them and overcounts the early exit's skipped probes)
+                     "traffic_GBps": traffic / (dom["ms"] / 1e3) / 1e9 if traffic else None,
+                     "traffic_frac": traffic / (dom["ms"] / 1e3) / HBM_PEAK if traffic else None,
+                     "algo_bytes": dom.get("algo_bytes"), "keys_per_launch": batch,
                      "kernel_ms": dom["ms"], "timing": "HIP events on the launch stream around each kernel, "
                                                        "inside the timed region (bf_profile)"},
         "cpu_baseline": cpu,

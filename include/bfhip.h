@@ -158,6 +158,30 @@ int  bf_include_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
                          uint64_t n, uint8_t* d_out, void* stream);
 int  bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets,
                          uint64_t n, uint64_t* d_out, void* stream);
+/* ---- SHA-1 words as a reusable intermediate.  A key's k offsets depend only on the first
+ *      four big-endian words H0..H3 of its SHA-1 (ruby.rb:42-47's h[0..3]), so a batch hashed
+ *      once can be inserted and tested without hashing again (the reference's check-then-add
+ *      loop, bf_10_000.rb:34-43, hashes every key twice).  Digests: 4 uint32 per key, H0..H3,
+ *      16-byte aligned.
+ *   bf_hash_many_dev        keys -> digests
+ *   bf_insert_digests_dev   bf_insert_many_dev on digests (d_per_key_new must be NULL)
+ *   bf_include_digests_dev  bf_include_many_dev on digests
+ *   bf_include_hash_dev     include? of one key batch fused with hashing another batch into
+ *                           digests: the include? is bound by its probes' memory latency and
+ *                           its VALUs mostly idle, so the other batch's SHA-1 runs there
+ *                           nearly free — e.g. the next insert batch of a stream of
+ *                           insert + include? steps, which then goes in with
+ *                           bf_insert_digests_dev and skips its own hash pass.  The include?
+ *                           answers are those of the filter as it stands (the hashing touches
+ *                           no filter state). */
+int  bf_hash_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                      uint32_t* d_digests, void* stream);
+int  bf_insert_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint32_t* d_any_new,
+                           uint8_t* d_per_key_new, void* stream);
+int  bf_include_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint8_t* d_out, void* stream);
+int  bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                         uint8_t* d_out, const uint8_t* d_next_key_bytes, const uint64_t* d_next_offsets,
+                         uint64_t n_next, uint32_t* d_next_digests, void* stream);
 /* The device bitset (Redis byte order, device_bytes long, zero past the reachable prefix). */
 int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
 /* How an insert batch of n keys will run (no launch): *binned = 1 for the binned

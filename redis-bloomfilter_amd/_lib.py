@@ -83,6 +83,10 @@ SIGNATURES = {
     "bf_include_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_indexes_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_device_bits": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), _u64p]),
+    "bf_hash_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_insert_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp, _vp]),
+    "bf_include_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
+    "bf_include_hash_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_insert_plan": (ctypes.c_int, [_vp, _u64, _u32p, _u64p]),
     "bf_track_dirty": (ctypes.c_int, [_vp, _u32]),
     "bf_dirty_ranges": (ctypes.c_int, [_vp, _u64p, _u32, _u32p, _u64p, _u32]),
@@ -383,6 +387,24 @@ class Filter:
 
     def indexes_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream=None) -> None:
         _check(self._lib.bf_indexes_many_dev(self.handle, d_keys, d_offsets, int(n), d_out,
+                                             self._s(stream)), self._h)
+
+    # -- SHA-1 words as an intermediate (digests: 4 uint32 per key, 16-byte aligned)
+    def hash_many_dev(self, d_keys: int, d_offsets: int, n: int, d_digests: int, stream=None) -> None:
+        _check(self._lib.bf_hash_many_dev(self.handle, d_keys, d_offsets, int(n), d_digests, self._s(stream)),
+               self._h)
+
+    def insert_digests_dev(self, d_digests: int, n: int, d_any_new: int = 0, stream=None) -> None:
+        _check(self._lib.bf_insert_digests_dev(self.handle, d_digests, int(n), d_any_new or None, None,
+                                               self._s(stream)), self._h)
+
+    def include_digests_dev(self, d_digests: int, n: int, d_out: int, stream=None) -> None:
+        _check(self._lib.bf_include_digests_dev(self.handle, d_digests, int(n), d_out, self._s(stream)), self._h)
+
+    def include_hash_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, d_next_keys: int,
+                         d_next_offsets: int, n_next: int, d_next_digests: int, stream=None) -> None:
+        _check(self._lib.bf_include_hash_dev(self.handle, d_keys, d_offsets, int(n), d_out, d_next_keys or None,
+                                             d_next_offsets or None, int(n_next), d_next_digests or None,
                                              self._s(stream)), self._h)
 
     def _s(self, stream):

@@ -1353,6 +1353,104 @@ int bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
     return run_dev(h, BF_OP_INDEXES, d_key_bytes, d_offsets, n, nullptr, d_out, nullptr, stream);
 }
 
+namespace {
+// The digest ops: binned insert when it pays (as for keys), else one direct lane per digest.
+int run_digests(bf_handle* h, BfOp op, const uint32_t* d_dig, uint64_t n, uint8_t* d_out8, uint32_t* d_flag,
+                void* stream) {
+    if (!h) return BF_EINVAL;
+    if (h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (n == 0) return BF_OK;
+    if (!d_dig) return set_err(h, BF_EINVAL, "d_digests is NULL");
+    if (reinterpret_cast<uintptr_t>(d_dig) & 15u) return set_err(h, BF_EINVAL, "d_digests must be 16-byte aligned");
+    if (op == BF_OP_INCLUDE && !d_out8) return set_err(h, BF_EINVAL, "d_out is NULL");
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter");
+    if (h->engine != BF_ENGINE_RUBY) return set_err(h, BF_EINVAL, "digests carry the ruby driver's derivation only");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    const uint4* dig = reinterpret_cast<const uint4*>(d_dig);
+    const bool is_insert = op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS;
+    BfBinPlan plan;
+    const uint64_t sub = std::max<uint64_t>(1, bf_binned_max_keys(h->k, h->dev_bytes, h->bin_region_log2));
+    if (is_insert && use_binned(h, std::min(n, sub), false, &plan)) {
+        for (uint64_t c0 = 0; c0 < n; c0 += sub) {
+            const uint64_t cn = std::min(sub, n - c0);
+            if (cn != std::min(n, sub) && !bf_binned_plan(h->dev_bytes, cn, h->k, h->bin_region_log2, false, &plan))
+                return set_err(h, BF_EINVAL, "binned plan failed for a tail of %llu keys", (unsigned long long)cn);
+            int rc = ensure_scratch(h, plan.scratch_bytes);
+            if (rc) return rc;
+            BfMarks* mk = prof_begin(h, so.s);
+            HIPCHK(h, bf_launch_insert_binned_digests(h->g, plan, h->dev_bytes, dig + c0, cn, h->d_bin_scratch,
+                                                      op == BF_OP_INSERT_FLAGS ? d_flag : nullptr, so.s, mk));
+        }
+        return BF_OK;
+    }
+    BfMarks* mk = prof_begin(h, so.s);
+    HIPCHK(h, bf_launch_digests(op, h->g, dig, n, d_out8, nullptr, d_flag, so.s));
+    bf_mark(mk, so.s, op == BF_OP_INCLUDE ? "digest_kernel<INCLUDE>" : "digest_kernel<INSERT>");
+    return BF_OK;
+}
+}  // namespace
+
+int bf_hash_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                     uint32_t* d_digests, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (n && !d_digests) return set_err(h, BF_EINVAL, "d_digests is NULL");
+    if (reinterpret_cast<uintptr_t>(d_digests) & 15u) return set_err(h, BF_EINVAL, "d_digests must be 16-byte aligned");
+    if (n == 0) return BF_OK;
+    if (!d_offsets || !d_key_bytes) return set_err(h, BF_EINVAL, "NULL device pointer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    uint64_t bias = 0;
+    const uint8_t* k16 = align_keys(d_key_bytes, &bias);
+    BfMarks* mk = prof_begin(h, so.s);
+    HIPCHK(h, bf_launch_keys(BF_OP_HASH, h->g, k16, d_offsets, bias, n, nullptr,
+                             reinterpret_cast<uint64_t*>(d_digests), nullptr, so.s));
+    bf_mark(mk, so.s, "bf_keys_kernel<HASH>");
+    return BF_OK;
+}
+
+int bf_insert_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint32_t* d_any_new,
+                          uint8_t* d_per_key_new, void* stream) {
+    if (h && !h->multi && d_per_key_new) return set_err(h, BF_EINVAL, "per_key_new needs the keys (bf_insert_many_dev)");
+    return run_digests(h, d_any_new ? BF_OP_INSERT_FLAGS : BF_OP_INSERT, d_digests, n, nullptr, d_any_new, stream);
+}
+
+int bf_include_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint8_t* d_out, void* stream) {
+    return run_digests(h, BF_OP_INCLUDE, d_digests, n, d_out, nullptr, stream);
+}
+
+int bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                        uint8_t* d_out, const uint8_t* d_next_key_bytes, const uint64_t* d_next_offsets,
+                        uint64_t n_next, uint32_t* d_next_digests, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (n && (!d_key_bytes || !d_offsets || !d_out)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (n_next && (!d_next_key_bytes || !d_next_offsets || !d_next_digests))
+        return set_err(h, BF_EINVAL, "NULL device pointer (next batch)");
+    if (reinterpret_cast<uintptr_t>(d_next_digests) & 15u)
+        return set_err(h, BF_EINVAL, "d_next_digests must be 16-byte aligned");
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter");
+    if (h->engine != BF_ENGINE_RUBY) return set_err(h, BF_EINVAL, "digests carry the ruby driver's derivation only");
+    if (n + n_next == 0) return BF_OK;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    uint64_t bias = 0, nbias = 0;
+    const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
+    const uint8_t* nk16 = n_next ? align_keys(d_next_key_bytes, &nbias) : nullptr;
+    BfMarks* mk = prof_begin(h, so.s);
+    HIPCHK(h, bf_launch_include_hash(h->g, k16, d_offsets, bias, n, d_out, nk16, d_next_offsets, nbias, n_next,
+                                     reinterpret_cast<uint4*>(d_next_digests), so.s));
+    bf_mark(mk, so.s, "include_hash_kernel");
+    return BF_OK;
+}
+
 int bf_stream(bf_handle* h, void** stream) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h || !stream) return BF_EINVAL;

@@ -97,7 +97,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     return r;
 }
 
-template <bool KEYS, int SLOTS>
+// DIG: the keys arrive as their SHA-1 words (keys16 is then a uint4 array, 16 B per key,
+// offsets unused): no staging, no hashing — the front pass is a partition pass.
+template <bool KEYS, int SLOTS, bool DIG = false>
 __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                           const uint64_t* __restrict__ offsets, uint64_t bias,
                                                           uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
@@ -128,19 +130,25 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
         const uint64_t key0 = tile * tile_keys;
         const uint32_t tk = (uint32_t)((n - key0) < (uint64_t)tile_keys ? (n - key0) : tile_keys);
         uint4 H0 = make_uint4(0, 0, 0, 0), H1 = make_uint4(0, 0, 0, 0);
-        for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off, s_stage,
-            [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+        if constexpr (DIG) {
+            const uint4* dig = reinterpret_cast<const uint4*>(keys16);
+            if (t < tk) H0 = dig[key0 + t];
+            if (kTile + t < tk) H1 = dig[key0 + kTile + t];
+        } else {
+            for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off,
+                                           s_stage, [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
                 uint32_t H[5];
                 sha1_any<decltype(staged)::value>(src, s, L, H);
                 H0 = make_uint4(H[0], H[1], H[2], H[3]);
             });
-        if (tk > (uint32_t)kTile) {   // workgroup-uniform: the second key of each lane
-            for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0 + kTile, tk - kTile, s_off, s_stage,
-                [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
-                    uint32_t H[5];
-                    sha1_any<decltype(staged)::value>(src, s, L, H);
-                    H1 = make_uint4(H[0], H[1], H[2], H[3]);
-                });
+            if (tk > (uint32_t)kTile) {   // workgroup-uniform: the second key of each lane
+                for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0 + kTile, tk - kTile, s_off, s_stage,
+                    [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                        uint32_t H[5];
+                        sha1_any<decltype(staged)::value>(src, s, L, H);
+                        H1 = make_uint4(H[0], H[1], H[2], H[3]);
+                    });
+            }
         }
         const bool live0 = t < tk;
         const bool live1 = kpl == 2 && kTile + t < tk;
@@ -202,17 +210,18 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
 }
 
 // insert: 8 waves per SIMD (2 workgroups per CU: 77 KiB of LDS, <= 64 VGPRs)
+template <bool DIG>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_front_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
                       uint64_t bias, uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block, uint32_t sup_log2,
                       uint32_t nsup, uint32_t* __restrict__ level1, uint32_t* __restrict__ level1_key,
                       uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint8_t* __restrict__ out8) {
-    bin_front_body<false, kSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1,
-                                  level1_key, stab, gcnt, out8);
+    bin_front_body<false, kSlots, DIG>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup,
+                                       level1, level1_key, stab, gcnt, out8);
 }
 
 // 12 < k <= 16: 16 probe slots per lane (64 KiB sort buffer, one workgroup per CU)
-template <bool KEYS>
+template <bool KEYS, bool DIG = false>
 __global__ __launch_bounds__(kTile) void bin_front_wide_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
                                                                const uint64_t* __restrict__ offsets, uint64_t bias,
                                                                uint64_t n, uint32_t tile_keys,
@@ -221,8 +230,8 @@ __global__ __launch_bounds__(kTile) void bin_front_wide_kernel(BfGeom g, const u
                                                                uint32_t* __restrict__ level1_key,
                                                                uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt,
                                                                uint8_t* __restrict__ out8) {
-    bin_front_body<KEYS, kWideSlots>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup, level1,
-                                     level1_key, stab, gcnt, out8);
+    bin_front_body<KEYS, kWideSlots, DIG>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup,
+                                          level1, level1_key, stab, gcnt, out8);
 }
 
 // include?: key indices ride along (123 KiB of LDS: one workgroup per CU)
@@ -1049,10 +1058,24 @@ hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c
 }
 
 // bin_front .. bin_mid: the batch's probes in region-sorted chunk blocks.
+// dig: keys16 holds the keys' SHA-1 words (uint4 per key) instead of key bytes (inserts only).
 hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c, const uint8_t* keys16,
                             const uint64_t* offsets, uint64_t bias, uint64_t n, uint8_t* out8, hipStream_t s,
-                            BfMarks* mk) {
+                            BfMarks* mk, bool dig = false) {
     const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
+    if (dig) {
+        if (p.with_keys) return hipErrorInvalidValue;
+        if (g.k > (uint32_t)kSlots)
+            hipLaunchKernelGGL((bin_front_wide_kernel<false, true>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16,
+                               offsets, bias, n, p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1,
+                               c.level1_key, c.stab, c.gcnt, out8);
+        else
+            hipLaunchKernelGGL(bin_front_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+                               p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab,
+                               c.gcnt, out8);
+        bf_mark(mk, s, "bin_front_digest");
+        return launch_groups_mid(g, p, c, s, mk);
+    }
     if (g.k > (uint32_t)kSlots) {
         if (p.with_keys)
             hipLaunchKernelGGL(bin_front_wide_kernel<true>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
@@ -1067,7 +1090,7 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
                            p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
                            out8);
     else
-        hipLaunchKernelGGL(bin_front_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
+        hipLaunchKernelGGL(bin_front_kernel<false>, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n,
                            p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab, c.gcnt,
                            out8);
     bf_mark(mk, s, p.with_keys ? "bin_front_keys" : "bin_front");
@@ -1195,6 +1218,17 @@ hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t
     if (p.with_keys) return hipErrorInvalidValue;
     const Carve c = carve(p, scratch);
     hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, nullptr, s, mk);
+    if (e != hipSuccess) return e;
+    return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
+}
+
+hipError_t bf_launch_insert_binned_digests(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                           const uint4* dig, uint64_t n, void* scratch, uint32_t* any_flag,
+                                           hipStream_t s, BfMarks* mk) {
+    if (n == 0) return hipSuccess;
+    if (p.with_keys) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_partition(g, p, c, reinterpret_cast<const uint8_t*>(dig), nullptr, 0, n, nullptr, s, mk, true);
     if (e != hipSuccess) return e;
     return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
 }

@@ -34,6 +34,7 @@ enum BfOp : int {
     BF_OP_INSERT_FLAGS = 3,  // ... and report which keys / whether any bit flipped (ruby.rb:61-62)
     BF_OP_ROUTE        = 4,  // owner-local offset (out64) + owner shard (out8) per probe,
                              // per-owner probe counts accumulated into counts[P]
+    BF_OP_HASH         = 5,  // the key's SHA-1 words H0..H3 (16 B per key, out64 as uint4[])
 };
 
 // Keys: byte j of the packed buffer for offset o is keys16[o + bias - 0] where
@@ -94,6 +95,10 @@ bool bf_binned_plan(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t pref
 hipError_t bf_launch_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                    const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                    void* scratch, uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr);
+// The same on keys given as their SHA-1 words (bf_hash_many_dev's output): no hash pass.
+hipError_t bf_launch_insert_binned_digests(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                           const uint4* dig, uint64_t n, void* scratch, uint32_t* any_flag,
+                                           hipStream_t s, BfMarks* marks = nullptr);
 // Owner side of a partitioned filter: `count` routed shard-local offsets (uint32
 // when route32, else uint64) ORed into the shard through the same pipeline.
 uint64_t bf_binned_max_offsets(uint64_t bitset_bytes, uint32_t pref_region_log2);
@@ -188,3 +193,11 @@ hipError_t bf_launch_or(uint32_t* dst, const uint32_t* src, uint64_t nwords, hip
 
 // out[i] = in[i] (uint32 -> uint64), i < count: the host-pointer calls' relative offsets.
 hipError_t bf_launch_widen_offsets(const uint32_t* in, uint64_t* out, uint64_t count, hipStream_t s);
+
+// The ops (INDEXES, INCLUDE, INSERT, INSERT_FLAGS) on precomputed SHA-1 words (16 B per key).
+hipError_t bf_launch_digests(BfOp op, const BfGeom& g, const uint4* dig, uint64_t n, uint8_t* out8, uint64_t* out64,
+                             uint32_t* any_flag, hipStream_t s);
+// include? of (keys16, offsets, n) -> out8, fused with the SHA-1 of (skeys16, soffsets, sn) -> sdig.
+hipError_t bf_launch_include_hash(const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets, uint64_t bias,
+                                  uint64_t n, uint8_t* out8, const uint8_t* skeys16, const uint64_t* soffsets,
+                                  uint64_t sbias, uint64_t sn, uint4* sdig, hipStream_t s);

@@ -24,30 +24,14 @@ namespace {
 
 using namespace bfdev;
 
-// include? probe load policy (A/B knob, build-time): 0 plain, 1 non-temporal,
-// 2 relaxed agent-scope load (L1 bypass).  Random 4 B probes never hit L1.
-#ifndef BF_PROBE_LOAD
-#define BF_PROBE_LOAD 0
-#endif
-__device__ __forceinline__ uint32_t probe_load(const uint32_t* p) {
-#if BF_PROBE_LOAD == 1
-    return __builtin_nontemporal_load(p);
-#elif BF_PROBE_LOAD == 2
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    return *p;
-#endif
-}
-
-template <int OP, bool STAGED>
-__device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uint32_t s, uint32_t L,
-                                       uint64_t key, uint8_t* __restrict__ out8,
-                                       uint64_t* __restrict__ out64, uint32_t& newflag,
-                                       uint32_t* hist) {
-    uint32_t H[5];
-    sha1_any<STAGED>(src, s, L, H);
+template <int OP, typename Side>
+__device__ __forceinline__ void digest_op(const BfGeom& g, const uint32_t H[4], uint64_t key,
+                                          uint8_t* __restrict__ out8, uint64_t* __restrict__ out64,
+                                          uint32_t& newflag, uint32_t* hist, Side&& side) {
     const uint32_t k = g.k;
-    if constexpr (OP == BF_OP_INDEXES) {
+    if constexpr (OP == BF_OP_HASH) {
+        reinterpret_cast<uint4*>(out64)[key] = make_uint4(H[0], H[1], H[2], H[3]);
+    } else if constexpr (OP == BF_OP_INDEXES) {
         for (uint32_t i = 0; i < k; ++i)
             out64[key * k + i] = probe_offset(g, H[0], H[1], H[2], H[3], i);
     } else if constexpr (OP == BF_OP_ROUTE) {
@@ -67,6 +51,7 @@ __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uin
         uint32_t ok = 1u;
         uint32_t i0 = 0;
         uint32_t rend = (g.first_round && g.first_round < k) ? g.first_round : k;
+        bool first = true;
         while (i0 < k) {
             const uint32_t e = (i0 + kChunk < rend) ? i0 + kChunk : rend;
             uint32_t v[kChunk], sh[kChunk];
@@ -76,8 +61,12 @@ __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uin
                 if (i0 + c < e) {
                     const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + c);
                     sh[c] = (uint32_t)(o ^ 7u) & 31u;
-                    v[c] = probe_load(g.bits + (o >> 5));
+                    v[c] = g.bits[o >> 5];
                 }
+            }
+            if (first) {
+                side();
+                first = false;
             }
 #pragma unroll
             for (int c = 0; c < kChunk; ++c) ok &= v[c] >> sh[c];
@@ -122,6 +111,20 @@ __device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uin
             newflag = isnew;
         }
     }
+}
+
+struct NoSide {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+template <int OP, bool STAGED>
+__device__ __forceinline__ void key_op(const BfGeom& g, const uint32_t* src, uint32_t s, uint32_t L,
+                                       uint64_t key, uint8_t* __restrict__ out8,
+                                       uint64_t* __restrict__ out64, uint32_t& newflag,
+                                       uint32_t* hist) {
+    uint32_t H[5];
+    sha1_any<STAGED>(src, s, L, H);
+    digest_op<OP>(g, H, key, out8, out64, newflag, hist, NoSide{});
 }
 
 template <int OP>
@@ -183,6 +186,109 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
             if (b != 0ull && (t & 63u) == (uint32_t)__builtin_ctzll(b))
                 __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+}
+
+// The ops on precomputed SHA-1 words (bf_hash_many_dev's output, 16 B per key): one lane per
+// key, no hashing.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void bf_digest_kernel(BfGeom g, const uint4* __restrict__ dig, uint64_t n,
+                                                           uint8_t* __restrict__ out8, uint64_t* __restrict__ out64,
+                                                           uint32_t* __restrict__ any_flag) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint32_t newflag = 0;
+    if (j < n) {
+        const uint4 d = dig[j];
+        const uint32_t H[4] = {d.x, d.y, d.z, d.w};
+        digest_op<OP>(g, H, j, out8, out64, newflag, nullptr, NoSide{});
+    }
+    if constexpr (OP == BF_OP_INSERT_FLAGS) {
+        if (any_flag) {
+            const unsigned long long b = __ballot(newflag != 0);
+            if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
+                __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// include? of batch Q fused with the SHA-1 of another batch S (S's digests out): both key
+// tiles are staged into LDS up front (8 KiB each, so the LDS per workgroup — and the 32
+// waves per CU the include? needs for its memory parallelism — stay what the plain include?
+// kernel has); the lane hashes its Q key, issues the first probe round, hashes its S key
+// while those loads are in flight, stores the S digest, then finishes the probes.  The
+// include? waits on its probes' memory latency with its VALUs mostly idle, so S's hashing
+// costs little here, and S's insert then skips its own hash pass (bin_front_digest).
+// A tile whose bytes exceed its 8 KiB stage hashes from global memory instead.
+constexpr int kHalfStageVec = 480;   // 7.5 KiB per stage: 2 stages + offsets <= 20 KiB, 8 workgroups per CU
+
+// Stages one tile's offsets and bytes; returns whether the bytes fit the stage (uniform).
+__device__ __forceinline__ bool stage_tile(const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
+                                           uint64_t bias, uint64_t key0, uint32_t cnt, uint64_t* s_off,
+                                           uint4* s_stage, uint64_t* abase_out) {
+    const uint32_t t = threadIdx.x;
+    if (cnt == 0) return true;
+    // s_off was filled (and a barrier passed) by the caller
+    const uint64_t start = s_off[0];
+    const uint64_t end = s_off[cnt];
+    const uint64_t abase = start & ~(uint64_t)15;
+    const uint64_t nvec = (end - abase + 15) >> 4;
+    *abase_out = abase;
+    if (nvec > (uint64_t)kHalfStageVec) return false;
+    const uint4* gv = reinterpret_cast<const uint4*>(keys16 + abase);
+    for (uint32_t v = t; v < (uint32_t)nvec; v += kBlock) s_stage[v] = gv[v];
+    (void)offsets; (void)bias; (void)key0;
+    return true;
+}
+
+__device__ __forceinline__ void hash_tile_key(const uint8_t* __restrict__ keys16, const uint64_t* s_off,
+                                              const uint4* s_stage, bool staged, uint64_t abase, uint32_t t,
+                                              uint32_t H[5]) {
+    if (staged) {
+        sha1_key_staged(reinterpret_cast<const uint32_t*>(s_stage), (uint32_t)(s_off[t] - abase),
+                        (uint32_t)(s_off[t + 1] - s_off[t]), H);
+    } else {
+        const uint64_t ks = s_off[t];
+        const uint64_t kbase = ks & ~(uint64_t)3;
+        sha1_key(reinterpret_cast<const uint32_t*>(keys16 + kbase), (uint32_t)(ks - kbase),
+                 (uint32_t)(s_off[t + 1] - ks), H);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void bf_include_hash_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
+                                                                 const uint64_t* __restrict__ offsets, uint64_t bias,
+                                                                 uint64_t n, uint8_t* __restrict__ out8,
+                                                                 const uint8_t* __restrict__ skeys16,
+                                                                 const uint64_t* __restrict__ soffsets, uint64_t sbias,
+                                                                 uint64_t sn, uint4* __restrict__ sdig) {
+    __shared__ uint64_t s_off[kBlock + 1], s_soff[kBlock + 1];
+    __shared__ uint4 s_stage[kHalfStageVec + kStageSlackVec], s_sstage[kHalfStageVec + kStageSlackVec];
+    const uint64_t blk0 = (uint64_t)blockIdx.x * kBlock;
+    const uint32_t t = threadIdx.x;
+    const uint32_t cnt = blk0 < n ? (n - blk0 < (uint64_t)kBlock ? (uint32_t)(n - blk0) : (uint32_t)kBlock) : 0u;
+    const uint32_t scnt = blk0 < sn ? (sn - blk0 < (uint64_t)kBlock ? (uint32_t)(sn - blk0) : (uint32_t)kBlock) : 0u;
+    if (t < cnt) s_off[t] = offsets[blk0 + t] + bias;
+    if (t == 0 && cnt) s_off[cnt] = offsets[blk0 + cnt] + bias;
+    if (t < scnt) s_soff[t] = soffsets[blk0 + t] + sbias;
+    if (t == 0 && scnt) s_soff[scnt] = soffsets[blk0 + scnt] + sbias;
+    __syncthreads();
+    uint64_t abase = 0, sabase = 0;
+    const bool qstaged = stage_tile(keys16, offsets, bias, blk0, cnt, s_off, s_stage, &abase);
+    const bool sstaged = stage_tile(skeys16, soffsets, sbias, blk0, scnt, s_soff, s_sstage, &sabase);
+    __syncthreads();
+    auto side = [&]() {
+        if (t < scnt) {
+            uint32_t H[5];
+            hash_tile_key(skeys16, s_soff, s_sstage, sstaged, sabase, t, H);
+            sdig[blk0 + t] = make_uint4(H[0], H[1], H[2], H[3]);
+        }
+    };
+    if (t < cnt) {
+        uint32_t H[5];
+        hash_tile_key(keys16, s_off, s_stage, qstaged, abase, t, H);
+        uint32_t newflag = 0;
+        digest_op<BF_OP_INCLUDE>(g, H, blk0 + t, out8, nullptr, newflag, nullptr, side);
+    } else {
+        side();
     }
 }
 
@@ -431,6 +537,7 @@ hipError_t bf_launch_keys(BfOp op, const BfGeom& g, const uint8_t* keys16, const
         case BF_OP_INCLUDE: BF_LAUNCH(BF_OP_INCLUDE); break;
         case BF_OP_INSERT: BF_LAUNCH(BF_OP_INSERT); break;
         case BF_OP_INSERT_FLAGS: BF_LAUNCH(BF_OP_INSERT_FLAGS); break;
+        case BF_OP_HASH: BF_LAUNCH(BF_OP_HASH); break;
         case BF_OP_ROUTE:
             if (!counts || g.shards == 0 || g.shards > 255) return hipErrorInvalidValue;
             BF_LAUNCH(BF_OP_ROUTE);
@@ -554,5 +661,33 @@ hipError_t bf_launch_or(uint32_t* dst, const uint32_t* src, uint64_t nwords, hip
 hipError_t bf_launch_widen_offsets(const uint32_t* in, uint64_t* out, uint64_t count, hipStream_t s) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(widen_offsets_kernel, dim3(stream_grid(count)), dim3(256), 0, s, in, out, count);
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_digests(BfOp op, const BfGeom& g, const uint4* dig, uint64_t n, uint8_t* out8, uint64_t* out64,
+                             uint32_t* any_flag, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)blocks), block(kBlock);
+    switch (op) {
+        case BF_OP_INDEXES: hipLaunchKernelGGL(bf_digest_kernel<BF_OP_INDEXES>, grid, block, 0, s, g, dig, n, out8, out64, any_flag); break;
+        case BF_OP_INCLUDE: hipLaunchKernelGGL(bf_digest_kernel<BF_OP_INCLUDE>, grid, block, 0, s, g, dig, n, out8, out64, any_flag); break;
+        case BF_OP_INSERT: hipLaunchKernelGGL(bf_digest_kernel<BF_OP_INSERT>, grid, block, 0, s, g, dig, n, out8, out64, any_flag); break;
+        case BF_OP_INSERT_FLAGS: hipLaunchKernelGGL(bf_digest_kernel<BF_OP_INSERT_FLAGS>, grid, block, 0, s, g, dig, n, out8, out64, any_flag); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_include_hash(const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets, uint64_t bias,
+                                  uint64_t n, uint8_t* out8, const uint8_t* skeys16, const uint64_t* soffsets,
+                                  uint64_t sbias, uint64_t sn, uint4* sdig, hipStream_t s) {
+    const uint64_t m = n > sn ? n : sn;
+    if (m == 0) return hipSuccess;
+    const uint64_t blocks = (m + kBlock - 1) / kBlock;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bf_include_hash_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, s, g, keys16, offsets, bias, n,
+                       out8, skeys16, soffsets, sbias, sn, sdig);
     return hipGetLastError();
 }
