@@ -248,8 +248,9 @@ int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_of
  *                        as uint32, in an unspecified order, with d_slot (nullable)
  *                        alongside; each window feeds one send of a grouped send/recv
  *                        exchange.  d_counts holds nwin uint64.  If some d_counts[w] >
- *                        window_cap (a skewed batch), that window's contents are undefined:
- *                        route again with window_cap = n*k, which always fits.
+ *                        window_cap (a skewed batch), that window's contents are undefined
+ *                        (the windowed owner ops and combines skip it): route again with
+ *                        window_cap = n*k, which always fits.
  * bf_shard_insert_hi_dev / bf_shard_test_hi_dev   the owner ops on the uint32 entries of
  *                        sub-range hi (local offset = (hi << 32) | entry).
  * bf_combine_windows_dev bf_combine_dev over that layout: d_bits and d_slot indexed by window
@@ -277,6 +278,24 @@ int  bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d
 int  bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint32_t* d_slot,
                                    uint64_t window_cap, uint32_t nwin, const uint64_t* d_counts, uint64_t n,
                                    uint8_t* d_out, void* stream);
+/* The sync-free exchange (no host wait for counts): every source sends its whole windows,
+ * window_cap entries each, so the receive layout is fixed and the live counts stay on the
+ * device.  The owner ops then run over nwin received windows of sub-range hi: window w holds
+ * d_local32[w*window_cap ..], of which the first min(d_counts[w*count_stride], window_cap)
+ * entries are live (local offset (hi << 32) | entry); the test writes one byte per window
+ * entry to d_bits (entries past a count: unspecified).  A window whose count exceeds
+ * window_cap overflowed in the route (runs past the cap were dropped, leaving unwritten
+ * entries below it) and is skipped whole, here and by the windowed combines: the caller
+ * learns of it from the counts and re-does the batch (PartitionedFilter replays it through
+ * the synced exchange).  A window_cap that is a multiple of
+ * BF_WINDOW_CAP_ALIGN lets the owner take the binned (sort by region) path. */
+#define BF_WINDOW_CAP_ALIGN 12288
+int  bf_shard_insert_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
+                                 const uint64_t* d_counts, uint32_t count_stride, uint32_t hi, uint32_t* d_any_new,
+                                 void* stream);
+int  bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
+                               const uint64_t* d_counts, uint32_t count_stride, uint32_t hi, uint8_t* d_bits,
+                               void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
 int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,

@@ -103,6 +103,8 @@ SIGNATURES = {
     "bf_route_window_split": (ctypes.c_int, [_vp, _u32p]),
     "bf_route_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     "bf_shard_insert_hi_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
+    "bf_shard_insert_windows_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u32, _u32, _vp, _vp]),
+    "bf_shard_test_windows_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u32, _u32, _vp, _vp]),
     "bf_shard_test_hi_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
     "bf_combine_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp]),
     "bf_pack_segments_dev": (ctypes.c_int, [_vp, _vp, _vp, _u32, _u64, _vp, _vp]),
@@ -472,6 +474,17 @@ class Filter:
                                    n: int, d_out: int, stream=None) -> None:
         _check(self._lib.bf_combine_windows_packed_dev(self.handle, d_packed, d_slot, int(window_cap), int(nwin),
                                                        d_counts, int(n), d_out, self._s(stream)), self._h)
+
+    def shard_insert_windows_dev(self, d_local32: int, window_cap: int, nwin: int, d_counts: int, count_stride: int,
+                                 hi: int, d_any_new: int = 0, stream=None) -> None:
+        _check(self._lib.bf_shard_insert_windows_dev(self.handle, d_local32, int(window_cap), int(nwin), d_counts,
+                                                     int(count_stride), int(hi), d_any_new or None, self._s(stream)),
+               self._h)
+
+    def shard_test_windows_dev(self, d_local32: int, window_cap: int, nwin: int, d_counts: int, count_stride: int,
+                               hi: int, d_bits: int, stream=None) -> None:
+        _check(self._lib.bf_shard_test_windows_dev(self.handle, d_local32, int(window_cap), int(nwin), d_counts,
+                                                   int(count_stride), int(hi), d_bits, self._s(stream)), self._h)
 
     def shard_insert_hi_dev(self, d_local32: int, count: int, hi: int, d_any_new: int = 0, stream=None) -> None:
         _check(self._lib.bf_shard_insert_hi_dev(self.handle, d_local32, int(count), int(hi), d_any_new or None,

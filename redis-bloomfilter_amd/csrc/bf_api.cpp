@@ -1156,7 +1156,7 @@ int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
 namespace {
 // Owner-side OR of `count` routed local offsets: uint32 entries when u32 (+ bias), else uint64.
 int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint32_t* d_any_new,
-                      void* stream) {
+                      void* stream, const BfWindows& win = BfWindows{}) {
     if (!h) return BF_EINVAL;
     if (count && !d_local) return set_err(h, BF_EINVAL, "d_local is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1171,7 +1171,16 @@ int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias
     const bool binned = h->binned_mode != 0 &&
                         bf_binned_plan_offsets(h->dev_bytes, std::min(count, sub), h->bin_region_log2, &plan) &&
                         (h->binned_mode == 1 || (h->dev_bytes >= (64ull << 20) &&
-                                                 (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
+                                                 (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes)) &&
+                        (!win.counts || (win.cap % BF_WINDOW_CAP_ALIGN == 0 && count <= sub));
+    if (binned && win.counts) {   // the windows as one binned pass (entries past a window's count skipped)
+        int rc = ensure_scratch(h, plan.scratch_bytes);
+        if (rc) return rc;
+        BfMarks* mk = prof_begin(h, s);
+        HIPCHK(h, bf_launch_shard_insert_binned(h->g, plan, h->dev_bytes, d_local, u32, count, h->d_bin_scratch,
+                                                d_any_new, s, mk, bias, win));
+        return BF_OK;
+    }
     if (binned) {
         const size_t esz = u32 ? 4 : 8;
         for (uint64_t c0 = 0; c0 < count; c0 += sub) {
@@ -1188,7 +1197,7 @@ int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, u32, s, bias, h->g.dirty));
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, u32, s, bias, h->g.dirty, win));
     bf_mark(mk, s, "shard_insert");
     return BF_OK;
 }
@@ -1210,7 +1219,7 @@ int bf_shard_insert_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t cou
 
 namespace {
 int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint8_t* d_bits,
-                    void* stream) {
+                    void* stream, const BfWindows& win = BfWindows{}) {
     if (!h) return BF_EINVAL;
     if (count && (!d_local || !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1227,7 +1236,16 @@ int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, 
     const bool binned = mode != 0 &&
                         bf_binned_plan_offsets(h->dev_bytes, std::min(count, sub), h->bin_region_log2, &plan, true) &&
                         (mode == 1 || (h->dev_bytes >= (64ull << 20) &&
-                                       (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
+                                       (double)count * 128.0 > kBinnedCostRatio * (double)h->dev_bytes)) &&
+                        (!win.counts || (win.cap % BF_WINDOW_CAP_ALIGN == 0 && count <= sub));
+    if (binned && win.counts) {
+        int rc = ensure_scratch(h, plan.scratch_bytes);
+        if (rc) return rc;
+        BfMarks* mk = prof_begin(h, s);
+        HIPCHK(h, bf_launch_shard_test_binned(h->g, plan, h->dev_bytes, d_local, u32, count, h->d_bin_scratch, d_bits,
+                                              s, mk, bias, win));
+        return BF_OK;
+    }
     if (binned) {
         const size_t esz = u32 ? 4 : 8;
         for (uint64_t c0 = 0; c0 < count; c0 += sub) {
@@ -1245,11 +1263,46 @@ int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, 
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, u32, s, bias));
+    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, u32, s, bias, win));
     bf_mark(mk, s, "shard_test");
     return BF_OK;
 }
+
+BfWindows make_windows(const uint64_t* d_counts, uint32_t stride, uint32_t nwin, uint64_t cap) {
+    BfWindows w;
+    w.counts = reinterpret_cast<const unsigned long long*>(d_counts);
+    w.stride = stride ? stride : 1;
+    w.nwin = nwin;
+    w.cap = cap;
+    return w;
+}
 }  // namespace
+
+int bf_shard_insert_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
+                                const uint64_t* d_counts, uint32_t count_stride, uint32_t hi, uint32_t* d_any_new,
+                                void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (((uint64_t)hi << 32) >= h->local_bits) return set_err(h, BF_EINVAL, "hi=%u is past the shard", hi);
+    if (nwin && window_cap && !d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
+    if (window_cap && (uint64_t)nwin > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window sizes overflow");
+    if (nwin > 65535) return set_err(h, BF_EINVAL, "at most 65535 windows");
+    return shard_insert_impl(h, d_local32, true, (uint64_t)hi << 32, (uint64_t)nwin * window_cap, d_any_new, stream,
+                             make_windows(d_counts, count_stride, nwin, window_cap));
+}
+
+int bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
+                              const uint64_t* d_counts, uint32_t count_stride, uint32_t hi, uint8_t* d_bits,
+                              void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (((uint64_t)hi << 32) >= h->local_bits) return set_err(h, BF_EINVAL, "hi=%u is past the shard", hi);
+    if (nwin && window_cap && !d_counts) return set_err(h, BF_EINVAL, "d_counts is NULL");
+    if (window_cap && (uint64_t)nwin > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window sizes overflow");
+    if (nwin > 65535) return set_err(h, BF_EINVAL, "at most 65535 windows");
+    return shard_test_impl(h, d_local32, true, (uint64_t)hi << 32, (uint64_t)nwin * window_cap, d_bits, stream,
+                           make_windows(d_counts, count_stride, nwin, window_cap));
+}
 
 int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits, void* stream) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");

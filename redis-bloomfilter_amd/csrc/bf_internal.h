@@ -27,6 +27,15 @@ struct BfGeom {
 
 constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = BF_DIRTY_BLOCK_BYTES of the string
 
+// The sync-free exchange's receive layout: nwin windows of cap entries, window w's live count
+// min(counts[w * stride], cap) on the device.  counts == NULL: one run of `count` entries.
+struct BfWindows {
+    const unsigned long long* counts = nullptr;
+    uint32_t stride = 1;
+    uint32_t nwin = 1;
+    uint64_t cap = 0;
+};
+
 enum BfOp : int {
     BF_OP_INDEXES      = 0,  // write the k offsets of each key (ruby.rb:41-55)
     BF_OP_INCLUDE      = 1,  // AND of the k bits (ruby.rb:20-30)
@@ -104,15 +113,18 @@ hipError_t bf_launch_insert_binned_digests(const BfGeom& g, const BfBinPlan& p, 
 uint64_t bf_binned_max_offsets(uint64_t bitset_bytes, uint32_t pref_region_log2);
 bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref_region_log2, BfBinPlan* plan,
                             bool with_keys = false);
+// Window layout (w.counts != NULL): count = nwin * cap entries, cap a multiple of
+// BF_WINDOW_CAP_ALIGN; entries past a window's live count are skipped.
 hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                          const void* local, bool route32, uint64_t count, void* scratch,
                                          uint32_t* any_flag, hipStream_t s, BfMarks* marks = nullptr,
-                                         uint64_t bias = 0);
+                                         uint64_t bias = 0, const BfWindows& w = BfWindows{});
 // Binned shard test (owner side of a partitioned include?): out8[i] = bit of local[i].
 // Plan with bf_binned_plan_offsets(..., with_keys = true).
 hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const void* local, bool route32, uint64_t count, void* scratch, uint8_t* out8,
-                                       hipStream_t s, BfMarks* mk, uint64_t bias = 0);
+                                       hipStream_t s, BfMarks* mk, uint64_t bias = 0,
+                                       const BfWindows& w = BfWindows{});
 // plan.with_keys must be set; out8 gets the n answers.
 hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                     const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
@@ -176,9 +188,10 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
 // dirty (nullable): the shard's bf_track_dirty map
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count,
                                   uint32_t* any_flag, bool route32, hipStream_t s, uint64_t bias = 0,
-                                  uint8_t* dirty = nullptr);
+                                  uint8_t* dirty = nullptr, const BfWindows& w = BfWindows{});
 hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count,
-                                uint8_t* out, bool route32, hipStream_t s, uint64_t bias = 0);
+                                uint8_t* out, bool route32, hipStream_t s, uint64_t bias = 0,
+                                const BfWindows& w = BfWindows{});
 // out[j] = AND of bits[p] over the n*k send entries p with slot[p] == j.
 hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t n, uint32_t k,
                              uint8_t* out, hipStream_t s);

@@ -377,14 +377,24 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const Off* __restric
     }
 }
 
+// Window layout (wcounts != NULL): blockIdx.y is window w, whose entries sit at w * wcap and
+// whose live count is min(wcounts[w * wstride], wcap) (the sync-free exchange's fixed
+// receive windows); otherwise one run of `count` entries.
 template <bool FLAGS, typename Off>
 __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
                                                            const Off* __restrict__ local,
                                                            uint64_t count, uint32_t* __restrict__ any_flag,
-                                                           uint64_t bias, uint8_t* __restrict__ dirty) {
+                                                           uint64_t bias, uint8_t* __restrict__ dirty,
+                                                           uint64_t wcap, const unsigned long long* __restrict__ wcounts,
+                                                           uint32_t wstride) {
     // Test-then-set as in the direct insert: 4 probes per lane in flight, an atomic
     // only for bits still 0 (a 1 seen here is final within the launch).
     constexpr int U = 4;
+    if (wcounts) {
+        local += (uint64_t)blockIdx.y * wcap;
+        count = wcounts[(uint64_t)blockIdx.y * wstride];
+        if (count > wcap) count = 0;   // an overflowed window holds unwritten entries: skip it whole
+    }
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t isnew = 0;
     for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < count; p0 += U * stride) {
@@ -424,8 +434,16 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
 template <typename Off>
 __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits,
                                                          const Off* __restrict__ local, uint64_t count,
-                                                         uint8_t* __restrict__ out, uint64_t bias) {
+                                                         uint8_t* __restrict__ out, uint64_t bias, uint64_t wcap,
+                                                         const unsigned long long* __restrict__ wcounts,
+                                                         uint32_t wstride) {
     constexpr int U = 4;   // 4 independent probe loads per lane in flight
+    if (wcounts) {   // window layout, as shard_insert_kernel
+        local += (uint64_t)blockIdx.y * wcap;
+        out += (uint64_t)blockIdx.y * wcap;
+        count = wcounts[(uint64_t)blockIdx.y * wstride];
+        if (count > wcap) count = 0;   // an overflowed window holds unwritten entries: skip it whole
+    }
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p0 < count; p0 += U * stride) {
         uint32_t v[U], sh[U];
@@ -465,7 +483,9 @@ __global__ __launch_bounds__(256) void combine_windows_kernel(const uint8_t* __r
                                                               uint32_t P, uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t s = blockIdx.y;   // one grid row per window
-    const uint64_t live = counts[s] < wcap ? counts[s] : wcap;
+    // an overflowed window (counts[s] > wcap) holds unwritten entries: it is skipped whole
+    // (the synced exchange re-routes such a batch; the sync-free one replays it)
+    const uint64_t live = counts[s] <= wcap ? counts[s] : 0;
     const uint8_t* wb = bits + s * wcap;
     const uint32_t* ws = slot + s * wcap;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < live; i += stride)
@@ -499,7 +519,9 @@ __global__ __launch_bounds__(256) void combine_windows_packed_kernel(const uint8
                                                                      uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t s = blockIdx.y;
-    const uint64_t live = counts[s] < wcap ? counts[s] : wcap;
+    // an overflowed window (counts[s] > wcap) holds unwritten entries: it is skipped whole
+    // (the synced exchange re-routes such a batch; the sync-free one replays it)
+    const uint64_t live = counts[s] <= wcap ? counts[s] : 0;
     const uint8_t* wb = packed + s * wcap8;
     const uint32_t* ws = slot + s * wcap;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < live; i += stride)
@@ -565,35 +587,44 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
     return hipGetLastError();
 }
 
+// Grid of a windowed launch: `count` entries over nwin windows of wcap (nwin = 1: one run).
+static dim3 window_grid(uint64_t count, uint32_t nwin) {
+    if (nwin <= 1) return dim3(stream_grid(count));
+    uint32_t gx = stream_grid(count) / nwin;
+    return dim3(gx ? gx : 1u, nwin);
+}
+
 template <typename Off>
 static void launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag, uint64_t bias,
-                                uint8_t* dirty, hipStream_t s) {
+                                uint8_t* dirty, hipStream_t s, const BfWindows& w) {
     const Off* l = static_cast<const Off*>(local);
+    const dim3 grid = window_grid(count, w.counts ? w.nwin : 1u);
     if (any_flag)
-        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count,
-                           any_flag, bias, dirty);
+        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), grid, dim3(256), 0, s, bits, l, count, any_flag, bias,
+                           dirty, w.cap, w.counts, w.stride);
     else
-        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), dim3(stream_grid(count)), dim3(256), 0, s, bits, l, count,
-                           any_flag, bias, dirty);
+        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), grid, dim3(256), 0, s, bits, l, count, any_flag, bias,
+                           dirty, w.cap, w.counts, w.stride);
 }
 
 hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag,
-                                  bool route32, hipStream_t s, uint64_t bias, uint8_t* dirty) {
+                                  bool route32, hipStream_t s, uint64_t bias, uint8_t* dirty, const BfWindows& w) {
     if (count == 0) return hipSuccess;
-    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, bias, dirty, s);
-    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, bias, dirty, s);
+    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, bias, dirty, s, w);
+    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, bias, dirty, s, w);
     return hipGetLastError();
 }
 
 hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count, uint8_t* out,
-                                bool route32, hipStream_t s, uint64_t bias) {
+                                bool route32, hipStream_t s, uint64_t bias, const BfWindows& w) {
     if (count == 0) return hipSuccess;
+    const dim3 grid = window_grid(count, w.counts ? w.nwin : 1u);
     if (route32)
-        hipLaunchKernelGGL(shard_test_kernel<uint32_t>, dim3(stream_grid(count)), dim3(256), 0, s, bits,
-                           static_cast<const uint32_t*>(local), count, out, bias);
+        hipLaunchKernelGGL(shard_test_kernel<uint32_t>, grid, dim3(256), 0, s, bits,
+                           static_cast<const uint32_t*>(local), count, out, bias, w.cap, w.counts, w.stride);
     else
-        hipLaunchKernelGGL(shard_test_kernel<uint64_t>, dim3(stream_grid(count)), dim3(256), 0, s, bits,
-                           static_cast<const uint64_t*>(local), count, out, bias);
+        hipLaunchKernelGGL(shard_test_kernel<uint64_t>, grid, dim3(256), 0, s, bits,
+                           static_cast<const uint64_t*>(local), count, out, bias, w.cap, w.counts, w.stride);
     return hipGetLastError();
 }
 

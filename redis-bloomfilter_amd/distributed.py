@@ -148,6 +148,18 @@ class HipEngine:
                                                counts.data_ptr(), n, out.data_ptr(), stream=self._stream())
         return out
 
+    def shard_insert_windows(self, recv: torch.Tensor, cap: int, nwin: int, counts: torch.Tensor, col: int,
+                             stride: int, hi: int) -> None:
+        """OR nwin received windows of cap uint32 entries (sub-range hi); window w's live count
+        is counts.view(-1)[w * stride + col], on the device."""
+        self.filter.shard_insert_windows_dev(recv.data_ptr(), cap, nwin, counts.data_ptr() + 8 * col, stride, hi,
+                                             stream=self._stream())
+
+    def shard_test_windows(self, recv: torch.Tensor, cap: int, nwin: int, counts: torch.Tensor, col: int,
+                           stride: int, hi: int, out: torch.Tensor) -> None:
+        self.filter.shard_test_windows_dev(recv.data_ptr(), cap, nwin, counts.data_ptr() + 8 * col, stride, hi,
+                                           out.data_ptr(), stream=self._stream())
+
     def shard_insert_hi(self, local32: torch.Tensor, hi: int) -> None:
         self.filter.shard_insert_hi_dev(local32.data_ptr(), local32.numel(), hi, stream=self._stream())
 
@@ -244,8 +256,10 @@ class PartitionedFilter:
     sends/receives, so no pass regroups them owner-major; a batch that overflows a window
     takes the contiguous bf_route_dev path instead (same exchange, same answers)."""
 
+    WINDOW_ALIGN = 12288   # BF_WINDOW_CAP_ALIGN: windows the owner's binned path can take whole
+
     def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None,
-                 windows: bool = True, pack_answers: bool = True):
+                 windows: bool = True, pack_answers: bool = True, sync_free: bool = True):
         self.group = group
         self.P = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -259,6 +273,11 @@ class PartitionedFilter:
         self.windows = windows
         self.pack_answers = pack_answers   # window route: include? answers return as bits
         self.window_overflows = 0
+        # sync-free exchange: whole windows travel, counts stay on the device (needs the
+        # window route and the engine's windowed owner ops)
+        self.sync_free = bool(sync_free and windows and hasattr(engine, "shard_insert_windows"))
+        self.replays = 0
+        self._pk_seg = {}
 
     # -- exchange helpers
     def _splits(self, counts: torch.Tensor):
@@ -406,21 +425,143 @@ class PartitionedFilter:
             return self.engine.combine_windows(back, rt["slot"], rt["counts"], cap, n)
         return self.engine.combine(back, rt["slot"], n)
 
-    # -- device-resident batch API (keys already in device memory)
-    def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
+    # -- the sync-free exchange: fixed windows, counts on the device --------------------------
+    #
+    # Every rank sends its whole windows (cap entries each, cap a multiple of WINDOW_ALIGN),
+    # so the exchange's shape is known without the counts: the counts travel by an async
+    # all_to_all beside it, together with each rank's window-overflow flag, and the owner ops
+    # read the live counts on the device.  Nothing on the host waits for the device before
+    # the whole batch is enqueued.  The host then waits for one early event (after the routes
+    # and the count exchange, long done by then) to learn whether any rank's window
+    # overflowed (a skewed batch); only then is the batch replayed through the synced path —
+    # inserts are idempotent, and include? answers are recomputed into the same tensor — so
+    # the results never depend on it.
+
+    def _cap_sf(self, n: int) -> int:
+        a = self.WINDOW_ALIGN
+        return -(-self._cap(n) // a) * a
+
+    def _sf_start(self, kb, ko, n: int, want_slot: bool) -> dict:
+        e, P, nh = self.engine, self.P, self.engine.nh
+        cap = self._cap_sf(n)
+        send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
+        flag = (counts > cap).any().to(torch.int64).view(1, 1)
+        msg = torch.cat([counts.view(P, nh), flag.expand(P, 1)], dim=1).contiguous()
+        rmsg = torch.empty_like(msg)   # rmsg[s, h]: source s's count for my window h; [s, nh]: its flag
+        work = dist.all_to_all_single(rmsg, msg, group=self.group, async_op=True)
+        sseg = [(o, (o * nh + h) * cap, cap) for o in range(P) for h in range(nh)]
+        rseg = [(src, (h * P + src) * cap, cap) for h in range(nh) for src in range(P)]
+        recv = torch.empty(nh * P * cap, dtype=send.dtype, device=send.device)
+        works = self._p2p(send, sseg, recv, rseg)
+        return dict(kb=kb, ko=ko, n=n, cap=cap, send=send, slot=slot, counts=counts, rmsg=rmsg, work=work,
+                    recv=recv, works=works)
+
+    def _sf_flag(self, st: dict) -> None:
+        """Enqueue the global overflow flag's trip to pinned host memory (after the count
+        exchange) and an event behind it."""
+        st["work"].wait()
+        ovf = st["rmsg"][:, -1].max().view(1)
+        host = torch.empty(1, dtype=torch.int64, pin_memory=torch.cuda.is_available() and ovf.is_cuda)
+        host.copy_(ovf, non_blocking=True)
+        ev = torch.cuda.Event() if ovf.is_cuda else None
+        if ev is not None:
+            ev.record()
+        st["ovf"], st["ovf_ev"] = host, ev
+
+    def _sf_overflowed(self, st: dict) -> bool:
+        if st["ovf_ev"] is not None:
+            st["ovf_ev"].synchronize()
+        return bool(st["ovf"].item())
+
+    def _sf_insert(self, st: dict) -> None:
+        e, P, nh, cap = self.engine, self.P, self.engine.nh, st["cap"]
+        for w in st["works"]:
+            w.wait()
+        for h in range(nh):
+            e.shard_insert_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h)
+
+    def _sf_answer(self, st: dict) -> torch.Tensor:
+        e, P, nh, cap, n = self.engine, self.P, self.engine.nh, st["cap"], st["n"]
+        for w in st["works"]:
+            w.wait()
+        bits = torch.empty(nh * P * cap, dtype=torch.uint8, device=st["recv"].device)
+        for h in range(nh):
+            e.shard_test_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h,
+                                 bits[h * P * cap:(h + 1) * P * cap])
+        if self.pack_answers and hasattr(e, "pack_answers"):   # one bit per probe on the way back
+            cap8 = (cap + 7) // 8
+            key = (cap, P, nh)
+            if key not in self._pk_seg:   # (src, count, dst): window (src, h) -> packed[(src*nh + h)*cap8]
+                self._pk_seg[key] = torch.tensor([[(h * P + src) * cap, cap, (src * nh + h) * cap8]
+                                                  for src in range(P) for h in range(nh)],
+                                                 dtype=torch.int64).to(bits.device)
+            packed = e.pack_answers(bits, self._pk_seg[key], cap, P * nh * cap8)
+            back = torch.empty(P * nh * cap8, dtype=torch.uint8, device=bits.device)
+            seg = [(src, (src * nh + h) * cap8, cap8) for src in range(P) for h in range(nh)]
+            for w in self._p2p(packed, seg, back, seg):
+                w.wait()
+            return e.combine_windows_packed(back, st["slot"], st["counts"], cap, n)
+        back = torch.empty(P * nh * cap, dtype=torch.uint8, device=bits.device)
+        sseg = [(src, (h * P + src) * cap, cap) for src in range(P) for h in range(nh)]
+        rseg = [(o, (o * nh + h) * cap, cap) for o in range(P) for h in range(nh)]
+        for w in self._p2p(bits, sseg, back, rseg):
+            w.wait()
+        return e.combine_windows(back, st["slot"], st["counts"], cap, n)
+
+    def _synced_insert(self, kb, ko, n: int) -> None:
         recv, rt, works = self._exchange(kb, ko, n, want_slot=False)
         for w in works:
             w.wait()
         self._shard_insert(recv, rt)
 
-    def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
+    def _synced_include(self, kb, ko, n: int) -> torch.Tensor:
         recv, rt, works = self._exchange(kb, ko, n, want_slot=True)
         for w in works:
             w.wait()
         return self._answer(self._shard_test(recv, rt), rt, n)
 
+    # -- device-resident batch API (keys already in device memory)
+    def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
+        if not self.sync_free:
+            return self._synced_insert(kb, ko, n)
+        st = self._sf_start(kb, ko, n, want_slot=False)
+        self._sf_flag(st)
+        self._sf_insert(st)
+        if self._sf_overflowed(st):   # a skewed batch: replay it through the synced path
+            self.replays += 1
+            self._synced_insert(kb, ko, n)
+
+    def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
+        if not self.sync_free:
+            return self._synced_include(kb, ko, n)
+        st = self._sf_start(kb, ko, n, want_slot=True)
+        self._sf_flag(st)
+        out = self._sf_answer(st)
+        if self._sf_overflowed(st):
+            self.replays += 1
+            out.copy_(self._synced_include(kb, ko, n))
+        return out
+
     def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
                            qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
+        if self.sync_free:
+            # route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test |
+            # send(back) | combine, all enqueued before the host waits for anything
+            st_i = self._sf_start(ikb, iko, ni, want_slot=False)
+            st_q = self._sf_start(qkb, qko, nq, want_slot=True)
+            self._sf_flag(st_i)
+            self._sf_flag(st_q)
+            self._sf_insert(st_i)
+            out = self._sf_answer(st_q)
+            if self._sf_overflowed(st_i) or self._sf_overflowed(st_q):
+                self.replays += 1
+                self._synced_insert(ikb, iko, ni)
+                out.copy_(self._synced_include(qkb, qko, nq))
+            return out
+        return self._insert_include_synced(ikb, iko, ni, qkb, qko, nq)
+
+    def _insert_include_synced(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
+                               qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
         """insert_many_dev(ikb, iko, ni) then include_many_dev(qkb, qko, nq), same results,
         with the exchanges overlapped with the other batch's kernels:
 

@@ -59,6 +59,7 @@ def main():
     m, k, b = cfg["m"], cfg["k"], cfg["block_log2"]
     orc = O.COracle()
     pf = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    assert pf.sync_free
     rng = np.random.default_rng([cfg["seed"], rank])
     mine = [("r%d-%d" % (rank, int(v))) for v in rng.integers(0, 10**9, cfg["n"])]
     pf.insert_many(mine)
@@ -105,14 +106,22 @@ def main():
     del pf, pf3
     # the same step through the contiguous route (windows off), and with every window
     # overflowing (each rank falls back to the contiguous route after the count exchange)
+    # ... and through the synced exchange (host waits for the counts), the sync-free one with
+    # every window overflowing (the batch is replayed through the synced path), and bytes
+    # instead of bits on the way back
     got45 = []
-    for kw, cap in (({"windows": False}, None), ({}, 3), ({"pack_answers": False}, None)):
+    for kw, cap in (({"windows": False}, None), ({"sync_free": False}, 3), ({}, "sf"),
+                    ({"pack_answers": False}, None), ({"pack_answers": False, "sync_free": False}, None)):
         pf4 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc), **kw)
-        if cap is not None:
+        if cap == "sf":
+            pf4._cap_sf = lambda n: 8
+        elif cap is not None:
             pf4._cap = lambda n, c=cap: c
         got45.append(pf4.insert_include(mine, probe))
         same_shard = same_shard and hashlib.sha1(pf4.engine.shard_export().tobytes()).hexdigest() == shard_sha
-        if cap is not None:
+        if cap == "sf":
+            same_shard = same_shard and pf4.sync_free and pf4.replays == 1
+        elif cap is not None:
             same_shard = same_shard and pf4.window_overflows == 2
         del pf4
     ok = True

@@ -89,6 +89,20 @@ class NumpyEngine:
     def shard_test_hi(self, local32, hi, out):
         out.copy_(self.shard_test(self._hi(local32, hi)))
 
+    def shard_insert_windows(self, recv, cap, nwin, counts, col, stride, hi):
+        c = counts.reshape(-1).numpy()
+        for w in range(nwin):
+            live = min(int(c[w * stride + col]), cap)
+            if live:
+                self.shard_insert_hi(recv[w * cap: w * cap + live], hi)
+
+    def shard_test_windows(self, recv, cap, nwin, counts, col, stride, hi, out):
+        c = counts.reshape(-1).numpy()
+        for w in range(nwin):
+            live = min(int(c[w * stride + col]), cap)
+            if live:
+                out[w * cap: w * cap + live] = self.shard_test(self._hi(recv[w * cap: w * cap + live], hi))
+
     def shard_insert(self, local):
         lo = local.numpy().view(np.uint64)
         assert (lo < np.uint64(self.local_bits)).all(), "owner-local offset outside the shard"

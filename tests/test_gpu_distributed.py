@@ -245,14 +245,26 @@ def test_torch_distributed_world1(pkg, oracle):
             f.close()
         # the overlapped insert + include? step (async RCCL sends beside the kernels), through
         # the window route, the contiguous route, and the overflow fallback
-        for kw, cap in (({}, None), ({"windows": False}, None), ({}, 5), ({"pack_answers": False}, None)):
+        # sync-free (default) and synced exchanges, forced overflows of each (the sync-free one
+        # replays the step through the synced path), bytes instead of bits on the way back
+        for kw, cap in (({}, None), ({"windows": False}, None), ({"sync_free": False}, 5), ({}, "sf"),
+                        ({"pack_answers": False}, None), ({"pack_answers": False, "sync_free": False}, None)):
             f = D.PartitionedFilter(m, k, block_log2=16, **kw)
-            if cap is not None:
+            if cap == "sf":
+                f._cap_sf = lambda n: f.WINDOW_ALIGN   # 12288 < 50k keys x 6 probes: every batch overflows
+            elif cap is not None:
                 f._cap = lambda n, c=cap: c
+            assert f.sync_free == (kw.get("sync_free", True) and kw.get("windows", True))
             np.testing.assert_array_equal(f.insert_include(keys, probe), want)
             assert f.export_redis() == oracle.redis_string(bits)
-            assert f.window_overflows == (2 if cap is not None else 0)
+            assert f.window_overflows == (2 if cap == 5 else 0)
+            assert f.replays == (1 if cap == "sf" else 0)
             f.close()
+        # the sync-free insert and include? calls on their own
+        f = D.PartitionedFilter(m, k, block_log2=16)
+        f.insert_many(keys)
+        np.testing.assert_array_equal(f.include_many(probe), want)
+        f.close()
         # a shard past 2^32 bits (the north-star filter, 1.2 GB, in one shard): the window
         # route splits it into nh = 3 sub-range windows of uint32 entries
         m, k = 9585058377, 6
