@@ -37,7 +37,9 @@ class NumpyEngine:
     def route_windows(self, kb, ko, n, cap, want_slot=True):
         """route() in the window layout (window = owner * nh + local >> 32, uint32 entries);
         each window's entries shuffled, since the HIP route leaves their order unspecified
-        (the exchange must not depend on it)."""
+        (the exchange must not depend on it).  Entries past a window's count, and the whole of
+        an overflowed window (count > cap: the HIP route leaves holes there), are poison
+        (0xFFFFFFFF, slot -1) that the owner ops' bounds assertion trips on if ever read."""
         buf = kb.numpy()
         offs = ko.numpy().view(np.uint64)
         idx = self.orc.indexes_many(buf, offs, self.m, self.k).reshape(-1)
@@ -45,20 +47,27 @@ class NumpyEngine:
         win = owner.astype(np.int64) * self.nh + (local >> np.uint64(32)).astype(np.int64)
         nwin = self.P * self.nh
         counts = np.bincount(win, minlength=nwin).astype(np.int64)
-        wsend = np.zeros(nwin * cap, np.int32)
+        wsend = np.full(nwin * cap, -1, np.int32)
         wslot = np.full(nwin * cap, -1, np.int32)
         key_of = (np.arange(n * self.k, dtype=np.int64) // self.k).astype(np.int32)
         rng = np.random.default_rng(int(counts.sum()) + 7)
         for w in range(nwin):
             sel = np.flatnonzero(win == w)
-            sel = rng.permutation(sel)[: min(len(sel), cap)]
+            if len(sel) > cap:
+                continue
+            sel = rng.permutation(sel)
             wsend[w * cap: w * cap + len(sel)] = (local[sel] & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
             wslot[w * cap: w * cap + len(sel)] = key_of[sel]
         return torch.from_numpy(wsend), torch.from_numpy(wslot) if want_slot else None, torch.from_numpy(counts)
 
+    @staticmethod
+    def _live(c, cap):
+        """A window's live entries: its count, or none when it overflowed (as the HIP kernels)."""
+        return int(c) if int(c) <= cap else 0
+
     def combine_windows(self, bits, slot, counts, cap, n):
         c = counts.numpy()
-        live = np.concatenate([np.arange(w * cap, w * cap + min(int(c[w]), cap)) for w in range(len(c))])
+        live = np.concatenate([np.arange(w * cap, w * cap + self._live(c[w], cap)) for w in range(len(c))])
         return self.combine(bits[torch.from_numpy(live)], slot[torch.from_numpy(live)], n)
 
     def pack_answers(self, bits, seg, max_count, total):
@@ -75,7 +84,7 @@ class NumpyEngine:
         c = counts.numpy()
         bits = np.ones(len(c) * cap, np.uint8)
         for w in range(len(c)):
-            live = min(int(c[w]), cap)
+            live = self._live(c[w], cap)
             bits[w * cap: w * cap + live] = np.unpackbits(p[w * cap8: (w + 1) * cap8], bitorder="little")[:live]
         return self.combine_windows(torch.from_numpy(bits), slot, counts, cap, n)
 
@@ -92,14 +101,14 @@ class NumpyEngine:
     def shard_insert_windows(self, recv, cap, nwin, counts, col, stride, hi):
         c = counts.reshape(-1).numpy()
         for w in range(nwin):
-            live = min(int(c[w * stride + col]), cap)
+            live = self._live(c[w * stride + col], cap)
             if live:
                 self.shard_insert_hi(recv[w * cap: w * cap + live], hi)
 
     def shard_test_windows(self, recv, cap, nwin, counts, col, stride, hi, out):
         c = counts.reshape(-1).numpy()
         for w in range(nwin):
-            live = min(int(c[w * stride + col]), cap)
+            live = self._live(c[w * stride + col], cap)
             if live:
                 out[w * cap: w * cap + live] = self.shard_test(self._hi(recv[w * cap: w * cap + live], hi))
 
@@ -111,6 +120,7 @@ class NumpyEngine:
 
     def shard_test(self, local):
         lo = local.numpy().view(np.uint64)
+        assert (lo < np.uint64(self.local_bits)).all(), "owner-local offset outside the shard"
         b = (self.bits[(lo >> np.uint64(3)).astype(np.int64)] >> (np.uint64(7) - (lo & np.uint64(7))).astype(np.uint8)) & 1
         return torch.from_numpy(b.astype(np.uint8))
 

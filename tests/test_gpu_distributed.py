@@ -206,6 +206,13 @@ def test_pack_segments_and_packed_combine(pkg):
     e.close()
 
 
+def _trace(torch, *a):
+    """BF_TRACE=1 (with pytest -s): a synchronize + progress line after each step."""
+    if os.environ.get("BF_TRACE"):
+        torch.cuda.synchronize()
+        print("[world1]", *a, flush=True)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -235,13 +242,17 @@ def test_torch_distributed_world1(pkg, oracle):
                         (D.ReplicatedFilter, {"insert_mode": "or"})):
             f = cls(m, k, **kw)
             f.insert_many(keys)
+            _trace(torch, cls.__name__, kw, "insert")
             np.testing.assert_array_equal(f.include_many(probe), want)
+            _trace(torch, "include")
             assert f.export_redis() == oracle.redis_string(bits)
+            _trace(torch, "export")
             if cls is D.PartitionedFilter:   # per-rank SETRANGE of the rank's blocks
                 r = pkg.FakeRedis()
                 r.set("bf", b"stale")
                 f.write_redis(r, "bf", chunk_bytes=1 << 14)
                 assert r.get("bf") == oracle.redis_string(bits)
+                _trace(torch, "write_redis")
             f.close()
         # the overlapped insert + include? step (async RCCL sends beside the kernels), through
         # the window route, the contiguous route, and the overflow fallback
@@ -256,6 +267,7 @@ def test_torch_distributed_world1(pkg, oracle):
                 f._cap = lambda n, c=cap: c
             assert f.sync_free == (kw.get("sync_free", True) and kw.get("windows", True))
             np.testing.assert_array_equal(f.insert_include(keys, probe), want)
+            _trace(torch, "insert_include", kw, cap)
             assert f.export_redis() == oracle.redis_string(bits)
             assert f.window_overflows == (2 if cap == 5 else 0)
             assert f.replays == (1 if cap == "sf" else 0)
@@ -275,6 +287,7 @@ def test_torch_distributed_world1(pkg, oracle):
             f = D.PartitionedFilter(m, k, block_log2=20, **kw)
             assert f.engine.nh == 3
             np.testing.assert_array_equal(f.insert_include(keys, probe), want)
+            _trace(torch, "1.2 GB insert_include", kw)
             shard = f.engine.shard_export()
             assert np.array_equal(shard[: len(bits.view(np.uint8))], bits.view(np.uint8)[: len(shard)])
             f.close()
