@@ -23,7 +23,10 @@ KERNELS = {
     "bf_keys_kernel<INCLUDE>": re.compile(r"bf_keys_kernel<1>"),
     "bf_keys_kernel<INSERT>": re.compile(r"bf_keys_kernel<2>"),
     "bf_keys_kernel<INSERT_FLAGS>": re.compile(r"bf_keys_kernel<3>"),
-    "bin_front": re.compile(r"bin_front_kernel"),
+    "bf_include_hash_kernel": re.compile(r"bf_include_hash_kernel"),
+    "bf_keys_kernel<HASH>": re.compile(r"bf_keys_kernel<5>"),
+    "bin_front": re.compile(r"bin_front_kernel<false>"),
+    "bin_front_digest": re.compile(r"bin_front_kernel<true>"),
     "bin_front_wide": re.compile(r"bin_front_wide_kernel"),
     "bin_mid": re.compile(r"bin_mid_kernel"),
     "bin_apply": re.compile(r"bin_apply_kernel"),
