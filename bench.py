@@ -42,6 +42,10 @@ import pkgload  # noqa: E402
 
 HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md chip table (spec)
 GRANULE = 64               # B per random probe (SURVEY §8 d)
+# Random 4-B probes of a buffer past L2 leave it as 128-B line fills whatever the memory type
+# or cache policy, at ~55 G fills/s for any working set from 64 MiB to 1.2 GB (Infinity Cache
+# residency does not raise it): tools/probe_granularity.hip, profiles/r02_probe_granularity.log
+FILL_CEILING = 55.1e9      # fills/s, plain loads, 1143 MiB working set
 SEED = 0x5EED
 
 CONFIGS = {
@@ -542,6 +546,18 @@ def main():
     achieved = dom["algo_bytes"] / (dom["ms"] / 1e3) if "algo_bytes" in dom else None
     traffic = load_traffic(args.config, dom_name)
     n, p, batch, _ = CONFIGS[args.config]
+    fills = None
+    if dom_name in ("include_hash_kernel", "bf_keys_kernel<INCLUDE>"):
+        # the direct include?'s random line fills per key: members probe all k offsets,
+        # non-members stop at the first 0 bit (bit density d = fp^(1/k) from the batch's
+        # observed false-positive rate), half of each in the batch
+        kk, fp = main_res["k"], inc["observed_fp_rate"]
+        d = fp ** (1.0 / kk) if fp > 0 else 0.0
+        per_key = 0.5 * kk + 0.5 * ((1 - fp) / (1 - d) if d < 1 else kk)
+        rate = batch * per_key / (dom["ms"] / 1e3)
+        fills = {"fills_per_key": per_key, "bit_density": d, "fills_per_s": rate, "ceiling_fills_per_s": FILL_CEILING,
+                 "frac": rate / FILL_CEILING,
+                 "ceiling_source": "tools/probe_granularity.hip (profiles/r02_probe_granularity.log)"}
     line = {
         "metric": "keys/sec (insert, include?) per GPU and whole node; % of HBM random-access roofline",
         "value": main_res["keys_per_s"],
@@ -577,6 +593,9 @@ def main():
                      "traffic_GBps": traffic / (dom["ms"] / 1e3) / 1e9 if traffic else None,
                      "traffic_frac": traffic / (dom["ms"] / 1e3) / HBM_PEAK if traffic else None,
                      "algo_bytes": dom.get("algo_bytes"), "keys_per_launch": batch,
+                     # the include? kernel's own bound: random 128-B line fills per second
+                     # against the measured random-fill ceiling of this chip
+                     "random_fill": fills,
                      "kernel_ms": dom["ms"], "timing": "HIP events on the launch stream around each kernel, "
                                                        "inside the timed region (bf_profile)"},
         "cpu_baseline": cpu,

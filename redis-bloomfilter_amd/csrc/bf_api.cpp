@@ -1268,14 +1268,6 @@ int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, 
     return BF_OK;
 }
 
-BfWindows make_windows(const uint64_t* d_counts, uint32_t stride, uint32_t nwin, uint64_t cap) {
-    BfWindows w;
-    w.counts = reinterpret_cast<const unsigned long long*>(d_counts);
-    w.stride = stride ? stride : 1;
-    w.nwin = nwin;
-    w.cap = cap;
-    return w;
-}
 }  // namespace
 
 int bf_shard_insert_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
@@ -1288,7 +1280,7 @@ int bf_shard_insert_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_
     if (window_cap && (uint64_t)nwin > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window sizes overflow");
     if (nwin > 65535) return set_err(h, BF_EINVAL, "at most 65535 windows");
     return shard_insert_impl(h, d_local32, true, (uint64_t)hi << 32, (uint64_t)nwin * window_cap, d_any_new, stream,
-                             make_windows(d_counts, count_stride, nwin, window_cap));
+                             BfWindows(d_counts, count_stride, nwin, window_cap));
 }
 
 int bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
@@ -1301,7 +1293,7 @@ int bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t 
     if (window_cap && (uint64_t)nwin > ~0ull / window_cap) return set_err(h, BF_EINVAL, "window sizes overflow");
     if (nwin > 65535) return set_err(h, BF_EINVAL, "at most 65535 windows");
     return shard_test_impl(h, d_local32, true, (uint64_t)hi << 32, (uint64_t)nwin * window_cap, d_bits, stream,
-                           make_windows(d_counts, count_stride, nwin, window_cap));
+                           BfWindows(d_counts, count_stride, nwin, window_cap));
 }
 
 int bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits, void* stream) {

@@ -59,7 +59,7 @@ constexpr uint32_t kMaxTilesPerBlock = 16;    // <= 1024 tiles per group: one ru
 constexpr uint32_t kBlockProbes = 8192;       // probes per level-2 chunk block (one bin_mid workgroup)
 constexpr int kChunkPerLane = kBlockProbes / kTile;
 constexpr uint32_t kRunsPerPass = 1024;       // run-table entries per gather pass (one lane each)
-constexpr uint32_t kMidParts = 2;             // bin_mid workgroups per level-2 window
+constexpr uint32_t kMidParts = 2;             // bin_mid workgroups per level-2 window (1 and 4: same time)
 constexpr uint32_t kApplyLanes = 1024;
 
 // Exclusive prefix sum of v over the workgroup (blockDim.x a multiple of 64,

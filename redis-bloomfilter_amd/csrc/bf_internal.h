@@ -34,6 +34,9 @@ struct BfWindows {
     uint32_t stride = 1;
     uint32_t nwin = 1;
     uint64_t cap = 0;
+    BfWindows() = default;
+    BfWindows(const uint64_t* c, uint32_t s, uint32_t n, uint64_t wcap)
+        : counts(reinterpret_cast<const unsigned long long*>(c)), stride(s ? s : 1u), nwin(n), cap(wcap) {}
 };
 
 enum BfOp : int {
