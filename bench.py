@@ -496,6 +496,26 @@ def load_traffic(workload: str, kernel: str):
     return rec.get("hbm_bytes_per_launch") if isinstance(rec, dict) else None
 
 
+PMC_FILES = {"nstar": "pmc_r02i_nstar.json", "1m_big": "pmc_r02_1m_big.json", "10b": "pmc_r02_10b.json"}
+
+
+def load_pmc(workload: str):
+    """VALU and traffic counters per kernel from the committed PMC passes of this workload
+    (tools/pmc_passes.sh + tools/pmc_summary.py; rocprofv3 cannot run inside the bench
+    itself): valu_busy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)."""
+    name = PMC_FILES.get(workload)
+    if not name:
+        return None
+    try:
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
+            t = json.load(fh).get(workload) or {}
+    except (OSError, ValueError):
+        return None
+    keep = ("valu_busy", "valu_lane_insts_per_key", "hbm_bytes_per_launch", "profiled_ms_mean")
+    return {"source": "profiles/" + name,
+            "kernels": {kn: {x: rec.get(x) for x in keep} for kn, rec in t.items() if isinstance(rec, dict)}}
+
+
 def main():
     # Libraries (RCCL's version banner, HIP) may write to stdout; the contract is ONE JSON
     # line there, so fd 1 goes to stderr for the run and the JSON to the original stdout.
@@ -524,13 +544,17 @@ def main():
                                   mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline))
     secondary = {}
     if D.world == 1 and not args.no_secondary:
-        for name in ("1m", "100m", "10b"):
+        # 1m_big: the L2-resident 1M@1 % filter at 2^24-key batches (hash-bound; 1m's 2^20-key
+        # batches are launch- and latency-bound)
+        for name in ("1m", "1m_big", "100m", "10b"):
             if name != args.config:
                 r, _ = time_config(pkg, D, name, max(3, args.steps // 2), 1)
                 secondary[name] = {"keys_per_s": r["keys_per_s"],
                                    "insert_keys_per_s": r["insert"]["keys_per_s"],
                                    "include_keys_per_s": r["include"]["keys_per_s"],
-                                   "m": r["m"], "k": r["k"], "batch": r["batch"]}
+                                   "m": r["m"], "k": r["k"], "batch": r["batch"],
+                                   "kernels": {kn: round(v["ms"], 4) for kn, v in r["kernels"].items()},
+                                   "pmc": load_pmc(name)}
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(data)
@@ -598,6 +622,7 @@ def main():
                      "random_fill": fills,
                      "kernel_ms": dom["ms"], "timing": "HIP events on the launch stream around each kernel, "
                                                        "inside the timed region (bf_profile)"},
+        "pmc": load_pmc(args.config),
         "cpu_baseline": cpu,
         "ops": {"insert": ins, "include": inc},
         "kernels": kern,

@@ -894,9 +894,10 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     const uint64_t v0 = (uint64_t)r * kVec;
     const uint64_t nvec = nwords / 4;
     uint4* gv = reinterpret_cast<uint4*>(bits);
-    // Dense batch (at least one probe per 16-B vector on average: most vectors are
-    // touched): the region's vectors are loaded first, so that read overlaps the
-    // probe pass.  Sparse batch: only the touched vectors are read, after it.
+    // Dense batch (dense >= 1: at least one probe per 128-B line on average, so nearly every
+    // line is touched): the region's vectors are loaded first, so that read overlaps the probe
+    // pass; dense == 2 (a probe per 16-B vector) also writes the region back whole, in full
+    // lines.  Sparse batch: only the touched vectors are read, after it.
     uint4 old[kPer];
 #pragma unroll
     for (uint32_t c = 0; c < kPer; ++c) {
@@ -926,7 +927,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
 #pragma unroll
     for (uint32_t c = 0; c < kPer; ++c) {
         const uint32_t v = c * LANES + t;
-        if (v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) {
+        if (v0 + v < nvec && (dense == 2 || (msk[c].x | msk[c].y | msk[c].z | msk[c].w))) {
             const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
                                 (msk[c].w & ~old[c].w);
             fresh |= fr;
@@ -1173,7 +1174,12 @@ namespace {
 hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes,
                         uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
     const uint64_t nwords = bitset_bytes / 4;
-    const uint32_t dense = p.probes >= (uint64_t)p.nbins * (1ull << (p.region_log2 - 7)) ? 1u : 0u;
+    // dense = 2: at least one probe per 16-B vector on average (the region is read before the
+    // probe pass and written back whole); 1: at least one per 128-B line (read first, touched
+    // vectors written); 0: sparse.  Measured at 1B@1 % (13 probes / line, 2: 0.503 -> 0.492
+    // ms) and 10B@0.01 % (4 / line, 1: 2.81 -> 2.65 ms; writing whole lines there: 2.81)
+    const uint64_t vecs = (uint64_t)p.nbins << (p.region_log2 - 7);
+    const uint32_t dense = p.probes >= vecs ? 2u : (p.probes >= vecs / 8 ? 1u : 0u);
     if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
