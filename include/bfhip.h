@@ -232,7 +232,10 @@ int  bf_sync(bf_handle* h);                    /* synchronise the handle's own s
  *                               with d_slot[p] == j (include? answer)
  *
  *  Works on any handle: on a whole-filter handle shard_count = 1 routes everything to 0.
- *  d_counts must hold shard_count uint64 and is written, not accumulated. */
+ *  d_counts must hold shard_count uint64 and is written, not accumulated.
+ *  The owner ops take device data from the caller (or from a peer): a local offset at or past
+ *  the shard's local_bits is dropped by the inserts and answers 0 in the tests, and a combine
+ *  slot >= n is ignored, so no entry ever addresses memory outside the bitset or the answers. */
 int  bf_shard_info(const bf_handle* h, uint32_t* shard_count, uint32_t* shard_index,
                    uint32_t* block_log2, uint64_t* local_bits);
 int  bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,

@@ -808,6 +808,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.block_log2 = h->block_log2;
     h->g.inv_shards = 1.0 / (double)h->shards;
     h->g.route32 = h->route32 ? 1u : 0u;
+    h->g.limit = h->local_bits;
     h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k, h->dev_bytes));
     h->g.next_round = env_u32("BFHIP_INCLUDE_NEXT_ROUND", default_next_round(h->dev_bytes));
     h->g.route_agg = env_u32("BFHIP_ROUTE_AGG", 1);   // P = 1 only: at P = 8 the per-owner loop costs more than the LDS atomics (sim_rank A/B)
@@ -1197,7 +1198,7 @@ int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_insert(h->g.bits, d_local, count, d_any_new, u32, s, bias, h->g.dirty, win));
+    HIPCHK(h, bf_launch_shard_insert(h->g.bits, h->local_bits, d_local, count, d_any_new, u32, s, bias, h->g.dirty, win));
     bf_mark(mk, s, "shard_insert");
     return BF_OK;
 }
@@ -1263,7 +1264,7 @@ int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, 
         return BF_OK;
     }
     BfMarks* mk = prof_begin(h, s);
-    HIPCHK(h, bf_launch_shard_test(h->g.bits, d_local, count, d_bits, u32, s, bias, win));
+    HIPCHK(h, bf_launch_shard_test(h->g.bits, h->local_bits, d_local, count, d_bits, u32, s, bias, win));
     bf_mark(mk, s, "shard_test");
     return BF_OK;
 }

@@ -256,7 +256,8 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
                                                        uint32_t* __restrict__ level1_key,
                                                        uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt,
                                                        uint64_t bias, const unsigned long long* __restrict__ wcounts,
-                                                       uint32_t wstride, uint64_t wcap) {
+                                                       uint32_t wstride, uint64_t wcap, uint64_t limit,
+                                                       uint8_t* __restrict__ oob_out) {
     __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_sorted[kTileProbes];
@@ -288,9 +289,13 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
             loc[q] = 0;
             if (j < tp) {
                 const uint64_t o = (uint64_t)local[p0 + j] + bias;
-                const uint32_t sb = (uint32_t)(o >> sup_log2);
-                tag[q] = (sb << 16) | atomicAdd(s_cnt + sb, 1u);
-                loc[q] = (uint32_t)(o & smask);
+                if (o < limit) {
+                    const uint32_t sb = (uint32_t)(o >> sup_log2);
+                    tag[q] = (sb << 16) | atomicAdd(s_cnt + sb, 1u);
+                    loc[q] = (uint32_t)(o & smask);
+                } else if (oob_out) {   // an offset past the shard: dropped (insert), answered 0 (test)
+                    oob_out[p0 + j] = 0;
+                }
             }
         }
         __syncthreads();
@@ -324,9 +329,10 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_front_offsets_kernel(const Off* __restrict__ local, uint64_t count, uint32_t tiles_per_block,
                               uint32_t sup_log2, uint32_t nsup, uint32_t* __restrict__ level1,
                               uint16_t* __restrict__ stab, uint32_t* __restrict__ gcnt, uint64_t bias,
-                              const unsigned long long* __restrict__ wcounts, uint32_t wstride, uint64_t wcap) {
+                              const unsigned long long* __restrict__ wcounts, uint32_t wstride, uint64_t wcap,
+                              uint64_t limit) {
     bin_front_offsets_body<Off, false>(local, count, tiles_per_block, sup_log2, nsup, level1, nullptr, stab, gcnt,
-                                       bias, wcounts, wstride, wcap);
+                                       bias, wcounts, wstride, wcap, limit, nullptr);
 }
 
 // 76 KiB of LDS (u16 positions): two workgroups per CU at 8 waves per SIMD, as the plain pass
@@ -339,9 +345,10 @@ void bin_front_offsets_keys_kernel(const Off* __restrict__ local, uint64_t count
                                                                        uint16_t* __restrict__ stab,
                                                                        uint32_t* __restrict__ gcnt, uint64_t bias,
                                                                        const unsigned long long* __restrict__ wcounts,
-                                                                       uint32_t wstride, uint64_t wcap) {
+                                                                       uint32_t wstride, uint64_t wcap, uint64_t limit,
+                                                                       uint8_t* __restrict__ out8) {
     bin_front_offsets_body<Off, true>(local, count, tiles_per_block, sup_log2, nsup, level1, level1_key, stab, gcnt,
-                                      bias, wcounts, wstride, wcap);
+                                      bias, wcounts, wstride, wcap, limit, out8);
 }
 
 // gsum[sb][q] = probes of superbin sb in the tiles of front workgroups [64q, 64q + 64).
@@ -1234,11 +1241,11 @@ hipError_t bf_launch_shard_insert_binned(const BfGeom& g, const BfBinPlan& p, ui
     if (route32)
         hipLaunchKernelGGL(bin_front_offsets_kernel<uint32_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint32_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.stab, c.gcnt, bias, w.counts, w.stride, w.cap);
+                           c.stab, c.gcnt, bias, w.counts, w.stride, w.cap, g.limit);
     else
         hipLaunchKernelGGL(bin_front_offsets_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.stab, c.gcnt, bias, w.counts, w.stride, w.cap);
+                           c.stab, c.gcnt, bias, w.counts, w.stride, w.cap, g.limit);
     bf_mark(mk, s, "bin_front_offsets");
     hipError_t e = launch_groups_mid(g, p, c, s, mk);
     if (e != hipSuccess) return e;
@@ -1284,11 +1291,11 @@ hipError_t bf_launch_shard_test_binned(const BfGeom& g, const BfBinPlan& p, uint
     if (route32)
         hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint32_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint32_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.level1_key, c.stab, c.gcnt, bias, w.counts, w.stride, w.cap);
+                           c.level1_key, c.stab, c.gcnt, bias, w.counts, w.stride, w.cap, g.limit, out8);
     else
         hipLaunchKernelGGL(bin_front_offsets_keys_kernel<uint64_t>, dim3(p.nblocks), dim3(kTile), 0, s,
                            static_cast<const uint64_t*>(local), count, p.tiles_per_block, sup_log2, p.nsup, c.level1,
-                           c.level1_key, c.stab, c.gcnt, bias, w.counts, w.stride, w.cap);
+                           c.level1_key, c.stab, c.gcnt, bias, w.counts, w.stride, w.cap, g.limit, out8);
     bf_mark(mk, s, "bin_front_offsets_keys");
     if ((e = launch_groups_mid(g, p, c, s, mk)) != hipSuccess) return e;
     return launch_test(g, p, c, bitset_bytes, out8, s, mk);

@@ -23,12 +23,15 @@ struct BfGeom {
     uint32_t  route32;      // BF_FLAG_ROUTE32: routed owner-local offsets are uint32
     uint8_t*  dirty;        // nullable: one byte per 2^kDirtyShiftBits-bit block, set to 1 when an
                             // insert may have changed the block (bf_track_dirty)
+    uint64_t  limit;        // the handle's local bits: owner-side kernels drop routed offsets >= limit
+                            // (caller-supplied device data never addresses past the bitset)
 };
 
 constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = BF_DIRTY_BLOCK_BYTES of the string
 
 // The sync-free exchange's receive layout: nwin windows of cap entries, window w's live count
-// min(counts[w * stride], cap) on the device.  counts == NULL: one run of `count` entries.
+// counts[w * stride] on the device, or none when that exceeds cap (an overflowed window holds
+// unwritten entries).  counts == NULL: one run of `count` entries.
 struct BfWindows {
     const unsigned long long* counts = nullptr;
     uint32_t stride = 1;
@@ -189,10 +192,10 @@ hipError_t bf_launch_route_scatter(const void* local, const uint8_t* owner, uint
                                    bool route32, hipStream_t s);
 // bias: added to every local offset (the 2^32-bit sub-range of a split window route)
 // dirty (nullable): the shard's bf_track_dirty map
-hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count,
+hipError_t bf_launch_shard_insert(uint32_t* bits, uint64_t limit, const void* local, uint64_t count,
                                   uint32_t* any_flag, bool route32, hipStream_t s, uint64_t bias = 0,
                                   uint8_t* dirty = nullptr, const BfWindows& w = BfWindows{});
-hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count,
+hipError_t bf_launch_shard_test(const uint32_t* bits, uint64_t limit, const void* local, uint64_t count,
                                 uint8_t* out, bool route32, hipStream_t s, uint64_t bias = 0,
                                 const BfWindows& w = BfWindows{});
 // out[j] = AND of bits[p] over the n*k send entries p with slot[p] == j.

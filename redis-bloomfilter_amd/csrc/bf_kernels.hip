@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void route_scatter_kernel(const Off* __restric
 // whose live count is min(wcounts[w * wstride], wcap) (the sync-free exchange's fixed
 // receive windows); otherwise one run of `count` entries.
 template <bool FLAGS, typename Off>
-__global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits,
+__global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict__ bits, uint64_t limit,
                                                            const Off* __restrict__ local,
                                                            uint64_t count, uint32_t* __restrict__ any_flag,
                                                            uint64_t bias, uint8_t* __restrict__ dirty,
@@ -406,9 +406,11 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
             mask[u] = 0; v[u] = 0; w[u] = 0;
             if (p < count) {
                 const uint64_t o = (uint64_t)local[p] + bias;
-                w[u] = o >> 5;
-                mask[u] = 1u << ((uint32_t)(o ^ 7u) & 31u);
-                v[u] = bits[w[u]];
+                if (o < limit) {   // an offset past the shard is dropped, never dereferenced
+                    w[u] = o >> 5;
+                    mask[u] = 1u << ((uint32_t)(o ^ 7u) & 31u);
+                    v[u] = bits[w[u]];
+                }
             }
         }
 #pragma unroll
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
 }
 
 template <typename Off>
-__global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits,
+__global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restrict__ bits, uint64_t limit,
                                                          const Off* __restrict__ local, uint64_t count,
                                                          uint8_t* __restrict__ out, uint64_t bias, uint64_t wcap,
                                                          const unsigned long long* __restrict__ wcounts,
@@ -453,8 +455,10 @@ __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restr
             v[u] = 0; sh[u] = 0;
             if (p < count) {
                 const uint64_t o = (uint64_t)local[p] + bias;
-                sh[u] = (uint32_t)(o ^ 7u) & 31u;
-                v[u] = bits[o >> 5];
+                if (o < limit) {   // an offset past the shard answers 0, never dereferenced
+                    sh[u] = (uint32_t)(o ^ 7u) & 31u;
+                    v[u] = bits[o >> 5];
+                }
             }
         }
 #pragma unroll
@@ -469,10 +473,10 @@ __global__ __launch_bounds__(256) void shard_test_kernel(const uint32_t* __restr
 // writer stores the same 0, so no atomics are needed).
 __global__ __launch_bounds__(256) void combine_kernel(const uint8_t* __restrict__ bits,
                                                       const uint32_t* __restrict__ slot, uint64_t total,
-                                                      uint8_t* __restrict__ out) {
+                                                      uint64_t n, uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += stride)
-        if (!bits[p]) out[slot[p]] = 0;
+        if (!bits[p] && slot[p] < n) out[slot[p]] = 0;
 }
 
 // The same over the window layout of bf_route_windows_dev: window s holds counts[s] live
@@ -480,7 +484,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const uint8_t* __restrict_
 __global__ __launch_bounds__(256) void combine_windows_kernel(const uint8_t* __restrict__ bits,
                                                               const uint32_t* __restrict__ slot, uint64_t wcap,
                                                               const unsigned long long* __restrict__ counts,
-                                                              uint32_t P, uint8_t* __restrict__ out) {
+                                                              uint32_t P, uint64_t n, uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t s = blockIdx.y;   // one grid row per window
     // an overflowed window (counts[s] > wcap) holds unwritten entries: it is skipped whole
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(256) void combine_windows_kernel(const uint8_t* __r
     const uint8_t* wb = bits + s * wcap;
     const uint32_t* ws = slot + s * wcap;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < live; i += stride)
-        if (!wb[i]) out[ws[i]] = 0;
+        if (!wb[i] && ws[i] < n) out[ws[i]] = 0;
 }
 
 // Answer bytes -> bits for the return trip of a partitioned include?: segment q =
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(256) void combine_windows_packed_kernel(const uint8
                                                                      const uint32_t* __restrict__ slot, uint64_t wcap,
                                                                      uint64_t wcap8,
                                                                      const unsigned long long* __restrict__ counts,
-                                                                     uint8_t* __restrict__ out) {
+                                                                     uint64_t n, uint8_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t s = blockIdx.y;
     // an overflowed window (counts[s] > wcap) holds unwritten entries: it is skipped whole
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(256) void combine_windows_packed_kernel(const uint8
     const uint8_t* wb = packed + s * wcap8;
     const uint32_t* ws = slot + s * wcap;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < live; i += stride)
-        if (!((wb[i >> 3] >> (i & 7)) & 1u)) out[ws[i]] = 0;
+        if (!((wb[i >> 3] >> (i & 7)) & 1u) && ws[i] < n) out[ws[i]] = 0;
 }
 
 // Host-pointer calls ship each chunk's offsets as uint32 relative to the chunk's first key
@@ -595,35 +599,36 @@ static dim3 window_grid(uint64_t count, uint32_t nwin) {
 }
 
 template <typename Off>
-static void launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag, uint64_t bias,
-                                uint8_t* dirty, hipStream_t s, const BfWindows& w) {
+static void launch_shard_insert(uint32_t* bits, uint64_t limit, const void* local, uint64_t count, uint32_t* any_flag,
+                                uint64_t bias, uint8_t* dirty, hipStream_t s, const BfWindows& w) {
     const Off* l = static_cast<const Off*>(local);
     const dim3 grid = window_grid(count, w.counts ? w.nwin : 1u);
     if (any_flag)
-        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), grid, dim3(256), 0, s, bits, l, count, any_flag, bias,
-                           dirty, w.cap, w.counts, w.stride);
+        hipLaunchKernelGGL((shard_insert_kernel<true, Off>), grid, dim3(256), 0, s, bits, limit, l, count, any_flag,
+                           bias, dirty, w.cap, w.counts, w.stride);
     else
-        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), grid, dim3(256), 0, s, bits, l, count, any_flag, bias,
-                           dirty, w.cap, w.counts, w.stride);
+        hipLaunchKernelGGL((shard_insert_kernel<false, Off>), grid, dim3(256), 0, s, bits, limit, l, count, any_flag,
+                           bias, dirty, w.cap, w.counts, w.stride);
 }
 
-hipError_t bf_launch_shard_insert(uint32_t* bits, const void* local, uint64_t count, uint32_t* any_flag,
-                                  bool route32, hipStream_t s, uint64_t bias, uint8_t* dirty, const BfWindows& w) {
+hipError_t bf_launch_shard_insert(uint32_t* bits, uint64_t limit, const void* local, uint64_t count,
+                                  uint32_t* any_flag, bool route32, hipStream_t s, uint64_t bias, uint8_t* dirty,
+                                  const BfWindows& w) {
     if (count == 0) return hipSuccess;
-    if (route32) launch_shard_insert<uint32_t>(bits, local, count, any_flag, bias, dirty, s, w);
-    else launch_shard_insert<uint64_t>(bits, local, count, any_flag, bias, dirty, s, w);
+    if (route32) launch_shard_insert<uint32_t>(bits, limit, local, count, any_flag, bias, dirty, s, w);
+    else launch_shard_insert<uint64_t>(bits, limit, local, count, any_flag, bias, dirty, s, w);
     return hipGetLastError();
 }
 
-hipError_t bf_launch_shard_test(const uint32_t* bits, const void* local, uint64_t count, uint8_t* out,
+hipError_t bf_launch_shard_test(const uint32_t* bits, uint64_t limit, const void* local, uint64_t count, uint8_t* out,
                                 bool route32, hipStream_t s, uint64_t bias, const BfWindows& w) {
     if (count == 0) return hipSuccess;
     const dim3 grid = window_grid(count, w.counts ? w.nwin : 1u);
     if (route32)
-        hipLaunchKernelGGL(shard_test_kernel<uint32_t>, grid, dim3(256), 0, s, bits,
+        hipLaunchKernelGGL(shard_test_kernel<uint32_t>, grid, dim3(256), 0, s, bits, limit,
                            static_cast<const uint32_t*>(local), count, out, bias, w.cap, w.counts, w.stride);
     else
-        hipLaunchKernelGGL(shard_test_kernel<uint64_t>, grid, dim3(256), 0, s, bits,
+        hipLaunchKernelGGL(shard_test_kernel<uint64_t>, grid, dim3(256), 0, s, bits, limit,
                            static_cast<const uint64_t*>(local), count, out, bias, w.cap, w.counts, w.stride);
     return hipGetLastError();
 }
@@ -634,7 +639,7 @@ hipError_t bf_launch_combine(const uint8_t* bits, const uint32_t* slot, uint64_t
     hipError_t e = hipMemsetAsync(out, 1, n, s);
     if (e != hipSuccess) return e;
     const uint64_t total = n * k;
-    hipLaunchKernelGGL(combine_kernel, dim3(stream_grid(total)), dim3(256), 0, s, bits, slot, total, out);
+    hipLaunchKernelGGL(combine_kernel, dim3(stream_grid(total)), dim3(256), 0, s, bits, slot, total, n, out);
     return hipGetLastError();
 }
 
@@ -647,7 +652,7 @@ hipError_t bf_launch_combine_windows(const uint8_t* bits, const uint32_t* slot, 
     if (wcap == 0) return hipSuccess;
     uint32_t gx = stream_grid(wcap) / P;
     hipLaunchKernelGGL(combine_windows_kernel, dim3(gx ? gx : 1u, P), dim3(256), 0, s, bits, slot, wcap, counts, P,
-                       out);
+                       n, out);
     return hipGetLastError();
 }
 
@@ -668,7 +673,7 @@ hipError_t bf_launch_combine_windows_packed(const uint8_t* packed, const uint32_
     if (wcap == 0) return hipSuccess;
     uint32_t gx = stream_grid(wcap) / P;
     hipLaunchKernelGGL(combine_windows_packed_kernel, dim3(gx ? gx : 1u, P), dim3(256), 0, s, packed, slot, wcap,
-                       (wcap + 7) / 8, counts, out);
+                       (wcap + 7) / 8, counts, n, out);
     return hipGetLastError();
 }
 

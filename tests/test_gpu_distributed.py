@@ -206,6 +206,54 @@ def test_pack_segments_and_packed_combine(pkg):
     e.close()
 
 
+@pytest.mark.parametrize("binned", ["0", "1"])
+def test_owner_ops_drop_offsets_past_the_shard(pkg, monkeypatch, binned):
+    """Owner-side insert / test over caller-supplied device offsets never touch memory past the
+    handle's local bits: such an offset is dropped by the insert and answers 0 in the test, on
+    the direct and the binned passes; a combine slot >= n is ignored.  The bad offsets lie in
+    the bitset allocation's rounding slack, so the check sees a dropped offset apart from an
+    honoured one without relying on a fault."""
+    import torch
+    monkeypatch.setenv("BFHIP_INSERT_BINNED", binned)
+    monkeypatch.setenv("BFHIP_SHARD_TEST_BINNED", binned)
+    D = pkg.distributed
+    m = 95851
+    f = pkg.Filter(m, 6, device=0)
+    _, total = f.device_bits()   # allocation bytes, rounded up to 256
+    assert total * 8 > m + 64
+    view = D.device_bytes_view(f)
+    rng = np.random.default_rng(5)
+    good = rng.integers(0, m, 3000).astype(np.int64)
+    bad = np.array([m, m + 1, m + 63, total * 8 - 1], np.int64)
+    local = torch.from_numpy(np.concatenate([good, bad])).cuda()
+    f.shard_insert_dev(local.data_ptr(), local.numel(), stream=0)
+    torch.cuda.synchronize()
+    want = np.zeros(total, np.uint8)
+    np.bitwise_or.at(want, (good >> 3).astype(np.int64), (0x80 >> (good & 7)).astype(np.uint8))
+    np.testing.assert_array_equal(view.cpu().numpy(), want)
+    # every bit past m set by hand: a test of an offset there still answers 0
+    view[m >> 3] |= (1 << (8 - (m & 7))) - 1
+    view[(m >> 3) + 1:] = 0xFF
+    out = torch.empty(local.numel(), dtype=torch.uint8, device="cuda")
+    f.shard_test_dev(local.data_ptr(), local.numel(), out.data_ptr(), stream=0)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert o[: len(good)].all() and not o[len(good):].any()
+    # combine (n keys x k probes): a 0 answer whose slot is past the n keys is ignored
+    n = 10
+    sl = (np.arange(n * 6) // 6).astype(np.int32)
+    sl[7], sl[13] = n + 5, 2 * n
+    b = np.ones(n * 6, np.uint8)
+    b[[7, 13, 20]] = 0   # two stray slots, and one real 0 answer for key 20 // 6 = 3
+    ans = torch.full((n + 64,), 7, dtype=torch.uint8, device="cuda")
+    bits_t, slot_t = torch.from_numpy(b).cuda(), torch.from_numpy(sl).cuda()
+    f.combine_dev(bits_t.data_ptr(), slot_t.data_ptr(), n, ans.data_ptr(), stream=0)
+    torch.cuda.synchronize()
+    a = ans.cpu().numpy()
+    assert a[:n].tolist() == [1, 1, 1, 0, 1, 1, 1, 1, 1, 1] and (a[n:] == 7).all()
+    f.close()
+
+
 def _trace(torch, *a):
     """BF_TRACE=1 (with pytest -s): a synchronize + progress line after each step."""
     if os.environ.get("BF_TRACE"):

@@ -82,6 +82,15 @@ def derive(c):
         out["valu_busy"] = av * 4 / (1024 * gui / 8)
     if g("SQ_INSTS_VALU") is not None and g("SQ_BUSY_CYCLES") is not None:
         out["valu_insts_per_busy_cycle"] = g("SQ_INSTS_VALU") / max(g("SQ_BUSY_CYCLES"), 1)
+    # where the waves' time goes (quad-cycles, disjoint): parked at s_waitcnt / barriers,
+    # stalled at issue, issuing (MI355X_MICROARCH.md PMC table)
+    wc = g("SQ_WAVE_CYCLES")
+    if wc:
+        for nm in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+            if g(nm) is not None:
+                out[nm.lower().replace("sq_", "frac_")] = g(nm) / wc
+    if g("SQ_LDS_IDX_ACTIVE") and g("SQ_LDS_BANK_CONFLICT") is not None:
+        out["lds_bank_conflict_frac"] = g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE")
     tot = sum(out.get(k) or 0 for k in ("read_bytes", "write_bytes"))
     out["hbm_bytes"] = tot if tot else None
     return out
