@@ -221,3 +221,11 @@ def test_product_does_not_import_oracle():
     lib = os.path.join(pkg_dir, "lib", "libbfhip.so")
     out = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True)
     assert "bforacle" not in out.stdout
+
+
+def test_bfbench_binary_is_built_and_reports_its_version():
+    """The C++ bench binary links libbfhip.so; --version needs no GPU."""
+    import subprocess
+    exe = os.path.join(ROOT, "redis-bloomfilter_amd", "lib", "bfbench")
+    out = subprocess.run([exe, "--version"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.startswith("bfhip ")
