@@ -198,8 +198,9 @@ static int prepare_round(BfMulti* mh, uint32_t d, const uint8_t* keys, const uin
     return BF_OK;
 }
 
-// Hash + route device d's part into its windows and bring the window counts to the host.
-static int route_round(BfMulti* mh, uint32_t d, bool want_slot) {
+// Enqueue the hash + route of device d's part into its windows and the window counts' trip
+// to the host (route_wait collects them), so every device routes at the same time.
+static int route_enqueue(BfMulti* mh, uint32_t d, bool want_slot) {
     DevScratch& x = mh->ds[d];
     DevGuard g(mh->dev[d]);
     const uint32_t nwin = mh->D * mh->nh;
@@ -207,7 +208,12 @@ static int route_round(BfMulti* mh, uint32_t d, bool want_slot) {
                                   x.counts, x.s);
     if (rc) return sub_rc(mh, d, rc);
     MCHK(mh, hipMemcpyAsync(x.cnt.data(), x.counts, nwin * sizeof(uint64_t), hipMemcpyDeviceToHost, x.s));
-    MCHK(mh, hipStreamSynchronize(x.s));
+    return BF_OK;
+}
+
+static int route_wait(BfMulti* mh, uint32_t d) {
+    DevGuard g(mh->dev[d]);
+    MCHK(mh, hipStreamSynchronize(mh->ds[d].s));
     return BF_OK;
 }
 
@@ -217,7 +223,7 @@ static int partitioned_round(BfMulti* mh, const uint8_t* keys, const uint64_t* o
                              bool* any_new) {
     const uint32_t D = mh->D, nh = mh->nh, nwin = D * nh;
     int rc;
-    for (uint32_t d = 0; d < D; ++d) {
+    for (uint32_t d = 0; d < D; ++d) {   // every device's route in flight at once
         DevScratch& x = mh->ds[d];
         x.cap = window_cap(mh, x.n);
         if (x.n == 0) {
@@ -225,12 +231,18 @@ static int partitioned_round(BfMulti* mh, const uint8_t* keys, const uint64_t* o
             continue;
         }
         if ((rc = prepare_round(mh, d, keys, offsets, include))) return rc;
-        if ((rc = route_round(mh, d, include))) return rc;
+        if ((rc = route_enqueue(mh, d, include))) return rc;
+    }
+    for (uint32_t d = 0; d < D; ++d) {
+        DevScratch& x = mh->ds[d];
+        if (x.n == 0) continue;
+        if ((rc = route_wait(mh, d))) return rc;
         const uint64_t mx = *std::max_element(x.cnt.begin(), x.cnt.end());
         if (mx > x.cap) {   // a skewed part: windows that always fit
             x.cap = std::max<uint64_t>(x.n * mh->k, 1);
             if ((rc = prepare_round(mh, d, keys, offsets, include))) return rc;
-            if ((rc = route_round(mh, d, include))) return rc;
+            if ((rc = route_enqueue(mh, d, include))) return rc;
+            if ((rc = route_wait(mh, d))) return rc;
         }
     }
     // owners pull their windows (sub-range major, then source), apply or test them, and
