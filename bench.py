@@ -25,6 +25,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -484,6 +485,106 @@ def cpu_baseline(data, budget_s: float = 10.0):
                                           "README.md:80-95 numbers are quoted"}}
 
 
+def _w8_words(rng, count: int):
+    """bf_10_000.rb:8-11 rand_word: 8 distinct letters of a..z, sampled in order."""
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", dtype=np.uint8)
+    return [letters[rng.permutation(26)[:8]].tobytes().decode() for _ in range(count)]
+
+
+def reference_shapes(pkg, per_key_ops: int = 20000, words_n: int = 10000, flat_items: int = 100000,
+                     big_keys: int = 1 << 22):
+    """The reference's own benchmark loops, run through the Python facade
+    (``Bloomfilter(driver: 'hip' | 'hip-lua' | 'hip-test')``) against the in-process FakeRedis,
+    write-through sync on (every insert that flips a bit SETRANGEs the changed 64 KiB blocks):
+
+    * ``bf_10_000`` — BASELINE configs[0], benchmark/bf_10_000.rb:20-43: 10,000 W8 words, per
+      key include? (counted against a visited set) then insert, for each hip driver;
+    * ``flat`` — benchmark/bf_100_000_flat.rb:8-24 (README.md:80-95 at 1M): a 100,000-item
+      filter, ``per_key_ops`` per-key inserts of rand(items) then as many include?s, and the
+      whole 100,000 of each as one batched call;
+    * ``100m_sync`` — BASELINE configs[2]: the 100M@0.1 % filter (180 MB string), one
+      insert_many of 2^22 keys with write-through (the whole string changes, so it is all
+      SETRANGEd in 8 MiB chunks), then include_many of 2^22 keys.
+
+    Per-key ops pay Python + ctypes + one host-pointer round trip each; the reference pays a
+    Redis round trip per op (~160-230 us, README.md:86-93)."""
+    fr = pkg.fakeredis
+    rng = np.random.default_rng(SEED)
+    out = {}
+    words = _w8_words(rng, words_n)
+    for drv in ("hip", "hip-lua", "hip-test"):
+        bf = pkg.Bloomfilter(size=words_n, error_rate=0.01, key_name="bloom-filter-bench-" + drv, driver=drv,
+                             redis=fr.FakeRedis())
+        bf.clear()
+        error, first, visited = 0, 0, set()
+        t0 = time.perf_counter()
+        for i, w in enumerate(words):
+            if bf.include(w) != (w in visited):
+                error += 1
+                if error == 1:
+                    first = i
+            visited.add(w)
+            bf.insert(w)
+        dt = time.perf_counter() - t0
+        out.setdefault("bf_10_000", {})[drv] = {
+            "ops_per_s": 2 * len(words) / dt, "us_per_op": dt / (2 * len(words)) * 1e6,
+            "errors": error, "first_error_at": first, "bits": bf.options["bits"], "hashes": bf.options["hashes"],
+            "redis_string_sha1": hashlib.sha1(bf.redis.get("bloom-filter-bench-" + drv) or b"").hexdigest()
+            if drv != "hip-lua" else None}
+        bf.driver.close()
+    items = flat_items
+    vals = rng.integers(0, items, size=items)
+    for drv in ("hip", "hip-lua"):
+        bf = pkg.Bloomfilter(size=items, error_rate=0.01, key_name="bloom-filter-bench-flat-" + drv, driver=drv,
+                             redis=fr.FakeRedis())
+        bf.clear()
+        sample = [int(v) for v in vals[:per_key_ops]]
+        t0 = time.perf_counter()
+        for v in sample:
+            bf.insert(v)
+        t_ins = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for v in sample:
+            bf.include(v)
+        t_inc = time.perf_counter() - t0
+        bf.clear()
+        t0 = time.perf_counter()
+        bf.insert_many(vals)
+        b_ins = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        hits = bf.include_many(vals)
+        b_inc = time.perf_counter() - t0
+        assert bool(np.all(hits)), "flat: an inserted key answered false"
+        out.setdefault("flat", {})[drv] = {
+            "per_key_insert_ops_per_s": len(sample) / t_ins, "per_key_include_ops_per_s": len(sample) / t_inc,
+            "per_key_sample": len(sample),
+            "batched_insert_keys_per_s": items / b_ins, "batched_include_keys_per_s": items / b_inc}
+        bf.driver.close()
+    n_items, err = CONFIGS["100m"][:2]
+    bf = pkg.Bloomfilter(size=n_items, error_rate=err, key_name="bench-100m", driver="hip", redis=fr.FakeRedis())
+    r = bf.redis
+    ikeys = rng.integers(0, 1 << 62, size=big_keys)
+    half = big_keys // 2
+    qkeys = np.concatenate([ikeys[:half], rng.integers(0, 1 << 62, size=big_keys - half)])
+    t0 = time.perf_counter()
+    bf.insert_many(ikeys)
+    t_ins = time.perf_counter() - t0
+    slen = r.strlen("bench-100m")
+    t0 = time.perf_counter()
+    hits = bf.include_many(qkeys)
+    t_inc = time.perf_counter() - t0
+    assert bool(np.all(hits[:half])), "100m_sync: an inserted key answered false"
+    out["100m_sync"] = {"bits": bf.options["bits"], "hashes": bf.options["hashes"], "keys": len(ikeys),
+                        "insert_with_sync_s": t_ins, "insert_keys_per_s": len(ikeys) / t_ins,
+                        "redis_string_bytes": slen, "sync_GBps_bound": slen / t_ins / 1e9,
+                        "include_keys_per_s": len(qkeys) / t_inc,
+                        "note": "host keys (numpy ints -> decimal strings), PCIe round trips and the "
+                                "SETRANGE of the whole changed string are inside insert_with_sync_s"}
+    bf.driver.close()
+    out["redis"] = "in-process FakeRedis (redis-bloomfilter_amd/fakeredis.py); no redis-server on the box"
+    return out
+
+
 def load_traffic(workload: str, kernel: str):
     """PMC-measured HBM bytes per launch of `kernel` (profiles/pmc_traffic.json, tools/pmc_summary.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -529,6 +630,9 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
+    ap.add_argument("--no-reference-shapes", action="store_true",
+                    help="skip the reference benchmark loops through the facade (bf_10_000.rb, "
+                         "bf_100_000_flat.rb, 100M with Redis sync)")
     ap.add_argument("--mode", default="auto", choices=["auto", "single", "partitioned", "replicated"],
                     help="auto: single GPU at N=1, replicated at N=2 (filter fits one GPU), partitioned from N=4")
     ap.add_argument("--no-overlap", action="store_true",
@@ -555,6 +659,9 @@ def main():
                                    "m": r["m"], "k": r["k"], "batch": r["batch"],
                                    "kernels": {kn: round(v["ms"], 4) for kn, v in r["kernels"].items()},
                                    "pmc": load_pmc(name)}
+    shapes = None
+    if D.world == 1 and not args.no_reference_shapes:
+        shapes = reference_shapes(pkg)
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(data)
@@ -628,6 +735,7 @@ def main():
         "kernels": kern,
         "host_api": main_res.get("host_api"),
         "secondary": secondary or None,
+        "reference_shapes": shapes,
         "reference_published_keys_per_s": {"ruby_insert": 5103, "ruby_include": 4322,
                                            "lua_insert": 6235, "lua_include": 5712,
                                            "source": "reference README.md:80-95, 1M items, hardware unstated"},

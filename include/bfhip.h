@@ -21,6 +21,8 @@
  *   bf_destroy         (driver object going out of scope)
  *   bf_insert_many     Ruby#insert / #set, one key per call          ruby.rb:15-17, 57-63
  *                      (k pipelined SETBIT; `any_new` = !found, which drives EXPIRE at ruby.rb:62)
+ *   bf_insert_many_changes  Ruby#insert, with the bits it set          ruby.rb:57-63
+ *                      (the SETBITs that changed something: what write-through replays)
  *   bf_include_many    Ruby#include?                                  ruby.rb:20-30
  *   bf_indexes_many    Ruby#indexes_for (protected)                   ruby.rb:41-55
  *   bf_clear           Ruby#clear (DEL key_name)                      ruby.rb:33-35
@@ -203,6 +205,16 @@ int  bf_track_dirty(bf_handle* h, uint32_t enable);
 int  bf_dirty_ranges(bf_handle* h, uint64_t* ranges /* 2*cap */, uint32_t cap, uint32_t* n_out,
                      uint64_t* redis_len /* nullable */, uint32_t clear);
 int  bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf);
+/* Per-key write-through (ruby.rb:57-63 issues k SETBITs per insert): inserts a small batch
+ * (n * k <= 4096 probes, <= 64 KiB of key bytes) and lists every bit offset it flipped from
+ * 0 to 1, each once, in out_bits[0 .. *count) (cap >= n * k).  SETBIT of exactly those
+ * offsets brings a Redis copy of the filter to the device's state — the same string the
+ * ruby driver's k SETBITs per key build, since a SETBIT that changes nothing neither
+ * changes nor grows the string — and *count > 0 is the ref's `!found` (EXPIRE).  Leaves
+ * the dirty-block map untouched.  Whole-filter, SHA-1-engine handles only (BF_EINVAL
+ * otherwise: use bf_dirty_ranges). */
+int  bf_insert_many_changes(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                            uint64_t* out_bits, uint64_t cap, uint64_t* count);
 
 /* ---- per-kernel timing.  While enabled, every keyed launch (insert / include? /
  *      indexes, host or device API) records HIP events on its stream between its

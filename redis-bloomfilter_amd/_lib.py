@@ -91,6 +91,7 @@ SIGNATURES = {
     "bf_track_dirty": (ctypes.c_int, [_vp, _u32]),
     "bf_dirty_ranges": (ctypes.c_int, [_vp, _u64p, _u32, _u32p, _u64p, _u32]),
     "bf_export_range": (ctypes.c_int, [_vp, _u64, _u64, _vp]),
+    "bf_insert_many_changes": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _u64p]),
     "bf_profile": (ctypes.c_int, [_vp, _u32]),
     "bf_profile_read": (ctypes.c_int, [_vp, _vp, _vp, _vp, _u32, _u32p, _u32]),
     "bf_sync": (ctypes.c_int, [_vp]),
@@ -316,6 +317,20 @@ class Filter:
         _check(self._lib.bf_insert_many(self.handle, _ptr(keys), _ptr(offsets), n,
                                         ctypes.byref(flag) if any_new else None, _ptr(pk)), self._h)
         return (bool(flag.value) if any_new else None), (pk[:n] if per_key_new else None)
+
+    # bf_insert_many_changes limits (include/bfhip.h)
+    CHANGES_MAX_PROBES = 4096
+    CHANGES_MAX_BYTES = 64 << 10
+
+    def insert_many_changes(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        """Insert a small batch; returns the bit offsets it flipped 0 -> 1 (each once, uint64):
+        the SETBITs that bring a Redis copy up to date (ruby.rb:57-63)."""
+        keys, offsets, n = self._keys(keys, offsets)
+        out = np.zeros(max(n * self.k, 1), np.uint64)
+        cnt = ctypes.c_uint64(0)
+        _check(self._lib.bf_insert_many_changes(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(out), len(out),
+                                                ctypes.byref(cnt)), self._h)
+        return out[: cnt.value]
 
     def include_many(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
         keys, offsets, n = self._keys(keys, offsets)

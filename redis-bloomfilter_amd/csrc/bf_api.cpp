@@ -170,6 +170,10 @@ struct bf_handle {
     uint32_t* d_flag = nullptr;
     unsigned long long* d_scan = nullptr;
     uint32_t* h_flag = nullptr;   // pinned
+    // latency path of small host-pointer calls (run_small): one pinned and one device arena
+    uint8_t* h_small = nullptr;
+    uint8_t* d_small = nullptr;
+    uint64_t small_cap = 0;
     // incremental Redis sync (bf_track_dirty): one byte per BF_DIRTY_BLOCK_BYTES of the string
     uint8_t* d_dirty = nullptr;
     uint64_t dirty_blocks = 0;
@@ -475,6 +479,77 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
     return BF_OK;
 }
 
+// Latency path for small host-pointer calls (a Ruby per-key insert / include?): flag word,
+// result bytes, uint64 offsets and key bytes share ONE pinned staging block and ONE device
+// block, so a call is one H2D copy (which also zeroes the flag), the op's kernel, one D2H
+// copy of [flag | results] and one stream sync — no copy stream, no offset widening, no
+// event hand-offs.  Layout: [0, 16) flag, [16, 16 + R) results, then n + 1 offsets, then the
+// key bytes + 16 B of slack (the key stager's whole-vector reads).
+constexpr uint64_t kSmallKeys = 2048;
+constexpr uint64_t kSmallBytes = 64ull << 10;
+
+bool small_call(BfOp op, uint64_t n, uint64_t total) {
+    return (op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS || op == BF_OP_INCLUDE) && n <= kSmallKeys &&
+           total <= kSmallBytes;
+}
+
+// flips (bf_insert_many_changes): the direct flagging kernel also lists every bit it flipped,
+// after the results, at most kSmallFlips of them; the flip count rides at [8, 16).
+constexpr uint64_t kSmallFlips = 4096;
+
+int run_small(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* out8,
+              uint8_t* any_new, uint64_t* flips = nullptr, uint64_t* flip_count = nullptr) {
+    const uint64_t total = offsets[n] - offsets[0];
+    const uint64_t res = round_up(n, 16);
+    const uint64_t flip_at = 16 + res, nflip = flips ? (uint64_t)n * h->k : 0;
+    const uint64_t off_at = flip_at + nflip * 8, key_at = off_at + round_up((n + 1) * 8, 16);
+    const uint64_t end = key_at + round_up(total + 16, 16);
+    if (h->small_cap < end) {
+        const uint64_t cap = 16 + round_up(kSmallKeys, 16) + kSmallFlips * 8 + round_up((kSmallKeys + 1) * 8, 16) +
+                             kSmallBytes + 16;
+        if (!h->h_small) HIPCHK(h, hipHostMalloc((void**)&h->h_small, cap, hipHostMallocDefault));
+        if (!h->d_small) HIPCHK(h, hipMalloc((void**)&h->d_small, cap));
+        h->small_cap = cap;
+    }
+    uint8_t* hb = h->h_small;
+    memset(hb, 0, 16);
+    uint64_t* ho = reinterpret_cast<uint64_t*>(hb + off_at);
+    const uint64_t base = offsets[0];
+    for (uint64_t j = 0; j <= n; ++j) ho[j] = offsets[j] - base;
+    memcpy(hb + key_at, keys + base, total);
+    memset(hb + key_at + total, 0, 16);
+    HIPCHK(h, hipMemcpyAsync(h->d_small, hb, end, hipMemcpyHostToDevice, h->stream));
+    const bool want_flag = op == BF_OP_INSERT_FLAGS && any_new;
+    uint8_t* d_out8 = (op == BF_OP_INCLUDE || (op == BF_OP_INSERT_FLAGS && out8)) ? h->d_small + 16 : nullptr;
+    const uint8_t* d_keys = h->d_small + key_at;
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(h->d_small + off_at);
+    uint32_t* d_flag = want_flag ? reinterpret_cast<uint32_t*>(h->d_small) : nullptr;
+    if (flips) {   // the direct flagging kernel (never binned or sequential), dirty map untouched
+        BfGeom g = h->g;
+        g.dirty = nullptr;
+        g.flips = reinterpret_cast<unsigned long long*>(h->d_small + flip_at);
+        g.flip_count = reinterpret_cast<unsigned long long*>(h->d_small + 8);
+        g.flip_cap = nflip;
+        BfMarks* mk = prof_begin(h, h->stream);
+        HIPCHK(h, bf_launch_keys(BF_OP_INSERT_FLAGS, g, d_keys, d_off, 0, n, nullptr, nullptr, d_flag, h->stream));
+        bf_mark(mk, h->stream, op_kernel_name(BF_OP_INSERT_FLAGS));
+    } else {
+        int rc = launch_op(h, op, d_keys, d_off, 0, n, d_out8, nullptr, d_flag, h->stream);
+        if (rc) return rc;
+    }
+    const uint64_t back = flips ? flip_at + nflip * 8 : d_out8 ? 16 + n : (want_flag ? 4 : 0);
+    if (back) HIPCHK(h, hipMemcpyAsync(hb, h->d_small, back, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (d_out8 && out8) memcpy(out8, hb + 16, n);
+    if (want_flag) *any_new = *reinterpret_cast<const uint32_t*>(hb) ? 1 : 0;
+    if (flips) {
+        const uint64_t c = std::min<uint64_t>(*reinterpret_cast<const uint64_t*>(hb + 8), nflip);
+        memcpy(flips, hb + flip_at, c * 8);
+        *flip_count = c;
+    }
+    return BF_OK;
+}
+
 // Host-pointer driver: chunk, stage, launch, copy results back, as a 3-slot pipeline over
 // two streams.  For chunk c: the host (a thread pool) copies its key bytes and its offsets,
 // as uint32 relative to the chunk's first key, into the slot's pinned buffers; the copy
@@ -518,6 +593,7 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
     if (maxkey >= (1ull << 31))
         return set_err(h, BF_EINVAL, "a key of %llu bytes: host-pointer calls take keys below 2 GiB",
                        (unsigned long long)maxkey);
+    if (small_call(op, n, offsets[n] - offsets[0])) return run_small(h, op, keys, offsets, n, out8, any_new);
 
     const uint64_t out_per_key = op == BF_OP_INDEXES ? (uint64_t)h->k * 8 : 1;
     // Chunks of n/8 keys (at least 2^20, at most batch_keys): enough chunks that the
@@ -834,6 +910,8 @@ int bf_destroy(bf_handle* h) {
         if (h->order_valid) (void)hipEventSynchronize(h->order_ev);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         free_staging(h);
+        if (h->h_small) (void)hipHostFree(h->h_small);
+        if (h->d_small) (void)hipFree(h->d_small);
         if (h->g.bits) (void)hipFree(h->g.bits);
         if (h->d_flag) (void)hipFree(h->d_flag);
         if (h->d_scan) (void)hipFree(h->d_scan);
@@ -877,6 +955,30 @@ int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offse
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return BF_OK;
+}
+
+int bf_insert_many_changes(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                           uint64_t* out_bits, uint64_t cap, uint64_t* count) {
+    if (!h) return BF_EINVAL;
+    if (!count) return set_err(h, BF_EINVAL, "count is NULL");
+    *count = 0;
+    if (h->multi) return set_err(h, BF_EINVAL, "bf_insert_many_changes: a multi-device handle (use bf_dirty_ranges)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = check_keys_args(h, key_bytes, offsets, n);
+    if (rc) return rc;
+    if (n == 0) return BF_OK;
+    if (h->engine != BF_ENGINE_RUBY || h->shards > 1)
+        return set_err(h, BF_EINVAL, "bf_insert_many_changes: RubyTest engines and shards use bf_dirty_ranges");
+    if (n * h->k > kSmallFlips || offsets[n] < offsets[0] || offsets[n] - offsets[0] > kSmallBytes)
+        return set_err(h, BF_EINVAL, "bf_insert_many_changes takes at most %llu probes and %llu key bytes",
+                       (unsigned long long)kSmallFlips, (unsigned long long)kSmallBytes);
+    if (!out_bits || cap < n * h->k) return set_err(h, BF_EINVAL, "out_bits must hold n * k offsets");
+    for (uint64_t j = 0; j < n; ++j)
+        if (offsets[j + 1] < offsets[j]) return set_err(h, BF_EINVAL, "offsets must be non-decreasing");
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, h->stream);
+    return run_small(h, BF_OP_INSERT_FLAGS, key_bytes, offsets, n, nullptr, nullptr, out_bits, count);
 }
 
 int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n, uint8_t* out) {

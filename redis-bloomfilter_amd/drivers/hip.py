@@ -61,12 +61,16 @@ class Hip:
         devices = options.get("devices")
         if isinstance(devices, int):   # `devices: 8` -> the first 8 GPUs
             devices = list(range(devices))
+        flags = self._filter_flags()
         self.filter = Filter(m, k, device=options.get("device", -1),
                              batch_keys=options.get("batch_keys", 0),
                              batch_bytes=options.get("batch_bytes", 0),
-                             flags=self._filter_flags(),
+                             flags=flags,
                              devices=devices, mode=str(options.get("mode", "replicated")))
         self.filter.track_dirty(True)
+        # small write-through inserts replay their SETBITs (bf_insert_many_changes): SHA-1
+        # engine, whole-filter handles
+        self._changes_ok = flags == 0 and not devices
         self.chunk_bytes = int(options.get("chunk_bytes", 8 << 20))
         if self.chunk_bytes <= 0:
             raise ArgumentError("chunk_bytes must be positive")
@@ -120,14 +124,41 @@ class Hip:
         buf, offs = _keys.pack(keys)
         # ruby.rb:62 `if !found && expire`: any expire but nil/false counts, 0 included
         armed = expire is not None and expire is not False
-        want = armed or (self._redis is not None and self.sync_mode == "write_through")
+        write = self._redis is not None and self.sync_mode == "write_through"
+        n = len(offs) - 1
+        if write and self._changes_ok and n * self.filter.k <= Filter.CHANGES_MAX_PROBES and \
+                int(offs[-1]) - int(offs[0]) <= Filter.CHANGES_MAX_BYTES:
+            # a per-key (small) insert: replay the SETBITs that changed something (ruby.rb:58-60)
+            # rather than SETRANGE whole 64 KiB blocks — a few bytes, and a concurrent
+            # writer's bits in those blocks are never overwritten
+            flips = self.filter.insert_many_changes(buf, offs)
+            any_new = len(flips) > 0
+            if any_new:
+                self._setbits(flips)
+            if any_new and armed:
+                self._arm(expire)
+            return any_new
+        want = armed or write
         any_new, _ = self.filter.insert_many(buf, offs, any_new=want)
         if any_new:
-            if self._redis is not None and self.sync_mode == "write_through":
+            if write:
                 self.flush()
             if armed:
                 self._arm(expire)
         return bool(any_new) if want else None
+
+    def _setbits(self, offsets: np.ndarray) -> None:
+        """SETBIT key o 1 for every offset, pipelined when the client can (ruby.rb:58-60)."""
+        name, r = self.key_name, self._redis
+        pipe = getattr(r, "pipeline", None)
+        if pipe is not None:
+            p = pipe(transaction=False)
+            for o in offsets.tolist():
+                p.setbit(name, o, 1)
+            p.execute()
+        else:
+            for o in offsets.tolist():
+                r.setbit(name, o, 1)
 
     # -- ruby.rb:20-30
     def include(self, key) -> bool:

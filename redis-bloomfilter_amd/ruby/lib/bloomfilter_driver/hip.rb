@@ -79,6 +79,8 @@ class Redis
       attach_function :bf_track_dirty, %i[pointer uint32], :int, blocking: true
       attach_function :bf_dirty_ranges, %i[pointer pointer uint32 pointer pointer uint32], :int, blocking: true
       attach_function :bf_export_range, %i[pointer uint64 uint64 pointer], :int, blocking: true
+      attach_function :bf_insert_many_changes, %i[pointer pointer pointer uint64 pointer uint64 pointer], :int,
+                      blocking: true
       attach_function :bf_indexes, %i[pointer uint64 uint64 uint32 pointer], :int, blocking: true
     end
 
@@ -125,11 +127,15 @@ class Redis
       def insert_many(keys, expire = nil)
         expire_if_due
         buf, offs, n = pack(keys)
-        flag = FFI::MemoryPointer.new(:uint8)
-        check(HipFFI.bf_insert_many(@handle, buf, offs, n, flag, nil))
-        changed = flag.read_uint8 == 1
+        if @redis && @sync == :write_through && changes_path?(n, offs)
+          changed = insert_setbits(buf, offs, n)
+        else
+          flag = FFI::MemoryPointer.new(:uint8)
+          check(HipFFI.bf_insert_many(@handle, buf, offs, n, flag, nil))
+          changed = flag.read_uint8 == 1
+          flush if changed && @redis && @sync == :write_through
+        end
         if changed
-          flush if @redis && @sync == :write_through
           if expire
             @deadline = now + expire   # taken before EXPIRE: never after the server's deadline
             @redis.expire(@options[:key_name], expire) if @redis && @sync == :write_through
@@ -235,6 +241,31 @@ class Redis
       # bf_config.flags of the device filter (HipTest picks a hash engine here).
       def config_flags
         0
+      end
+
+      # bf_insert_many_changes limits (include/bfhip.h)
+      CHANGES_MAX_PROBES = 4096
+      CHANGES_MAX_BYTES = 64 << 10
+
+      # A per-key (small) write-through insert replays the SETBITs that changed something,
+      # pipelined like ruby.rb:58-60, instead of SETRANGEing whole 64 KiB blocks: tiny, and a
+      # concurrent writer's bits in those blocks are never overwritten.
+      def changes_path?(n, offs)
+        config_flags.zero? && @options[:devices].nil? && n * @options[:hashes] <= CHANGES_MAX_PROBES &&
+          offs.get_uint64(8 * n) - offs.get_uint64(0) <= CHANGES_MAX_BYTES
+      end
+
+      def insert_setbits(buf, offs, n)
+        cap = [n * @options[:hashes], 1].max
+        out = FFI::MemoryPointer.new(:uint64, cap)
+        cnt = FFI::MemoryPointer.new(:uint64)
+        check(HipFFI.bf_insert_many_changes(@handle, buf, offs, n, out, cap, cnt))
+        flips = out.read_array_of_uint64(cnt.read_uint64)
+        unless flips.empty?
+          name = @options[:key_name]
+          @redis.pipelined { flips.each { |o| @redis.setbit(name, o, 1) } }
+        end
+        !flips.empty?
       end
 
       # `devices: [0, 1, ...]` (or a count) and `mode: :replicated | :partitioned`: one filter

@@ -6,7 +6,7 @@
 # goes to gpurun_out/prof_ab_<tag>.
 export TMPDIR=/tmp
 TAG=$1; shift
-BENCH="python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api ${BENCH_EXTRA:-}"
+BENCH="python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes ${BENCH_EXTRA:-}"
 i=0
 for v in "$@"; do
     echo "variant $i: $v" >> gpurun_out/ab_${TAG}.txt

@@ -9,5 +9,5 @@ if [ "$SEL" = "all" ]; then KOPT=(); else KOPT=(-k "$SEL"); fi
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${KOPT[@]}" \
     > gpurun_out/tests_${TAG}.log 2>&1 &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- \
-    python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api \
+    python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes \
     > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err

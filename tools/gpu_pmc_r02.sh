@@ -5,7 +5,7 @@
 export TMPDIR=/tmp
 for cfg in 1m_big 10b; do
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r02_${cfg} -o run -- \
-        python bench.py --config $cfg --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api \
+        python bench.py --config $cfg --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes \
         > gpurun_out/bench_prof_r02_${cfg}.json 2> gpurun_out/bench_prof_r02_${cfg}.err || exit 1
     bash tools/pmc_passes.sh $cfg r02_${cfg} valu rd wr || exit 1
 done

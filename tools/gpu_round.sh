@@ -15,7 +15,7 @@ for st in $STEPS; do
         bench) timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
                    > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
         prof)  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- \
-                   python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api \
+                   python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes \
                    > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/bench_prof_${TAG}.err ;;
         pmc)   bash tools/pmc_passes.sh nstar ${TAG}_nstar ;;
     esac || { echo "step $st failed: $?"; exit 1; }

@@ -10,5 +10,5 @@ for P in 8 2; do
     timeout -k 10 120 python tools/sim_rank.py --shards $P --windows > gpurun_out/${T}_sim_P${P}_win.json 2> gpurun_out/${T}_sim_P${P}_win.err || exit 1
 done &&
 R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533" &&
-B="bench.py --mode partitioned --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api" &&
+B="bench.py --mode partitioned --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes" &&
 timeout -k 10 200 $R $B > gpurun_out/${T}_part_N1.json 2> gpurun_out/${T}_part_N1.err

@@ -11,7 +11,7 @@ if [ $# -gt 2 ]; then shift 2; PASSES="$*"; else PASSES="rd wr dram valu"; fi
 run() {   # pass, counters...
     local pass=$1; shift
     timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_${TAG}_${pass} -o run -- \
-        python bench.py --config $CONFIG --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api \
+        python bench.py --config $CONFIG --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes \
         > gpurun_out/pmc_${TAG}_${pass}.log 2>&1
 }
 for p in $PASSES; do
