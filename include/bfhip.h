@@ -211,8 +211,8 @@ int  bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf);
  * offsets brings a Redis copy of the filter to the device's state — the same string the
  * ruby driver's k SETBITs per key build, since a SETBIT that changes nothing neither
  * changes nor grows the string — and *count > 0 is the ref's `!found` (EXPIRE).  Leaves
- * the dirty-block map untouched.  Whole-filter, SHA-1-engine handles only (BF_EINVAL
- * otherwise: use bf_dirty_ranges). */
+ * the dirty-block map untouched.  Whole-filter handles only (every hash engine; a
+ * multi-device handle or a shard: BF_EINVAL, use bf_dirty_ranges). */
 int  bf_insert_many_changes(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                             uint64_t* out_bits, uint64_t cap, uint64_t* count);
 
@@ -331,6 +331,10 @@ int  bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mo
  *                        layer index(count + 1) and INCRs the count iff it set a new bit
  *                        (add.lua:6-54); per_key_new[j] = that INCR; *new_layers bit n-1
  *                        = layer n got a new item (the keys add.lua:52 EXPIREs)
+ *   bf_lua_insert_many_changes  the same, plus every bit the batch flipped 0 -> 1 (each once)
+ *                        as (layer << 58) | offset in out_bits[0 .. *count): the SETBITs
+ *                        add.lua:43-47 issued that changed a layer string, which write-through
+ *                        replays; *count > cap: BF_ERANGE after the insert is applied
  *   bf_lua_include_many  check.lua: 0 without a count, else any of layers 1..index(count)
  *                        holding all of its k_n bits (check.lua:1-61)
  *   bf_lua_clear         lua.rb:28-30 (KEYS name:* + DEL): layers and count dropped
@@ -343,6 +347,10 @@ int  bf_lua_destroy(bf_lua* h);
 const char* bf_lua_last_error(const bf_lua* h);   /* h == NULL: last error of bf_lua_create */
 int  bf_lua_insert_many(bf_lua* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                         uint8_t* per_key_new /* nullable */, uint64_t* new_layers /* nullable */);
+int  bf_lua_insert_many_changes(bf_lua* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
+                                uint8_t* per_key_new /* nullable */, uint64_t* new_layers /* nullable */,
+                                uint64_t* out_bits, uint64_t cap, uint64_t* count);
+#define BF_LUA_LAYER_SHIFT 58   /* out_bits of bf_lua_insert_many_changes: layer << 58 | offset */
 int  bf_lua_include_many(bf_lua* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                          uint8_t* out);
 int  bf_lua_clear(bf_lua* h);

@@ -117,6 +117,7 @@ SIGNATURES = {
     "bf_lua_destroy": (ctypes.c_int, [_vp]),
     "bf_lua_last_error": (ctypes.c_char_p, [_vp]),
     "bf_lua_insert_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64p]),
+    "bf_lua_insert_many_changes": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64p, _vp, _u64, _u64p]),
     "bf_lua_include_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
     "bf_lua_clear": (ctypes.c_int, [_vp]),
     "bf_lua_get_count": (ctypes.c_int, [_vp, _u64p]),
@@ -605,6 +606,25 @@ class LuaFilter:
         _lua_check(self._lib.bf_lua_insert_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(pk),
                                                 ctypes.byref(mask)), self._h)
         return pk[:n], [i + 1 for i in range(64) if mask.value >> i & 1]
+
+    LAYER_SHIFT = 58   # BF_LUA_LAYER_SHIFT
+
+    def insert_many_changes(self, keys: np.ndarray, offsets: np.ndarray):
+        """-> (per-key new flags, layers that got a new item, [(layer, bit offset), ...] of every
+        bit the batch flipped, each once: the SETBITs add.lua issued that changed something)."""
+        keys, offsets, n = Filter._keys(keys, offsets)
+        pk = np.zeros(max(n, 1), np.uint8)
+        mask = ctypes.c_uint64(0)
+        cap = max(64 * n, 1)   # BF_MAX_K probes per key at most
+        out = np.zeros(cap, np.uint64)
+        cnt = ctypes.c_uint64(0)
+        _lua_check(self._lib.bf_lua_insert_many_changes(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(pk),
+                                                        ctypes.byref(mask), _ptr(out), cap, ctypes.byref(cnt)),
+                   self._h)
+        flips = out[: cnt.value]
+        sh = np.uint64(self.LAYER_SHIFT)
+        pairs = list(zip((flips >> sh).tolist(), (flips & ((np.uint64(1) << sh) - np.uint64(1))).tolist()))
+        return pk[:n], [i + 1 for i in range(64) if mask.value >> i & 1], pairs
 
     def include_many(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
         keys, offsets, n = Filter._keys(keys, offsets)

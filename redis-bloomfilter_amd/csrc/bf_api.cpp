@@ -531,8 +531,14 @@ int run_small(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offset
         g.flip_count = reinterpret_cast<unsigned long long*>(h->d_small + 8);
         g.flip_cap = nflip;
         BfMarks* mk = prof_begin(h, h->stream);
-        HIPCHK(h, bf_launch_keys(BF_OP_INSERT_FLAGS, g, d_keys, d_off, 0, n, nullptr, nullptr, d_flag, h->stream));
-        bf_mark(mk, h->stream, op_kernel_name(BF_OP_INSERT_FLAGS));
+        if (h->engine != BF_ENGINE_RUBY) {   // RubyTest engines: their one-lane-per-probe insert
+            HIPCHK(h, bf_launch_engine(h->engine, BF_OP_INSERT, g, d_keys, d_off, 0, n, nullptr, nullptr, d_flag,
+                                       h->stream));
+            bf_mark(mk, h->stream, h->engine == BF_ENGINE_MD5 ? "engine_kernel<MD5>" : "engine_kernel<SHA1>");
+        } else {
+            HIPCHK(h, bf_launch_keys(BF_OP_INSERT_FLAGS, g, d_keys, d_off, 0, n, nullptr, nullptr, d_flag, h->stream));
+            bf_mark(mk, h->stream, op_kernel_name(BF_OP_INSERT_FLAGS));
+        }
     } else {
         int rc = launch_op(h, op, d_keys, d_off, 0, n, d_out8, nullptr, d_flag, h->stream);
         if (rc) return rc;
@@ -967,8 +973,7 @@ int bf_insert_many_changes(bf_handle* h, const uint8_t* key_bytes, const uint64_
     int rc = check_keys_args(h, key_bytes, offsets, n);
     if (rc) return rc;
     if (n == 0) return BF_OK;
-    if (h->engine != BF_ENGINE_RUBY || h->shards > 1)
-        return set_err(h, BF_EINVAL, "bf_insert_many_changes: RubyTest engines and shards use bf_dirty_ranges");
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "bf_insert_many_changes: a partitioned shard");
     if (n * h->k > kSmallFlips || offsets[n] < offsets[0] || offsets[n] - offsets[0] > kSmallBytes)
         return set_err(h, BF_EINVAL, "bf_insert_many_changes takes at most %llu probes and %llu key bytes",
                        (unsigned long long)kSmallFlips, (unsigned long long)kSmallBytes);

@@ -128,7 +128,8 @@ __device__ __forceinline__ uint64_t engine_offset(const uint8_t* key, uint32_t L
 
 // One lane per (key, probe).  INDEXES: offsets out (key-major); INCLUDE: out8 preset to 1,
 // a probe on a 0 bit clears its key's answer (ruby_test.rb:22-31); INSERT: test, then
-// atomicOr for a 0 bit, any_new by ballot, dirty blocks marked (ruby_test.rb:63-68).
+// atomicOr for a 0 bit, any_new by ballot, dirty blocks marked, flipped bits listed when
+// g.flips is set (ruby_test.rb:63-68).
 template <uint32_t ENGINE, BfOp OP>
 __global__ __launch_bounds__(kLanes) void engine_kernel(BfGeom g, const uint8_t* __restrict__ keys16,
                                                         const uint64_t* __restrict__ offsets, uint64_t bias,
@@ -153,6 +154,10 @@ __global__ __launch_bounds__(kLanes) void engine_kernel(BfGeom g, const uint8_t*
             if (!(g.bits[w] & mask)) {
                 if (g.dirty) g.dirty[w >> (kDirtyShiftBits - 5)] = 1;
                 fresh = !(atomicOr(g.bits + w, mask) & mask);
+                if (fresh && g.flips) {   // bf_insert_many_changes: this lane flipped it
+                    const unsigned long long at = atomicAdd(g.flip_count, 1ull);
+                    if (at < g.flip_cap) g.flips[at] = o | g.flip_tag;
+                }
             }
         }
     }

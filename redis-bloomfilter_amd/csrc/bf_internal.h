@@ -25,11 +25,12 @@ struct BfGeom {
                             // insert may have changed the block (bf_track_dirty)
     uint64_t  limit;        // the handle's local bits: owner-side kernels drop routed offsets >= limit
                             // (caller-supplied device data never addresses past the bitset)
-    // nullable (BF_OP_INSERT_FLAGS, direct kernel): every bit this launch flipped 0 -> 1 is
-    // appended once to flips[0 .. *flip_count) (entries past flip_cap are counted, not stored)
+    // nullable (BF_OP_INSERT_FLAGS direct kernel, seq_mark): every bit this launch flipped 0 -> 1
+    // is appended once to flips[0 .. *flip_count) (entries past flip_cap are counted, not stored)
     unsigned long long* flips;
     unsigned long long* flip_count;
     uint64_t  flip_cap;
+    uint64_t  flip_tag;     // ORed into every reported offset (the Lua layout: layer << 58)
 };
 
 constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = BF_DIRTY_BLOCK_BYTES of the string

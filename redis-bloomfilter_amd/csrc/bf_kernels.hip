@@ -103,7 +103,7 @@ __device__ __forceinline__ void digest_op(const BfGeom& g, const uint32_t H[4], 
                         if (g.flips && !(old & mask[c])) {   // this lane flipped it: report it once
                             const unsigned long long at = atomicAdd(g.flip_count, 1ull);
                             if (at < g.flip_cap)
-                                g.flips[at] = (w[c] << 5) | ((uint64_t)(__builtin_ctz(mask[c]) ^ 7u));
+                                g.flips[at] = ((w[c] << 5) | ((uint64_t)(__builtin_ctz(mask[c]) ^ 7u))) | g.flip_tag;
                         }
                     } else {
                         __hip_atomic_fetch_or(g.bits + w[c], mask[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

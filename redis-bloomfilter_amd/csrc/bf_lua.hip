@@ -80,6 +80,8 @@ struct bf_lua {
     uint64_t* d_off = nullptr;
     uint64_t keys_cap = 0, n_cap = 0;
     unsigned long long* d_last = nullptr;
+    unsigned long long* d_flips = nullptr;   // bf_lua_insert_many_changes: [count | entries]
+    uint64_t flips_cap = 0;
     std::string err;
 };
 
@@ -280,7 +282,7 @@ int bf_lua_destroy(bf_lua* h) {
         (void)hipStreamSynchronize(h->stream);
         for (BfGeom& g : h->layers) (void)hipFree(g.bits);
         for (void* p : {(void*)h->d_layers, (void*)h->scratch, (void*)h->d_keys, (void*)h->d_out, (void*)h->d_off,
-                        (void*)h->d_last})
+                        (void*)h->d_last, (void*)h->d_flips})
             if (p) (void)hipFree(p);
         if (h->h_out) (void)hipHostFree(h->h_out);
         (void)hipStreamDestroy(h->stream);
@@ -322,16 +324,37 @@ int bf_lua_clear(bf_lua* h) {
     return BF_OK;
 }
 
-int bf_lua_insert_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* per_key_new,
-                       uint64_t* new_layers) {
+}  // extern "C"
+
+namespace {
+
+// flips (bf_lua_insert_many_changes): every bit the batch flips, (layer << 58) | offset, into
+// a device list of `cap` entries that is copied to `flips` at the end; *flip_count = all of them.
+int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* per_key_new,
+               uint64_t* new_layers, uint64_t* flips, uint64_t cap, uint64_t* flip_count) {
     if (!h) return BF_EINVAL;
     if (new_layers) *new_layers = 0;
+    if (flip_count) *flip_count = 0;
     if (n == 0) return BF_OK;
     if (!offsets || (!keys && offsets[n] != offsets[0])) return lua_err(h, BF_EINVAL, "NULL keys / offsets");
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
     int rc = stage_keys(h, keys, offsets, n);
     if (rc) return rc;
+    unsigned long long* d_flips = nullptr;
+    if (flips) {   // [count | cap entries], kept on the handle
+        if (h->flips_cap < cap) {
+            LUACHK(h, hipStreamSynchronize(h->stream));
+            if (h->d_flips) (void)hipFree(h->d_flips);
+            h->d_flips = nullptr;
+            h->flips_cap = 0;
+            const uint64_t c = std::max<uint64_t>(cap, 4096);
+            LUACHK(h, hipMalloc((void**)&h->d_flips, (c + 1) * 8));
+            h->flips_cap = c;
+        }
+        d_flips = h->d_flips;
+        LUACHK(h, hipMemsetAsync(d_flips, 0, 8, h->stream));
+    }
     uint64_t s = 0;
     while (s < n) {
         const uint32_t layer = lua_index(h->entries, (double)(h->count + 1));   // add.lua:6-15
@@ -354,14 +377,47 @@ int bf_lua_insert_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, 
                 break;
             }
         }
-        LUACHK(h, bf_launch_seq_mark(g, 1, cn, take, h->scratch, nullptr, nullptr, h->stream));
+        BfGeom ga = g;
+        if (d_flips) {
+            ga.flips = d_flips + 1;
+            ga.flip_count = d_flips;
+            ga.flip_cap = cap;
+            ga.flip_tag = (uint64_t)layer << 58;
+        }
+        LUACHK(h, bf_launch_seq_mark(ga, 1, cn, take, h->scratch, nullptr, nullptr, h->stream));
         if (per_key_new) memcpy(per_key_new + s, h->h_out, take);
         if (fresh && new_layers && layer <= 64) *new_layers |= 1ull << (layer - 1);
         h->count += fresh;
         s += take;
     }
+    if (d_flips) {
+        unsigned long long c = 0;
+        LUACHK(h, hipMemcpyAsync(&c, d_flips, 8, hipMemcpyDeviceToHost, h->stream));
+        LUACHK(h, hipStreamSynchronize(h->stream));
+        *flip_count = c;
+        if (c > cap) return lua_err(h, BF_ERANGE, "%llu bits flipped, out_bits holds %llu (the insert is applied)",
+                                    c, (unsigned long long)cap);
+        if (c) LUACHK(h, hipMemcpy(flips, d_flips + 1, c * 8, hipMemcpyDeviceToHost));
+    }
     LUACHK(h, hipStreamSynchronize(h->stream));
     return BF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bf_lua_insert_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* per_key_new,
+                       uint64_t* new_layers) {
+    return lua_insert(h, keys, offsets, n, per_key_new, new_layers, nullptr, 0, nullptr);
+}
+
+int bf_lua_insert_many_changes(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n,
+                               uint8_t* per_key_new, uint64_t* new_layers, uint64_t* out_bits, uint64_t cap,
+                               uint64_t* count) {
+    if (!h) return BF_EINVAL;
+    if (!count || (cap && !out_bits)) return lua_err(h, BF_EINVAL, "NULL out_bits / count");
+    return lua_insert(h, keys, offsets, n, per_key_new, new_layers, out_bits, cap, count);
 }
 
 int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* out) {

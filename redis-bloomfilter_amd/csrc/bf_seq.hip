@@ -98,6 +98,11 @@ __global__ __launch_bounds__(256) void seq_mark_kernel(BfGeom g, uint32_t i0, ui
                     __hip_atomic_fetch_or(g.bits + (o >> 5), 1u << ((uint32_t)(o ^ 7u) & 31u), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
                     if (g.dirty) g.dirty[o >> kDirtyShiftBits] = 1;
+                    // the bit flips once, reported by the first key of the batch that probes it
+                    if (g.flips && tvals[slot] == (uint32_t)j) {
+                        const unsigned long long at = atomicAdd(g.flip_count, 1ull);
+                        if (at < g.flip_cap) g.flips[at] = o | g.flip_tag;
+                    }
                 }
             }
         }

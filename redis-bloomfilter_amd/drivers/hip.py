@@ -68,9 +68,9 @@ class Hip:
                              flags=flags,
                              devices=devices, mode=str(options.get("mode", "replicated")))
         self.filter.track_dirty(True)
-        # small write-through inserts replay their SETBITs (bf_insert_many_changes): SHA-1
-        # engine, whole-filter handles
-        self._changes_ok = flags == 0 and not devices
+        # small write-through inserts replay their SETBITs (bf_insert_many_changes): whole-filter
+        # (single-device) handles
+        self._changes_ok = not devices
         self.chunk_bytes = int(options.get("chunk_bytes", 8 << 20))
         if self.chunk_bytes <= 0:
             raise ArgumentError("chunk_bytes must be positive")

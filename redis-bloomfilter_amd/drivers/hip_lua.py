@@ -59,6 +59,8 @@ class HipLua:
     def key_name(self) -> str:
         return self.options["key_name"]
 
+    CHANGES_MAX_KEYS = 64   # batches up to this many keys sync by SETBIT replay
+
     def _layer_key(self, n: int) -> str:
         return "%s:%d" % (self.key_name, n)
 
@@ -80,9 +82,19 @@ class HipLua:
         """Insert in order, as one EVALSHA per key would; returns each key's INCR flag."""
         self._expired()
         buf, offs = _keys.pack(keys)
-        pk, touched = self.filter.insert_many(buf, offs)
-        if touched and self._redis is not None and self.sync_mode == "write_through":
-            self._write(touched)
+        write = self._redis is not None and self.sync_mode == "write_through"
+        if write and len(offs) - 1 <= self.CHANGES_MAX_KEYS:
+            # per-key (small) inserts replay the SETBITs that changed a layer (add.lua:43-47)
+            # instead of SETRANGEing whole layer strings (a large filter's layer is 100s of MB)
+            pk, touched, flips = self.filter.insert_many_changes(buf, offs)
+            for layer, o in flips:
+                self._redis.setbit(self._layer_key(layer), o, 1)
+            if touched:
+                self._redis.set("%s:count" % self.key_name, str(self.filter.count))
+        else:
+            pk, touched = self.filter.insert_many(buf, offs)
+            if touched and write:
+                self._write(touched)
         if touched and expire is not None and expire is not False:   # add.lua:51 tonumber(ARGV[4]): 0 is truthy
             t0 = self._clock()
             for n in touched:

@@ -251,7 +251,7 @@ class Redis
       # pipelined like ruby.rb:58-60, instead of SETRANGEing whole 64 KiB blocks: tiny, and a
       # concurrent writer's bits in those blocks are never overwritten.
       def changes_path?(n, offs)
-        config_flags.zero? && @options[:devices].nil? && n * @options[:hashes] <= CHANGES_MAX_PROBES &&
+        @options[:devices].nil? && n * @options[:hashes] <= CHANGES_MAX_PROBES &&
           offs.get_uint64(8 * n) - offs.get_uint64(0) <= CHANGES_MAX_BYTES
       end
 

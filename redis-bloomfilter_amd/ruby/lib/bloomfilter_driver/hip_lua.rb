@@ -23,6 +23,8 @@ class Redis
       attach_function :bf_lua_destroy, [:pointer], :int, blocking: true
       attach_function :bf_lua_last_error, [:pointer], :string
       attach_function :bf_lua_insert_many, %i[pointer pointer pointer uint64 pointer pointer], :int, blocking: true
+      attach_function :bf_lua_insert_many_changes,
+                      %i[pointer pointer pointer uint64 pointer pointer pointer uint64 pointer], :int, blocking: true
       attach_function :bf_lua_include_many, %i[pointer pointer pointer uint64 pointer], :int, blocking: true
       attach_function :bf_lua_clear, [:pointer], :int, blocking: true
       attach_function :bf_lua_get_count, %i[pointer pointer], :int
@@ -35,6 +37,9 @@ class Redis
 
     class HipLua
       attr_reader :redis
+
+      CHANGES_MAX_KEYS = 64   # batches up to this many keys sync by SETBIT replay
+      LAYER_SHIFT = 58        # BF_LUA_LAYER_SHIFT
 
       def initialize(options = {})
         @options = options
@@ -68,9 +73,23 @@ class Redis
         buf, offs, n = HipFFI.pack(keys)
         flags = FFI::MemoryPointer.new(:uint8, [n, 1].max)
         mask = FFI::MemoryPointer.new(:uint64)
-        check(HipLuaFFI.bf_lua_insert_many(@handle, buf, offs, n, flags, mask))
-        touched = (0...64).select { |i| mask.read_uint64[i] == 1 }.map { |i| i + 1 }
-        write(touched) if !touched.empty? && @redis && @sync == :write_through
+        if @redis && @sync == :write_through && n <= CHANGES_MAX_KEYS
+          # per-key inserts replay the SETBITs that changed a layer (add.lua:43-47), not whole layers
+          cap = [64 * n, 1].max
+          out = FFI::MemoryPointer.new(:uint64, cap)
+          cnt = FFI::MemoryPointer.new(:uint64)
+          check(HipLuaFFI.bf_lua_insert_many_changes(@handle, buf, offs, n, flags, mask, out, cap, cnt))
+          touched = (0...64).select { |i| mask.read_uint64[i] == 1 }.map { |i| i + 1 }
+          flips = out.read_array_of_uint64(cnt.read_uint64)
+          @redis.pipelined do
+            flips.each { |f| @redis.setbit(layer_key(f >> LAYER_SHIFT), f & ((1 << LAYER_SHIFT) - 1), 1) }
+            @redis.set("#{@options[:key_name]}:count", device_count.to_s) unless touched.empty?
+          end
+        else
+          check(HipLuaFFI.bf_lua_insert_many(@handle, buf, offs, n, flags, mask))
+          touched = (0...64).select { |i| mask.read_uint64[i] == 1 }.map { |i| i + 1 }
+          write(touched) if !touched.empty? && @redis && @sync == :write_through
+        end
         if !touched.empty? && expire
           t0 = now   # before EXPIRE: never after the server's deadline
           touched.each do |l|
@@ -167,9 +186,13 @@ class Redis
           check(HipLuaFFI.bf_lua_export_layer(@handle, l, buf, n, len))
           @redis.setrange(layer_key(l), 0, buf.read_bytes(n))
         end
+        @redis.set("#{@options[:key_name]}:count", device_count.to_s)
+      end
+
+      def device_count
         count = FFI::MemoryPointer.new(:uint64)
         check(HipLuaFFI.bf_lua_get_count(@handle, count))
-        @redis.set("#{@options[:key_name]}:count", count.read_uint64.to_s)
+        count.read_uint64
       end
 
       def check(rc, handle = @handle)

@@ -94,3 +94,32 @@ def test_spec_scalable_filter_via_hip_lua(pkg):
         bf.insert(a)
     assert errors / 150 <= bf.options["error_rate"]
     bf.clear()
+
+
+def test_hip_lua_per_key_setbit_replay(pkg):
+    """Per-key inserts (the SETBIT-replay write-through, bf_lua_insert_many_changes): after
+    every insert the driver's Redis keys equal what add.lua leaves, across layer growth, and
+    the flipped bits reported are exactly the layers' new bits."""
+    rng = np.random.default_rng(21)
+    keys = ["p%d" % v for v in rng.integers(0, 300, 260)]
+    mine, ref = pkg.FakeRedis(), pkg.FakeRedis()
+    bf = pkg.Bloomfilter(size=50, error_rate=0.01, key_name="pk", driver="hip-lua", redis=mine)
+    for i, key in enumerate(keys):
+        got = bf.insert(key)
+        want = L.add(ref, "pk", 50, 0.01, key)
+        assert bool(got[0]) == bool(want), i
+        assert sorted(mine.keys("pk:*")) == sorted(ref.keys("pk:*")), i
+        for k in ref.keys("pk:*"):
+            assert mine.get(k) == ref.get(k), (i, k)
+    assert len(layers_of(ref, "pk")) >= 3   # the batch crossed layer thresholds
+    f = bf.driver.filter
+    before = {n: f.export_layer(n) for n in range(1, f.layers + 1)}
+    b, o = pkg.keys.pack(["fresh%d" % i for i in range(40)])
+    _, touched, flips = f.insert_many_changes(b, o)
+    for n in range(1, f.layers + 1):
+        old, new = before.get(n, b""), f.export_layer(n)
+        old_bits = np.unpackbits(np.frombuffer(old.ljust(len(new), b"\0"), np.uint8)) if new else np.zeros(0, np.uint8)
+        new_bits = np.unpackbits(np.frombuffer(new, np.uint8)) if new else np.zeros(0, np.uint8)
+        want = set(np.flatnonzero(new_bits & ~old_bits).tolist())
+        assert {o for (lay, o) in flips if lay == n} == want, n
+    bf.driver.close()

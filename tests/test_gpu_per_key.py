@@ -105,3 +105,22 @@ def test_write_through_setbits_match_ruby_driver(pkg, O):
     bf.insert_many(["w%d" % i for i in range(2000)])              # a large batch: dirty-block flush
     assert r_hip.get("wt") == bf.driver.to_redis_string()
     bf.driver.close()
+
+
+@pytest.mark.parametrize("engine", ["md5", "sha1"])
+def test_write_through_setbits_ruby_test_engines(pkg, O, engine):
+    """hip-test per-key write-through replays the engine kernel's flipped bits: the Redis
+    string equals the RubyTest driver's SETBITs (ruby_test.rb:43-68) over the same keys."""
+    m = O.py_optimal_m(500, 0.01)
+    k = O.py_optimal_k(500, m)
+    r = pkg.FakeRedis()
+    bf = pkg.Bloomfilter(size=500, error_rate=0.01, key_name="rt", driver="hip-test", hash_engine=engine, redis=r)
+    ref = O.PyBitstring()
+    for i in range(150):
+        key = "rt-%d" % (i % 120)
+        changed = [ref.setbit(o, 1) for o in O.py_engine_indexes(key, m, k, engine)]
+        got = bf.insert(key)
+        assert got == (0 in changed), i
+        assert r.get("rt") == ref.value(), i
+    assert bf.driver.filter.dirty_ranges(clear=False)[0] == []
+    bf.driver.close()
