@@ -74,6 +74,7 @@ struct bf_lua {
     std::vector<BfGeom> layers;   // layers[n - 1]: bitset of layer n (allocated on first use)
     std::vector<uint64_t> layer_bytes;
     BfGeom* d_layers = nullptr;   // device copy of the layer table for lua_check_kernel
+    uint32_t d_layers_n = 0;      // layers of that copy (layers never change once made; clear resets)
     void* scratch = nullptr;
     uint64_t scratch_cap = 0;
     uint8_t *d_keys = nullptr, *d_out = nullptr, *h_out = nullptr;
@@ -81,7 +82,9 @@ struct bf_lua {
     uint64_t keys_cap = 0, n_cap = 0;
     unsigned long long* d_last = nullptr;
     unsigned long long* d_flips = nullptr;   // bf_lua_insert_many_changes: [count | entries]
+    unsigned long long* h_flips = nullptr;   // pinned mirror of d_flips (small calls read it back at once)
     uint64_t flips_cap = 0;
+    uint8_t* h_stage = nullptr;              // pinned [offsets | keys] of small calls (one H2D)
     std::string err;
 };
 
@@ -208,6 +211,11 @@ int ensure_lua_scratch(bf_lua* h, uint64_t bytes) {
     return BF_OK;
 }
 
+// Small calls (a per-key insert / include?): offsets and key bytes go through one pinned block
+// and one H2D copy, with no host sync (every call ends with one, so the block is free again).
+constexpr uint64_t kLuaSmallKeys = 2048;
+constexpr uint64_t kLuaSmallBytes = 64ull << 10;
+
 // Keys to the device (offsets rebased to 0), 16-byte aligned with slack.
 int stage_keys(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n) {
     for (uint64_t j = 0; j < n; ++j)
@@ -216,6 +224,19 @@ int stage_keys(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     const uint64_t base = offsets[0], nbytes = offsets[n] - offsets[0];
     int rc = ensure_io(h, nbytes, n);
     if (rc) return rc;
+    if (n <= kLuaSmallKeys && nbytes <= kLuaSmallBytes) {
+        const uint64_t off_bytes = (kLuaSmallKeys + 1) * 8;
+        if (!h->h_stage) LUACHK(h, hipHostMalloc((void**)&h->h_stage, off_bytes + kLuaSmallBytes + 16,
+                                                 hipHostMallocDefault));
+        uint64_t* ho = reinterpret_cast<uint64_t*>(h->h_stage);
+        for (uint64_t j = 0; j <= n; ++j) ho[j] = offsets[j] - base;
+        uint8_t* hk = h->h_stage + off_bytes;
+        if (nbytes) memcpy(hk, keys + base, nbytes);
+        memset(hk + nbytes, 0, 16);
+        LUACHK(h, hipMemcpyAsync(h->d_off, ho, (n + 1) * 8, hipMemcpyHostToDevice, h->stream));
+        LUACHK(h, hipMemcpyAsync(h->d_keys, hk, nbytes + 16, hipMemcpyHostToDevice, h->stream));
+        return BF_OK;
+    }
     std::vector<uint64_t> rebased(n + 1);
     for (uint64_t j = 0; j <= n; ++j) rebased[j] = offsets[j] - base;
     if (nbytes) LUACHK(h, hipMemcpyAsync(h->d_keys, keys + base, nbytes, hipMemcpyHostToDevice, h->stream));
@@ -285,6 +306,8 @@ int bf_lua_destroy(bf_lua* h) {
                         (void*)h->d_last, (void*)h->d_flips})
             if (p) (void)hipFree(p);
         if (h->h_out) (void)hipHostFree(h->h_out);
+        if (h->h_flips) (void)hipHostFree(h->h_flips);
+        if (h->h_stage) (void)hipHostFree(h->h_stage);
         (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -320,6 +343,7 @@ int bf_lua_clear(bf_lua* h) {
     for (BfGeom& g : h->layers) (void)hipFree(g.bits);
     h->layers.clear();
     h->layer_bytes.clear();
+    h->d_layers_n = 0;
     h->count = 0;
     return BF_OK;
 }
@@ -342,16 +366,20 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     int rc = stage_keys(h, keys, offsets, n);
     if (rc) return rc;
     unsigned long long* d_flips = nullptr;
+    constexpr uint64_t kSmallFlips = 4096;   // lists up to this long come back with the flags
+    const bool small_flips = flips && cap <= kSmallFlips;
+    bool last_read = false;   // the last chunk's flags D2H also carried the flip list
     if (flips) {   // [count | cap entries], kept on the handle
         if (h->flips_cap < cap) {
             LUACHK(h, hipStreamSynchronize(h->stream));
             if (h->d_flips) (void)hipFree(h->d_flips);
             h->d_flips = nullptr;
             h->flips_cap = 0;
-            const uint64_t c = std::max<uint64_t>(cap, 4096);
+            const uint64_t c = std::max<uint64_t>(cap, kSmallFlips);
             LUACHK(h, hipMalloc((void**)&h->d_flips, (c + 1) * 8));
             h->flips_cap = c;
         }
+        if (!h->h_flips) LUACHK(h, hipHostMalloc((void**)&h->h_flips, (kSmallFlips + 1) * 8, hipHostMallocDefault));
         d_flips = h->d_flips;
         LUACHK(h, hipMemsetAsync(d_flips, 0, 8, h->stream));
     }
@@ -365,18 +393,6 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
         if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, nullptr)))) return rc;
         // which keys would set a new bit of this layer, in order (nothing applied yet)
         LUACHK(h, bf_launch_seq_candidates(g, 1, h->d_keys, h->d_off + s, 0, cn, h->scratch, h->stream));
-        LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, h->d_out, nullptr, h->stream));
-        LUACHK(h, hipMemcpyAsync(h->h_out, h->d_out, cn, hipMemcpyDeviceToHost, h->stream));
-        LUACHK(h, hipStreamSynchronize(h->stream));
-        // cut after the key whose INCR fills the layer (add.lua:48-50); later keys go up a layer
-        uint64_t take = cn, fresh = 0;
-        for (uint64_t j = 0; j < cn; ++j) {
-            fresh += h->h_out[j];
-            if (fresh == room) {
-                take = j + 1;
-                break;
-            }
-        }
         BfGeom ga = g;
         if (d_flips) {
             ga.flips = d_flips + 1;
@@ -384,20 +400,51 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
             ga.flip_cap = cap;
             ga.flip_tag = (uint64_t)layer << 58;
         }
-        LUACHK(h, bf_launch_seq_mark(ga, 1, cn, take, h->scratch, nullptr, nullptr, h->stream));
+        uint64_t take = cn, fresh = 0;
+        bool read_now = false;
+        if (room >= cn) {
+            // no key of the chunk can fill the layer before the last one: flags and apply in ONE
+            // mark pass, one sync (the per-key insert's case)
+            LUACHK(h, bf_launch_seq_mark(ga, 1, cn, cn, h->scratch, h->d_out, nullptr, h->stream));
+            LUACHK(h, hipMemcpyAsync(h->h_out, h->d_out, cn, hipMemcpyDeviceToHost, h->stream));
+            if (d_flips && small_flips)
+                LUACHK(h, hipMemcpyAsync(h->h_flips, d_flips, (cap + 1) * 8, hipMemcpyDeviceToHost, h->stream));
+            LUACHK(h, hipStreamSynchronize(h->stream));
+            read_now = d_flips && small_flips;
+            for (uint64_t j = 0; j < cn; ++j) fresh += h->h_out[j];
+        } else {
+            LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, h->d_out, nullptr, h->stream));
+            LUACHK(h, hipMemcpyAsync(h->h_out, h->d_out, cn, hipMemcpyDeviceToHost, h->stream));
+            LUACHK(h, hipStreamSynchronize(h->stream));
+            // cut after the key whose INCR fills the layer (add.lua:48-50); later keys go up a layer
+            for (uint64_t j = 0; j < cn; ++j) {
+                fresh += h->h_out[j];
+                if (fresh == room) {
+                    take = j + 1;
+                    break;
+                }
+            }
+            LUACHK(h, bf_launch_seq_mark(ga, 1, cn, take, h->scratch, nullptr, nullptr, h->stream));
+        }
         if (per_key_new) memcpy(per_key_new + s, h->h_out, take);
         if (fresh && new_layers && layer <= 64) *new_layers |= 1ull << (layer - 1);
         h->count += fresh;
         s += take;
+        last_read = read_now;
     }
     if (d_flips) {
         unsigned long long c = 0;
-        LUACHK(h, hipMemcpyAsync(&c, d_flips, 8, hipMemcpyDeviceToHost, h->stream));
-        LUACHK(h, hipStreamSynchronize(h->stream));
+        if (small_flips && last_read) {   // read back with the last chunk's flags
+            c = h->h_flips[0];
+            if (c <= cap && c) memcpy(flips, h->h_flips + 1, c * 8);
+        } else {
+            LUACHK(h, hipMemcpyAsync(&c, d_flips, 8, hipMemcpyDeviceToHost, h->stream));
+            LUACHK(h, hipStreamSynchronize(h->stream));
+            if (c <= cap && c) LUACHK(h, hipMemcpy(flips, d_flips + 1, c * 8, hipMemcpyDeviceToHost));
+        }
         *flip_count = c;
         if (c > cap) return lua_err(h, BF_ERANGE, "%llu bits flipped, out_bits holds %llu (the insert is applied)",
                                     c, (unsigned long long)cap);
-        if (c) LUACHK(h, hipMemcpy(flips, d_flips + 1, c * 8, hipMemcpyDeviceToHost));
     }
     LUACHK(h, hipStreamSynchronize(h->stream));
     return BF_OK;
@@ -434,7 +481,11 @@ int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets,
     int rc = ensure_layer(h, index);
     if (rc) return rc;
     if ((rc = stage_keys(h, keys, offsets, n))) return rc;
-    LUACHK(h, hipMemcpyAsync(h->d_layers, h->layers.data(), index * sizeof(BfGeom), hipMemcpyHostToDevice, h->stream));
+    if (h->d_layers_n < index) {   // upload the table only when a layer was added
+        LUACHK(h, hipMemcpyAsync(h->d_layers, h->layers.data(), index * sizeof(BfGeom), hipMemcpyHostToDevice,
+                                 h->stream));
+        h->d_layers_n = index;
+    }
     hipLaunchKernelGGL(lua_check_kernel, dim3((uint32_t)((n + kLuaTile - 1) / kLuaTile)), dim3(kLuaTile), 0,
                        h->stream, h->d_layers, index, h->d_keys, h->d_off, (uint64_t)0, n, h->d_out);
     LUACHK(h, hipGetLastError());

@@ -56,6 +56,10 @@ def main():
     bf.driver.redis = None
     res["facade_insert_no_redis"] = med_us(lambda i: bf.insert(words[3 * it + i]), it)
     bf.driver.close()
+    lua = pkg.Bloomfilter(size=args.size, error_rate=0.01, key_name="latl", driver="hip-lua", redis=pkg.FakeRedis())
+    res["lua_facade_insert_write_through"] = med_us(lambda i: lua.insert(words[i]), it)
+    res["lua_facade_include"] = med_us(lambda i: lua.include(words[i]), it)
+    lua.driver.close()
     print(json.dumps(res))
 
 
