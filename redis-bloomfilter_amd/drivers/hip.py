@@ -40,7 +40,7 @@ from typing import Iterable, Optional
 import numpy as np
 
 from .. import keys as _keys
-from .._lib import ArgumentError, BF_IMPORT_REPLACE, Filter
+from .._lib import ArgumentError, BF_IMPORT_REPLACE, DIRTY_BLOCK_BYTES, Filter
 
 
 class Hip:
@@ -125,19 +125,19 @@ class Hip:
         # ruby.rb:62 `if !found && expire`: any expire but nil/false counts, 0 included
         armed = expire is not None and expire is not False
         write = self._redis is not None and self.sync_mode == "write_through"
-        n = len(offs) - 1
-        if write and self._changes_ok and n * self.filter.k <= Filter.CHANGES_MAX_PROBES and \
-                int(offs[-1]) - int(offs[0]) <= Filter.CHANGES_MAX_BYTES:
-            # a per-key (small) insert: replay the SETBITs that changed something (ruby.rb:58-60)
-            # rather than SETRANGE whole 64 KiB blocks — a few bytes, and a concurrent
-            # writer's bits in those blocks are never overwritten
-            flips = self.filter.insert_many_changes(buf, offs)
-            any_new = len(flips) > 0
-            if any_new:
-                self._setbits(flips)
-            if any_new and armed:
-                self._arm(expire)
-            return any_new
+        if write and self._changes_ok and self._setbit_sync(offs):
+            # replay the SETBITs that changed something (ruby.rb:58-60) rather than SETRANGE whole
+            # 64 KiB blocks: fewer bytes and Redis work whenever the batch flips fewer bits than
+            # _setbit_sync's budget, and a concurrent writer's bits in those blocks are never
+            # overwritten
+            flips = self._insert_changes(buf, offs)
+            if flips is not None:
+                any_new = len(flips) > 0
+                if any_new:
+                    self._setbits(flips)
+                if any_new and armed:
+                    self._arm(expire)
+                return any_new
         want = armed or write
         any_new, _ = self.filter.insert_many(buf, offs, any_new=want)
         if any_new:
@@ -146,6 +146,36 @@ class Hip:
             if armed:
                 self._arm(expire)
         return bool(any_new) if want else None
+
+    # Redis-side cost model of the two write-through forms: a pipelined SETBIT costs the server
+    # about as much as SETRANGEing ~1 KB (~1 us vs ~1 ns per byte), so replay the flipped bits
+    # while the batch's probes (an upper bound on its flips) stay under 1/1024 of the bytes the
+    # dirty-block flush would send, and always for per-key calls.
+    SETBIT_BYTES = 1024
+
+    def _setbit_sync(self, offs: np.ndarray) -> bool:
+        probes = (len(offs) - 1) * self.filter.k
+        if probes <= Filter.CHANGES_MAX_PROBES:
+            return True
+        blocks = -(-self.filter.device_bytes // DIRTY_BLOCK_BYTES)
+        flush_bytes = min(probes, blocks) * DIRTY_BLOCK_BYTES
+        return probes * self.SETBIT_BYTES <= flush_bytes
+
+    def _insert_changes(self, buf: np.ndarray, offs: np.ndarray):
+        """Insert in bf_insert_many_changes-sized pieces; the flipped bits of all of them, or None
+        (nothing inserted) when a key alone exceeds a piece's byte limit."""
+        n = len(offs) - 1
+        per = max(1, Filter.CHANGES_MAX_PROBES // self.filter.k)
+        o64 = offs.astype(np.int64)
+        if n and int(np.max(np.diff(o64))) > Filter.CHANGES_MAX_BYTES:
+            return None
+        parts, i = [], 0
+        while i < n:
+            j = int(np.searchsorted(o64, o64[i] + Filter.CHANGES_MAX_BYTES, side="right")) - 1
+            j = min(j, i + per, n)
+            parts.append(self.filter.insert_many_changes(buf, offs[i:j + 1]))
+            i = j
+        return np.concatenate(parts) if parts else np.zeros(0, np.uint64)
 
     def _setbits(self, offsets: np.ndarray) -> None:
         """SETBIT key o 1 for every offset, pipelined when the client can (ruby.rb:58-60)."""

@@ -127,9 +127,8 @@ class Redis
       def insert_many(keys, expire = nil)
         expire_if_due
         buf, offs, n = pack(keys)
-        if @redis && @sync == :write_through && changes_path?(n, offs)
-          changed = insert_setbits(buf, offs, n)
-        else
+        changed = insert_setbits(buf, offs, n) if @redis && @sync == :write_through && changes_path?(n)
+        if changed.nil?
           flag = FFI::MemoryPointer.new(:uint8)
           check(HipFFI.bf_insert_many(@handle, buf, offs, n, flag, nil))
           changed = flag.read_uint8 == 1
@@ -246,24 +245,48 @@ class Redis
       # bf_insert_many_changes limits (include/bfhip.h)
       CHANGES_MAX_PROBES = 4096
       CHANGES_MAX_BYTES = 64 << 10
+      BF_DIRTY_BLOCK_BYTES = 65_536
 
-      # A per-key (small) write-through insert replays the SETBITs that changed something,
-      # pipelined like ruby.rb:58-60, instead of SETRANGEing whole 64 KiB blocks: tiny, and a
-      # concurrent writer's bits in those blocks are never overwritten.
-      def changes_path?(n, offs)
-        @options[:devices].nil? && n * @options[:hashes] <= CHANGES_MAX_PROBES &&
-          offs.get_uint64(8 * n) - offs.get_uint64(0) <= CHANGES_MAX_BYTES
+      # Write-through replays the SETBITs an insert flipped (pipelined like ruby.rb:58-60) instead
+      # of SETRANGEing whole 64 KiB blocks while that costs Redis less: a pipelined SETBIT is about
+      # as much server work as ~1 KB of SETRANGE (SETBIT_BYTES), so per-key calls always, and
+      # batches while their probes stay under 1/1024 of the bytes the block flush would send.  A
+      # concurrent writer's bits in those blocks are never overwritten either.
+      SETBIT_BYTES = 1024
+
+      def changes_path?(n)
+        return false unless @options[:devices].nil?
+
+        probes = n * @options[:hashes]
+        return true if probes <= CHANGES_MAX_PROBES
+
+        reach = [@options[:bits], @options[:hashes] * 0xFFFFFFFF + 1].min
+        blocks = ((reach + 7) / 8 + BF_DIRTY_BLOCK_BYTES - 1) / BF_DIRTY_BLOCK_BYTES
+        probes * SETBIT_BYTES <= [probes, blocks].min * BF_DIRTY_BLOCK_BYTES
       end
 
+      # bf_insert_many_changes in pieces of <= CHANGES_MAX_PROBES probes and CHANGES_MAX_BYTES
+      # key bytes; nil (nothing inserted) when one key alone is longer than a piece may be.
       def insert_setbits(buf, offs, n)
-        cap = [n * @options[:hashes], 1].max
-        out = FFI::MemoryPointer.new(:uint64, cap)
-        cnt = FFI::MemoryPointer.new(:uint64)
-        check(HipFFI.bf_insert_many_changes(@handle, buf, offs, n, out, cap, cnt))
-        flips = out.read_array_of_uint64(cnt.read_uint64)
+        o = offs.read_array_of_uint64(n + 1)
+        return nil if (0...n).any? { |j| o[j + 1] - o[j] > CHANGES_MAX_BYTES }
+
+        per = [CHANGES_MAX_PROBES / @options[:hashes], 1].max
+        flips = []
+        i = 0
+        while i < n
+          j = [i + per, n].min
+          j -= 1 while o[j] - o[i] > CHANGES_MAX_BYTES
+          cap = (j - i) * @options[:hashes]
+          out = FFI::MemoryPointer.new(:uint64, [cap, 1].max)
+          cnt = FFI::MemoryPointer.new(:uint64)
+          check(HipFFI.bf_insert_many_changes(@handle, buf, offs + 8 * i, j - i, out, cap, cnt))
+          flips.concat(out.read_array_of_uint64(cnt.read_uint64))
+          i = j
+        end
         unless flips.empty?
           name = @options[:key_name]
-          @redis.pipelined { flips.each { |o| @redis.setbit(name, o, 1) } }
+          @redis.pipelined { flips.each { |b| @redis.setbit(name, b, 1) } }
         end
         !flips.empty?
       end

@@ -124,3 +124,29 @@ def test_write_through_setbits_ruby_test_engines(pkg, O, engine):
         assert r.get("rt") == ref.value(), i
     assert bf.driver.filter.dirty_ranges(clear=False)[0] == []
     bf.driver.close()
+
+
+def test_write_through_batches_pick_the_cheaper_sync(pkg):
+    """A 10k-key batch into the 180 MB (100M@0.1 %) string replays its flipped bits as SETBITs
+    in bf_insert_many_changes-sized pieces (100k probes x 1 KB < the 180 MB block flush); a
+    5k-key batch into a 12 KB string flushes dirty blocks.  Either way Redis ends equal to the
+    device, and the replayed bits are each set once."""
+    big = pkg.Bloomfilter(size=10 ** 8, error_rate=0.001, key_name="big", driver="hip", redis=pkg.FakeRedis())
+    keys = np.random.default_rng(5).integers(0, 1 << 60, size=10000)
+    assert big.driver._setbit_sync(pkg.keys.pack(keys)[1])
+    assert big.insert_many(keys) is True
+    r = big.redis
+    calls = [c for c, _ in r.calls]
+    assert "SETRANGE" not in calls and calls.count("SETBIT") > 50000
+    assert r.get("big") == big.driver.to_redis_string()
+    assert big.driver.filter.dirty_ranges(clear=False)[0] == []
+    assert big.insert_many(keys) is False                        # nothing flips: no SETBIT either
+    assert [c for c, _ in r.calls].count("SETBIT") == calls.count("SETBIT")
+    big.driver.close()
+    small = pkg.Bloomfilter(size=10000, error_rate=0.01, key_name="small", driver="hip", redis=pkg.FakeRedis())
+    ks = ["s%d" % i for i in range(5000)]
+    assert not small.driver._setbit_sync(pkg.keys.pack(ks)[1])
+    small.insert_many(ks)
+    assert "SETRANGE" in [c for c, _ in small.redis.calls]
+    assert small.redis.get("small") == small.driver.to_redis_string()
+    small.driver.close()
