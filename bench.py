@@ -69,10 +69,18 @@ def log(*a):
 
 
 class Dist:
-    def __init__(self, need_group: bool = False):
+    """One process per GPU.  backend "nccl" (RCCL over xGMI) is the measured path; "gloo"
+    is a rehearsal of the same multi-rank step with host-staged exchanges (distributed.py),
+    which also runs several ranks on one GPU (rank r on device r % device_count) — what a
+    one-GPU box can check of the N > 1 path; its times say nothing about xGMI."""
+
+    def __init__(self, need_group: bool = False, backend: str = "nccl"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = backend
+        if backend == "gloo":
+            self.local %= max(torch.cuda.device_count(), 1)
         self.group = self.world > 1 or need_group
         if self.group:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -85,7 +93,10 @@ class Dist:
                 os.environ.setdefault("RANK", "0")
                 os.environ.setdefault("WORLD_SIZE", "1")
             torch.cuda.set_device(self.local)
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", self.local))
+            if backend == "nccl":
+                dist.init_process_group(backend="nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(backend=backend)
         else:
             torch.cuda.set_device(0)
 
@@ -96,7 +107,7 @@ class Dist:
     def max(self, x: float) -> float:
         if self.world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if self.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -659,9 +670,12 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="single GPU: 1 = pipelined steps (next insert batch hashed inside the include? "
                          "kernel, inserted from its SHA-1 words), 0 = plain insert_many + include_many")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL) is the measured path; gloo rehearses N > 1 with host-staged "
+                         "exchanges, several ranks per GPU allowed (not a performance number)")
     args = ap.parse_args()
 
-    D = Dist(need_group=(args.mode in ("partitioned", "replicated")))
+    D = Dist(need_group=(args.mode in ("partitioned", "replicated")), backend=args.dist_backend)
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
                                   mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline))
@@ -732,7 +746,10 @@ def main():
                                                  "over RCCL and every replica applies every batch, or own batch + "
                                                  "OR-all-reduce of the bitset when that moves fewer bytes: %s)"
                                                  % (D.world, main_res.get("replicated_insert_mode")),
-                                   "single": "single GPU"}[main_res["mode"]]},
+                                   "single": "single GPU"}[main_res["mode"]]
+                   + ("" if args.dist_backend == "nccl" else
+                      " [REHEARSAL over gloo, host-staged exchanges, %d GPU(s) shared: not a "
+                      "performance number]" % max(torch.cuda.device_count(), 1))},
         "roofline": {"bound": "hbm", "kernel": dom_name,
                      "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK if achieved else None,

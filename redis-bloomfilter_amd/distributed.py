@@ -40,6 +40,90 @@ from . import keys as _keys
 from ._lib import BF_FLAG_ROUTE32, ArgumentError, Filter
 
 
+
+# -- collectives -------------------------------------------------------------------------
+# RCCL (backend "nccl") moves device tensors directly.  Under gloo the device tensors are
+# staged through host memory (synchronously: the returned works are already complete), so
+# the same exchange runs over gloo with several ranks sharing one GPU — the multi-rank
+# rehearsal of the HIP engine on a one-GPU box (tests/test_gpu_distributed.py), where RCCL
+# refuses a communicator whose ranks share a device.
+
+
+class _Done:
+    """A completed work handle (host-staged collectives finish before they return)."""
+
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def _staged(t: torch.Tensor, group) -> bool:
+    return t.is_cuda and dist.get_backend(group) == dist.Backend.GLOO
+
+
+def _all_to_all_single(recv: torch.Tensor, send: torch.Tensor, group=None, async_op: bool = False):
+    if not _staged(recv, group):
+        return dist.all_to_all_single(recv, send, group=group, async_op=async_op)
+    host = torch.empty(recv.shape, dtype=recv.dtype)
+    dist.all_to_all_single(host, send.cpu(), group=group)
+    recv.copy_(host)
+    return _Done() if async_op else None
+
+
+def _all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
+    if not _staged(out, group):
+        return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+    host = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_gather_into_tensor(host, inp.cpu(), group=group)
+    out.copy_(host)
+    return _Done() if async_op else None
+
+
+def _all_reduce(t: torch.Tensor, op, group=None) -> None:
+    if not _staged(t, group):
+        dist.all_reduce(t, op=op, group=group)
+        return
+    host = t.cpu()
+    dist.all_reduce(host, op=op, group=group)
+    t.copy_(host)
+
+
+def _send(t: torch.Tensor, dst: int, group=None) -> None:
+    dist.send(t.cpu() if _staged(t, group) else t, dst, group=group)
+
+
+def _recv(t: torch.Tensor, src: int, group=None) -> None:
+    if not _staged(t, group):
+        dist.recv(t, src, group=group)
+        return
+    host = torch.empty(t.shape, dtype=t.dtype)
+    dist.recv(host, src, group=group)
+    t.copy_(host)
+
+
+def _batch_p2p(sends, recvs, group=None):
+    """sends / recvs: [(global peer, tensor)]; one group of isend/irecv (messages between two
+    ranks match in list order).  Returns the works to wait on."""
+    ref = sends[0][1] if sends else (recvs[0][1] if recvs else None)
+    if ref is None:
+        return []
+    if not _staged(ref, group):
+        ops = [dist.P2POp(dist.isend, t, g, group) for g, t in sends]
+        ops += [dist.P2POp(dist.irecv, t, g, group) for g, t in recvs]
+        return dist.batch_isend_irecv(ops)
+    hs = [(g, t.cpu()) for g, t in sends]
+    hr = [(g, torch.empty(t.shape, dtype=t.dtype)) for g, t in recvs]
+    ops = [dist.P2POp(dist.isend, t, g, group) for g, t in hs]
+    ops += [dist.P2POp(dist.irecv, t, g, group) for g, t in hr]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    for (_, t), (_, h) in zip(recvs, hr):
+        t.copy_(h)
+    return [_Done()]
+
+
 def block_owner_local(offsets: np.ndarray, P: int, block_log2: int) -> Tuple[np.ndarray, np.ndarray]:
     """Host restatement of the ownership map in include/bfhip.h (for tooling and tests)."""
     o = offsets.astype(np.uint64)
@@ -227,12 +311,12 @@ def or_allreduce_(t: torch.Tensor, group=None) -> torch.Tensor:
     buf = torch.zeros(P * per, dtype=torch.uint8, device=t.device)
     buf[:n] = t
     recv = torch.empty_like(buf)
-    dist.all_to_all_single(recv, buf, group=group)
+    _all_to_all_single(recv, buf, group=group)
     parts = recv.view(P, per // 8, 8).view(torch.int64).view(P, per // 8)
     acc = parts[0].clone()
     for r in range(1, P):
         acc.bitwise_or_(parts[r])
-    dist.all_gather_into_tensor(buf, acc.view(torch.uint8).view(-1), group=group)
+    _all_gather_into_tensor(buf, acc.view(torch.uint8).view(-1), group=group)
     t.copy_(buf[:n])
     return t
 
@@ -284,7 +368,7 @@ class PartitionedFilter:
         """Per-owner send counts -> (send splits, receive splits) on the host (one small
         all-to-all; the host waits for it)."""
         recv_counts = torch.empty_like(counts)
-        dist.all_to_all_single(recv_counts, counts, group=self.group)
+        _all_to_all_single(recv_counts, counts, group=self.group)
         cnt = torch.stack([counts, recv_counts]).cpu()
         return cnt[0].tolist(), cnt[1].tolist()
 
@@ -307,7 +391,7 @@ class PartitionedFilter:
             cap = None
             send, slot, counts = e.route(kb, ko, n, want_slot=want_slot)
         recv_counts = torch.empty_like(counts)
-        work = dist.all_to_all_single(recv_counts, counts, group=self.group, async_op=True)
+        work = _all_to_all_single(recv_counts, counts, group=self.group, async_op=True)
         return dict(kb=kb, ko=ko, n=n, want_slot=want_slot, send=send, slot=slot, counts=counts,
                     recv_counts=recv_counts, work=work, cap=cap)
 
@@ -366,21 +450,18 @@ class PartitionedFilter:
         group of ncclSend/ncclRecv on the process group's stream; messages between two
         ranks match in list order).  The self segments are device copies on the current
         stream.  Returns the works to wait on."""
-        ops = []
         mine_s = [(o, c) for p_, o, c in sseg if p_ == self.rank]
         mine_r = [(o, c) for p_, o, c in rseg if p_ == self.rank]
         for (so, c), (ro, _) in zip(mine_s, mine_r):
             if c:
                 recv[ro: ro + c].copy_(send[so: so + c])
-        for peer, off, c in sseg:
-            if peer != self.rank and c:
-                g = peer if self.group is None else dist.get_global_rank(self.group, peer)
-                ops.append(dist.P2POp(dist.isend, send[off: off + c], g, self.group))
-        for peer, off, c in rseg:
-            if peer != self.rank and c:
-                g = peer if self.group is None else dist.get_global_rank(self.group, peer)
-                ops.append(dist.P2POp(dist.irecv, recv[off: off + c], g, self.group))
-        return dist.batch_isend_irecv(ops) if ops else []
+
+        def g(peer):
+            return peer if self.group is None else dist.get_global_rank(self.group, peer)
+
+        sends = [(g(peer), send[off: off + c]) for peer, off, c in sseg if peer != self.rank and c]
+        recvs = [(g(peer), recv[off: off + c]) for peer, off, c in rseg if peer != self.rank and c]
+        return _batch_p2p(sends, recvs, self.group)
 
     def _exchange(self, kb, ko, n: int, want_slot: bool):
         """route, then the offsets to their owners (async): returns (recv, route, works)."""
@@ -448,7 +529,7 @@ class PartitionedFilter:
         flag = (counts > cap).any().to(torch.int64).view(1, 1)
         msg = torch.cat([counts.view(P, nh), flag.expand(P, 1)], dim=1).contiguous()
         rmsg = torch.empty_like(msg)   # rmsg[s, h]: source s's count for my window h; [s, nh]: its flag
-        work = dist.all_to_all_single(rmsg, msg, group=self.group, async_op=True)
+        work = _all_to_all_single(rmsg, msg, group=self.group, async_op=True)
         sseg = [(o, (o * nh + h) * cap, cap) for o in range(P) for h in range(nh)]
         rseg = [(src, (h * P + src) * cap, cap) for h in range(nh) for src in range(P)]
         recv = torch.empty(nh * P * cap, dtype=send.dtype, device=send.device)
@@ -618,8 +699,8 @@ class PartitionedFilter:
         nblocks = (self.reach_bits + (1 << self.block_log2) - 1) >> self.block_log2
         if self.rank != dst:
             if mine.numel():
-                dist.send(mine, dist.get_global_rank(self.group, dst) if self.group is not None else dst,
-                          group=self.group)
+                _send(mine, dist.get_global_rank(self.group, dst) if self.group is not None else dst,
+                      group=self.group)
             return None
         out = np.zeros(nblocks * bb, dtype=np.uint8)
         view = out.reshape(nblocks, bb)
@@ -633,8 +714,8 @@ class PartitionedFilter:
             if s_ == self.rank:
                 part = mine[:nb]
             else:
-                dist.recv(buf[:nb], dist.get_global_rank(self.group, s_) if self.group is not None else s_,
-                          group=self.group)
+                _recv(buf[:nb], dist.get_global_rank(self.group, s_) if self.group is not None else s_,
+                      group=self.group)
                 part = buf[:nb]
             host = part.cpu().numpy()
             if len(host) < cnt * bb:   # a whole-filter handle (P == 1) stops at the reachable prefix
@@ -660,7 +741,7 @@ class PartitionedFilter:
             lb = int(nz[-1])
             last = ((lb // bb) * self.P + self.rank) * bb + lb % bb
         t = torch.tensor([last], dtype=torch.int64, device=self._shard_tensor().device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        _all_reduce(t, dist.ReduceOp.MAX, group=self.group)
         length = int(t.item()) + 1
         if replace and self.rank == 0:
             redis.delete(key)
@@ -749,7 +830,7 @@ class ReplicatedFilter:
         # (bytes, keys, longest key, first offset): one small all-gather, one host wait
         sizes = torch.cat([ko[n: n + 1] - ko[0:1], z + n, lens.max().view(1) if n else z, ko[0:1]])
         all_sizes = torch.empty(self.P * 4, dtype=torch.int64, device=self.device)
-        dist.all_gather_into_tensor(all_sizes, sizes, group=self.group)
+        _all_gather_into_tensor(all_sizes, sizes, group=self.group)
         all_sizes = all_sizes.view(self.P, 4).cpu().tolist()
         nbytes, _, _, ko0 = all_sizes[dist.get_rank(self.group)]
         all_sizes = [sz[:3] for sz in all_sizes]
@@ -774,8 +855,8 @@ class ReplicatedFilter:
         ln_p[:n] = lens.to(ldt)
         gk = torch.empty(self.P * max_b, dtype=torch.uint8, device=self.device)
         gl = torch.empty(self.P * max_n, dtype=ldt, device=self.device)
-        w1 = dist.all_gather_into_tensor(gk, kb_p, group=self.group, async_op=True)
-        w2 = dist.all_gather_into_tensor(gl, ln_p, group=self.group, async_op=True)
+        w1 = _all_gather_into_tensor(gk, kb_p, group=self.group, async_op=True)
+        w2 = _all_gather_into_tensor(gl, ln_p, group=self.group, async_op=True)
         if n:   # own batch, beside the gather
             self.filter.insert_many_dev(kb.data_ptr(), ko.data_ptr(), n, stream=self._stream())
         w1.wait()

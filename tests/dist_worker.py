@@ -1,9 +1,12 @@
-"""One rank of the multi-process partitioned-filter test (launched by
-tests/test_distributed.py through torch.distributed.run, gloo on CPU).
+"""One rank of the multi-process partitioned-filter test (launched through
+torch.distributed.run over gloo by tests/test_distributed.py on the CPU and by
+tests/test_gpu_distributed.py on a GPU box).
 
-The exchange logic under test is redis-bloomfilter_amd/distributed.py; the
+The exchange logic under test is redis-bloomfilter_amd/distributed.py.  The
 per-rank primitives come from a numpy engine built on the oracle (test
-infrastructure), since this container has no GPU.  Rank 0 checks the
+infrastructure) on the CPU, or — cfg "engine": "hip" — from libbfhip.so's
+HipEngine with every rank on GPU 0 (gloo stages the device tensors through
+host memory; RCCL refuses ranks that share a device).  Every rank checks the
 assembled Redis string and every include? answer against a single-filter
 oracle run over all ranks' keys.
 """
@@ -30,14 +33,15 @@ from redis_bloomfilter_amd import distributed as D  # noqa: E402
 from ref_engine import NumpyEngine  # noqa: E402
 
 
-def or_allreduce_case(rank, P):
+def or_allreduce_case(rank, P, dev=None):
     """distributed.or_allreduce_ against the OR of every rank's tensor, for sizes that do
-    not divide into P 16-byte chunks."""
+    not divide into P 16-byte chunks (dev: a device tensor, host-staged under gloo)."""
     ok = True
     for n in (1, 15, 1000, 4099):
         mine = torch.from_numpy(np.random.default_rng([n, rank]).integers(0, 256, n, dtype=np.uint8))
-        t = mine.clone()
+        t = mine.clone() if dev is None else mine.to(dev)
         D.or_allreduce_(t)
+        t = t.cpu()
         want = np.zeros(n, np.uint8)
         for r in range(P):
             want |= np.random.default_rng([n, r]).integers(0, 256, n, dtype=np.uint8)
@@ -45,20 +49,59 @@ def or_allreduce_case(rank, P):
     return ok
 
 
+def replicated_case(rank, P, cfg, dev):
+    """ReplicatedFilter on the HIP engine: both insert forms (gather, OR-all-reduce) leave
+    every replica's Redis string equal to one oracle filter over all ranks' keys, and the
+    local include? answers equal the oracle's."""
+    m, k = cfg["m"], cfg["k"]
+    orc = O.COracle()
+    keys = [["q%d-%d" % (r, int(v)) for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, cfg["n"])]
+            for r in range(P)]
+    all_keys = [x for ks in keys for x in ks]
+    ib, io = O.pack_keys(all_keys)
+    bits = orc.new_bitset(m, k)
+    orc.insert_many(bits, m, k, ib, io)
+    want_s = orc.redis_string(bits)
+    probe = all_keys + ["fresh-%d-%d" % (rank, i) for i in range(cfg["n"])]
+    pb, po = O.pack_keys(probe)
+    want = orc.include_many(bits, m, k, pb, po).astype(bool)
+    ok = True
+    for mode in ("gather", "or"):
+        rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
+        rf.insert_many(keys[rank])
+        ok = ok and rf.last_insert_mode == mode and rf.export_redis() == want_s
+        ok = ok and bool((rf.include_many(probe) == want).all())
+        rf.close()
+    return ok
+
+
 def main():
     dist.init_process_group("gloo")
     rank, P = dist.get_rank(), dist.get_world_size()
     cfg = json.loads(os.environ["BF_DIST_CFG"])
+    hip = cfg.get("engine") == "hip"
+    dev = torch.device("cuda", 0) if hip else None
+    if cfg.get("case") == "replicated":
+        flag = torch.tensor([1 if replicated_case(rank, P, cfg, dev) else 0])
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            print("DIST_RESULT", "ok" if flag.item() == 1 else "fail", flush=True)
+        dist.destroy_process_group()
+        sys.exit(0 if flag.item() == 1 else 1)
     if cfg.get("case") == "or_allreduce":
-        flag = torch.tensor([1 if or_allreduce_case(rank, P) else 0])
+        flag = torch.tensor([1 if or_allreduce_case(rank, P, dev) else 0])
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if rank == 0:
             print("DIST_RESULT", "ok" if flag.item() == 1 else "fail", flush=True)
         dist.destroy_process_group()
         sys.exit(0 if flag.item() == 1 else 1)
     m, k, b = cfg["m"], cfg["k"], cfg["block_log2"]
+
+    def engine(m, k, P, rank, b, orc, dev):
+        return D.HipEngine(m, k, P, rank, b, dev) if dev is not None else NumpyEngine(m, k, P, rank, b, orc)
+
     orc = O.COracle()
-    pf = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    pf = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
     assert pf.sync_free
     rng = np.random.default_rng([cfg["seed"], rank])
     mine = [("r%d-%d" % (rank, int(v))) for v in rng.integers(0, 10**9, cfg["n"])]
@@ -94,12 +137,12 @@ def main():
         write_ok = merged.tobytes() == want_s and width == len(want_s)
     s = want_s if rank != 0 else s
     # round trip: a fresh partitioned filter loaded from the string answers identically
-    pf2 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    pf2 = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
     pf2.import_redis(s)
     got2 = pf2.include_many(probe)
     # the overlapped insert + include? step gives the sequential form's shard bytes and answers
     del pf2   # the 10B case holds 3.5 GB per shard copy
-    pf3 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc))
+    pf3 = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
     got3 = pf3.insert_include(mine, probe)
     same_shard = bool(np.array_equal(pf3.engine.shard_export(), pf.engine.shard_export()))
     shard_sha = hashlib.sha1(pf.engine.shard_export().tobytes()).hexdigest()
@@ -112,7 +155,7 @@ def main():
     got45 = []
     for kw, cap in (({"windows": False}, None), ({"sync_free": False}, 3), ({}, "sf"),
                     ({"pack_answers": False}, None), ({"pack_answers": False, "sync_free": False}, None)):
-        pf4 = D.PartitionedFilter(m, k, block_log2=b, engine=NumpyEngine(m, k, P, rank, b, orc), **kw)
+        pf4 = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev), **kw)
         if cap == "sf":
             pf4._cap_sf = lambda n: 8
         elif cap is not None:

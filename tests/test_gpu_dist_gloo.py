@@ -1,0 +1,92 @@
+"""The multi-rank exchange on the HIP engine, several ranks on the box's one GPU.
+
+RCCL refuses a communicator whose ranks share a device ("Duplicate GPU detected"), so
+these runs use gloo: distributed.py stages the device tensors through host memory and
+everything else — HipEngine's route / window / owner / pack / combine kernels, the
+sync-free and synced exchanges, the overflow replays, the gather export, per-rank
+write_redis, both replicated insert forms and bench.py's N > 1 step — is the code the
+RCCL runs execute.  Results are checked against the single-filter oracle
+(tests/dist_worker.py).  Times from these runs are not performance numbers.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def torchrun(world, script, args=(), env_extra=None, timeout=240):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2", **(env_extra or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), script, *args]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,m,k,block_log2", [
+    (2, 95851, 6, 10),              # 10k@1 %, small blocks: many blocks per shard
+    (4, 9585058, 6, 12),            # 1M@1 %, four owners
+    (3, 1437758757, 10, 20),        # 100M@0.1 %, odd shard count, 2^20-bit blocks
+    (2, 191701167547, 13, 20),      # 10B@0.01 %: shards past 2^32 bits (nh > 1, uint64 routes)
+])
+def test_partitioned_hip_multirank(world, m, k, block_log2):
+    cfg = {"m": m, "k": k, "block_log2": block_log2, "n": 800, "seed": 11, "engine": "hip"}
+    out = torchrun(world, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
+                   timeout=280)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_replicated_hip_multirank(world):
+    cfg = {"case": "replicated", "m": 9585058, "k": 6, "n": 2000, "seed": 5, "engine": "hip"}
+    out = torchrun(world, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
+                   timeout=110)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
+def test_or_allreduce_device_tensors():
+    cfg = {"case": "or_allreduce", "engine": "hip"}
+    out = torchrun(3, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
+                   timeout=110)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,config,layout", [
+    (2, "1m_big", "replicated"),    # the driver's N = 2 layout (auto)
+    (4, "1m_big", "partitioned"),   # N >= 4 (auto)
+    (2, "nstar", "replicated"),     # the north-star filter at N = 2 (auto: gather insert)
+    (4, "nstar", "partitioned"),    # ... and at N = 4
+])
+def test_bench_multirank_rehearsal(world, config, layout):
+    """bench.py's N > 1 step, launched as the driver launches it (torch.distributed.run),
+    with --dist-backend gloo: one JSON line from rank 0, the auto layout, every step's
+    members found (bench.py asserts it on every rank)."""
+    args = ["--gpus", str(world), "--config", config, "--steps", "2", "--warmup", "1", "--dist-backend", "gloo",
+            "--no-secondary", "--no-cpu-baseline", "--no-host-api", "--no-reference-shapes"]
+    out = torchrun(world, os.path.join(ROOT, "bench.py"), args, timeout=280)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["value"] > 0
+    assert d["config"]["parallelism"].startswith(layout)
+    assert "REHEARSAL" in d["config"]["parallelism"]
