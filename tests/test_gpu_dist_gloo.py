@@ -43,6 +43,8 @@ def torchrun(world, script, args=(), env_extra=None, timeout=240):
     (4, 9585058, 6, 12),            # 1M@1 %, four owners
     (3, 1437758757, 10, 20),        # 100M@0.1 %, odd shard count, 2^20-bit blocks
     (2, 191701167547, 13, 20),      # 10B@0.01 %: shards past 2^32 bits (nh > 1, uint64 routes)
+    (8, 9585058377, 6, 20),         # the north-star filter over eight owners
+    (8, 3834023350947, 13, 20),     # BASELINE configs[4]: 200B@0.01 % partitioned x8 (nh = 2)
 ])
 def test_partitioned_hip_multirank(world, m, k, block_log2):
     cfg = {"m": m, "k": k, "block_log2": block_log2, "n": 800, "seed": 11, "engine": "hip"}
