@@ -270,6 +270,8 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
     __syncthreads();
     const uint64_t smask = (1ull << sup_log2) - 1ull;
     const uint64_t ntiles = (count + kTileProbes - 1) / kTileProbes;
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(local) & 15u) == 0;   // uniform
+    static_assert(kTileProbes == kTile * kSlots, "a tile is kSlots entries per lane");
     const uint64_t tb0 = (uint64_t)blockIdx.x * tiles_per_block;
     const uint64_t tb1 = (tb0 + tiles_per_block < ntiles) ? tb0 + tiles_per_block : ntiles;
     for (uint64_t tile = tb0; tile < tb1; ++tile) {
@@ -281,14 +283,30 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
             if (live > wcap) live = 0;   // an overflowed window holds unwritten entries: skip it whole
             tp = live > i0 ? (uint32_t)(live - i0 < (uint64_t)tp ? live - i0 : tp) : 0u;
         }
+        // Lane t takes entries [12t, 12t + 12): 48 (96) contiguous bytes, read as 16-B vectors
+        // when the tile's buffer is aligned and the lane's entries are all live (the tail lane
+        // and a misaligned caller buffer read entry by entry).
         uint32_t tag[kSlots], loc[kSlots];
+        Off ent[kSlots];
+        const uint32_t j0 = t * (uint32_t)kSlots;
+        if (vec_ok && j0 + kSlots <= tp) {
+            constexpr int kNV = kSlots * (int)sizeof(Off) / 16;
+            const uint4* src = reinterpret_cast<const uint4*>(local + p0 + j0);
+            uint4 vb[kNV];
 #pragma unroll
-        for (int q = 0; q < kSlots; ++q) {   // coalesced: slot q of lane t is entry q * 1024 + t
-            const uint32_t j = (uint32_t)q * kTile + t;
+            for (int v = 0; v < kNV; ++v) vb[v] = src[v];
+            __builtin_memcpy(ent, vb, sizeof(ent));
+        } else {
+#pragma unroll
+            for (int q = 0; q < kSlots; ++q) ent[q] = j0 + q < tp ? local[p0 + j0 + q] : (Off)0;
+        }
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+            const uint32_t j = j0 + (uint32_t)q;
             tag[q] = 0xFFFFFFFFu;
             loc[q] = 0;
             if (j < tp) {
-                const uint64_t o = (uint64_t)local[p0 + j] + bias;
+                const uint64_t o = (uint64_t)ent[q] + bias;
                 if (o < limit) {
                     const uint32_t sb = (uint32_t)(o >> sup_log2);
                     tag[q] = (sb << 16) | atomicAdd(s_cnt + sb, 1u);
@@ -313,7 +331,7 @@ __device__ __forceinline__ void bin_front_offsets_body(const Off* __restrict__ l
             if (tag[q] != 0xFFFFFFFFu) {
                 const uint32_t d = s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu);
                 s_sorted[d] = loc[q];
-                if constexpr (KEYS) s_key[d] = (uint16_t)((uint32_t)q * kTile + t);
+                if constexpr (KEYS) s_key[d] = (uint16_t)(t * (uint32_t)kSlots + (uint32_t)q);
             }
         __syncthreads();
         for (uint32_t j = t; j < tp; j += kTile) {

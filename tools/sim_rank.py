@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--windows", action="store_true",
                     help="route through bf_route_windows_dev (window send buffer, no gather pass); "
                          "a device copy of the windows stands in for the receive")
+    ap.add_argument("--sync-free", action="store_true",
+                    help="the default exchange's compute: whole windows of cap_sf entries, device-side "
+                         "counts, windowed owner ops, packed answers (PartitionedFilter._sf_*); the "
+                         "received windows are this rank's own (nh == 1 configs)")
     args = ap.parse_args()
     pkg = pkgload.load()
     n_items, err, batch, _ = bench.CONFIGS[args.config]
@@ -78,7 +82,26 @@ def main():
                 at += c[w]
         return eng.combine_windows(back, slot, counts, cap, batch)
 
+    def step_sf(b):
+        (ikb, iko), (qkb, qko) = b
+        A = 12288
+        capsf = -(-min(batch * k, batch * k // P + batch * k // (8 * P) + 4096) // A) * A
+        send, _, counts = eng.route_windows(ikb, iko, batch, capsf, want_slot=False)
+        rmsg = torch.cat([counts.view(P, 1), torch.zeros(P, 1, dtype=torch.int64, device=dev)], 1).contiguous()
+        eng.shard_insert_windows(send, capsf, P, rmsg, 0, 2, 0)
+        send, slot, counts = eng.route_windows(qkb, qko, batch, capsf)
+        rmsg = torch.cat([counts.view(P, 1), torch.zeros(P, 1, dtype=torch.int64, device=dev)], 1).contiguous()
+        bits = torch.empty(P * capsf, dtype=torch.uint8, device=dev)
+        eng.shard_test_windows(send, capsf, P, rmsg, 0, 2, 0, bits)
+        cap8 = (capsf + 7) // 8
+        seg = torch.tensor([[src * capsf, capsf, src * cap8] for src in range(P)], dtype=torch.int64).to(dev)
+        packed = eng.pack_answers(bits, seg, capsf, P * cap8)
+        return eng.combine_windows_packed(packed, slot, counts, capsf, batch)
+
     def step(b):
+        if args.sync_free:
+            assert nh == 1
+            return step_sf(b)
         if args.windows:
             return step_windows(b)
         (ikb, iko), (qkb, qko) = b
@@ -100,7 +123,7 @@ def main():
     prof = f.profile_read(reset=True)
     out = {"config": args.config, "shards": args.shards, "m": m, "k": k, "batch": batch,
            "shard_bytes": f.device_bytes, "route32": bool(eng.offset_dtype == torch.int32),
-           "route": "windows" if args.windows else "contiguous",
+           "route": "sync-free windows" if args.sync_free else ("windows" if args.windows else "contiguous"),
            "ms_per_step_compute": wall * 1e3,
            "kernels_ms_per_step": {name: ms / args.steps for name, (ms, _) in prof.items()},
            "kernels_ms_sum": sum(ms for ms, _ in prof.values()) / args.steps,
