@@ -62,6 +62,7 @@ constexpr uint32_t kMaxTilesPerBlock = 16;    // <= 1024 tiles per group: one ru
 constexpr uint32_t kBlockProbes = 8192;       // probes per level-2 chunk block (one bin_mid workgroup)
 constexpr int kChunkPerLane = kBlockProbes / kTile;
 constexpr uint32_t kRunsPerPass = 1024;       // run-table entries per gather pass (one lane each)
+constexpr uint32_t kMidBuckets = 128;         // bin_mid sort buckets per block (>= regions per superbin)
 constexpr uint32_t kMidParts = 2;             // bin_mid workgroups per level-2 window (1 and 4: same time)
 constexpr uint32_t kApplyLanes = 1024;
 
@@ -757,6 +758,12 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const uint32_t b0 = cb_base[w];
     const uint32_t R = 1u << rel_log2;
     const uint32_t rmask = (1u << region_log2) - 1u;
+    // Sort buckets = (region, low offset bits): at least kMidBuckets LDS counters however few
+    // the regions per superbin, so that the rank atomics do not pile onto R words (a 150 MB
+    // shard has R = 16); a region's sub-buckets are consecutive, so its probes stay one run.
+    uint32_t sub = 0;
+    while ((R << sub) < kMidBuckets) ++sub;
+    const uint32_t NB = R << sub, smask_b = (1u << sub) - 1u;
     // run table of the group's tiles (consecutive lanes, consecutive tiles: coalesced)
     const uint64_t tlo = (uint64_t)q * tiles_per_group;
     const uint64_t thi = (tlo + tiles_per_group < ntiles) ? tlo + tiles_per_group : ntiles;
@@ -797,24 +804,25 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     for (uint32_t c = c_lo; c < c_hi; ++c) {
         const uint32_t f0 = c * kBlockProbes;
         const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
-        if (t < R) s_cnt[t] = 0;
+        if (t < NB) s_cnt[t] = 0;
         __syncthreads();   // also orders the previous block's reads of s_sorted / s_cnt
         uint32_t tag[kChunkPerLane];
 #pragma unroll
         for (int u = 0; u < kChunkPerLane; ++u) {
             tag[u] = 0xFFFFFFFFu;
             if (lv[u] != 0xFFFFFFFFu) {
-                const uint32_t r = lv[u] >> region_log2;
-                tag[u] = (r << 16) | atomicAdd(s_cnt + r, 1u);
+                const uint32_t bk = ((lv[u] >> region_log2) << sub) | (lv[u] & smask_b);
+                tag[u] = (bk << 16) | atomicAdd(s_cnt + bk, 1u);
             }
         }
         uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
         if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
         __syncthreads();
-        const uint32_t cn = t < R ? s_cnt[t] : 0u;
+        const uint32_t cn = t < NB ? s_cnt[t] : 0u;
         const uint32_t cex = block_excl_scan(cn, s_w, nullptr);   // its barriers order the s_cnt reads first
-        if (t <= R) tabs[(uint64_t)t * max_chunks + b0 + c] = (uint16_t)cex;   // [region][block]
-        if (t < R) s_cnt[t] = cex;
+        if (!(t & smask_b) && (t >> sub) <= R)
+            tabs[(uint64_t)(t >> sub) * max_chunks + b0 + c] = (uint16_t)cex;   // [region][block]
+        if (t < NB) s_cnt[t] = cex;
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kChunkPerLane; ++u) {
