@@ -889,6 +889,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
     h->g.inv_shards = 1.0 / (double)h->shards;
+    h->g.shards_pow2 = (h->shards & (h->shards - 1u)) == 0 ? 1u : 0u;
+    h->g.shard_log2 = (uint32_t)__builtin_ctz(h->shards);
     h->g.route32 = h->route32 ? 1u : 0u;
     h->g.limit = h->local_bits;
     h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k, h->dev_bytes));

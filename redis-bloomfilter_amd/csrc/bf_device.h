@@ -171,6 +171,11 @@ __device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, u
 // block b = o >> block_log2 lives on shard b % P at local block b / P.
 __device__ __forceinline__ void owner_local(const BfGeom& g, uint64_t o, uint32_t& owner, uint64_t& local) {
     const uint64_t blk = o >> g.block_log2;
+    if (g.shards_pow2) {   // 2, 4, 8 ... GPUs: mask and shift
+        owner = (uint32_t)blk & (g.shards - 1u);
+        local = ((blk >> g.shard_log2) << g.block_log2) | (o & ((1ull << g.block_log2) - 1ull));
+        return;
+    }
     // blk < 2^44 is exact in a double and 1/P carries 2^-53 relative error: the estimate
     // is within one of blk / P, fixed exactly below (no 64-bit integer divide)
     uint64_t lblk = (uint64_t)((double)blk * g.inv_shards);

@@ -15,6 +15,8 @@ struct BfGeom {
     uint32_t  shards;  // partitioned filters: shard count P (1 = whole filter)
     uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
     double    inv_shards;  // 1.0 / P, for the division-free block -> (owner, local block) map
+    uint32_t  shards_pow2; // 1 iff P is a power of two: the map is a mask and a shift
+    uint32_t  shard_log2;  // log2(P) when shards_pow2
     // probe policies (tuning; results are identical for every setting)
     uint32_t  first_round;  // include?: probes loaded before the first early-exit check (0 = all k)
     uint32_t  next_round;   // include?: probes per later round (0 = all the rest at once)
