@@ -211,7 +211,7 @@ def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
 
 
 def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto",
-                overlap: bool = True, pipeline: bool = False):
+                overlap: bool = True, pipeline: bool = False, comm_prefetch: bool = False):
     n, p, batch, prefill = CONFIGS[name]
     B = pkg.Bloomfilter
     m = B.optimal_m(n, p)
@@ -258,10 +258,25 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         f.hash_many_dev(ikb0.data_ptr(), iko0.data_ptr(), batch, digs[0].data_ptr(), stream=sp)
         step_no = [0]
 
+    # Replicated, comm_prefetch: step i starts the all-gather of batch i+1's keys before its
+    # own work, so the exchange runs beside step i's inserts and include? (the process group's
+    # stream); step i then inserts every rank's batch i — its own with the others, as ONE
+    # insert — before its include?, so every answer still sees all of the step's inserts.  The
+    # last step gathers batch 0 again, so every step does the same work.
+    comm_prefetch = comm_prefetch and rf is not None
+    gpend, rstep = {}, [0]
+
     def insert(bt):
         ikb, iko = bt[0]
         if pipeline:
             f.insert_digests_dev(digs[step_no[0] % 2].data_ptr(), batch, stream=sp)
+        elif comm_prefetch:
+            i = rstep[0]
+            st = gpend.pop(i % len(batches), None) or rf.gather_start(ikb, iko, batch)
+            nxt = (i + 1) % len(batches)
+            gpend[nxt] = rf.gather_start(*batches[nxt][0], batch)
+            rf.insert_gathered(st)
+            rstep[0] = i + 1
         elif rf is not None:
             rf.insert_many_dev(ikb, iko, batch)
         elif pf is None:
@@ -314,6 +329,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     torch.cuda.synchronize()
     D.barrier()
     wall = time.perf_counter() - t_start
+    for st in gpend.values():   # the wrap-around gather of batch 0 (comm_prefetch)
+        for w in st.get("works", []):
+            w.wait()
     wall = D.max(wall)
     ins_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     inc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
@@ -670,6 +688,9 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="single GPU: 1 = pipelined steps (next insert batch hashed inside the include? "
                          "kernel, inserted from its SHA-1 words), 0 = plain insert_many + include_many")
+    ap.add_argument("--comm-prefetch", type=int, default=1,
+                    help="replicated: 1 = gather the next step's key batches during this step, then "
+                         "insert every rank's batch as one insert; 0 = gather beside the own insert")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL) is the measured path; gloo rehearses N > 1 with host-staged "
                          "exchanges, several ranks per GPU allowed (not a performance number)")
@@ -678,7 +699,8 @@ def main():
     D = Dist(need_group=(args.mode in ("partitioned", "replicated")), backend=args.dist_backend)
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
-                                  mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline))
+                                  mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline),
+                                  comm_prefetch=bool(args.comm_prefetch))
     secondary = {}
     if D.world == 1 and not args.no_secondary:
         # 1m_big: the L2-resident 1M@1 % filter at 2^24-key batches (hash-bound; 1m's 2^20-key
@@ -744,8 +766,10 @@ def main():
                                                   "batches routed to owner GPUs, grouped RCCL send/recv)" % D.world,
                                    "replicated": "replicated x%d (include? local; insert batches all-gathered "
                                                  "over RCCL and every replica applies every batch, or own batch + "
-                                                 "OR-all-reduce of the bitset when that moves fewer bytes: %s)"
-                                                 % (D.world, main_res.get("replicated_insert_mode")),
+                                                 "OR-all-reduce of the bitset when that moves fewer bytes: %s%s)"
+                                                 % (D.world, main_res.get("replicated_insert_mode"),
+                                                    "; the next step's batches gathered during this step"
+                                                    if args.comm_prefetch else ""),
                                    "single": "single GPU"}[main_res["mode"]]
                    + ("" if args.dist_backend == "nccl" else
                       " [REHEARSAL over gloo, host-staged exchanges, %d GPU(s) shared: not a "

@@ -825,6 +825,20 @@ class ReplicatedFilter:
         else int32) are all-gathered while this rank's own batch is inserted, then the
         other ranks' batches go in as ONE insert (one binned pass over the bitset).
         or: this rank's batch, then the bitset OR-all-reduced."""
+        st = self.gather_start(kb, ko, n)
+        if st["mode"] == "gather" and n:   # own batch, beside the gather
+            self.filter.insert_many_dev(kb.data_ptr(), ko.data_ptr(), n, stream=self._stream())
+            self.insert_gathered(st, own_inserted=True)
+        else:
+            self.insert_gathered(st)
+
+    def gather_start(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> dict:
+        """Enqueue the all-gather of this rank's batch (collective: every rank calls it, in
+        the same order); ``insert_gathered`` finishes it.  Between the two the gather runs on
+        the process group's stream beside whatever the caller enqueues — e.g. the previous
+        batch's inserts and include?s, so a pipelined caller hides the exchange.  Only the
+        batch sizes (one small all-gather) make the host wait.  In "or" mode nothing travels
+        here; ``insert_gathered`` inserts and OR-all-reduces."""
         z = torch.zeros(1, dtype=torch.int64, device=self.device)
         lens = (ko[1: n + 1] - ko[:n]) if n else z[:0]
         # (bytes, keys, longest key, first offset): one small all-gather, one host wait
@@ -839,12 +853,8 @@ class ReplicatedFilter:
             wide = max(sz[2] for sz in all_sizes) > 255
             gather_bytes = sum(sz[0] + sz[1] * (4 if wide else 1) for sz in all_sizes)
             mode = "or" if 2 * self.filter.device_bytes < gather_bytes else "gather"
-        self.last_insert_mode = mode
         if mode == "or":
-            if n:
-                self.filter.insert_many_dev(kb.data_ptr(), ko.data_ptr(), n, stream=self._stream())
-            or_allreduce_(device_bytes_view(self.filter), self.group)
-            return
+            return dict(mode="or", kb=kb, ko=ko, n=n)
         max_b = max(max(sz[0] for sz in all_sizes), 1)
         max_n = max(max(sz[1] for sz in all_sizes), 1)
         ldt = torch.uint8 if max(sz[2] for sz in all_sizes) <= 255 else torch.int32
@@ -855,13 +865,24 @@ class ReplicatedFilter:
         ln_p[:n] = lens.to(ldt)
         gk = torch.empty(self.P * max_b, dtype=torch.uint8, device=self.device)
         gl = torch.empty(self.P * max_n, dtype=ldt, device=self.device)
-        w1 = _all_gather_into_tensor(gk, kb_p, group=self.group, async_op=True)
-        w2 = _all_gather_into_tensor(gl, ln_p, group=self.group, async_op=True)
-        if n:   # own batch, beside the gather
-            self.filter.insert_many_dev(kb.data_ptr(), ko.data_ptr(), n, stream=self._stream())
-        w1.wait()
-        w2.wait()
-        ob, oo, on = merge_gathered(gk, gl, all_sizes, max_b, max_n, skip=dist.get_rank(self.group))
+        works = [_all_gather_into_tensor(gk, kb_p, group=self.group, async_op=True),
+                 _all_gather_into_tensor(gl, ln_p, group=self.group, async_op=True)]
+        return dict(mode="gather", kb=kb, ko=ko, n=n, gk=gk, gl=gl, send=(kb_p, ln_p), works=works,
+                    sizes=all_sizes, max_b=max_b, max_n=max_n)
+
+    def insert_gathered(self, st: dict, own_inserted: bool = False) -> None:
+        """Finish ``gather_start``: every rank's batch goes in — this rank's own with the
+        others as ONE insert (one binned pass over the bitset) unless ``own_inserted``."""
+        self.last_insert_mode = st["mode"]
+        if st["mode"] == "or":
+            if st["n"]:
+                self.filter.insert_many_dev(st["kb"].data_ptr(), st["ko"].data_ptr(), st["n"], stream=self._stream())
+            or_allreduce_(device_bytes_view(self.filter), self.group)
+            return
+        for w in st["works"]:
+            w.wait()
+        skip = dist.get_rank(self.group) if own_inserted else -1
+        ob, oo, on = merge_gathered(st["gk"], st["gl"], st["sizes"], st["max_b"], st["max_n"], skip=skip)
         if on:
             self.filter.insert_many_dev(ob.data_ptr(), oo.data_ptr(), on, stream=self._stream())
 

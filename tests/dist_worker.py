@@ -72,6 +72,19 @@ def replicated_case(rank, P, cfg, dev):
         ok = ok and rf.last_insert_mode == mode and rf.export_redis() == want_s
         ok = ok and bool((rf.include_many(probe) == want).all())
         rf.close()
+    # the pipelined form bench.py uses: the batch's gather started ahead of other work (here a
+    # second gather in flight), then every rank's batch, this rank's included, as one insert
+    half = len(keys[rank]) // 2
+    kb1, ko1, n1 = D._device_batch(keys[rank][:half], dev)
+    kb2, ko2, n2 = D._device_batch(keys[rank][half:], dev)
+    for mode in ("gather", "or"):
+        rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
+        st1 = rf.gather_start(kb1, ko1, n1)
+        st2 = rf.gather_start(kb2, ko2, n2)
+        rf.insert_gathered(st1)
+        rf.insert_gathered(st2)
+        ok = ok and rf.last_insert_mode == mode and rf.export_redis() == want_s
+        rf.close()
     return ok
 
 

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.parametrize("mode,config", [("partitioned", "1m_big"), ("replicated", "1m_big"),
-                                         ("partitioned", "nstar")])
+                                         ("partitioned", "nstar"), ("replicated", "nstar")])
 def test_bench_layouts_world1(mode, config):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", mode, "--config", config, "--steps", "2",
            "--warmup", "1", "--no-secondary", "--no-cpu-baseline", "--no-host-api", "--no-reference-shapes"]
