@@ -263,6 +263,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     # stream); step i then inserts every rank's batch i — its own with the others, as ONE
     # insert — before its include?, so every answer still sees all of the step's inserts.  The
     # last step gathers batch 0 again, so every step does the same work.
+    comm_prefetch_flag = comm_prefetch
     comm_prefetch = comm_prefetch and rf is not None
     gpend, rstep = {}, [0]
 
@@ -299,13 +300,22 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         else:
             out.copy_(pf.include_many_dev(pkb, pko, batch))
 
-    for bt in batches[:warmup]:
+    # Partitioned, comm_prefetch (sync-free exchange): step i routes and sends batch i+1's
+    # inserts beside its own owner kernels (PartitionedFilter.insert_include_dev next_insert);
+    # every step still applies all ranks' batch-i inserts before its include?.
+    pf_prefetch = comm_prefetch_flag and pf is not None and overlap and pf.sync_free
+
+    def part_step(i):
+        (ikb, iko), (pkb, pko) = batches[i]
+        nxt = (batches[(i + 1) % len(batches)][0] + (batch,)) if pf_prefetch else None
+        out.copy_(pf.insert_include_dev(ikb, iko, batch, pkb, pko, batch, next_insert=nxt))
+
+    for i, bt in enumerate(batches[:warmup]):
         if pf is None or not overlap:
             insert(bt)
             include(bt)
         else:
-            (ikb, iko), (pkb, pko) = bt
-            out.copy_(pf.insert_include_dev(ikb, iko, batch, pkb, pko, batch))
+            part_step(i)
     prof = pf.engine.filter if pf is not None else f
     prof.profile(True)      # per-kernel HIP events, recorded on the launch stream inside the timed region
     prof.profile_read(reset=True)
@@ -313,7 +323,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     torch.cuda.synchronize()
     ev = []
     t_start = time.perf_counter()
-    for bt in batches[warmup:]:
+    for i, bt in enumerate(batches[warmup:], start=warmup):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         e[0].record(stream)
         if pf is None or not overlap:
@@ -322,8 +332,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             include(bt)
         else:   # partitioned: one overlapped insert + include? step (same results)
             e[1].record(stream)
-            (ikb, iko), (pkb, pko) = bt
-            out.copy_(pf.insert_include_dev(ikb, iko, batch, pkb, pko, batch))
+            part_step(i)
         e[2].record(stream)
         ev.append(e)
     torch.cuda.synchronize()
@@ -332,6 +341,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     for st in gpend.values():   # the wrap-around gather of batch 0 (comm_prefetch)
         for w in st.get("works", []):
             w.wait()
+    if pf_prefetch:   # the wrap-around route of batch 0 (already inserted: idempotent)
+        pf.drain_prefetch()
     wall = D.max(wall)
     ins_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     inc_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
@@ -689,8 +700,9 @@ def main():
                     help="single GPU: 1 = pipelined steps (next insert batch hashed inside the include? "
                          "kernel, inserted from its SHA-1 words), 0 = plain insert_many + include_many")
     ap.add_argument("--comm-prefetch", type=int, default=1,
-                    help="replicated: 1 = gather the next step's key batches during this step, then "
-                         "insert every rank's batch as one insert; 0 = gather beside the own insert")
+                    help="1 = exchange the next step's insert batch during this step (replicated: gather "
+                         "its keys, then insert every rank's batch as one insert; partitioned: route and "
+                         "send its probes beside this step's owner kernels); 0 = within the step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL) is the measured path; gloo rehearses N > 1 with host-staged "
                          "exchanges, several ranks per GPU allowed (not a performance number)")
@@ -763,7 +775,9 @@ def main():
                                                                           main_res["k"], batch, batch),
                    "global_batch": 2 * batch * D.world,
                    "parallelism": {"partitioned": "partitioned x%d (block-cyclic 2^20-bit blocks; per-rank key "
-                                                  "batches routed to owner GPUs, grouped RCCL send/recv)" % D.world,
+                                                  "batches routed to owner GPUs, grouped RCCL send/recv%s)"
+                                                  % (D.world, "; the next step's inserts routed and sent during "
+                                                     "this step" if args.comm_prefetch else ""),
                                    "replicated": "replicated x%d (include? local; insert batches all-gathered "
                                                  "over RCCL and every replica applies every batch, or own batch + "
                                                  "OR-all-reduce of the bitset when that moves fewer bytes: %s%s)"

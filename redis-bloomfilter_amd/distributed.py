@@ -624,12 +624,22 @@ class PartitionedFilter:
         return out
 
     def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
-                           qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
+                           qkb: torch.Tensor, qko: torch.Tensor, nq: int, next_insert=None) -> torch.Tensor:
+        """insert_many_dev(ikb, iko, ni) then include_many_dev(qkb, qko, nq), exchanges overlapped.
+
+        ``next_insert`` = (kb, ko, n), sync-free exchange only: the NEXT call's insert batch is
+        routed and sent now, so its exchange runs beside this call's owner kernels; the next
+        call must then pass that same batch as (ikb, iko, ni)."""
+        pend, self._pending = getattr(self, "_pending", None), None
+        if pend is not None and not (pend["kb"] is ikb and pend["n"] == ni):
+            raise ArgumentError("insert_include_dev: the insert batch differs from the prefetched next_insert")
         if self.sync_free:
             # route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test |
             # send(back) | combine, all enqueued before the host waits for anything
-            st_i = self._sf_start(ikb, iko, ni, want_slot=False)
+            st_i = pend if pend is not None else self._sf_start(ikb, iko, ni, want_slot=False)
             st_q = self._sf_start(qkb, qko, nq, want_slot=True)
+            if next_insert is not None:
+                self._pending = self._sf_start(*next_insert, want_slot=False)
             self._sf_flag(st_i)
             self._sf_flag(st_q)
             self._sf_insert(st_i)
@@ -640,6 +650,16 @@ class PartitionedFilter:
                 out.copy_(self._synced_include(qkb, qko, nq))
             return out
         return self._insert_include_synced(ikb, iko, ni, qkb, qko, nq)
+
+    def drain_prefetch(self) -> None:
+        """Complete a prefetched next_insert that no call will consume: its batch is inserted."""
+        pend, self._pending = getattr(self, "_pending", None), None
+        if pend is not None:
+            self._sf_flag(pend)
+            self._sf_insert(pend)
+            if self._sf_overflowed(pend):
+                self.replays += 1
+                self._synced_insert(pend["kb"], pend["ko"], pend["n"])
 
     def _insert_include_synced(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
                                qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:

@@ -180,6 +180,21 @@ def main():
         elif cap is not None:
             same_shard = same_shard and pf4.window_overflows == 2
         del pf4
+    # the cross-step form bench.py uses: the next call's insert batch routed and sent during
+    # this call (next_insert), then consumed by the next call; a prefetch no call consumes
+    # is completed by drain_prefetch
+    half = len(mine) // 2
+    kb1, ko1, n1 = D._device_batch(mine[:half], dev or "cpu")
+    kb2, ko2, n2 = D._device_batch(mine[half:], dev or "cpu")
+    qkb, qko, nq = D._device_batch(probe, dev or "cpu")
+    pf6 = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
+    pf6.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2))
+    got6 = pf6.insert_include_dev(kb2, ko2, n2, qkb, qko, nq, next_insert=(kb1, ko1, n1))
+    pf6.drain_prefetch()
+    got6 = got6.cpu().numpy().astype(bool)
+    same_shard = same_shard and hashlib.sha1(pf6.engine.shard_export().tobytes()).hexdigest() == shard_sha
+    del pf6
+    got45.append(got6)
     ok = True
     if rank == 0 or True:
         bits = orc.new_bitset(m, k)
