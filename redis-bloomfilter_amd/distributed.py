@@ -39,13 +39,11 @@ import torch.distributed as dist
 from . import keys as _keys
 from ._lib import BF_FLAG_ROUTE32, ArgumentError, Filter
 
-
-
 # -- collectives -------------------------------------------------------------------------
 # RCCL (backend "nccl") moves device tensors directly.  Under gloo the device tensors are
 # staged through host memory (synchronously: the returned works are already complete), so
 # the same exchange runs over gloo with several ranks sharing one GPU — the multi-rank
-# rehearsal of the HIP engine on a one-GPU box (tests/test_gpu_distributed.py), where RCCL
+# rehearsal of the HIP engine on a one-GPU box (tests/test_gpu_dist_gloo.py), where RCCL
 # refuses a communicator whose ranks share a device.
 
 
