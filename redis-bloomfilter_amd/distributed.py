@@ -1,5 +1,6 @@
 """Multi-GPU filters: one process per GPU, collectives through torch.distributed
-(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests).
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests and, with device
+tensors staged through host memory, for several ranks sharing one GPU in the GPU tests).
 
 Two layouts (SURVEY §8 e):
 
