@@ -47,6 +47,15 @@ GRANULE = 64               # B per random probe (SURVEY §8 d)
 # or cache policy, at ~55 G fills/s for any working set from 64 MiB to 1.2 GB (Infinity Cache
 # residency does not raise it): tools/probe_granularity.hip, profiles/r02_probe_granularity.log
 FILL_CEILING = 55.1e9      # fills/s, plain loads, 1143 MiB working set
+# ... and 50.2 G/s over 6656 MiB, the reach-capped 10B / 200B bitsets (profiles/r02z_probe_sweep.log)
+FILL_CEILING_7GB = 50.2e9
+
+
+def fill_ceiling(bitset_bytes: int):
+    """The measured random-fill ceiling for a bitset of this size, and its source."""
+    if bitset_bytes > (2 << 30):
+        return FILL_CEILING_7GB, "tools/probe_granularity.hip sweep, 6656 MiB (profiles/r02z_probe_sweep.log)"
+    return FILL_CEILING, "tools/probe_granularity.hip (profiles/r02_probe_granularity.log)"
 SEED = 0x5EED
 
 CONFIGS = {
@@ -753,9 +762,9 @@ def main():
         d = fp ** (1.0 / kk) if fp > 0 else 0.0
         per_key = 0.5 * kk + 0.5 * ((1 - fp) / (1 - d) if d < 1 else kk)
         rate = batch * per_key / (dom["ms"] / 1e3)
-        fills = {"fills_per_key": per_key, "bit_density": d, "fills_per_s": rate, "ceiling_fills_per_s": FILL_CEILING,
-                 "frac": rate / FILL_CEILING,
-                 "ceiling_source": "tools/probe_granularity.hip (profiles/r02_probe_granularity.log)"}
+        ceil, ceil_src = fill_ceiling(main_res["bitset_bytes"])
+        fills = {"fills_per_key": per_key, "bit_density": d, "fills_per_s": rate, "ceiling_fills_per_s": ceil,
+                 "frac": rate / ceil, "ceiling_source": ceil_src}
     line = {
         "metric": "keys/sec (insert, include?) per GPU and whole node; % of HBM random-access roofline",
         "value": main_res["keys_per_s"],

@@ -5,6 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/probe_granularity tools/probe_granularity.hip
 //   ./tools/probe_granularity             (prints one line per variant)
+//   ./tools/probe_granularity sweep       (working-set sweep only, up to 6.98 GB)
 //   rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
 //       --kernel-trace -d <dir> -o run -- ./tools/probe_granularity
 //
@@ -82,7 +83,10 @@ static float run(const uint32_t* d, uint64_t words, uint64_t probes, uint32_t* o
     return ms / reps;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    // "sweep": only the working-set sweep, extended past the north-star filter to the
+    // reach-capped 10B / 200B bitsets (6.98 GB)
+    const bool sweep_only = argc > 1 && argv[1][0] == 's';
     const uint64_t bytes = 1198132288ull;   // 9585058377 bits rounded up to 64 B (the north-star filter)
     const uint64_t words = bytes / 4;
     const uint64_t probes = 1ull << 27;      // 134M random 4-B probes per launch
@@ -97,6 +101,7 @@ int main() {
         {"finegrained", hipDeviceMallocFinegrained, true},
     };
     for (const Mem& m : mems) {
+        if (sweep_only) break;
         uint32_t* d = nullptr;
         if (m.ext) {
             if (hipExtMallocWithFlags(reinterpret_cast<void**>(&d), bytes, m.flags) != hipSuccess) {
@@ -131,7 +136,8 @@ int main() {
     }
     // working-set sweep (plain loads, hipMalloc): L2 (4 MiB per XCD), Infinity Cache
     // (256 MiB), past it
-    for (uint64_t mb : {2ull, 16ull, 64ull, 128ull, 192ull, 256ull, 384ull, 600ull, 1143ull}) {
+    for (uint64_t mb : {2ull, 16ull, 64ull, 128ull, 192ull, 256ull, 384ull, 600ull, 1143ull, 2400ull, 4800ull, 6656ull}) {
+        if (!sweep_only && mb > 1143ull) break;
         const uint64_t b = mb << 20;
         uint32_t* d = nullptr;
         CHK(hipMalloc(&d, b));
