@@ -83,11 +83,16 @@ class Dist:
     which also runs several ranks on one GPU (rank r on device r % device_count) — what a
     one-GPU box can check of the N > 1 path; its times say nothing about xGMI."""
 
-    def __init__(self, need_group: bool = False, backend: str = "nccl"):
+    def __init__(self, need_group: bool = False, backend: str = "nccl", no_device: bool = False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.backend = backend
+        if no_device:   # --launch-check: the process group alone (gloo), no GPU touched
+            self.group = self.world > 1 or need_group
+            if self.group:
+                dist.init_process_group(backend="gloo")
+            return
         if backend == "gloo":
             self.local %= max(torch.cuda.device_count(), 1)
         self.group = self.world > 1 or need_group
@@ -276,10 +281,20 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     comm_prefetch = comm_prefetch and rf is not None
     gpend, rstep = {}, [0]
 
+    # Every timed insert asks for any_new, the reference's !found that drives EXPIRE
+    # (ruby.rb:61-62): one pre-zeroed flag word per step, so no memset joins the step.
+    flags = torch.zeros(len(batches), dtype=torch.int32, device=dev)
+    fstep = [0]
+
+    def any_new_ptr():
+        i = fstep[0]
+        fstep[0] = i + 1
+        return flags[i % len(batches)].data_ptr()
+
     def insert(bt):
         ikb, iko = bt[0]
         if pipeline:
-            f.insert_digests_dev(digs[step_no[0] % 2].data_ptr(), batch, stream=sp)
+            f.insert_digests_dev(digs[step_no[0] % 2].data_ptr(), batch, d_any_new=any_new_ptr(), stream=sp)
         elif comm_prefetch:
             i = rstep[0]
             st = gpend.pop(i % len(batches), None) or rf.gather_start(ikb, iko, batch)
@@ -290,7 +305,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         elif rf is not None:
             rf.insert_many_dev(ikb, iko, batch)
         elif pf is None:
-            f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, stream=sp)
+            f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, d_any_new=any_new_ptr(), stream=sp)
         else:
             pf.insert_many_dev(ikb, iko, batch)
 
@@ -364,6 +379,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     # sanity: the members (first half of the include? batch) must all be found
     got = out.cpu().numpy()
     assert got[: batch // 2].all(), "false negative in the include? batch"
+    any_new_steps = int(flags[:fstep[0]].ne(0).sum().item())
+    if fstep[0] and prefill == "random":   # 2^24 fresh keys into a half-empty filter flip bits
+        assert any_new_steps == fstep[0], "an insert batch reported any_new = false"
     fp_rate = float(got[batch // 2:].mean())
     Lmean = float(batches[-1][1][1][-1].item()) / batch
     P = batch * k
@@ -425,6 +443,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
                     "observed_fp_rate": fp_rate},
         "kernels": kernels,
         "bitset_bytes": bitset,
+        "any_new_requested": bool(fstep[0]), "any_new_steps": any_new_steps,
     }
     ib, io = to_host(*batches[0][0])
     pb, po = to_host(*batches[0][1])
@@ -685,6 +704,62 @@ def load_pmc(workload: str):
             "kernels": {kn: {x: rec.get(x) for x in keep} for kn, rec in t.items() if isinstance(rec, dict)}}
 
 
+def _free_port() -> int:
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(gpus: int, argv, json_out) -> int:
+    """``python bench.py --gpus N`` started without a launcher (no WORLD_SIZE): start the N
+    ranks as ONE child ``torch.distributed.run`` (a fresh process, started before this one
+    touches the GPU — no exec), relay rank 0's JSON line, and return the child's exit code.
+    The ranks see WORLD_SIZE = N, so the line's n_gpus is N or the run fails."""
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BFBENCH_SELF_LAUNCHED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    log("bench: --gpus %d without WORLD_SIZE: launching %d ranks (%s)" % (gpus, gpus, " ".join(cmd[1:6])))
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    relayed = 0
+    for ln in proc.stdout:   # rank 0's JSON line; anything else a library printed goes to stderr
+        if ln.lstrip().startswith("{"):
+            print(ln.rstrip("\n"), file=json_out, flush=True)
+            relayed += 1
+        else:
+            sys.stderr.write(ln)
+    rc = proc.wait()
+    if rc == 0 and relayed != 1:
+        log("bench: the %d-rank run printed %d JSON lines, expected 1" % (gpus, relayed))
+        return 3
+    return rc
+
+
+def check_world(gpus: int) -> None:
+    """A launcher's world size must be the --gpus asked for: a mismatch would report an N-GPU
+    number for another N."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None and int(world) != gpus:
+        log("bench: --gpus %d but WORLD_SIZE=%s: refusing to report a %s-rank run as %d GPUs"
+            % (gpus, world, world, gpus))
+        sys.exit(2)
+
+
+def launch_check(D: "Dist", json_out) -> None:
+    """--launch-check: the process group as bench.py builds it, then rank 0 reports the world
+    it saw and exits (no filter, no GPU work): what the CPU tests check of the N-rank launch."""
+    seen = dist.get_world_size() if dist.is_initialized() else 1
+    if D.rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": D.world, "world_size_seen": seen,
+                          "backend": D.backend,
+                          "self_launched": os.environ.get("BFBENCH_SELF_LAUNCHED") == "1"}),
+              file=json_out, flush=True)
+    D.close()
+
+
 def main():
     # Libraries (RCCL's version banner, HIP) may write to stdout; the contract is ONE JSON
     # line there, so fd 1 goes to stderr for the run and the JSON to the original stdout.
@@ -715,9 +790,24 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL) is the measured path; gloo rehearses N > 1 with host-staged "
                          "exchanges, several ranks per GPU allowed (not a performance number)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="build the process group, print the world size rank 0 saw, exit (no GPU work)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        json_out.flush()
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], json_out))
+    check_world(args.gpus)
 
-    D = Dist(need_group=(args.mode in ("partitioned", "replicated")), backend=args.dist_backend)
+    D = Dist(need_group=(args.mode in ("partitioned", "replicated")), backend=args.dist_backend,
+             no_device=args.launch_check)
+    if args.launch_check:
+        return launch_check(D, json_out)
+    world_seen = dist.get_world_size() if dist.is_initialized() else 1
+    if world_seen != args.gpus:
+        log("bench: the process group has %d ranks, --gpus %d" % (world_seen, args.gpus))
+        sys.exit(2)
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
                                   mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline),
@@ -770,6 +860,11 @@ def main():
         "value": main_res["keys_per_s"],
         "unit": "keys/s",
         "n_gpus": D.world,
+        # the process group's own size (RCCL communicator under nccl) and who started the ranks
+        "world_size_seen": world_seen,
+        "launcher": ("bench.py --gpus %d (one torch.distributed.run child)" % args.gpus
+                     if os.environ.get("BFBENCH_SELF_LAUNCHED") == "1" else
+                     "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ or D.world > 1 else "single process"),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": main_res["wall_s"] / args.steps * 1e3,

@@ -92,3 +92,21 @@ def test_bench_multirank_rehearsal(world, config, layout):
     assert d["n_gpus"] == world and d["value"] > 0
     assert d["config"]["parallelism"].startswith(layout)
     assert "REHEARSAL" in d["config"]["parallelism"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_plain_gpus_n_runs_n_ranks():
+    """``python bench.py --gpus 2`` with no launcher around it: bench.py
+    starts the two ranks itself and the line reports n_gpus == 2 from a 2-rank group."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "1m_big", "--steps", "2",
+            "--warmup", "1", "--dist-backend", "gloo", "--no-secondary", "--no-cpu-baseline", "--no-host-api",
+            "--no-reference-shapes"]
+    out = subprocess.run(args, env=env, capture_output=True, text=True, timeout=280, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size_seen"] == 2 and d["value"] > 0
+    assert d["launcher"].startswith("bench.py --gpus 2")
