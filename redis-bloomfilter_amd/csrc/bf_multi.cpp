@@ -169,7 +169,19 @@ uint64_t window_cap(const BfMulti* mh, uint64_t nd) {
 
 }  // namespace
 
-// Allocations of one device's round (keys, offsets, windows, counts).
+// The per-slot words every round may touch whatever its part's size: the window counts and
+// the owner's any_new flag.  Allocated on the slot's own device, for every slot — an owner
+// whose own part is empty still ORs other devices' windows and reports any_new.
+static int ensure_small(BfMulti* mh, uint32_t d) {
+    DevScratch& x = mh->ds[d];
+    if (x.counts && x.flag) return BF_OK;
+    DevGuard g(mh->dev[d]);
+    if (!x.counts) MCHK(mh, hipMalloc((void**)&x.counts, 256 * sizeof(uint64_t)));
+    if (!x.flag) MCHK(mh, hipMalloc((void**)&x.flag, 256));
+    return BF_OK;
+}
+
+// Allocations of one device's round (keys, offsets, windows).
 static int prepare_round(BfMulti* mh, uint32_t d, const uint8_t* keys, const uint64_t* offsets, bool want_slot) {
     DevScratch& x = mh->ds[d];
     DevGuard g(mh->dev[d]);
@@ -186,8 +198,6 @@ static int prepare_round(BfMulti* mh, uint32_t d, const uint8_t* keys, const uin
         if ((rc = grow(mh, &x.send, &x.send_cap, nwin * x.cap))) return rc;
         MCHK(mh, hipMalloc((void**)&x.slot, x.send_cap * sizeof(uint32_t)));
     }
-    if (!x.counts) MCHK(mh, hipMalloc((void**)&x.counts, 256 * sizeof(uint64_t)));
-    if (!x.flag) MCHK(mh, hipMalloc((void**)&x.flag, 256));
     x.rel.resize(x.n + 1);
     for (uint64_t j = 0; j <= x.n; ++j) x.rel[j] = offsets[x.a + j] - base;
     x.cnt.assign(nwin, 0);
@@ -223,6 +233,8 @@ static int partitioned_round(BfMulti* mh, const uint8_t* keys, const uint64_t* o
                              bool* any_new) {
     const uint32_t D = mh->D, nh = mh->nh, nwin = D * nh;
     int rc;
+    for (uint32_t d = 0; d < D; ++d)
+        if ((rc = ensure_small(mh, d))) return rc;
     for (uint32_t d = 0; d < D; ++d) {   // every device's route in flight at once
         DevScratch& x = mh->ds[d];
         x.cap = window_cap(mh, x.n);
@@ -245,6 +257,15 @@ static int partitioned_round(BfMulti* mh, const uint8_t* keys, const uint64_t* o
             if ((rc = route_wait(mh, d))) return rc;
         }
     }
+    // each requester's answer windows, on the requester's own device, before any owner
+    // pushes into them (a grow inside the owner loop would allocate on the owner's device)
+    if (include)
+        for (uint32_t d = 0; d < D; ++d) {
+            DevScratch& x = mh->ds[d];
+            if (!x.n) continue;
+            DevGuard g(mh->dev[d]);
+            if ((rc = grow(mh, &x.back, &x.back_cap, (uint64_t)nwin * x.cap))) return rc;
+        }
     // owners pull their windows (sub-range major, then source), apply or test them, and
     // (include?) push the answers back into each requester's window layout
     for (uint32_t o = 0; o < D; ++o) {
@@ -279,7 +300,6 @@ static int partitioned_round(BfMulti* mh, const uint8_t* keys, const uint64_t* o
                     DevScratch& x = mh->ds[d];
                     const uint64_t c = x.cnt[o * nh + h];
                     if (!c) continue;
-                    if ((rc = grow(mh, &x.back, &x.back_cap, (uint64_t)nwin * x.cap))) return rc;
                     MCHK(mh, hipMemcpyPeerAsync(x.back + (uint64_t)(o * nh + h) * x.cap, mh->dev[d], y.bits + bt,
                                                 mh->dev[o], c, y.s));
                     bt += c;
@@ -306,7 +326,6 @@ static int partitioned_round(BfMulti* mh, const uint8_t* keys, const uint64_t* o
         if (!x.n) continue;
         DevGuard g(mh->dev[d]);
         for (uint32_t o = 0; o < D; ++o) MCHK(mh, hipStreamWaitEvent(x.s, mh->ds[o].ev, 0));
-        if ((rc = grow(mh, &x.back, &x.back_cap, (uint64_t)nwin * x.cap))) return rc;
         if ((rc = grow(mh, &x.out, &x.out_cap, x.n))) return rc;
         rc = bf_combine_windows_dev(mh->sub[d], x.back, x.slot, x.cap, nwin, x.counts, x.n, x.out, x.s);
         if (rc) return sub_rc(mh, d, rc);

@@ -31,6 +31,7 @@ substitute a numpy engine to exercise this module's exchange logic over gloo.
 """
 from __future__ import annotations
 
+import os
 from typing import Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -183,6 +184,11 @@ class HipEngine:
         self.k, self.P = k, P
         self.offset_dtype = torch.int32 if route32 else torch.int64
         self.nh = self.filter.route_window_split()   # 2^32-bit sub-ranges per window-routed owner
+        # Test hook (PartitionedFilter(poison=...) / BFHIP_POISON_WINDOWS): the route's send
+        # windows and slots are filled before the route writes them, so an owner or combine
+        # that reads an entry past a window's live count reads a known wrong value instead of
+        # whatever the caching allocator handed back (the r02 illegal-address fault).
+        self.poison = None
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -205,6 +211,10 @@ class HipEngine:
         send = torch.empty(nwin * cap, dtype=torch.int32, device=self.device)
         slot = torch.empty(nwin * cap, dtype=torch.int32, device=self.device) if want_slot else None
         counts = torch.empty(nwin, dtype=torch.int64, device=self.device)
+        if self.poison is not None:
+            send.fill_(self.poison)
+            if slot is not None:
+                slot.fill_(0)   # a dead slot names key 0: a stray AND into it shows as a wrong answer
         self.filter.route_windows_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
                                       slot.data_ptr() if want_slot else 0, cap, counts.data_ptr(),
                                       stream=self._stream())
@@ -342,7 +352,8 @@ class PartitionedFilter:
     WINDOW_ALIGN = 12288   # BF_WINDOW_CAP_ALIGN: windows the owner's binned path can take whole
 
     def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None,
-                 windows: bool = True, pack_answers: bool = True, sync_free: bool = True):
+                 windows: bool = True, pack_answers: bool = True, sync_free: bool = True,
+                 batch_capacity: Optional[int] = None, poison: Optional[int] = None):
         self.group = group
         self.P = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -361,6 +372,26 @@ class PartitionedFilter:
         self.sync_free = bool(sync_free and windows and hasattr(engine, "shard_insert_windows"))
         self.replays = 0
         self._pk_seg = {}
+        self._pending = None
+        # The sync-free windows are sized from a batch bound every rank agrees on, never from
+        # the rank's own n: ranks that size them from different n would post p2p messages of
+        # different sizes (undefined under RCCL).  ``batch_capacity`` (the same on every rank)
+        # fixes it up front; otherwise the first sync-free call agrees on max n by one
+        # all-reduce.  A later call with n past the bound overflows its windows, which every
+        # rank sees in the overflow flag, and the synced replay (counts exchanged, any sizes)
+        # raises the bound on every rank together.
+        self._sf_n = int(batch_capacity) if batch_capacity else None
+        self.agreements = 0
+        # Test hook: every window buffer of the exchange (send windows, receive windows,
+        # returned answers) is filled with a known value before it is written, so that a read
+        # of a dead entry is a deterministic wrong bit or answer.  Routed
+        # entries get `poison` (an owner-local offset: 1 puts a stray bit where the oracle has
+        # none), answer bytes 0 (a stray AND turns a member false).
+        if poison is None and os.environ.get("BFHIP_POISON_WINDOWS"):
+            poison = int(os.environ["BFHIP_POISON_WINDOWS"], 0)
+        self.poison = poison
+        if poison is not None and hasattr(engine, "poison"):
+            engine.poison = poison
 
     # -- exchange helpers
     def _splits(self, counts: torch.Tensor):
@@ -466,8 +497,15 @@ class PartitionedFilter:
         """route, then the offsets to their owners (async): returns (recv, route, works)."""
         return self._send_routed(self._route(kb, ko, n, want_slot))
 
+    def _buf(self, n: int, dtype, device, answers: bool = False) -> torch.Tensor:
+        """An exchange buffer (uninitialised, or poisoned under the test hook)."""
+        t = torch.empty(n, dtype=dtype, device=device)
+        if self.poison is not None:
+            t.fill_(0 if answers else self.poison)
+        return t
+
     def _send_routed(self, rt: dict):
-        recv = torch.empty(rt["total"], dtype=rt["send"].dtype, device=rt["send"].device)
+        recv = self._buf(rt["total"], rt["send"].dtype, rt["send"].device)
         works = self._p2p(rt["send"], rt["sseg"], recv, rt["rseg"])
         return recv, rt, works
 
@@ -482,7 +520,7 @@ class PartitionedFilter:
     def _shard_test(self, recv: torch.Tensor, rt: dict) -> torch.Tensor:
         if rt["hruns"] is None:
             return self.engine.shard_test(recv)
-        bits = torch.empty(recv.numel(), dtype=torch.uint8, device=recv.device)
+        bits = self._buf(recv.numel(), torch.uint8, recv.device, answers=True)
         for h, a, b in rt["hruns"]:
             if b > a:
                 self.engine.shard_test_hi(recv[a:b], h, bits[a:b])
@@ -493,12 +531,12 @@ class PartitionedFilter:
         cap = rt["cap"]
         if "pseg" in rt:   # one bit per probe on the way back
             packed = self.engine.pack_answers(bits, rt["pseg"], rt["pk_max"], rt["pk_total"])
-            back = torch.empty(max(rt["counts"].numel() * rt["cap8"], 1), dtype=torch.uint8, device=bits.device)
+            back = self._buf(max(rt["counts"].numel() * rt["cap8"], 1), torch.uint8, bits.device, answers=True)
             for w in self._p2p(packed, rt["pk_send"], back, rt["pk_recv"]):
                 w.wait()
             return self.engine.combine_windows_packed(back, rt["slot"], rt["counts"], cap, n)
         size = rt["send"].numel() if cap is not None else sum(c for _, _, c in rt["sseg"])
-        back = torch.empty(size, dtype=torch.uint8, device=bits.device)
+        back = self._buf(size, torch.uint8, bits.device, answers=True)
         for w in self._p2p(bits, rt["rseg"], back, rt["sseg"]):
             w.wait()
         if cap is not None:
@@ -519,11 +557,22 @@ class PartitionedFilter:
 
     def _cap_sf(self, n: int) -> int:
         a = self.WINDOW_ALIGN
-        return -(-self._cap(n) // a) * a
+        return -(-self._cap(max(n, 1)) // a) * a
+
+    def _agree_batch(self, n: int) -> None:
+        """Collective (every rank calls it at the same point): the window bound becomes the
+        largest batch any rank has brought so far."""
+        t = torch.tensor([int(n), self._sf_n or 0], dtype=torch.int64, device=self.device)
+        _all_reduce(t, dist.ReduceOp.MAX, group=self.group)
+        self._sf_n = int(t.max().item())
+        self.agreements += 1
 
     def _sf_start(self, kb, ko, n: int, want_slot: bool) -> dict:
         e, P, nh = self.engine, self.P, self.engine.nh
-        cap = self._cap_sf(n)
+        if self._sf_n is None:
+            self._agree_batch(n)
+        # the same cap on every rank; a batch past the agreed bound overflows (global flag)
+        cap = self._cap_sf(self._sf_n)
         send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
         flag = (counts > cap).any().to(torch.int64).view(1, 1)
         msg = torch.cat([counts.view(P, nh), flag.expand(P, 1)], dim=1).contiguous()
@@ -531,7 +580,7 @@ class PartitionedFilter:
         work = _all_to_all_single(rmsg, msg, group=self.group, async_op=True)
         sseg = [(o, (o * nh + h) * cap, cap) for o in range(P) for h in range(nh)]
         rseg = [(src, (h * P + src) * cap, cap) for h in range(nh) for src in range(P)]
-        recv = torch.empty(nh * P * cap, dtype=send.dtype, device=send.device)
+        recv = self._buf(nh * P * cap, send.dtype, send.device)
         works = self._p2p(send, sseg, recv, rseg)
         return dict(kb=kb, ko=ko, n=n, cap=cap, send=send, slot=slot, counts=counts, rmsg=rmsg, work=work,
                     recv=recv, works=works)
@@ -564,7 +613,7 @@ class PartitionedFilter:
         e, P, nh, cap, n = self.engine, self.P, self.engine.nh, st["cap"], st["n"]
         for w in st["works"]:
             w.wait()
-        bits = torch.empty(nh * P * cap, dtype=torch.uint8, device=st["recv"].device)
+        bits = self._buf(nh * P * cap, torch.uint8, st["recv"].device, answers=True)
         for h in range(nh):
             e.shard_test_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h,
                                  bits[h * P * cap:(h + 1) * P * cap])
@@ -576,12 +625,12 @@ class PartitionedFilter:
                                                   for src in range(P) for h in range(nh)],
                                                  dtype=torch.int64).to(bits.device)
             packed = e.pack_answers(bits, self._pk_seg[key], cap, P * nh * cap8)
-            back = torch.empty(P * nh * cap8, dtype=torch.uint8, device=bits.device)
+            back = self._buf(P * nh * cap8, torch.uint8, bits.device, answers=True)
             seg = [(src, (src * nh + h) * cap8, cap8) for src in range(P) for h in range(nh)]
             for w in self._p2p(packed, seg, back, seg):
                 w.wait()
             return e.combine_windows_packed(back, st["slot"], st["counts"], cap, n)
-        back = torch.empty(P * nh * cap, dtype=torch.uint8, device=bits.device)
+        back = self._buf(P * nh * cap, torch.uint8, bits.device, answers=True)
         sseg = [(src, (h * P + src) * cap, cap) for src in range(P) for h in range(nh)]
         rseg = [(o, (o * nh + h) * cap, cap) for o in range(P) for h in range(nh)]
         for w in self._p2p(bits, sseg, back, rseg):
@@ -607,9 +656,10 @@ class PartitionedFilter:
         st = self._sf_start(kb, ko, n, want_slot=False)
         self._sf_flag(st)
         self._sf_insert(st)
-        if self._sf_overflowed(st):   # a skewed batch: replay it through the synced path
+        if self._sf_overflowed(st):   # a skewed or oversized batch: replay it through the synced path
             self.replays += 1
             self._synced_insert(kb, ko, n)
+            self._agree_batch(n)
 
     def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
         if not self.sync_free:
@@ -620,6 +670,7 @@ class PartitionedFilter:
         if self._sf_overflowed(st):
             self.replays += 1
             out.copy_(self._synced_include(kb, ko, n))
+            self._agree_batch(n)
         return out
 
     def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
@@ -629,9 +680,14 @@ class PartitionedFilter:
         ``next_insert`` = (kb, ko, n), sync-free exchange only: the NEXT call's insert batch is
         routed and sent now, so its exchange runs beside this call's owner kernels; the next
         call must then pass that same batch as (ikb, iko, ni)."""
-        pend, self._pending = getattr(self, "_pending", None), None
+        pend = self._pending
         if pend is not None and not (pend["kb"] is ikb and pend["n"] == ni):
-            raise ArgumentError("insert_include_dev: the insert batch differs from the prefetched next_insert")
+            # the prefetched batch is already routed and sent: complete it (it was announced
+            # as the next insert) before refusing the call, so no rank drops it
+            self.drain_prefetch()
+            raise ArgumentError("insert_include_dev: the insert batch differs from the prefetched next_insert "
+                                "(the prefetched batch was inserted)")
+        self._pending = None
         if self.sync_free:
             # route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test |
             # send(back) | combine, all enqueued before the host waits for anything
@@ -647,18 +703,28 @@ class PartitionedFilter:
                 self.replays += 1
                 self._synced_insert(ikb, iko, ni)
                 out.copy_(self._synced_include(qkb, qko, nq))
+                self._agree_batch(max(ni, nq))
             return out
         return self._insert_include_synced(ikb, iko, ni, qkb, qko, nq)
 
     def drain_prefetch(self) -> None:
         """Complete a prefetched next_insert that no call will consume: its batch is inserted."""
-        pend, self._pending = getattr(self, "_pending", None), None
+        pend, self._pending = self._pending, None
         if pend is not None:
             self._sf_flag(pend)
             self._sf_insert(pend)
             if self._sf_overflowed(pend):
                 self.replays += 1
                 self._synced_insert(pend["kb"], pend["ko"], pend["n"])
+                self._agree_batch(pend["n"])
+
+    def _no_pending(self, what: str) -> None:
+        """A prefetched next_insert is routed and sent but not yet applied: a call that
+        replaces or reads the whole filter would race it or miss it, so it must be consumed
+        (insert_include_dev) or completed (drain_prefetch) first."""
+        if self._pending is not None:
+            raise ArgumentError("%s: a prefetched next_insert is pending; pass it to insert_include_dev "
+                                "or call drain_prefetch() first" % what)
 
     def _insert_include_synced(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
                                qkb: torch.Tensor, qko: torch.Tensor, nq: int) -> torch.Tensor:
@@ -700,6 +766,7 @@ class PartitionedFilter:
         return self.insert_include_dev(ikb, iko, ni, qkb, qko, nq).cpu().numpy().astype(bool)
 
     def clear(self) -> None:
+        self._no_pending("clear")
         self.engine.clear()
 
     # -- Redis string (collective: every rank must call)
@@ -713,6 +780,7 @@ class PartitionedFilter:
         shards travel one at a time into one preallocated buffer of the largest shard's size
         (device memory under RCCL), so no rank but ``dst`` ever holds more than its own shard
         and ``dst`` holds the string once, on the host."""
+        self._no_pending("export_redis")
         mine = self._shard_tensor()
         bb = (1 << self.block_log2) // 8
         nblocks = (self.reach_bits + (1 << self.block_log2) - 1) >> self.block_log2
@@ -752,6 +820,7 @@ class PartitionedFilter:
         grows the key to exactly the length the SETBITs would have.
         ``replace``: rank 0 DELs the key first (a barrier orders it before the writes).
         Returns the bytes this rank sent."""
+        self._no_pending("write_redis")
         local = self.engine.shard_export()
         bb = (1 << self.block_log2) // 8
         nz = np.flatnonzero(local)
@@ -781,6 +850,7 @@ class PartitionedFilter:
         return sent
 
     def import_redis(self, data: bytes) -> None:
+        self._no_pending("import_redis")
         self.engine.shard_import(split_shard(data, self.P, self.rank, self.reach_bits, self.block_log2))
 
     def close(self):

@@ -88,6 +88,85 @@ def replicated_case(rank, P, cfg, dev):
     return ok
 
 
+def uneven_case(rank, P, cfg, dev, make_engine):
+    """Ranks that bring batches of different sizes (the sync-free windows must
+    not be sized from a rank's own n), one rank bringing none, and a later batch past the
+    agreed bound on one rank only (its windows overflow, every rank replays through the
+    synced path and the bound rises).  Shard bytes and answers must equal the oracle's."""
+    m, k = cfg["m"], cfg["k"]
+    orc = O.COracle()
+    sizes = [cfg["n"] + 97 * r if r != P - 1 or P < 3 else 0 for r in range(P)]
+
+    def keys_of(r, n, tag):
+        return ["%s%d-%d" % (tag, r, int(v)) for v in np.random.default_rng([cfg["seed"], r, n]).integers(0, 10**9, n)]
+
+    pf = D.PartitionedFilter(m, k, block_log2=cfg["block_log2"], engine=make_engine())
+    pf.insert_many(keys_of(rank, sizes[rank], "a"))                      # agrees on max n
+    probe1 = keys_of(rank, sizes[rank], "a")[: sizes[rank] // 2] + keys_of(rank, 50 + 13 * rank, "x")
+    got1 = pf.include_many(probe1)
+    # the bench's cross-step form with uneven batches (next_insert prefetched)
+    kb1, ko1, n1 = D._device_batch(keys_of(rank, sizes[rank] // 3, "b"), dev or "cpu")
+    kb2, ko2, n2 = D._device_batch(keys_of(rank, 7 * rank + 5, "c"), dev or "cpu")
+    probe2 = keys_of(rank, 40 + rank, "b") + keys_of(rank, sizes[rank] // 3, "b")[:20]
+    qkb, qko, nq = D._device_batch(probe2, dev or "cpu")
+    pf.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2))
+    got2 = pf.insert_include_dev(kb2, ko2, n2, qkb, qko, nq).cpu().numpy().astype(bool)
+    agreed = pf._sf_n
+    # rank 0 twice past its windows at the agreed bound (every window holds ~1/(P nh) of the probes)
+    nwin = P * getattr(pf.engine, "nh", 1)
+    big = [2 * pf._cap_sf(agreed) * nwin // k + 1 if r == 0 else cfg["n"] // 2 for r in range(P)]
+    # rank 0 alone past the bound: a global overflow, a synced replay, a raised bound
+    pf.insert_many(keys_of(rank, big[rank], "d"))
+    probe3 = keys_of(rank, big[rank], "d")[::3] + keys_of(rank, 30, "y")
+    got3 = pf.include_many(probe3)
+    ok = pf.replays >= 1 and pf._sf_n >= max(big) and agreed == max(sizes)
+    # the oracle over every rank's keys
+    allk = []
+    for r in range(P):
+        allk += keys_of(r, sizes[r], "a") + keys_of(r, sizes[r] // 3, "b") + keys_of(r, 7 * r + 5, "c")
+        allk += keys_of(r, big[r], "d")
+    ib, io = O.pack_keys(allk)
+    bits = orc.new_bitset(m, k)
+    orc.insert_many(bits, m, k, ib, io)
+    want_s = orc.redis_string(bits)
+    s = pf.export_redis()
+    ok = ok and ((s == want_s) if rank == 0 else s is None)
+    # answers: probe1 after the "a" inserts only, probe2 after a+b+c... — recompute in order
+    def answers(ins_sets, probe):
+        b2 = orc.new_bitset(m, k)
+        ks = [x for r in range(P) for fn in ins_sets for x in fn(r)]
+        kb_, ko_ = O.pack_keys(ks)
+        orc.insert_many(b2, m, k, kb_, ko_)
+        pb, po = O.pack_keys(probe)
+        return orc.include_many(b2, m, k, pb, po).astype(bool)
+    a_ = lambda r: keys_of(r, sizes[r], "a")
+    b_ = lambda r: keys_of(r, sizes[r] // 3, "b")
+    c_ = lambda r: keys_of(r, 7 * r + 5, "c")
+    d_ = lambda r: keys_of(r, big[r], "d")
+    ok = ok and bool((got1 == answers([a_], probe1)).all())
+    ok = ok and bool((got2 == answers([a_, b_, c_], probe2)).all())
+    ok = ok and bool((got3 == answers([a_, b_, c_, d_], probe3)).all())
+    if not ok:
+        print("rank %d uneven MISMATCH: replays %d agreed %s bound %s" % (rank, pf.replays, agreed, pf._sf_n),
+              flush=True)
+    # a pending prefetch blocks the whole-filter calls, and a mismatched consume still inserts it
+    pf.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2))
+    try:
+        pf.clear()
+        ok = False
+    except pkg.ArgumentError:
+        pass
+    try:
+        pf.insert_include_dev(kb1, ko1, n1, qkb, qko, nq)
+        ok = False
+    except pkg.ArgumentError:
+        pass
+    ok = ok and pf._pending is None
+    pf.clear()
+    pf.close()
+    return ok
+
+
 def main():
     dist.init_process_group("gloo")
     rank, P = dist.get_rank(), dist.get_world_size()
@@ -114,6 +193,13 @@ def main():
         return D.HipEngine(m, k, P, rank, b, dev) if dev is not None else NumpyEngine(m, k, P, rank, b, orc)
 
     orc = O.COracle()
+    if cfg.get("case") == "uneven":
+        flag = torch.tensor([1 if uneven_case(rank, P, cfg, dev, lambda: engine(m, k, P, rank, b, orc, dev)) else 0])
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            print("DIST_RESULT", "ok" if flag.item() == 1 else "fail", flush=True)
+        dist.destroy_process_group()
+        sys.exit(0 if flag.item() == 1 else 1)
     pf = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
     assert pf.sync_free
     rng = np.random.default_rng([cfg["seed"], rank])

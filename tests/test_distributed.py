@@ -44,6 +44,27 @@ def test_partitioned_gloo(world, m, k, block_log2):
     assert "DIST_RESULT ok" in out.stdout
 
 
+@pytest.mark.parametrize("world,m,k,block_log2", [
+    (2, 95851, 6, 10),
+    (3, 9585058, 6, 12),            # one rank brings an empty batch
+])
+def test_partitioned_uneven_batches_gloo(world, m, k, block_log2):
+    """Ranks with different batch sizes through the sync-free exchange, a batch
+    past the agreed window bound on one rank (global overflow -> synced replay), and the
+    pending-prefetch guards."""
+    env = dict(os.environ)
+    env["BF_DIST_CFG"] = json.dumps({"case": "uneven", "m": m, "k": k, "block_log2": block_log2, "n": 300,
+                                     "seed": 3})
+    env["BFHIP_STANDALONE"] = "1"
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(HERE, "dist_worker.py")]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_or_allreduce_gloo(world):
     """The replicated filter's OR-all-reduce (all_to_all + local OR + all_gather)."""

@@ -54,6 +54,40 @@ def test_partitioned_hip_multirank(world, m, k, block_log2):
     assert "DIST_RESULT ok" in out.stdout
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,m,k,block_log2", [
+    (2, 95851, 6, 10),
+    (8, 9585058377, 6, 20),         # the north-star filter over eight owners
+    (8, 3834023350947, 13, 20),     # 200B x8 (nh = 2)
+])
+def test_partitioned_hip_multirank_poisoned(world, m, k, block_log2):
+    """The same runs (forced overflows of the sync-free and synced exchanges included) with
+    every window buffer poisoned before it is written: routed entries
+    hold owner-local offset 1 (a bit the oracle leaves 0 at these sizes: a stray OR breaks
+    the Redis string) and answer bytes 0 (a stray AND turns a member false)."""
+    cfg = {"m": m, "k": k, "block_log2": block_log2, "n": 800, "seed": 11, "engine": "hip"}
+    out = torchrun(world, os.path.join(HERE, "dist_worker.py"),
+                   env_extra={"BF_DIST_CFG": json.dumps(cfg), "BFHIP_POISON_WINDOWS": "1"}, timeout=280)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,m,k,block_log2", [
+    (3, 9585058, 6, 12),            # one rank brings an empty batch
+    (2, 3834023350947, 13, 20),     # 200B at P = 2: shards past 2^32 bits, nh = 7 sub-range windows
+])
+def test_partitioned_hip_uneven_batches(world, m, k, block_log2):
+    """Ranks bringing different batch sizes through the sync-free exchange, one
+    rank past the agreed window bound (global overflow -> synced replay -> raised bound),
+    and the pending-prefetch guards, on the HIP engine, windows poisoned."""
+    cfg = {"case": "uneven", "m": m, "k": k, "block_log2": block_log2, "n": 300, "seed": 3, "engine": "hip"}
+    out = torchrun(world, os.path.join(HERE, "dist_worker.py"),
+                   env_extra={"BF_DIST_CFG": json.dumps(cfg), "BFHIP_POISON_WINDOWS": "1"}, timeout=280)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_replicated_hip_multirank(world):
     cfg = {"case": "replicated", "m": 9585058, "k": 6, "n": 2000, "seed": 5, "engine": "hip"}

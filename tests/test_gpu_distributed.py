@@ -269,10 +269,23 @@ def _free_port():
     return p
 
 
-def test_torch_distributed_world1(pkg, oracle):
-    """PartitionedFilter and ReplicatedFilter over RCCL (world size 1) match a single filter."""
+@pytest.mark.parametrize("poison", [None, "zero-bit"])
+def test_torch_distributed_world1(pkg, oracle, monkeypatch, poison):
+    """PartitionedFilter and ReplicatedFilter over RCCL (world size 1) match a single filter.
+
+    poison="zero-bit" (VERDICT r02 item 6): every exchange buffer is filled before it is
+    written — routed entries with the offset of a bit the oracle leaves 0, answer bytes with
+    0 — so a kernel that reads an entry past a window's live count (the r02 fault) sets that
+    bit or turns a member false, deterministically, instead of depending on what the caching
+    allocator hands back.  The forced-overflow cases below run under it."""
     import torch
     import torch.distributed as dist
+    if poison:
+        ob = oracle.new_bitset(9585058, 6)
+        ib_, io_ = pkg.keys.pack(["k%d" % i for i in range(50_000)])
+        oracle.insert_many(ob, 9585058, 6, ib_, io_)
+        raw = np.unpackbits(ob.view(np.uint8))
+        monkeypatch.setenv("BFHIP_POISON_WINDOWS", str(int(np.flatnonzero(raw == 0)[0])))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))

@@ -118,3 +118,25 @@ def test_hip_driver_devices_option(pkg, oracle):
         for key in keys:
             rd.insert(key)
         assert r.get("bf_" + mode) == ref.get("x")
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_partitioned_first_call_fewer_keys_than_devices(pkg, oracle, devices):
+    """a fresh partitioned handle whose FIRST call is a one-key insert asking for
+    any_new (the hip driver's per-key insert under write-through) — device slots with an
+    empty part own windows too, so their flag and counts must exist before the owner loop.
+    Then one- and two-key include?s, whose answer windows live on the requester's device."""
+    m, k = 95851, 6
+    for keys in (["solo"], ["a", "b"]):
+        ib, io = pkg.keys.pack(keys)
+        bits = oracle.new_bitset(m, k)
+        oracle.insert_many(bits, m, k, ib, io)
+        with pkg.Filter(m, k, devices=devices, mode="partitioned") as f:
+            any1, _ = f.insert_many(ib, io, any_new=True)
+            any2, _ = f.insert_many(ib, io, any_new=True)
+            assert (any1, any2) == (True, False)
+            assert f.export_redis() == oracle.redis_string(bits)
+            pb, po = pkg.keys.pack(keys[:1])
+            assert f.include_many(pb, po).tolist() == [1]
+            qb, qo = pkg.keys.pack(keys + ["absent-%d" % i for i in range(3)])
+            np.testing.assert_array_equal(f.include_many(qb, qo), oracle.include_many(bits, m, k, qb, qo))
