@@ -279,7 +279,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     # last step gathers batch 0 again, so every step does the same work.
     comm_prefetch_flag = comm_prefetch
     comm_prefetch = comm_prefetch and rf is not None
-    gpend, rstep = {}, [0]
+    gpend, rstep, szp = {}, [0], {}
 
     # Every timed insert asks for any_new, the reference's !found that drives EXPIRE
     # (ruby.rb:61-62): one pre-zeroed flag word per step, so no memset joins the step.
@@ -296,10 +296,13 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         if pipeline:
             f.insert_digests_dev(digs[step_no[0] % 2].data_ptr(), batch, d_any_new=any_new_ptr(), stream=sp)
         elif comm_prefetch:
-            i = rstep[0]
-            st = gpend.pop(i % len(batches), None) or rf.gather_start(ikb, iko, batch)
-            nxt = (i + 1) % len(batches)
-            gpend[nxt] = rf.gather_start(*batches[nxt][0], batch)
+            # the sizes of batch i+2 are all-gathered now, so step i+1's gather_start reads them
+            # from pinned memory without waiting for the kernels in flight
+            i, L = rstep[0], len(batches)
+            st = gpend.pop(i % L, None) or rf.gather_start(ikb, iko, batch)
+            nxt = (i + 1) % L
+            gpend[nxt] = rf.gather_start(*batches[nxt][0], batch, sizes=szp.pop(nxt, None))
+            szp[(i + 2) % L] = rf.sizes_start(*batches[(i + 2) % L][0], batch)
             rf.insert_gathered(st)
             rstep[0] = i + 1
         elif rf is not None:
@@ -346,6 +349,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     D.barrier()
     torch.cuda.synchronize()
     ev = []
+    host_wait0 = rf.host_wait_s if rf is not None else 0.0
     t_start = time.perf_counter()
     for i, bt in enumerate(batches[warmup:], start=warmup):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -474,6 +478,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     res["mode"] = mode
     if rf is not None:
         res["replicated_insert_mode"] = rf.last_insert_mode
+        # host time blocked on batch sizes inside the timed steps (pipelined: ~0)
+        res["replicated_host_wait_ms_per_step"] = (rf.host_wait_s - host_wait0) / steps * 1e3
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
@@ -912,6 +918,7 @@ def main():
         "ops": {"insert": ins, "include": inc},
         "kernels": kern,
         "host_api": main_res.get("host_api"),
+        "replicated_host_wait_ms_per_step": main_res.get("replicated_host_wait_ms_per_step"),
         "secondary": secondary or None,
         "reference_shapes": shapes,
         "reference_published_keys_per_s": {"ruby_insert": 5103, "ruby_include": 4322,

@@ -311,6 +311,48 @@ int  bf_shard_insert_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64
 int  bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t window_cap, uint32_t nwin,
                                const uint64_t* d_counts, uint32_t count_stride, uint32_t hi, uint8_t* d_bits,
                                void* stream);
+/* Chunked windows: the sync-free exchange without the owner's sort pass.  Replaces the
+ * owner-side half of SETBIT / GETBIT routing for ruby.rb:57-60 / :20-30 (the same offsets
+ * as bf_route_windows_dev reach the same bits; only their order inside a window and a
+ * directory beside it differ).
+ * bf_route_chunk_info       tiles = ceil(n_bound / keys per route tile), the directory
+ *                           capacity every rank must use for batches of <= n_bound keys, and
+ *                           dir_bytes = one window's directory; BF_EINVAL if this shard
+ *                           count cannot take chunked windows (the caller keeps the windows
+ *                           above).  Every rank gets the same values for the same n_bound.
+ *                           A directory is uint32 start[tiles] then uint16 tab[(superbins +
+ *                           1) * tiles] ([sb][tile] run starts, row superbins = run lengths).
+ * bf_route_chunks_dev       bf_route_windows_dev whose per-tile runs are sorted by the
+ *                           owner's superbin, plus window w's directory at d_dir +
+ *                           w*dir_bytes (tiles entries; route tile t's run: its place in the
+ *                           window and its superbin run table).  d_slot16 (nullable) holds
+ *                           each entry's key index relative to its route tile (uint16).
+ *                           n must be <= tiles * keys per tile.
+ * bf_shard_insert_chunks_dev / bf_shard_test_chunks_dev   owner: nsrc sources' received
+ *                           windows of every sub-range hi < nh, window (hi, src) at d_recv +
+ *                           (hi*nsrc + src)*window_cap with its directory at d_dir +
+ *                           (hi*nsrc + src)*dir_bytes and live count d_counts[src*count_stride
+ *                           + hi] (a window past window_cap is skipped whole); one call for
+ *                           every sub-range.  The test writes d_bits[(hi*nsrc + src)*window_cap
+ *                           + i] for the live entries i.
+ * bf_combine_chunks_packed_dev  requester: the include? answers from window w's answer bits
+ *                           at d_packed + w*ceil(window_cap/8), through this rank's own
+ *                           route directory and slots. */
+int  bf_route_chunk_info(const bf_handle* h, uint64_t n_bound, uint64_t* tiles, uint64_t* dir_bytes,
+                         uint32_t* superbins /* nullable: the owner superbins per window */);
+int  bf_route_chunks_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                         uint32_t* d_send /* nwin*window_cap */, uint16_t* d_slot16 /* nullable */,
+                         uint64_t window_cap, uint64_t* d_counts /* nwin */, uint8_t* d_dir /* nwin*dir_bytes */,
+                         uint64_t dir_bytes, uint64_t tiles, void* stream);
+int  bf_shard_insert_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                                const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                                uint32_t count_stride, uint32_t* d_any_new /* nullable */, void* stream);
+int  bf_shard_test_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                              const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                              uint32_t count_stride, uint8_t* d_bits, void* stream);
+int  bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint16_t* d_slot16,
+                                  uint64_t window_cap, const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
+                                  const uint64_t* d_counts /* nwin */, uint64_t n, uint8_t* d_out, void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
 int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,

@@ -110,6 +110,11 @@ SIGNATURES = {
     "bf_combine_windows_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp]),
     "bf_pack_segments_dev": (ctypes.c_int, [_vp, _vp, _vp, _u32, _u64, _vp, _vp]),
     "bf_combine_windows_packed_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp]),
+    "bf_route_chunk_info": (ctypes.c_int, [_vp, _u64, _u64p, _u64p, _u32p]),
+    "bf_route_chunks_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp]),
+    "bf_shard_insert_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
+    "bf_shard_test_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
+    "bf_combine_chunks_packed_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _u64, _vp, _u64, _vp, _vp]),
     "bf_shard_export": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_shard_import": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
     "bf_lua_create": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, ctypes.POINTER(bf_config),
@@ -333,9 +338,14 @@ class Filter:
                                                 ctypes.byref(cnt)), self._h)
         return out[: cnt.value]
 
-    def include_many(self, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    def include_many(self, keys: np.ndarray, offsets: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """include? of every key -> uint8 answers (1/0).  out: an optional caller-owned uint8
+        buffer of >= n entries (reused across calls, its pages are already mapped)."""
         keys, offsets, n = self._keys(keys, offsets)
-        out = np.zeros(max(n, 1), np.uint8)
+        if out is None:
+            out = np.empty(max(n, 1), np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.ndim != 1 or len(out) < max(n, 1):
+            raise ArgumentError("out must be a contiguous 1-D uint8 array of at least n entries")
         _check(self._lib.bf_include_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(out)), self._h)
         return out[:n]
 
@@ -480,6 +490,40 @@ class Filter:
         nh = ctypes.c_uint32()
         _check(self._lib.bf_route_window_split(self.handle, ctypes.byref(nh)), self._h)
         return int(nh.value)
+
+    # -- chunked windows (the owner skips its sort pass; include/bfhip.h)
+    def route_chunk_info(self, n_bound: int):
+        """(tiles, dir_bytes, superbins per window) for batches of <= n_bound keys, or None
+        when this shard count cannot take chunked windows."""
+        t, d, sb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()
+        if self._lib.bf_route_chunk_info(self.handle, int(n_bound), ctypes.byref(t), ctypes.byref(d),
+                                         ctypes.byref(sb)) != 0:
+            return None
+        return int(t.value), int(d.value), int(sb.value)
+
+    def route_chunks_dev(self, d_keys: int, d_offsets: int, n: int, d_send: int, d_slot16: int, window_cap: int,
+                         d_counts: int, d_dir: int, dir_bytes: int, tiles: int, stream=None) -> None:
+        _check(self._lib.bf_route_chunks_dev(self.handle, d_keys, d_offsets, int(n), d_send, d_slot16 or None,
+                                             int(window_cap), d_counts, d_dir, int(dir_bytes), int(tiles),
+                                             self._s(stream)), self._h)
+
+    def shard_insert_chunks_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int, tiles: int,
+                                d_counts: int, count_stride: int, d_any_new: int = 0, stream=None) -> None:
+        _check(self._lib.bf_shard_insert_chunks_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
+                                                    int(dir_bytes), int(tiles), d_counts, int(count_stride),
+                                                    d_any_new or None, self._s(stream)), self._h)
+
+    def shard_test_chunks_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int, tiles: int,
+                              d_counts: int, count_stride: int, d_bits: int, stream=None) -> None:
+        _check(self._lib.bf_shard_test_chunks_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
+                                                  int(dir_bytes), int(tiles), d_counts, int(count_stride), d_bits,
+                                                  self._s(stream)), self._h)
+
+    def combine_chunks_packed_dev(self, d_packed: int, d_slot16: int, window_cap: int, d_dir: int, dir_bytes: int,
+                                  tiles: int, d_counts: int, n: int, d_out: int, stream=None) -> None:
+        _check(self._lib.bf_combine_chunks_packed_dev(self.handle, d_packed, d_slot16, int(window_cap), d_dir,
+                                                      int(dir_bytes), int(tiles), d_counts, int(n), d_out,
+                                                      self._s(stream)), self._h)
 
     def pack_segments_dev(self, d_bits: int, d_seg: int, nseg: int, max_count: int, d_packed: int,
                           stream=None) -> None:

@@ -8,6 +8,8 @@
 #include "bf_multi.h"
 
 #include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -160,6 +162,13 @@ struct bf_handle {
     uint32_t include_binned_mode = 2;   // the same policy for include?
     uint32_t shard_test_binned_mode = 2;   // ... and for the owner-side test of routed probes
     uint32_t bin_region_log2 = 19;   // preferred region (LDS image) size of the apply pass
+    // chunked windows: route sort buckets (window x owner superbin x low bits).  256 (bigger
+    // superbins, longer runs) measured 3.38-3.40 ms per P = 8 rank step against 3.44 at 512
+    // (profiles/r03_sim_chunks_P8.jsonl); BFHIP_CHUNK_BUCKETS, A/B only
+    uint32_t chunk_buckets = 256;
+    // chunked include?: 1 = the superbin-major L2-local sweep (chunk_test_l2_kernel), 0 = sort
+    // by region + region test.  The sweep measured 1.53 ms against 1.08: off
+    uint32_t chunk_test_l2 = 0;
     void* d_bin_scratch = nullptr;   // digests, probe arrays and histograms of one binned launch
     uint64_t bin_scratch_cap = 0;
     uint64_t cap_keys = 0, cap_bytes = 0;   // chunk limits of the host-pointer calls (bf_config)
@@ -332,6 +341,32 @@ int ensure_staging(bf_handle* h, uint64_t keys, uint64_t bytes, uint64_t out_byt
     h->staging_ready = true;
     return BF_OK;
 }
+
+// The caller's result buffer of a large host-pointer call is typically fresh memory (numpy
+// zeros, an FFI::MemoryPointer): its first touch page-faults, and those faults would land in
+// the result memcpy of every retired chunk, on the pipeline's critical path.  A helper thread
+// populates the pages (MADV_POPULATE_WRITE: faulted in by the kernel, contents unchanged, so
+// it may race the memcpy harmlessly) while the first chunks are staged and run.  Kernels
+// without the advice (EINVAL) just keep the old behaviour.
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+constexpr uint64_t kPrefaultBytes = 1ull << 20;
+struct Prefault {
+    std::thread th;
+    Prefault(void* p, uint64_t bytes) {
+        if (!p || bytes < kPrefaultBytes || std::getenv("BFHIP_NO_PREFAULT")) return;
+        th = std::thread([p, bytes] {
+            const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+            const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(pg - 1);
+            const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + pg - 1) & ~(pg - 1);
+            (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_POPULATE_WRITE);
+        });
+    }
+    ~Prefault() {
+        if (th.joinable()) th.join();
+    }
+};
 
 // Waits for a slot's previous chunk and copies its results to the caller.
 int retire_slot(bf_handle* h, Slot& s) {
@@ -612,6 +647,8 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
 
     const bool want_flag = (op == BF_OP_INSERT_FLAGS) && any_new;
     if (want_flag) HIPCHK(h, hipMemsetAsync(h->d_flag, 0, sizeof(uint32_t), h->stream));
+    Prefault prefault(out8 ? static_cast<void*>(out8) : static_cast<void*>(out64),
+                      out8 ? n : (out64 ? n * h->k * sizeof(uint64_t) : 0));
 
     uint64_t i = 0;
     int c = 0;
@@ -899,6 +936,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);
+    h->chunk_buckets = env_u32("BFHIP_CHUNK_BUCKETS", 256);
+    h->chunk_test_l2 = env_u32("BFHIP_CHUNK_TEST_L2", 0);
     h->include_binned_mode = env_u32("BFHIP_INCLUDE_BINNED", kDefaultIncludeBinnedMode);
     h->shard_test_binned_mode = env_u32("BFHIP_SHARD_TEST_BINNED", 2);
     *out = h;
@@ -1264,8 +1303,194 @@ int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
 }
 
 namespace {
+// The chunked-window geometry of a shard handle's filter (the same on every rank: it depends
+// on the largest shard's size and the window count only).
+static bool handle_chunks(const bf_handle* h, BfChunks* cg, uint32_t* nh_out) {
+    uint32_t nh = 1;
+    bf_route_window_split(h, &nh);
+    const uint64_t nblocks = (h->reach + (1ull << h->block_log2) - 1) >> h->block_log2;
+    const uint64_t bits0 = h->shards == 1 ? h->reach : ((nblocks + h->shards - 1) / h->shards) << h->block_log2;
+    if (nh_out) *nh_out = nh;
+    return bf_chunk_geometry(bits0, h->shards * nh, h->bin_region_log2, cg, h->chunk_buckets);
+}
+
+static uint64_t route_tile_keys(uint32_t k) { return k <= 6 ? 2048 : 1024; }   // bf_route_plan's tiles
+
+static int check_chunk_args(bf_handle* h, const BfChunks& cg, uint64_t dir_bytes, uint64_t tiles) {
+    if (!tiles) return set_err(h, BF_EINVAL, "tiles is 0");
+    if (dir_bytes < bf_chunk_dir_bytes(cg, tiles) || (dir_bytes & 15))
+        return set_err(h, BF_EINVAL, "dir_bytes %llu does not hold %llu tiles (bf_route_chunk_info)",
+                       (unsigned long long)dir_bytes, (unsigned long long)tiles);
+    return BF_OK;
+}
+}  // namespace
+
+int bf_route_chunk_info(const bf_handle* h, uint64_t n_bound, uint64_t* tiles, uint64_t* dir_bytes,
+                        uint32_t* superbins) {
+    if (!h || h->multi || !tiles || !dir_bytes) return BF_EINVAL;
+    BfChunks cg;
+    if (!handle_chunks(h, &cg, nullptr)) return BF_EINVAL;
+    const uint64_t tk = route_tile_keys(h->k);
+    *tiles = std::max<uint64_t>(1, (n_bound + tk - 1) / tk);
+    *dir_bytes = bf_chunk_dir_bytes(cg, *tiles);
+    if (superbins) *superbins = cg.S;
+    return BF_OK;
+}
+
+int bf_route_chunks_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                        uint32_t* d_send, uint16_t* d_slot16, uint64_t window_cap, uint64_t* d_counts, uint8_t* d_dir,
+                        uint64_t dir_bytes, uint64_t tiles, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (!d_counts || !d_dir) return set_err(h, BF_EINVAL, "d_counts / d_dir is NULL");
+    if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    const uint64_t probes = n * h->k;
+    if (n && probes / n != h->k) return set_err(h, BF_EINVAL, "n*k overflows");
+    if (probes >= (1ull << 32)) return set_err(h, BF_EINVAL, "n*k must be < 2^32 per call");
+    if (window_cap >= (1ull << 32) - 1) return set_err(h, BF_EINVAL, "window_cap must be < 2^32 - 1");
+    BfChunks cg;
+    uint32_t nh = 1;
+    if (!handle_chunks(h, &cg, &nh)) return set_err(h, BF_EINVAL, "this shard count cannot take chunked windows");
+    const uint32_t nwin = h->shards * nh;
+    int rc = check_chunk_args(h, cg, dir_bytes, tiles);
+    if (rc) return rc;
+    if ((n + route_tile_keys(h->k) - 1) / route_tile_keys(h->k) > tiles)
+        return set_err(h, BF_EINVAL, "%llu keys need more than %llu route tiles", (unsigned long long)n,
+                       (unsigned long long)tiles);
+    if ((uint64_t)nwin > ~0ull / std::max<uint64_t>(window_cap, 1)) return set_err(h, BF_EINVAL, "window_cap overflows");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
+    BfBinPlan plan;
+    if (n && !bf_route_plan(n, h->k, nwin, false, d_slot16 != nullptr, &plan))
+        return set_err(h, BF_EINVAL, "batch of %llu keys at k=%u over %u windows exceeds one route pass",
+                       (unsigned long long)n, h->k, nwin);
+    if (!n) plan.nsup = nwin;
+    if (n && plan.tile_keys != route_tile_keys(h->k)) return set_err(h, BF_EINVAL, "route tile size mismatch");
+    cg.dir = d_dir;
+    cg.dir_bytes = dir_bytes;
+    cg.tiles = tiles;
+    uint64_t bias = 0;
+    const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_route_chunks(h->g, plan, nh, cg, k16, d_offsets, bias, n, d_send, d_slot16, window_cap,
+                                     reinterpret_cast<unsigned long long*>(d_counts), s, mk));
+    return BF_OK;
+}
+
+namespace {
+static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc, const uint8_t* d_dir,
+                      uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts, uint32_t count_stride,
+                      uint32_t* d_any_new, uint8_t* d_bits, bool test, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (!nsrc || !window_cap) return BF_OK;
+    if (!d_recv || !d_dir || !d_counts || (test && !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    BfChunks cg;
+    uint32_t nh = 1;
+    if (!handle_chunks(h, &cg, &nh)) return set_err(h, BF_EINVAL, "this shard count cannot take chunked windows");
+    int rc = check_chunk_args(h, cg, dir_bytes, tiles);
+    if (rc) return rc;
+    if (count_stride < nh) return set_err(h, BF_EINVAL, "count_stride %u < %u sub-ranges", count_stride, nh);
+    const uint64_t total = (uint64_t)nh * nsrc * window_cap;
+    if (total / window_cap != (uint64_t)nh * nsrc || total >= (1ull << 32))
+        return set_err(h, BF_EINVAL, "%u sub-ranges x %u windows x %llu entries must stay below 2^32", nh, nsrc,
+                       (unsigned long long)window_cap);
+    cg.tiles = tiles;
+    BfChunkIn ci;
+    ci.recv = d_recv;
+    ci.dir = d_dir;
+    ci.dir_bytes = dir_bytes;
+    ci.tiles = tiles;
+    ci.cap = window_cap;
+    ci.limit = h->local_bits;
+    ci.counts = reinterpret_cast<const unsigned long long*>(d_counts);
+    ci.cstride = count_stride;
+    ci.nsrc = nsrc;
+    ci.nh = nh;
+    ci.S = cg.S;
+    ci.sup_log2 = cg.sup_log2;
+    BfBinPlan plan;
+    const bool binned = (test ? h->shard_test_binned_mode : h->binned_mode) != 0 &&
+                        bf_chunk_plan(h->dev_bytes, cg, nh, nsrc, window_cap, test, &plan, h->chunk_test_l2 != 0) &&
+                        ((test ? h->shard_test_binned_mode : h->binned_mode) == 1 ||
+                         (h->dev_bytes >= (64ull << 20) &&
+                          (double)total * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
+    if (!binned) {   // the direct owner ops read the same windows (the directories unused)
+        for (uint32_t hi = 0; hi < nh; ++hi) {
+            const uint32_t* rw = d_recv + (uint64_t)hi * nsrc * window_cap;
+            const uint64_t* cw = d_counts + hi;
+            rc = test ? bf_shard_test_windows_dev(h, rw, window_cap, nsrc, cw, count_stride, hi,
+                                                  d_bits + (uint64_t)hi * nsrc * window_cap, stream)
+                      : bf_shard_insert_windows_dev(h, rw, window_cap, nsrc, cw, count_stride, hi, d_any_new, stream);
+            if (rc) return rc;
+        }
+        return BF_OK;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
+    if ((rc = ensure_scratch(h, plan.scratch_bytes))) return rc;
+    BfMarks* mk = prof_begin(h, s);
+    if (test)
+        HIPCHK(h, bf_launch_shard_test_chunks(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_bits, s, mk));
+    else
+        HIPCHK(h, bf_launch_shard_insert_chunks(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_any_new, s, mk));
+    return BF_OK;
+}
+}  // namespace
+
+int bf_shard_insert_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                               const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                               uint32_t count_stride, uint32_t* d_any_new, void* stream) {
+    return shard_chunks_impl(h, d_recv, window_cap, nsrc, d_dir, dir_bytes, tiles, d_counts, count_stride, d_any_new,
+                             nullptr, false, stream);
+}
+
+int bf_shard_test_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                             const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                             uint32_t count_stride, uint8_t* d_bits, void* stream) {
+    return shard_chunks_impl(h, d_recv, window_cap, nsrc, d_dir, dir_bytes, tiles, d_counts, count_stride, nullptr,
+                             d_bits, true, stream);
+}
+
+int bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint16_t* d_slot16, uint64_t window_cap,
+                                 const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                                 uint64_t n, uint8_t* d_out, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (n && (!d_packed || !d_slot16 || !d_dir || !d_counts || !d_out))
+        return set_err(h, BF_EINVAL, "NULL device pointer");
+    BfChunks cg;
+    uint32_t nh = 1;
+    if (!handle_chunks(h, &cg, &nh)) return set_err(h, BF_EINVAL, "this shard count cannot take chunked windows");
+    int rc = check_chunk_args(h, cg, dir_bytes, tiles);
+    if (rc) return rc;
+    const uint64_t tk = route_tile_keys(h->k);
+    if ((n + tk - 1) / tk > tiles) return set_err(h, BF_EINVAL, "n exceeds the directory's tiles");
+    cg.dir = const_cast<uint8_t*>(d_dir);
+    cg.dir_bytes = dir_bytes;
+    cg.tiles = tiles;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    hipStream_t s = so.s;
+    BfMarks* mk = prof_begin(h, s);
+    HIPCHK(h, bf_launch_combine_chunks_packed(d_packed, d_slot16, window_cap, cg, h->shards * nh,
+                                              reinterpret_cast<const unsigned long long*>(d_counts), n, (uint32_t)tk,
+                                              d_out, s));
+    bf_mark(mk, s, "combine_chunks");
+    return BF_OK;
+}
+
+namespace {
 // Owner-side OR of `count` routed local offsets: uint32 entries when u32 (+ bias), else uint64.
-int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint32_t* d_any_new,
+static int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint32_t* d_any_new,
                       void* stream, const BfWindows& win = BfWindows{}) {
     if (!h) return BF_EINVAL;
     if (count && !d_local) return set_err(h, BF_EINVAL, "d_local is NULL");
@@ -1328,7 +1553,7 @@ int bf_shard_insert_hi_dev(bf_handle* h, const uint32_t* d_local32, uint64_t cou
 }
 
 namespace {
-int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint8_t* d_bits,
+static int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t bias, uint64_t count, uint8_t* d_bits,
                     void* stream, const BfWindows& win = BfWindows{}) {
     if (!h) return BF_EINVAL;
     if (count && (!d_local || !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
@@ -1510,7 +1735,7 @@ int bf_indexes_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
 
 namespace {
 // The digest ops: binned insert when it pays (as for keys), else one direct lane per digest.
-int run_digests(bf_handle* h, BfOp op, const uint32_t* d_dig, uint64_t n, uint8_t* d_out8, uint32_t* d_flag,
+static int run_digests(bf_handle* h, BfOp op, const uint32_t* d_dig, uint64_t n, uint8_t* d_out8, uint32_t* d_flag,
                 void* stream) {
     if (!h) return BF_EINVAL;
     if (h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");

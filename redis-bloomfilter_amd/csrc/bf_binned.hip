@@ -47,12 +47,16 @@ namespace {
 constexpr int kTile = 1024;                   // lanes per workgroup of the front / mid passes
 constexpr int kStageVec = 16384 / 16;         // 16 KiB LDS key stage per 1024-key sub-tile
 constexpr uint32_t kMaxSup = 256;             // superbins (8-bit superbin in the sort tags)
+constexpr uint32_t kChunkBuckets = 512;       // route sort buckets of chunked windows (window x superbin x 2^sub2)
 // <= 512 regions per superbin: the reach-capped 10B / 200B bitsets (55.8e9 bits) then take
 // 2^19-bit regions (64 KiB of LDS, two apply workgroups per CU) instead of 2^20 (one):
 // bin_apply 2.65 -> 2.48 ms per 2^24 x 13 probes (r02)
 constexpr uint32_t kMaxRel = 9;
 constexpr uint32_t kMaxBlocks = 512;          // front workgroups before tiles per workgroup grow
-constexpr uint32_t kMaxFrontBlocks = 4096;    // front workgroups once they hold kMaxTilesPerBlock tiles each
+// front workgroups once they hold kMaxTilesPerBlock tiles each: 16384 x 16 tiles takes a
+// merged replicated insert (8 ranks x 2^24 keys at k = 13, 10B@0.01 %) in ONE pass, so the
+// bitset is streamed by one apply instead of one per sub-batch
+constexpr uint32_t kMaxFrontBlocks = 16384;
 constexpr uint32_t kGroupBlocks = 64;         // front workgroups per group (one wave in bin_group_sum)
 constexpr uint32_t kTileProbes = 12288;       // probes per front tile (LDS sort buffer)
 constexpr int kSlots = 12;                    // probes per lane per tile (k <= 12)
@@ -388,8 +392,8 @@ __global__ __launch_bounds__(kMaxBlocks) void bin_group_sum_kernel(const uint32_
 // all probes.  cb_base[i]: first chunk block of window i (ceil(size / kBlockProbes)
 // blocks each), cb_base[N] = all blocks; cb_window[b] / cb_start[b]: the window
 // and level-2 position of chunk block b.  One workgroup, kScanPer windows per lane
-// (N <= kMaxWindows).
-constexpr uint32_t kScanPer = 4;
+// (N <= kMaxWindows; only the chunk-block prefix stays in LDS: 128 KiB).
+constexpr uint32_t kScanPer = 32;
 constexpr uint32_t kMaxWindows = 1024 * kScanPer;
 __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __restrict__ gsum, uint32_t N,
                                                               uint32_t* __restrict__ base,
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
                                                               uint32_t* __restrict__ cb_start, uint32_t nq,
                                                               unsigned long long* __restrict__ totals) {
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_base[kMaxWindows + 1], s_cb[kMaxWindows + 1];
+    __shared__ uint32_t s_cb[kMaxWindows + 1];
     const uint32_t t = threadIdx.x;
     uint32_t v[kScanPer], cv[kScanPer], sum = 0, csum = 0;
 #pragma unroll
@@ -418,7 +422,6 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
         if (w < N) {
             base[w] = ex;
             cb_base[w] = cex;
-            s_base[w] = ex;
             s_cb[w] = cex;
             if (totals && v[e]) atomicAdd(totals + w / nq, (unsigned long long)v[e]);   // per-bucket totals
         }
@@ -441,7 +444,7 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
             if (s_cb[mid] <= blk) lo = mid; else hi = mid - 1;
         }
         cb_window[blk] = lo;
-        cb_start[blk] = s_base[lo] + (blk - s_cb[lo]) * kBlockProbes;
+        cb_start[blk] = base[lo] + (blk - s_cb[lo]) * kBlockProbes;   // base: this workgroup's own stores
     }
 }
 
@@ -491,7 +494,13 @@ __device__ __forceinline__ uint32_t wave_agg_rank(bool live, uint32_t owner, uin
 // (entries [s*wcap, s*wcap + wcounts[s]) in an unspecified order; slots ride along).  A run
 // that would pass wcap is dropped; wcounts[s] still ends at the owner's full total, so
 // the caller sees the overflow and re-routes through the contiguous path.
-template <bool WIDE, bool SLOT, int SLOTS, bool WIN>
+//
+// CHUNK (bf_route_chunks_dev): as WIN, but each tile's run for a window is itself sorted by
+// the owner's superbin (superbin = sub-range-local offset >> cg.sup_log2, cg.S per window),
+// and the tile records its chunk in the window's directory: the run's place in the window
+// and its superbin run table (BfChunks).  The owner then reads the received windows as a
+// level-1 array of chunks and skips its own front (sort) pass; slots are u16, tile-relative.
+template <bool WIDE, bool SLOT, int SLOTS, bool WIN, bool CHUNK = false>
 __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                  const uint64_t* __restrict__ offsets, uint64_t bias,
                                                  uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
@@ -501,7 +510,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                                                  uint32_t* __restrict__ gcnt, uint64_t wcap,
                                                  unsigned long long* __restrict__ wcounts,
                                                  void* __restrict__ wsend, uint32_t* __restrict__ wslot,
-                                                 uint32_t nh) {
+                                                 uint32_t nh, BfChunks cg = BfChunks{}) {
     // The key stage (offsets + bytes) is dead once the tile is hashed, so the sorted
     // tile-relative key indices (u16) reuse it: 76 KiB in all without WIDE, two
     // workgroups per CU.
@@ -513,22 +522,27 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
     uint64_t* s_off = reinterpret_cast<uint64_t*>(s_raw);
     uint4* s_stage = s_raw + kOffVec;
     uint16_t* s_key = reinterpret_cast<uint16_t*>(s_raw);
-    __shared__ uint32_t s_cnt[kMaxSup], s_lbase[kMaxSup], s_gcnt[kMaxSup];
+    // CHUNK: up to kChunkBuckets (window, superbin, low bits) buckets; the window route keeps
+    // no per-workgroup totals (s_gcnt), which keeps the LDS within two workgroups per CU
+    constexpr uint32_t NB = CHUNK ? kChunkBuckets : kMaxSup;
+    __shared__ uint32_t s_cnt[NB], s_lbase[NB], s_gcnt[WIN ? 1 : kMaxSup];
     __shared__ uint32_t s_w[16];
     __shared__ unsigned long long s_gbase[WIN ? kMaxSup : 1];
     __shared__ uint32_t s_obase[WIN ? kMaxSup : 1];
     // WIN: ~128 sort buckets however few the owners, so that the LDS rank atomics do not
     // all land on P words (the owner's buckets stay consecutive: one run per owner)
     uint32_t sub_log2 = 0;
-    if constexpr (WIN)
+    if constexpr (CHUNK)
+        sub_log2 = cg.sub2;   // buckets (window, superbin, low offset bits): P * S << sub2 <= kMaxSup
+    else if constexpr (WIN)
         while ((P << (sub_log2 + 1)) <= 128u) ++sub_log2;
+    const uint32_t wS = CHUNK ? cg.S : 1u;   // a window's first bucket: (w * wS) << sub_log2
     __shared__ uint32_t s_lo[kTile * SLOTS];
     __shared__ uint8_t s_hi[WIDE ? kTile * SLOTS : 1];
     const uint32_t t = threadIdx.x;
-    if (t < kMaxSup) {
-        s_cnt[t] = 0;
-        s_gcnt[t] = 0;
-    }
+    if (t < NB) s_cnt[t] = 0;
+    if constexpr (!WIN)
+        if (t < kMaxSup) s_gcnt[t] = 0;
     __syncthreads();
     const uint32_t k = g.k;
     const uint32_t kpl = tile_keys / kTile;
@@ -576,7 +590,13 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
             if constexpr (WIN) {   // bucket = (window, low offset bits): 2^sub_log2 LDS counters per window
                 if (live) {
                     const uint32_t win = owner * nh + hi[q];   // window = (owner, 2^32-bit sub-range)
-                    const uint32_t bkt = (win << sub_log2) | (lo[q] & ((1u << sub_log2) - 1u));
+                    uint32_t wb = win;
+                    if constexpr (CHUNK) {   // ... (window, owner superbin, low offset bits)
+                        uint32_t sb = lo[q] >> cg.sup_log2;
+                        if (sb >= cg.S) sb = cg.S - 1u;   // never for a valid offset (the geometry covers the shard)
+                        wb = win * cg.S + sb;
+                    }
+                    const uint32_t bkt = (wb << sub_log2) | (lo[q] & ((1u << sub_log2) - 1u));
                     tag[q] = (bkt << 16) | atomicAdd(s_cnt + bkt, 1u);
                 }
             } else if (P <= g.route_agg) {   // workgroup-uniform
@@ -587,24 +607,37 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
             }
         }
         __syncthreads();
-        const uint32_t c = t < kMaxSup ? s_cnt[t] : 0u;
+        const uint32_t c = t < NB ? s_cnt[t] : 0u;
         const uint32_t ex = block_excl_scan(c, s_w, nullptr);
         if constexpr (!WIN)
             if (t <= P) stab[(uint64_t)t * ntiles + tile] = (uint16_t)ex;   // [owner][tile]
-        if (t < kMaxSup) {
+        if (t < NB) {
             s_lbase[t] = ex;
-            s_gcnt[t] += c;
+            if constexpr (!WIN) s_gcnt[t] += c;
             s_cnt[t] = 0;
         }
         __syncthreads();
         if constexpr (WIN) {
             if (t < P) {   // claim this tile's owner-t run (its buckets, consecutive) in owner t's window
-                const uint32_t hi_b = (t + 1) << sub_log2;   // == kMaxSup only for the last of 256 owners
-                const uint32_t ob = s_lbase[t << sub_log2], oc = (hi_b < kMaxSup ? s_lbase[hi_b] : tk * k) - ob;
+                const uint32_t lo_b = (t * wS) << sub_log2, hi_b = ((t + 1) * wS) << sub_log2;
+                const uint32_t ob = s_lbase[lo_b], oc = (hi_b < NB ? s_lbase[hi_b] : tk * k) - ob;
                 unsigned long long gb = 0;
                 if (oc) gb = atomicAdd(wcounts + t, (unsigned long long)oc);
                 s_gbase[t] = (gb + oc <= wcap) ? (unsigned long long)t * wcap + gb : ~0ull;   // ~0: overflow
                 s_obase[t] = ob;
+                if constexpr (CHUNK)   // the chunk's place in window t (0xFFFFFFFF: dropped, the window overflows)
+                    reinterpret_cast<uint32_t*>(cg.dir + (uint64_t)t * cg.dir_bytes)[tile] =
+                        (gb + oc <= wcap) ? (uint32_t)gb : 0xFFFFFFFFu;
+            }
+            if constexpr (CHUNK) {   // the chunk's superbin run table in every window: [sb][tile], [S] = length
+                const uint32_t S1 = cg.S + 1u;
+                for (uint32_t e = t; e < P * S1; e += kTile) {
+                    const uint32_t w = e / S1, sb = e - w * S1;
+                    const uint32_t b0 = (w * cg.S) << sub_log2, b1 = (w * cg.S + sb) << sub_log2;
+                    const uint32_t v = (b1 < NB ? s_lbase[b1] : tk * k) - s_lbase[b0];
+                    reinterpret_cast<uint16_t*>(cg.dir + (uint64_t)w * cg.dir_bytes + 4 * cg.tiles)
+                        [(uint64_t)sb * cg.tiles + tile] = (uint16_t)v;
+                }
             }
         }
 #pragma unroll
@@ -629,7 +662,10 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 if (gb != ~0ull) {
                     const uint64_t d = gb + (j - s_obase[o]);
                     static_cast<uint32_t*>(wsend)[d] = s_lo[j];   // the window implies the high bits
-                    if constexpr (SLOT) wslot[d] = (uint32_t)key0 + s_key[j];
+                    if constexpr (SLOT) {
+                        if constexpr (CHUNK) reinterpret_cast<uint16_t*>(wslot)[d] = s_key[j];   // tile-relative
+                        else wslot[d] = (uint32_t)key0 + s_key[j];
+                    }
                 }
             }
             __syncthreads();   // s_gbase and the staged keys are rewritten by the next tile
@@ -654,16 +690,16 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         void* __restrict__ wsend, uint32_t* __restrict__ wslot, uint32_t nh
 #define BF_ROUTE_FRONT_PASS \
     g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt, wcap, wcounts, wsend, wslot, nh
-template <bool WIDE, bool SLOT, int SLOTS, bool WIN>
-__global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<WIDE, SLOT, SLOTS, WIN>(BF_ROUTE_FRONT_PASS);
+template <bool WIDE, bool SLOT, int SLOTS, bool WIN, bool CHUNK = false>
+__global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS, BfChunks cg) {
+    route_front_body<WIDE, SLOT, SLOTS, WIN, CHUNK>(BF_ROUTE_FRONT_PASS, cg);
 }
 // 32-bit offsets (shards of <= 2^32 bits): 76 KiB of LDS with or without slots, so two
 // workgroups per CU at 8 waves per SIMD, as bin_front
-template <bool SLOT, bool WIN>
+template <bool SLOT, bool WIN, bool CHUNK = false>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void route_front32_kernel(BF_ROUTE_FRONT_ARGS) {
-    route_front_body<false, SLOT, kSlots, WIN>(BF_ROUTE_FRONT_PASS);
+void route_front32_kernel(BF_ROUTE_FRONT_ARGS, BfChunks cg) {
+    route_front_body<false, SLOT, kSlots, WIN, CHUNK>(BF_ROUTE_FRONT_PASS, cg);
 }
 #undef BF_ROUTE_FRONT_PASS
 #undef BF_ROUTE_FRONT_ARGS
@@ -1023,11 +1059,293 @@ __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restr
         });
 }
 
+// ---- chunked windows, owner side (bf_route_chunks_dev's windows as level 1) ----------------
+
+// The run of superbin lsb (window-local) in chunk c of sub-range h: c = src * tiles + tile.
+// An overflowed window (live count past cap) or a dropped chunk has none.
+__device__ __forceinline__ void chunk_run(const BfChunkIn& ci, uint32_t h, uint32_t lsb, uint64_t c, uint32_t* len,
+                                          uint32_t* st) {
+    const uint32_t src = (uint32_t)(c / ci.tiles);
+    const uint64_t tile = c - (uint64_t)src * ci.tiles;
+    const uint32_t j = h * ci.nsrc + src;
+    *len = 0;
+    *st = 0;
+    if (ci.counts[(uint64_t)src * ci.cstride + h] > ci.cap) return;
+    const uint8_t* d = ci.dir + (uint64_t)j * ci.dir_bytes;
+    const uint32_t start = reinterpret_cast<const uint32_t*>(d)[tile];
+    if (start == 0xFFFFFFFFu) return;
+    const uint16_t* tab = reinterpret_cast<const uint16_t*>(d + 4 * ci.tiles);
+    const uint32_t a = tab[(uint64_t)lsb * ci.tiles + tile], b = tab[(uint64_t)(lsb + 1) * ci.tiles + tile];
+    if (b > a && (uint64_t)start + b <= ci.cap) {   // a directory never points past its window
+        *len = b - a;
+        *st = (uint32_t)((uint64_t)j * ci.cap + start + a);
+    }
+}
+
+// gsum[sb][q] = probes of (global) superbin sb in chunk group q (kRunsPerPass chunks of its
+// sub-range).  One workgroup per (superbin, group), one lane per chunk: coalesced table reads.
+// runs (nullable): window w = sb * nq + q's run table, (exclusive prefix of the run lengths,
+// the run's first receive index) for kRunsPerPass chunks, for chunk_test_l2_kernel.
+__global__ __launch_bounds__(kRunsPerPass) void chunk_group_sum_kernel(BfChunkIn ci, uint32_t nq,
+                                                                       uint32_t* __restrict__ gsum,
+                                                                       uint2* __restrict__ runs) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t sb = blockIdx.x, q = blockIdx.y, t = threadIdx.x;
+    const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
+    const uint64_t c = (uint64_t)q * kRunsPerPass + t;
+    uint32_t len = 0, st = 0;
+    if (c < (uint64_t)ci.nsrc * ci.tiles) chunk_run(ci, h, lsb, c, &len, &st);
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(len, s_w, &total);
+    if (t == 0) gsum[sb * nq + q] = total;
+    if (runs) runs[((uint64_t)sb * nq + q) * kRunsPerPass + t] = make_uint2(ex, st);
+}
+
+// Owner side of a chunked include? without sorting: the probes of superbin sb stay in their
+// receive order (runs of each chunk), and every workgroup sweeps the superbins in the same
+// order — item i = (sb, group q, part) goes to workgroup i % gridDim, and a superbin has at
+// least gridDim items — so at any time the chip probes about one superbin (a few MiB): its
+// lines stay in every XCD's L2 and the random probes hit there (tools/probe_xcd.hip: 4 MiB
+// windows per XCD take ~178 G probes/s against ~55 G/s beyond the caches).  Answers are
+// stored in receive order, so a run's byte stores are contiguous (no scatter); an entry
+// outside its superbin or past the shard answers 0.  Every live entry gets an answer.
+constexpr uint32_t kL2Lanes = 256;
+constexpr int kL2Loads = 8;
+constexpr uint32_t kL2Grid = 2048;   // 256 CUs x 8 workgroups of 4 waves: one full residency
+__global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
+                                                                 uint32_t nsup, uint32_t nq, uint32_t parts,
+                                                                 const uint32_t* __restrict__ gsum,
+                                                                 const uint2* __restrict__ runs,
+                                                                 uint8_t* __restrict__ out8) {
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
+    const uint32_t t = threadIdx.x;
+    const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles;
+    const uint64_t items = (uint64_t)nsup * nq * parts;
+    for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint32_t w = (uint32_t)(it / parts), part = (uint32_t)(it - (uint64_t)w * parts);
+        const uint32_t sb = w / nq, q = w - sb * nq;
+        const uint32_t E = gsum[w];
+        const uint32_t f0 = (uint32_t)((uint64_t)E * part / parts), f1 = (uint32_t)((uint64_t)E * (part + 1) / parts);
+        if (f0 >= f1) continue;   // workgroup-uniform
+        const uint64_t c0 = (uint64_t)q * kRunsPerPass;
+        const uint32_t nt = (uint32_t)(nch - c0 < kRunsPerPass ? nch - c0 : kRunsPerPass);
+        __syncthreads();   // the previous item's readers of s_pre / s_gst are done
+        for (uint32_t j = t; j < nt; j += kL2Lanes) {
+            const uint2 r = runs[(uint64_t)w * kRunsPerPass + j];
+            s_pre[j] = r.x;
+            s_gst[j] = r.y;
+        }
+        __syncthreads();
+        const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
+        const uint64_t hoff = (uint64_t)h << 32;
+        for (uint32_t fb = f0; fb < f1; fb += kL2Lanes * kL2Loads) {
+            uint32_t idx[kL2Loads], o[kL2Loads];
+#pragma unroll
+            for (int u = 0; u < kL2Loads; ++u) {
+                const uint32_t f = fb + u * kL2Lanes + t;
+                idx[u] = 0xFFFFFFFFu;
+                o[u] = 0;
+                if (f < f1) {
+                    const uint32_t i = run_of(s_pre, nt, f);
+                    idx[u] = s_gst[i] + (f - s_pre[i]);
+                    o[u] = ci.recv[idx[u]];
+                }
+            }
+            uint32_t v[kL2Loads];
+#pragma unroll
+            for (int u = 0; u < kL2Loads; ++u) {
+                v[u] = 0;
+                if (idx[u] != 0xFFFFFFFFu && (o[u] >> ci.sup_log2) == lsb && hoff + o[u] < ci.limit)
+                    v[u] = bits[(hoff + o[u]) >> 5];
+            }
+#pragma unroll
+            for (int u = 0; u < kL2Loads; ++u)
+                if (idx[u] != 0xFFFFFFFFu) {
+                    const bool ok = (o[u] >> ci.sup_log2) == lsb && hoff + o[u] < ci.limit;
+                    out8[idx[u]] = ok ? (uint8_t)((v[u] >> ((o[u] ^ 7u) & 31u)) & 1u) : (uint8_t)0;
+                }
+        }
+    }
+}
+
+// bin_mid over chunked windows: window w = (superbin sb, chunk group q) concatenates sb's runs
+// from the group's chunks; each 8192-probe block is sorted by region in LDS as in bin_mid.
+// The received entries are window-local offsets: an entry outside its superbin or past the
+// shard is dropped (KEYS: answered 0), so peer data never addresses outside the bitset.  KEYS:
+// each probe's position is its index in the receive buffer (no level-1 key array).
+template <bool KEYS>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
+                           const uint32_t* __restrict__ base, const uint32_t* __restrict__ cb_base,
+                           uint64_t max_chunks, uint16_t* __restrict__ tabs, uint32_t* __restrict__ level2,
+                           uint32_t* __restrict__ level2_key, uint8_t* __restrict__ out8) {
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
+    __shared__ uint32_t s_cnt[1u << kMaxRel];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_sorted[kBlockProbes];
+    __shared__ uint32_t s_key[KEYS ? kBlockProbes : 1];
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = blockIdx.x / kMidParts, part = blockIdx.x - w * kMidParts;
+    const uint32_t sb = w / nq, q = w - sb * nq;
+    const uint32_t wbase = base[w];
+    const uint32_t E = base[w + 1] - wbase;
+    const uint32_t nblk = (E + kBlockProbes - 1) / kBlockProbes;
+    const uint32_t c_lo = (uint32_t)((uint64_t)nblk * part / kMidParts);
+    const uint32_t c_hi = (uint32_t)((uint64_t)nblk * (part + 1) / kMidParts);
+    if (c_lo >= c_hi) return;   // workgroup-uniform
+    const uint32_t b0 = cb_base[w];
+    const uint32_t R = 1u << rel_log2;
+    const uint32_t rmask = (1u << region_log2) - 1u;
+    uint32_t sub = 0;
+    while ((R << sub) < kMidBuckets) ++sub;
+    const uint32_t NB = R << sub, smask_b = (1u << sub) - 1u;
+    const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
+    const uint64_t hoff = (uint64_t)h << 32;
+    const uint32_t smask = (1u << ci.sup_log2) - 1u;
+    // run table of the group's chunks
+    const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles, c0 = (uint64_t)q * kRunsPerPass;
+    const uint32_t nt = (uint32_t)(nch - c0 < kRunsPerPass ? nch - c0 : kRunsPerPass);
+    uint32_t len = 0, st = 0;
+    if (t < nt) chunk_run(ci, h, lsb, c0 + t, &len, &st);
+    const uint32_t ex = block_excl_scan(len, s_w, nullptr);
+    if (t < nt) {
+        s_pre[t] = ex;
+        s_gst[t] = st;
+    }
+    __syncthreads();
+    auto load = [&](uint32_t f0, uint32_t* lv, uint32_t* kv) {
+        const uint32_t fw = f0 + (t >> 6) * (64u * kChunkPerLane);
+        uint32_t i = run_of(s_pre, nt, fw < E ? fw : E - 1);
+#pragma unroll
+        for (int u = 0; u < kChunkPerLane; ++u) {
+            const uint32_t f = fw + u * 64 + (t & 63u);
+            lv[u] = 0xFFFFFFFFu;
+            kv[u] = 0;
+            if (f < E) {
+                while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
+                const uint32_t idx = s_gst[i] + (f - s_pre[i]);
+                const uint32_t o = ci.recv[idx];
+                if ((o >> ci.sup_log2) == lsb && hoff + o < ci.limit) {
+                    lv[u] = o & smask;
+                    kv[u] = idx;
+                } else if constexpr (KEYS) {
+                    out8[idx] = 0;   // an offset past the shard answers 0
+                }
+            }
+        }
+    };
+    uint32_t lv[kChunkPerLane], kv[kChunkPerLane];
+    load(c_lo * kBlockProbes, lv, kv);
+    for (uint32_t c = c_lo; c < c_hi; ++c) {
+        const uint32_t f0 = c * kBlockProbes;
+        const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
+        if (t < NB) s_cnt[t] = 0;
+        __syncthreads();
+        uint32_t tag[kChunkPerLane];
+#pragma unroll
+        for (int u = 0; u < kChunkPerLane; ++u) {
+            tag[u] = 0xFFFFFFFFu;
+            if (lv[u] != 0xFFFFFFFFu) {
+                const uint32_t bk = ((lv[u] >> region_log2) << sub) | (lv[u] & smask_b);
+                tag[u] = (bk << 16) | atomicAdd(s_cnt + bk, 1u);
+            }
+        }
+        uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
+        if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
+        __syncthreads();
+        const uint32_t cn = t < NB ? s_cnt[t] : 0u;
+        const uint32_t cex = block_excl_scan(cn, s_w, nullptr);
+        if (!(t & smask_b) && (t >> sub) <= R)
+            tabs[(uint64_t)(t >> sub) * max_chunks + b0 + c] = (uint16_t)cex;   // [region][block]
+        if (t < NB) s_cnt[t] = cex;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kChunkPerLane; ++u) {
+            if (tag[u] != 0xFFFFFFFFu) {
+                const uint32_t d = s_cnt[tag[u] >> 16] + (tag[u] & 0xFFFFu);
+                s_sorted[d] = lv[u] & rmask;
+                if constexpr (KEYS) s_key[d] = kv[u];
+            }
+        }
+        __syncthreads();
+        const uint32_t out0 = wbase + f0;
+        for (uint32_t j = t; j < f1 - f0; j += kTile) {
+            stage_store(level2 + out0 + j, s_sorted[j]);
+            if constexpr (KEYS) level2_key[out0 + j] = s_key[j];
+        }
+        if (c + 1 < c_hi) {
+#pragma unroll
+            for (int u = 0; u < kChunkPerLane; ++u) {
+                lv[u] = nlv[u];
+                kv[u] = nkv[u];
+            }
+        }
+    }
+}
+
+// Requester side of a chunked include?: one workgroup per route tile; the tile's chunk in
+// every window (its place and length from the directory the route wrote) gives each entry's
+// tile-relative key (slot16) and its answer bit; a 0 clears that key's answer in LDS, and the
+// tile's answers leave as one coalesced store.
+constexpr uint32_t kCombineLanes = 256;
+__global__ __launch_bounds__(kCombineLanes) void combine_chunks_packed_kernel(
+        const uint8_t* __restrict__ packed, const uint16_t* __restrict__ slot16, uint64_t wcap, uint64_t wcap8,
+        BfChunks cg, uint32_t nwin, const unsigned long long* __restrict__ counts, uint64_t n, uint32_t tile_keys,
+        uint8_t* __restrict__ out) {
+    __shared__ uint8_t s_ans[2 * kTile];
+    __shared__ uint32_t s_pre[kMaxSup], s_st[kMaxSup], s_w[16];
+    const uint32_t t = threadIdx.x;
+    const uint64_t tile = blockIdx.x, key0 = tile * tile_keys;
+    const uint32_t tk = (uint32_t)(n - key0 < tile_keys ? n - key0 : tile_keys);
+    for (uint32_t j = t; j < tile_keys; j += kCombineLanes) s_ans[j] = 1;
+    uint32_t len = 0, st = 0;
+    if (t < nwin && counts[t] <= wcap) {
+        const uint8_t* d = cg.dir + (uint64_t)t * cg.dir_bytes;
+        const uint32_t start = reinterpret_cast<const uint32_t*>(d)[tile];
+        const uint32_t l = reinterpret_cast<const uint16_t*>(d + 4 * cg.tiles)[(uint64_t)cg.S * cg.tiles + tile];
+        if (start != 0xFFFFFFFFu && (uint64_t)start + l <= wcap) {
+            len = l;
+            st = start;
+        }
+    }
+    uint32_t E;
+    const uint32_t ex = block_excl_scan(len, s_w, &E);
+    if (t < nwin) {
+        s_pre[t] = ex;
+        s_st[t] = st;
+    }
+    __syncthreads();
+    constexpr int U = 8;   // entries per lane in flight
+    for (uint32_t fb = 0; fb < E; fb += U * kCombineLanes) {
+        uint32_t key[U], byte[U], sh[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t f = fb + u * kCombineLanes + t;
+            key[u] = 0xFFFFFFFFu;
+            byte[u] = 0xFFu;
+            sh[u] = 0;
+            if (f < E) {
+                const uint32_t w = run_of(s_pre, nwin, f);
+                const uint64_t e = (uint64_t)s_st[w] + (f - s_pre[w]);
+                key[u] = slot16[(uint64_t)w * wcap + e];
+                byte[u] = packed[(uint64_t)w * wcap8 + (e >> 3)];
+                sh[u] = (uint32_t)(e & 7u);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (key[u] < tk && !((byte[u] >> sh[u]) & 1u)) s_ans[key[u]] = 0;   // every writer stores the same 0
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < tk; j += kCombineLanes) out[key0 + j] = s_ans[j];
+}
+
 uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Carve {
     uint32_t *level1, *level1_key, *level2, *level2_key, *gcnt, *gsum, *base, *cb_base, *cb_window, *cb_start;
     uint16_t *stab, *tabs;
+    uint2* runs;   // the chunked L2-local test's window run tables
     uint64_t bytes;
 };
 
@@ -1037,17 +1355,23 @@ Carve carve(const BfBinPlan& p, void* at0) {
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) { uint8_t* q = at ? at + off : nullptr; off += align256(bytes); return q; };
     const uint64_t N = (uint64_t)p.nsup * p.ngroups;
-    c.level1 = reinterpret_cast<uint32_t*>(take(p.probes * 4));
-    c.level2 = reinterpret_cast<uint32_t*>(take(p.probes * 4));
-    c.level1_key = p.with_keys ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
-    c.level2_key = p.with_keys ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
-    c.stab = reinterpret_cast<uint16_t*>(take(p.ntiles * (p.nsup + 1) * 2));   // [superbin][tile]
-    c.gcnt = reinterpret_cast<uint32_t*>(take((uint64_t)p.nblocks * p.nsup * 4));
+    const bool l1 = !p.chunked;   // a chunked plan's level 1 is the received windows themselves
+    c.level1 = l1 ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
+    c.level2 = p.l2test ? nullptr : reinterpret_cast<uint32_t*>(take(p.probes * 4));
+    c.level1_key = l1 && p.with_keys ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
+    c.level2_key = p.with_keys && !p.l2test ? reinterpret_cast<uint32_t*>(take(p.probes * 4)) : nullptr;
+    c.stab = l1 ? reinterpret_cast<uint16_t*>(take(p.ntiles * (p.nsup + 1) * 2)) : nullptr;   // [superbin][tile]
+    c.gcnt = l1 ? reinterpret_cast<uint32_t*>(take((uint64_t)p.nblocks * p.nsup * 4)) : nullptr;
     c.gsum = reinterpret_cast<uint32_t*>(take(N * 4));
     c.base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
     c.cb_base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
     c.cb_window = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
     c.cb_start = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
+    if (p.l2test) {   // sorts nothing: the window run tables only
+        c.runs = reinterpret_cast<uint2*>(take(N * kRunsPerPass * sizeof(uint2)));
+        c.bytes = off;
+        return c;
+    }
     c.tabs = reinterpret_cast<uint16_t*>(take(p.max_chunks * ((1ull << p.rel_log2) + 1) * 2));   // [region][block]
     c.bytes = off;
     return c;
@@ -1407,7 +1731,7 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
 #define BF_ROUTE_FRONT(W, S, SL)                                                                                  \
     hipLaunchKernelGGL((route_front_kernel<W, S, SL, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, \
                        bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,       \
-                       (uint64_t)0, nullptr, nullptr, nullptr, 1u)
+                       (uint64_t)0, nullptr, nullptr, nullptr, 1u, BfChunks{})
     if (g.k > (uint32_t)kSlots) {
         if (wide) { if (slot) BF_ROUTE_FRONT(true, true, kWideSlots); else BF_ROUTE_FRONT(true, false, kWideSlots); }
         else { if (slot) BF_ROUTE_FRONT(false, true, kWideSlots); else BF_ROUTE_FRONT(false, false, kWideSlots); }
@@ -1416,11 +1740,11 @@ hipError_t bf_launch_route_fused(const BfGeom& g, const BfBinPlan& p, bool wide,
     else if (slot)
         hipLaunchKernelGGL((route_front32_kernel<true, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
                            bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,
-                           (uint64_t)0, nullptr, nullptr, nullptr, 1u);
+                           (uint64_t)0, nullptr, nullptr, nullptr, 1u, BfChunks{});
     else
         hipLaunchKernelGGL((route_front32_kernel<false, false>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets,
                            bias, n, p.tile_keys, p.tiles_per_block, p.nsup, c.lo1, c.hi1, c.key1, c.stab, c.gcnt,
-                           (uint64_t)0, nullptr, nullptr, nullptr, 1u);
+                           (uint64_t)0, nullptr, nullptr, nullptr, 1u, BfChunks{});
 #undef BF_ROUTE_FRONT
     bf_mark(mk, s, slot ? "route_front_slot" : "route_front");
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
@@ -1454,7 +1778,7 @@ hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, uint32_t
 #define BF_ROUTE_WIN(KERNEL)                                                                                      \
     hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,      \
                        p.tiles_per_block, p.nsup, nullptr, nullptr, nullptr, nullptr, nullptr, wcap, counts, send, \
-                       slot, nh)
+                       slot, nh, BfChunks{})
     if (g.k > (uint32_t)kSlots) {
         if (slot) BF_ROUTE_WIN((route_front_kernel<false, true, kWideSlots, true>));
         else BF_ROUTE_WIN((route_front_kernel<false, false, kWideSlots, true>));
@@ -1463,5 +1787,149 @@ hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, uint32_t
     else BF_ROUTE_WIN((route_front32_kernel<false, true>));
 #undef BF_ROUTE_WIN
     bf_mark(mk, s, slot ? "route_win_slot" : "route_win");
+    return hipGetLastError();
+}
+
+// ---- chunked windows: geometry, plans, launches ----------------------------------------------
+
+bool bf_chunk_geometry(uint64_t shard0_bits, uint32_t nwin, uint32_t pref_region_log2, BfChunks* cg,
+                       uint32_t max_buckets) {
+    if (max_buckets == 0 || max_buckets > kChunkBuckets) max_buckets = kChunkBuckets;
+    if (nwin == 0 || nwin > kMaxSup) return false;
+    const uint32_t rl = (pref_region_log2 >= 18 && pref_region_log2 <= 20) ? pref_region_log2 : 19u;
+    uint64_t nbins0 = (shard0_bits + (1ull << rl) - 1) >> rl;
+    if (nbins0 == 0) nbins0 = 1;
+    for (uint32_t rel = 0; rel <= kMaxRel; ++rel) {
+        const uint32_t sup_log2 = rl + rel;
+        const uint64_t per_sub = 1ull << (32 - sup_log2);   // superbins per 2^32-bit sub-range window
+        const uint64_t S = std::min<uint64_t>((nbins0 + (1ull << rel) - 1) >> rel, per_sub);
+        if ((uint64_t)nwin * S > max_buckets) continue;
+        BfChunks c{};
+        c.S = (uint32_t)S;
+        c.sup_log2 = sup_log2;
+        c.region_log2 = rl;
+        c.rel_log2 = rel;
+        c.sub2 = 0;
+        while (((uint64_t)nwin * S << (c.sub2 + 1)) <= max_buckets) ++c.sub2;
+        *cg = c;
+        return true;
+    }
+    return false;
+}
+
+uint64_t bf_chunk_dir_bytes(const BfChunks& cg, uint64_t tiles) {
+    return (4 * tiles + 2 * (uint64_t)(cg.S + 1) * tiles + 15) & ~(uint64_t)15;
+}
+
+bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint32_t nsrc, uint64_t cap,
+                   bool with_keys, BfBinPlan* plan, bool l2test) {
+    if (nh == 0 || nsrc == 0 || cap == 0 || cg.tiles == 0) return false;
+    const uint64_t probes = (uint64_t)nh * nsrc * cap;
+    if (probes >= (1ull << 32)) return false;
+    BfBinPlan p{};
+    p.chunked = true;
+    p.with_keys = with_keys;
+    p.l2test = l2test && with_keys;
+    p.region_log2 = cg.region_log2;
+    p.rel_log2 = cg.rel_log2;
+    const uint64_t bits = bitset_bytes * 8;
+    const uint64_t nbins = (bits + (1ull << p.region_log2) - 1) >> p.region_log2;
+    p.nbins = (uint32_t)nbins;
+    p.nsup = (uint32_t)((nbins + (1ull << p.rel_log2) - 1) >> p.rel_log2);
+    if (p.nsup == 0 || p.nsup > (uint64_t)nh * cg.S) return false;
+    p.ngroups = (uint32_t)(((uint64_t)nsrc * cg.tiles + kRunsPerPass - 1) / kRunsPerPass);
+    if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) return false;
+    p.probes = probes;
+    p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
+    p.scratch_bytes = carve(p, nullptr).bytes;
+    *plan = p;
+    return true;
+}
+
+namespace {
+hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn& ci, uint8_t* out8, hipStream_t s,
+                            BfMarks* mk) {
+    hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
+                       c.gsum, (uint2*)nullptr);
+    hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
+                       c.cb_base, c.cb_window, c.cb_start, p.ngroups, (unsigned long long*)nullptr);
+    bf_mark(mk, s, "chunk_group");
+    if (p.with_keys)
+        hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
+                           p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           c.level2_key, out8);
+    else
+        hipLaunchKernelGGL(bin_mid_chunks_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
+                           p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           c.level2_key, out8);
+    bf_mark(mk, s, p.with_keys ? "mid_chunks_keys" : "mid_chunks");
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                         const BfChunkIn& ci, void* scratch, uint32_t* any_flag, hipStream_t s,
+                                         BfMarks* mk) {
+    if (!p.chunked || p.with_keys) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_chunk_mid(p, c, ci, nullptr, s, mk);
+    if (e != hipSuccess) return e;
+    return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
+}
+
+hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                       const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,
+                                       BfMarks* mk) {
+    if (!p.chunked || !p.with_keys || !out8) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    if (p.l2test) {   // no sort: a superbin-major sweep, probes in receive order, answers stored in place
+        hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
+                           c.gsum, c.runs);
+        bf_mark(mk, s, "chunk_group");
+        // >= kL2Grid items per superbin, so the whole grid sweeps one superbin at a time
+        const uint32_t parts = (kL2Grid + p.ngroups - 1) / p.ngroups;
+        hipLaunchKernelGGL(chunk_test_l2_kernel, dim3(kL2Grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup, p.ngroups,
+                           parts, c.gsum, c.runs, out8);
+        bf_mark(mk, s, "test_l2");
+        return hipGetLastError();
+    }
+    hipError_t e = hipMemsetAsync(out8, 1, p.probes, s);   // every entry's answer starts true
+    if (e != hipSuccess) return e;
+    if ((e = launch_chunk_mid(p, c, ci, out8, s, mk)) != hipSuccess) return e;
+    return launch_test(g, p, c, bitset_bytes, out8, s, mk);
+}
+
+hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const BfChunks& cg,
+                                  const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
+                                  void* send, uint16_t* slot16, uint64_t wcap, unsigned long long* counts,
+                                  hipStream_t s, BfMarks* mk) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(counts, 0, (uint64_t)p.nsup * sizeof(unsigned long long), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(cg.dir, 0, (uint64_t)p.nsup * cg.dir_bytes, s)) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    uint32_t* slot = reinterpret_cast<uint32_t*>(slot16);   // the CHUNK body stores u16 through it
+#define BF_ROUTE_CH(KERNEL)                                                                                       \
+    hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,      \
+                       p.tiles_per_block, p.nsup, nullptr, nullptr, nullptr, nullptr, nullptr, wcap, counts, send, \
+                       slot, nh, cg)
+    if (g.k > (uint32_t)kSlots) {
+        if (slot16) BF_ROUTE_CH((route_front_kernel<false, true, kWideSlots, true, true>));
+        else BF_ROUTE_CH((route_front_kernel<false, false, kWideSlots, true, true>));
+    }
+    else if (slot16) BF_ROUTE_CH((route_front32_kernel<true, true, true>));
+    else BF_ROUTE_CH((route_front32_kernel<false, true, true>));
+#undef BF_ROUTE_CH
+    bf_mark(mk, s, slot16 ? "route_chunks_slot" : "route_chunks");
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t* slot16, uint64_t wcap,
+                                           const BfChunks& cg, uint32_t nwin, const unsigned long long* counts,
+                                           uint64_t n, uint32_t tile_keys, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (nwin > kMaxSup || tile_keys > 2 * kTile || tile_keys == 0) return hipErrorInvalidValue;
+    const uint64_t grid = (n + tile_keys - 1) / tile_keys;
+    hipLaunchKernelGGL(combine_chunks_packed_kernel, dim3((uint32_t)grid), dim3(kCombineLanes), 0, s, packed, slot16,
+                       wcap, (wcap + 7) / 8, cg, nwin, counts, n, tile_keys, out);
     return hipGetLastError();
 }

@@ -50,6 +50,37 @@ struct BfWindows {
         : counts(reinterpret_cast<const unsigned long long*>(c)), stride(s ? s : 1u), nwin(n), cap(wcap) {}
 };
 
+// Chunked windows (bf_route_chunks_dev): every route tile's run for a window is sorted by
+// the owner's superbin, and the window carries a directory of those runs, so the owner's
+// binned pass starts at bin_mid.  Window w's directory at dir + w * dir_bytes: uint32
+// start[tiles] (the run's first entry in the window; 0xFFFFFFFF = dropped, the window
+// overflowed), then uint16 tab[(S + 1) * tiles]: tab[sb * tiles + tile] = the run's first
+// entry of superbin sb, relative to start, and tab[S * tiles + tile] = the run's length.
+struct BfChunks {
+    uint8_t* dir = nullptr;
+    uint64_t dir_bytes = 0;
+    uint64_t tiles = 0;        // directory capacity in route tiles (>= every sender's ntiles)
+    uint32_t S = 1;            // owner superbins per window (a window-local offset >> sup_log2)
+    uint32_t sup_log2 = 0;     // = region_log2 + rel_log2 of the owner's plan
+    uint32_t sub2 = 0;         // route sort buckets per (window, superbin): 2^sub2 (low offset bits)
+    uint32_t region_log2 = 19, rel_log2 = 0;
+};
+// The geometry every rank derives alike from the largest shard's size (shard 0) and the
+// window count; false when nwin * S cannot fit the route's sort buckets (max_buckets <= 512).
+bool bf_chunk_geometry(uint64_t shard0_bits, uint32_t nwin, uint32_t pref_region_log2, BfChunks* cg,
+                       uint32_t max_buckets = 0 /* 0: the route's 512 */);
+uint64_t bf_chunk_dir_bytes(const BfChunks& cg, uint64_t tiles);
+
+// Owner side: the received windows (slot j = h * nsrc + src at recv + j * cap, its live
+// count counts[src * cstride + h]) with their directories.
+struct BfChunkIn {
+    const uint32_t* recv = nullptr;
+    const uint8_t* dir = nullptr;
+    uint64_t dir_bytes = 0, tiles = 0, cap = 0, limit = 0;
+    const unsigned long long* counts = nullptr;
+    uint32_t cstride = 1, nsrc = 1, nh = 1, S = 1, sup_log2 = 0;
+};
+
 enum BfOp : int {
     BF_OP_INDEXES      = 0,  // write the k offsets of each key (ruby.rb:41-55)
     BF_OP_INCLUDE      = 1,  // AND of the k bits (ruby.rb:20-30)
@@ -93,6 +124,8 @@ struct BfBinPlan {
     uint64_t probes;        // n * k (< 2^32)
     uint64_t max_chunks;    // bound on level-2 chunk blocks (bin_mid grid)
     uint64_t scratch_bytes; // device scratch the launch needs
+    bool     chunked;       // level 1 = received chunked windows (no front pass, no level-1 arrays)
+    bool     l2test;        // chunked include?: the superbin-major L2-local test (no mid sort, no level 2)
 };
 // Optional per-kernel timing: when a BfMarks is passed, a launcher records
 // marks->ev[i] after its i-th kernel (ev[0] before the first), named names[i].
@@ -157,6 +190,29 @@ hipError_t bf_launch_seq_mark(const BfGeom& g, uint32_t i0, uint64_t n, uint64_t
 hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets, uint64_t bias,
                                 uint64_t n, void* scratch, uint8_t* out8, uint32_t* any_flag, hipStream_t s,
                                 BfMarks* marks = nullptr);
+
+// Chunked windows, owner side (bf_binned.hip): plan over the shard for nh sub-ranges x nsrc
+// windows of cap entries and `tiles` chunks each; insert (any_flag nullable) or test (out8[i]
+// = bit of recv entry i, for every live entry; plan with_keys).
+bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint32_t nsrc, uint64_t cap,
+                   bool with_keys, BfBinPlan* plan, bool l2test = false);
+hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                         const BfChunkIn& ci, void* scratch, uint32_t* any_flag, hipStream_t s,
+                                         BfMarks* marks = nullptr);
+hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                       const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,
+                                       BfMarks* marks = nullptr);
+// Requester side: the window route with directories (cg.dir zeroed here first; slot16
+// nullable: tile-relative key indices).
+hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const BfChunks& cg,
+                                  const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
+                                  void* send, uint16_t* slot16, uint64_t wcap, unsigned long long* counts,
+                                  hipStream_t s, BfMarks* marks = nullptr);
+// out[j] = AND over every window's chunk of j's tile of the packed answer bits (window w at
+// packed + w * ceil(wcap / 8)); one workgroup per route tile, answers gathered in LDS.
+hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t* slot16, uint64_t wcap,
+                                           const BfChunks& cg, uint32_t nwin, const unsigned long long* counts,
+                                           uint64_t n, uint32_t tile_keys, uint8_t* out, hipStream_t s);
 
 // Partitioned filters, requester side, fused (bf_binned.hip): hash + per-tile
 // LDS sort by owner, then an owner-major gather into send[] (uint64 entries when

@@ -32,6 +32,7 @@ substitute a numpy engine to exercise this module's exchange logic over gloo.
 from __future__ import annotations
 
 import os
+import time
 from typing import Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -220,6 +221,50 @@ class HipEngine:
                                       stream=self._stream())
         return send, slot, counts
 
+    # -- chunked windows: the owner's sort pass moves into the route (include/bfhip.h)
+    def chunk_info(self, n_bound: int):
+        """(tiles, dir_bytes) of the chunk directories for batches of <= n_bound keys (the same
+        on every rank), or None when this shard count cannot take chunked windows."""
+        info = self.filter.route_chunk_info(n_bound)
+        return info[:2] if info else None
+
+    def route_chunks(self, kb: torch.Tensor, ko: torch.Tensor, n: int, cap: int, tiles: int, dir_bytes: int,
+                     want_slot: bool = True):
+        """route_windows whose per-tile runs are sorted by owner superbin, plus one directory
+        per window (dir_bytes each) and tile-relative uint16 slots."""
+        nwin = self.P * self.nh
+        send = torch.empty(nwin * cap, dtype=torch.int32, device=self.device)
+        slot = torch.empty(nwin * cap, dtype=torch.int16, device=self.device) if want_slot else None
+        counts = torch.empty(nwin, dtype=torch.int64, device=self.device)
+        dirb = torch.empty(nwin * dir_bytes, dtype=torch.uint8, device=self.device)
+        if self.poison is not None:
+            send.fill_(self.poison)
+            if slot is not None:
+                slot.fill_(0)
+        self.filter.route_chunks_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
+                                     slot.data_ptr() if want_slot else 0, cap, counts.data_ptr(), dirb.data_ptr(),
+                                     dir_bytes, tiles, stream=self._stream())
+        return send, slot, counts, dirb
+
+    def shard_insert_chunks(self, recv: torch.Tensor, cap: int, nsrc: int, rdir: torch.Tensor, dir_bytes: int,
+                            tiles: int, counts: torch.Tensor, cstride: int) -> None:
+        """OR every sub-range's received chunked windows (window (h, src) at (h*nsrc + src)*cap,
+        live count counts.view(-1)[src*cstride + h]) in one call."""
+        self.filter.shard_insert_chunks_dev(recv.data_ptr(), cap, nsrc, rdir.data_ptr(), dir_bytes, tiles,
+                                            counts.data_ptr(), cstride, stream=self._stream())
+
+    def shard_test_chunks(self, recv: torch.Tensor, cap: int, nsrc: int, rdir: torch.Tensor, dir_bytes: int,
+                          tiles: int, counts: torch.Tensor, cstride: int, out: torch.Tensor) -> None:
+        self.filter.shard_test_chunks_dev(recv.data_ptr(), cap, nsrc, rdir.data_ptr(), dir_bytes, tiles,
+                                          counts.data_ptr(), cstride, out.data_ptr(), stream=self._stream())
+
+    def combine_chunks_packed(self, packed: torch.Tensor, slot: torch.Tensor, cap: int, dirb: torch.Tensor,
+                              dir_bytes: int, tiles: int, counts: torch.Tensor, n: int) -> torch.Tensor:
+        out = torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)[:n]
+        self.filter.combine_chunks_packed_dev(packed.data_ptr(), slot.data_ptr(), cap, dirb.data_ptr(), dir_bytes,
+                                              tiles, counts.data_ptr(), n, out.data_ptr(), stream=self._stream())
+        return out
+
     def combine_windows(self, bits: torch.Tensor, slot: torch.Tensor, counts: torch.Tensor, cap: int,
                         n: int) -> torch.Tensor:
         out = torch.empty(n, dtype=torch.uint8, device=self.device)
@@ -353,7 +398,7 @@ class PartitionedFilter:
 
     def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None,
                  windows: bool = True, pack_answers: bool = True, sync_free: bool = True,
-                 batch_capacity: Optional[int] = None, poison: Optional[int] = None):
+                 batch_capacity: Optional[int] = None, poison: Optional[int] = None, chunks: bool = True):
         self.group = group
         self.P = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -373,6 +418,12 @@ class PartitionedFilter:
         self.replays = 0
         self._pk_seg = {}
         self._pending = None
+        # chunked windows (sync-free exchange on an engine that has them): the route sorts each
+        # window's runs by the owner's superbin and sends a directory beside them, so the owner
+        # skips its sort pass; BFHIP_CHUNKS=0 keeps the plain windows
+        self.chunks = bool(chunks and self.sync_free and hasattr(engine, "route_chunks")
+                           and os.environ.get("BFHIP_CHUNKS", "1") != "0")
+        self._chunk_geo = {}
         # The sync-free windows are sized from a batch bound every rank agrees on, never from
         # the rank's own n: ranks that size them from different n would post p2p messages of
         # different sizes (undefined under RCCL).  ``batch_capacity`` (the same on every rank)
@@ -567,13 +618,33 @@ class PartitionedFilter:
         self._sf_n = int(t.max().item())
         self.agreements += 1
 
+    def _chunk_geometry(self):
+        """(tiles, dir_bytes) for the agreed batch bound, or None (plain windows)."""
+        if not self.chunks:
+            return None
+        if self._sf_n not in self._chunk_geo:
+            self._chunk_geo[self._sf_n] = self.engine.chunk_info(max(self._sf_n, 1))
+        return self._chunk_geo[self._sf_n]
+
     def _sf_start(self, kb, ko, n: int, want_slot: bool) -> dict:
         e, P, nh = self.engine, self.P, self.engine.nh
         if self._sf_n is None:
             self._agree_batch(n)
         # the same cap on every rank; a batch past the agreed bound overflows (global flag)
         cap = self._cap_sf(self._sf_n)
-        send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
+        geo = self._chunk_geometry()
+        if geo is not None and n > self._sf_n:   # past the directory's tiles: overflow the windows instead
+            geo = None
+        dirb = None
+        if geo is not None:
+            send, slot, counts, dirb = e.route_chunks(kb, ko, n, cap, geo[0], geo[1], want_slot=want_slot)
+        elif self.chunks:
+            # a batch the directories cannot hold: its windows are declared overflowed, so every
+            # rank replays the step through the synced path and the bound rises
+            send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
+            counts.fill_(cap + 1)
+        else:
+            send, slot, counts = e.route_windows(kb, ko, n, cap, want_slot=want_slot)
         flag = (counts > cap).any().to(torch.int64).view(1, 1)
         msg = torch.cat([counts.view(P, nh), flag.expand(P, 1)], dim=1).contiguous()
         rmsg = torch.empty_like(msg)   # rmsg[s, h]: source s's count for my window h; [s, nh]: its flag
@@ -582,8 +653,21 @@ class PartitionedFilter:
         rseg = [(src, (h * P + src) * cap, cap) for h in range(nh) for src in range(P)]
         recv = self._buf(nh * P * cap, send.dtype, send.device)
         works = self._p2p(send, sseg, recv, rseg)
-        return dict(kb=kb, ko=ko, n=n, cap=cap, send=send, slot=slot, counts=counts, rmsg=rmsg, work=work,
-                    recv=recv, works=works)
+        st = dict(kb=kb, ko=ko, n=n, cap=cap, send=send, slot=slot, counts=counts, rmsg=rmsg, work=work,
+                  recv=recv, works=works, geo=None, own_chunks=dirb is not None)
+        if self.chunks:
+            # every rank sends directories when chunked windows are on: a rank whose batch took
+            # plain windows (declared overflowed) still posts them, so the message sizes match
+            tiles, dbytes = self._chunk_geometry() or (0, 0)
+            if dbytes:
+                if dirb is None:
+                    dirb = torch.zeros(P * nh * dbytes, dtype=torch.uint8, device=send.device)
+                dseg = [(o, (o * nh + h) * dbytes, dbytes) for o in range(P) for h in range(nh)]
+                drseg = [(src, (h * P + src) * dbytes, dbytes) for h in range(nh) for src in range(P)]
+                rdir = torch.empty(nh * P * dbytes, dtype=torch.uint8, device=send.device)
+                st["works"] = works + self._p2p(dirb, dseg, rdir, drseg)
+                st.update(geo=(tiles, dbytes), dir=dirb, rdir=rdir)
+        return st
 
     def _sf_flag(self, st: dict) -> None:
         """Enqueue the global overflow flag's trip to pinned host memory (after the count
@@ -606,6 +690,10 @@ class PartitionedFilter:
         e, P, nh, cap = self.engine, self.P, self.engine.nh, st["cap"]
         for w in st["works"]:
             w.wait()
+        if st["geo"] is not None:   # every sub-range in one binned pass, no owner sort
+            tiles, dbytes = st["geo"]
+            e.shard_insert_chunks(st["recv"], cap, P, st["rdir"], dbytes, tiles, st["rmsg"], nh + 1)
+            return
         for h in range(nh):
             e.shard_insert_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h)
 
@@ -614,9 +702,13 @@ class PartitionedFilter:
         for w in st["works"]:
             w.wait()
         bits = self._buf(nh * P * cap, torch.uint8, st["recv"].device, answers=True)
-        for h in range(nh):
-            e.shard_test_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h,
-                                 bits[h * P * cap:(h + 1) * P * cap])
+        if st["geo"] is not None:
+            tiles, dbytes = st["geo"]
+            e.shard_test_chunks(st["recv"], cap, P, st["rdir"], dbytes, tiles, st["rmsg"], nh + 1, bits)
+        else:
+            for h in range(nh):
+                e.shard_test_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h,
+                                     bits[h * P * cap:(h + 1) * P * cap])
         if self.pack_answers and hasattr(e, "pack_answers"):   # one bit per probe on the way back
             cap8 = (cap + 7) // 8
             key = (cap, P, nh)
@@ -629,12 +721,29 @@ class PartitionedFilter:
             seg = [(src, (src * nh + h) * cap8, cap8) for src in range(P) for h in range(nh)]
             for w in self._p2p(packed, seg, back, seg):
                 w.wait()
+            if st["geo"] is not None and not st["own_chunks"]:
+                # this rank's batch took plain windows declared overflowed: the step is replayed
+                return torch.zeros(n, dtype=torch.uint8, device=bits.device)
+            if st["geo"] is not None:
+                tiles, dbytes = st["geo"]
+                return e.combine_chunks_packed(back, st["slot"], cap, st["dir"], dbytes, tiles, st["counts"], n)
             return e.combine_windows_packed(back, st["slot"], st["counts"], cap, n)
         back = self._buf(P * nh * cap, torch.uint8, bits.device, answers=True)
         sseg = [(src, (h * P + src) * cap, cap) for src in range(P) for h in range(nh)]
         rseg = [(o, (o * nh + h) * cap, cap) for o in range(P) for h in range(nh)]
         for w in self._p2p(bits, sseg, back, rseg):
             w.wait()
+        if st["geo"] is not None and not st["own_chunks"]:   # declared overflowed: the step is replayed
+            return torch.zeros(n, dtype=torch.uint8, device=bits.device)
+        if st["geo"] is not None:   # bytes came back: pack them here for the chunked combine
+            tiles, dbytes = st["geo"]
+            cap8 = (cap + 7) // 8
+            key = ("local", cap, P, nh)
+            if key not in self._pk_seg:
+                self._pk_seg[key] = torch.tensor([[w * cap, cap, w * cap8] for w in range(P * nh)],
+                                                 dtype=torch.int64).to(bits.device)
+            packed = e.pack_answers(back, self._pk_seg[key], cap, P * nh * cap8)
+            return e.combine_chunks_packed(packed, st["slot"], cap, st["dir"], dbytes, tiles, st["counts"], n)
         return e.combine_windows(back, st["slot"], st["counts"], cap, n)
 
     def _synced_insert(self, kb, ko, n: int) -> None:
@@ -884,13 +993,17 @@ class ReplicatedFilter:
       them — about L + 1 bytes per key on the wire, but the insert work grows with P;
     * ``"or"`` (ii): every replica inserts only its own batch, then the bitsets are
       OR-all-reduced (``or_allreduce_``) — 2 (P-1)/P of the bitset on the wire per rank,
-      the insert work stays flat.
+      the insert work stays flat;
+    * ``"digests"``: (i) with every key hashed once, by its own rank: the 16-B SHA-1 words
+      (``ruby.rb:42-47``'s h[0..3]) are all-gathered and every replica inserts all of them
+      from words (no hash pass) — 16 B per key on the wire instead of ~L + 1, and P - 1
+      fewer SHA-1 passes per replica (``tools/sim_rank.py --replicated P --gathered``).
 
     ``insert_mode="auto"`` takes (ii) when the bitset is small next to the gathered batches
     (2 * bitset bytes < all ranks' key bytes + lengths), e.g. the 1M@1 % filter (1.2 MB)
     against 2^24-key batches, and (i) otherwise, e.g. the north-star filter (1.2 GB)."""
 
-    MODES = ("auto", "gather", "or")
+    MODES = ("auto", "gather", "or", "digests")
 
     def __init__(self, m: int, k: int, group=None, device=None, insert_mode: str = "auto"):
         if insert_mode not in self.MODES:
@@ -902,6 +1015,7 @@ class ReplicatedFilter:
         self.k = k
         self.insert_mode = insert_mode
         self.last_insert_mode = None
+        self.host_wait_s = 0.0   # time the host spent waiting for batch sizes (gather_start)
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -921,20 +1035,45 @@ class ReplicatedFilter:
         else:
             self.insert_gathered(st)
 
-    def gather_start(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> dict:
-        """Enqueue the all-gather of this rank's batch (collective: every rank calls it, in
-        the same order); ``insert_gathered`` finishes it.  Between the two the gather runs on
-        the process group's stream beside whatever the caller enqueues — e.g. the previous
-        batch's inserts and include?s, so a pipelined caller hides the exchange.  Only the
-        batch sizes (one small all-gather) make the host wait.  In "or" mode nothing travels
-        here; ``insert_gathered`` inserts and OR-all-reduces."""
+    def sizes_start(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> dict:
+        """Enqueue the all-gather of this batch's sizes (collective) and their copy to pinned
+        host memory behind an event; ``gather_start(..., sizes=)`` then reads them without
+        draining the device.  A caller that starts the sizes one batch ahead of the gather (the
+        bench's pipelined step) never makes the host wait for in-flight kernels."""
         z = torch.zeros(1, dtype=torch.int64, device=self.device)
         lens = (ko[1: n + 1] - ko[:n]) if n else z[:0]
-        # (bytes, keys, longest key, first offset): one small all-gather, one host wait
+        # (bytes, keys, longest key, first offset)
         sizes = torch.cat([ko[n: n + 1] - ko[0:1], z + n, lens.max().view(1) if n else z, ko[0:1]])
         all_sizes = torch.empty(self.P * 4, dtype=torch.int64, device=self.device)
         _all_gather_into_tensor(all_sizes, sizes, group=self.group)
-        all_sizes = all_sizes.view(self.P, 4).cpu().tolist()
+        dev = all_sizes.is_cuda
+        host = torch.empty(self.P * 4, dtype=torch.int64, pin_memory=dev)
+        host.copy_(all_sizes, non_blocking=dev)
+        ev = None
+        if dev:
+            ev = torch.cuda.Event()
+            ev.record()
+        return dict(host=host, ev=ev, lens=lens, n=n)
+
+    def gather_start(self, kb: torch.Tensor, ko: torch.Tensor, n: int, sizes: Optional[dict] = None) -> dict:
+        """Enqueue the all-gather of this rank's batch (collective: every rank calls it, in
+        the same order); ``insert_gathered`` finishes it.  Between the two the gather runs on
+        the process group's stream beside whatever the caller enqueues — e.g. the previous
+        batch's inserts and include?s, so a pipelined caller hides the exchange.  The batch
+        sizes come from ``sizes`` (a ``sizes_start`` of this batch issued earlier: the host
+        waits only for that small all-gather's event) or from a sizes_start made here (the
+        host then waits for everything enqueued before it).  In "or" mode nothing travels
+        here; ``insert_gathered`` inserts and OR-all-reduces."""
+        if sizes is None:
+            sizes = self.sizes_start(kb, ko, n)
+        if sizes["n"] != n:
+            raise ArgumentError("gather_start: sizes were taken for a batch of %d keys, not %d" % (sizes["n"], n))
+        if sizes["ev"] is not None:
+            t0 = time.perf_counter()
+            sizes["ev"].synchronize()
+            self.host_wait_s += time.perf_counter() - t0
+        lens = sizes["lens"]
+        all_sizes = sizes["host"].view(self.P, 4).tolist()
         nbytes, _, _, ko0 = all_sizes[dist.get_rank(self.group)]
         all_sizes = [sz[:3] for sz in all_sizes]
         mode = self.insert_mode
@@ -944,6 +1083,15 @@ class ReplicatedFilter:
             mode = "or" if 2 * self.filter.device_bytes < gather_bytes else "gather"
         if mode == "or":
             return dict(mode="or", kb=kb, ko=ko, n=n)
+        if mode == "digests":   # this rank hashes its batch once; the words travel
+            max_n = max(max(sz[1] for sz in all_sizes), 1)
+            mine = torch.zeros((max_n, 4), dtype=torch.int32, device=self.device)
+            if n:
+                self.filter.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, mine.data_ptr(), stream=self._stream())
+            gd = torch.empty((self.P * max_n, 4), dtype=torch.int32, device=self.device)
+            works = [_all_gather_into_tensor(gd.view(-1), mine.view(-1), group=self.group, async_op=True)]
+            return dict(mode="digests", kb=kb, ko=ko, n=n, gd=gd, send=mine, works=works, sizes=all_sizes,
+                        max_n=max_n)
         max_b = max(max(sz[0] for sz in all_sizes), 1)
         max_n = max(max(sz[1] for sz in all_sizes), 1)
         ldt = torch.uint8 if max(sz[2] for sz in all_sizes) <= 255 else torch.int32
@@ -970,6 +1118,17 @@ class ReplicatedFilter:
             return
         for w in st["works"]:
             w.wait()
+        if st["mode"] == "digests":   # every rank's words as ONE insert (padding rows cut out)
+            counts = [sz[1] for sz in st["sizes"]]
+            mx = st["max_n"]
+            if all(c == mx for c in counts):
+                dg, dn = st["gd"], self.P * mx
+            else:
+                dg = torch.cat([st["gd"][r * mx: r * mx + c] for r, c in enumerate(counts) if c])
+                dn = int(sum(counts))
+            if dn:
+                self.filter.insert_digests_dev(dg.data_ptr(), dn, stream=self._stream())
+            return
         skip = dist.get_rank(self.group) if own_inserted else -1
         ob, oo, on = merge_gathered(st["gk"], st["gl"], st["sizes"], st["max_b"], st["max_n"], skip=skip)
         if on:

@@ -66,7 +66,7 @@ def replicated_case(rank, P, cfg, dev):
     pb, po = O.pack_keys(probe)
     want = orc.include_many(bits, m, k, pb, po).astype(bool)
     ok = True
-    for mode in ("gather", "or"):
+    for mode in ("gather", "or", "digests"):
         rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
         rf.insert_many(keys[rank])
         ok = ok and rf.last_insert_mode == mode and rf.export_redis() == want_s
@@ -77,7 +77,7 @@ def replicated_case(rank, P, cfg, dev):
     half = len(keys[rank]) // 2
     kb1, ko1, n1 = D._device_batch(keys[rank][:half], dev)
     kb2, ko2, n2 = D._device_batch(keys[rank][half:], dev)
-    for mode in ("gather", "or"):
+    for mode in ("gather", "or", "digests"):
         rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
         st1 = rf.gather_start(kb1, ko1, n1)
         st2 = rf.gather_start(kb2, ko2, n2)
@@ -85,6 +85,28 @@ def replicated_case(rank, P, cfg, dev):
         rf.insert_gathered(st2)
         ok = ok and rf.last_insert_mode == mode and rf.export_redis() == want_s
         rf.close()
+    # uneven batches (rank r brings n - 50 r keys): every insert form pads and cuts correctly
+    cut = [len(keys[r]) - 50 * r for r in range(P)]
+    sub = [x for r in range(P) for x in keys[r][:cut[r]]]
+    sb_, so_ = O.pack_keys(sub)
+    ub = orc.new_bitset(m, k)
+    orc.insert_many(ub, m, k, sb_, so_)
+    want_u = orc.redis_string(ub)
+    for mode in ("gather", "or", "digests"):
+        rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
+        rf.insert_many(keys[rank][:cut[rank]])
+        ok = ok and rf.export_redis() == want_u
+        rf.close()
+    # ... with the sizes all-gathered one batch ahead (sizes_start), as bench.py pipelines them
+    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="gather")
+    sz1 = rf.sizes_start(kb1, ko1, n1)
+    sz2 = rf.sizes_start(kb2, ko2, n2)
+    st1 = rf.gather_start(kb1, ko1, n1, sizes=sz1)
+    rf.insert_gathered(st1)
+    st2 = rf.gather_start(kb2, ko2, n2, sizes=sz2)
+    rf.insert_gathered(st2)
+    ok = ok and rf.export_redis() == want_s
+    rf.close()
     return ok
 
 

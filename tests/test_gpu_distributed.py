@@ -173,6 +173,128 @@ def test_route_windows(pkg, oracle, m, k, P, b):
     e.close()
 
 
+@pytest.mark.parametrize("owner", ["direct", "sorted", "l2"])
+@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (9585058377, 6, 2, 20),
+                                     (191701167547, 13, 4, 20), (9585058377, 6, 1, 20),
+                                     (3834023350947, 13, 8, 20)])   # 200B x8: nh = 2
+def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
+    """bf_route_chunks_dev + the owner ops over chunked windows + bf_combine_chunks_packed_dev,
+    with P shards simulated on one GPU and the exchange done by copies: every window holds
+    exactly its owner's (key, local offset) pairs, the directories partition each window into
+    one run per route tile, the owners' shards rebuild the oracle's Redis string and the
+    requesters' answers equal the oracle's include?.  owner: "direct" = the direct kernels over
+    the same windows; "sorted" = the binned pass straight off the chunks (bin_mid, then the
+    region apply / test); "l2" = the binned insert and the superbin-major L2-local test."""
+    import torch
+    binned = "0" if owner == "direct" else "1"
+    monkeypatch.setenv("BFHIP_INSERT_BINNED", binned)
+    monkeypatch.setenv("BFHIP_SHARD_TEST_BINNED", binned)
+    monkeypatch.setenv("BFHIP_CHUNK_TEST_L2", "1" if owner == "l2" else "0")
+    D = pkg.distributed
+    dev = torch.device("cuda", 0)
+    shards = [D.HipEngine(m, k, P, s, b, dev) for s in range(P)]
+    nh = shards[0].nh
+    nwin = P * nh
+    n = 6000
+    geo = shards[0].chunk_info(n)
+    assert geo is not None and all(e.chunk_info(n) == geo for e in shards)
+    tiles, dbytes = geo
+    S = shards[0].filter.route_chunk_info(n)[2]
+    assert dbytes == -(-(4 * tiles + 2 * (S + 1) * tiles) // 16) * 16
+    tile_keys = 2048 if k <= 6 else 1024
+    assert tiles == -(-n // tile_keys)
+    A = 12288
+    cap = -(-min(n * k, n * k // P + n * k // (8 * P) + 4096) // A) * A
+    rng = np.random.default_rng(23)
+    per_rank = [["c%d-%d" % (r, int(v)) for v in rng.integers(0, 10**12, n)] for r in range(P)]
+
+    def route_all(batches, want_slot):
+        out = []
+        for r in range(P):
+            kb, ko, nn, buf, offs = dev_batch(pkg, torch, batches[r])
+            out.append(shards[r].route_chunks(kb, ko, nn, cap, tiles, dbytes, want_slot=want_slot) + (buf, offs))
+        torch.cuda.synchronize()
+        return out
+
+    def check_route(send, slot, counts, dirb, buf, offs):
+        idx = oracle.indexes_many(buf, offs, m, k).reshape(-1)
+        owner, local = D.block_owner_local(idx, P, b)
+        win = owner.astype(np.int64) * nh + (local >> np.uint64(32)).astype(np.int64)
+        want_c = np.bincount(win, minlength=nwin)
+        c = counts.cpu().numpy()
+        assert c.tolist() == want_c.tolist()
+        s_np = send.cpu().numpy().view(np.uint32).astype(np.uint64)
+        sl = slot.cpu().numpy().view(np.uint16).astype(np.int64)
+        d = dirb.cpu().numpy()
+        key_of = np.arange(len(idx)) // k
+        for w in range(nwin):
+            dw = d[w * dbytes:(w + 1) * dbytes]
+            start = dw[: 4 * tiles].view(np.uint32).astype(np.int64)
+            tab = dw[4 * tiles: 4 * tiles + 2 * (S + 1) * tiles].view(np.uint16).reshape(S + 1, tiles)
+            length = tab[S].astype(np.int64)
+            assert (np.diff(tab.astype(np.int64), axis=0) >= 0).all()   # superbin runs in order
+            # the chunks tile [0, count) of the window, one per route tile, runs monotone inside
+            live = length > 0
+            spans = sorted(zip(start[live].tolist(), (start[live] + length[live]).tolist()))
+            at = 0
+            for a, e in spans:
+                assert a == at
+                at = e
+            assert at == int(want_c[w])
+            got, keys_w = [], []
+            for t in np.flatnonzero(live):
+                seg = slice(w * cap + int(start[t]), w * cap + int(start[t] + length[t]))
+                got += (s_np[seg] | np.uint64((w % nh) << 32)).tolist()
+                keys_w += (sl[seg] + t * tile_keys).tolist()
+            assert sorted(zip(keys_w, got)) == sorted(zip(key_of[win == w].tolist(), local[win == w].tolist()))
+
+    def deliver(routed, o):
+        recv = torch.cat([routed[src][0][(o * nh + h) * cap:(o * nh + h + 1) * cap] for h in range(nh)
+                          for src in range(P)])
+        rdir = torch.cat([routed[src][3][(o * nh + h) * dbytes:(o * nh + h + 1) * dbytes] for h in range(nh)
+                          for src in range(P)])
+        rmsg = torch.zeros(P, nh + 1, dtype=torch.int64, device=dev)
+        for src in range(P):
+            rmsg[src, :nh] = routed[src][2][o * nh:(o + 1) * nh]
+        return recv, rdir, rmsg
+
+    ins = route_all(per_rank, want_slot=True)
+    for r in range(P):
+        check_route(*ins[r][:4], ins[r][4], ins[r][5])
+    for o in range(P):
+        recv, rdir, rmsg = deliver(ins, o)
+        shards[o].shard_insert_chunks(recv, cap, P, rdir, dbytes, tiles, rmsg, nh + 1)
+    torch.cuda.synchronize()
+    ib, io = pkg.keys.pack([x for r in range(P) for x in per_rank[r]])
+    bits = oracle.new_bitset(m, k)
+    oracle.insert_many(bits, m, k, ib, io)
+    got_str = D.interleave_shards([e.shard_export() for e in shards], shards[0].filter.reach_bits, b)
+    assert got_str == oracle.redis_string(bits)
+    # include?: members of two ranks + fresh keys per requester
+    probes = [per_rank[r][: n // 3] + per_rank[(r + 1) % P][: n // 3] + ["fresh%d-%d" % (r, i) for i in range(n // 3)]
+              for r in range(P)]
+    qs = route_all(probes, want_slot=True)
+    cap8 = (cap + 7) // 8
+    answers = []
+    for o in range(P):
+        recv, rdir, rmsg = deliver(qs, o)
+        out = torch.zeros(nh * P * cap, dtype=torch.uint8, device=dev)
+        shards[o].shard_test_chunks(recv, cap, P, rdir, dbytes, tiles, rmsg, nh + 1, out)
+        answers.append(out)
+    for r in range(P):
+        back = torch.zeros(nwin * cap8, dtype=torch.uint8, device=dev)
+        for o in range(P):
+            seg = torch.tensor([[(h * P + r) * cap, cap, (o * nh + h) * cap8] for h in range(nh)],
+                               dtype=torch.int64).to(dev)
+            packed = shards[o].pack_answers(answers[o], seg, cap, nwin * cap8)
+            back[o * nh * cap8:(o + 1) * nh * cap8] = packed[o * nh * cap8:(o + 1) * nh * cap8]
+        send, slot, counts, dirb, pb, po = qs[r]
+        got = shards[r].combine_chunks_packed(back, slot, cap, dirb, dbytes, tiles, counts, len(probes[r]))
+        np.testing.assert_array_equal(got.cpu().numpy(), oracle.include_many(bits, m, k, pb, po))
+    for e in shards:
+        e.close()
+
+
 def test_pack_segments_and_packed_combine(pkg):
     """bf_pack_segments_dev at odd offsets and counts (LSB-first, ceil(count/8) bytes each),
     and bf_combine_windows_packed_dev equal to the byte-per-probe windowed combine."""

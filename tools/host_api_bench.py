@@ -28,12 +28,30 @@ def main():
     f.insert_many(ib, io)
     f.include_many(pb, po)
     res = {}
-    for name, fn in (("insert", lambda: f.insert_many(ib, io)), ("include", lambda: f.include_many(pb, po))):
-        ts = []
-        for _ in range(REPS):
-            t = time.perf_counter()
-            fn()
-            ts.append(time.perf_counter() - t)
+    keep = np.empty(B, np.uint8)
+
+    def no_prefault(fn):
+        def g():
+            os.environ["BFHIP_NO_PREFAULT"] = "1"
+            try:
+                return fn()
+            finally:
+                del os.environ["BFHIP_NO_PREFAULT"]
+        return g
+    cases = (("insert", lambda: f.insert_many(ib, io)), ("include", lambda: f.include_many(pb, po)),
+             # the result buffer's page faults: without the library's prefault thread, and into a
+             # caller-owned buffer that is already mapped
+             ("include_no_prefault", no_prefault(lambda: f.include_many(pb, po))),
+             ("include_reused_out", lambda: f.include_many(pb, po, out=keep)))
+    for rep in range(2):   # interleaved passes: the box's CPU share is noisy
+        for name, fn in cases:
+            ts = res.setdefault("_t_" + name, [])
+            for _ in range(REPS // 2):
+                t = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t)
+    for name, _ in cases:
+        ts = res.pop("_t_" + name)
         res[name + "_keys_per_s_best"] = B / min(ts)
         res[name + "_keys_per_s_median"] = B / statistics.median(ts)
     res["lib"] = os.environ.get("BFHIP_LIB", "in-tree")

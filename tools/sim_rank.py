@@ -38,8 +38,22 @@ def main():
                     help="the default exchange's compute: whole windows of cap_sf entries, device-side "
                          "counts, windowed owner ops, packed answers (PartitionedFilter._sf_*); the "
                          "received windows are this rank's own (nh == 1 configs)")
+    ap.add_argument("--chunks", action="store_true",
+                    help="the sync-free exchange with chunked windows (bf_route_chunks_dev: the route sorts "
+                         "each window's runs by owner superbin and writes a directory, the owner skips its "
+                         "sort pass; the combine gathers per route tile); the received windows are this "
+                         "rank's own, permuted into the receive layout (any nh)")
+    ap.add_argument("--replicated", type=int, default=0,
+                    help="R > 0: one replica's step of the replicated layout at world size R (BASELINE "
+                         "configs[3]): ONE merged insert of every rank's batch (R x batch keys) into the whole "
+                         "filter, then this rank's include? batch")
+    ap.add_argument("--gathered", default="keys", choices=["keys", "digests"],
+                    help="replicated: what travels — key bytes (every replica hashes every batch: "
+                         "ReplicatedFilter) or 16-B SHA-1 words (each key hashed once, by its own rank)")
     args = ap.parse_args()
     pkg = pkgload.load()
+    if args.replicated:
+        return replicated(args, pkg)
     n_items, err, batch, _ = bench.CONFIGS[args.config]
     m = pkg.Bloomfilter.optimal_m(n_items, err)
     k = pkg.Bloomfilter.optimal_k(n_items, m)
@@ -98,7 +112,38 @@ def main():
         packed = eng.pack_answers(bits, seg, capsf, P * cap8)
         return eng.combine_windows_packed(packed, slot, counts, capsf, batch)
 
+    def step_chunks(b):
+        (ikb, iko), (qkb, qko) = b
+        A = 12288
+        capsf = -(-min(batch * k, batch * k // P + batch * k // (8 * P) + 4096) // A) * A
+        tiles, dbytes = eng.chunk_info(batch)
+        perm = [o * nh + h for h in range(nh) for o in range(P)]   # receive slot h*P + src <- send window
+
+        def deliver(send, dirb, counts):
+            if nh == 1:
+                recv, rdir = send, dirb
+            else:   # the exchange's job (not a library kernel): windows into the receive layout
+                recv = send.view(P * nh, capsf)[perm].reshape(-1)
+                rdir = dirb.view(P * nh, dbytes)[perm].reshape(-1)
+            rmsg = torch.cat([counts.view(P, nh), torch.zeros(P, 1, dtype=torch.int64, device=dev)], 1).contiguous()
+            return recv, rdir, rmsg
+
+        send, _, counts, dirb = eng.route_chunks(ikb, iko, batch, capsf, tiles, dbytes, want_slot=False)
+        recv, rdir, rmsg = deliver(send, dirb, counts)
+        eng.shard_insert_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1)
+        send, slot, counts, dirb = eng.route_chunks(qkb, qko, batch, capsf, tiles, dbytes)
+        recv, rdir, rmsg = deliver(send, dirb, counts)
+        bits = torch.empty(nh * P * capsf, dtype=torch.uint8, device=dev)
+        eng.shard_test_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1, bits)
+        cap8 = (capsf + 7) // 8
+        seg = torch.tensor([[(h * P + src) * capsf, capsf, (src * nh + h) * cap8] for src in range(P)
+                            for h in range(nh)], dtype=torch.int64).to(dev)
+        packed = eng.pack_answers(bits, seg, capsf, P * nh * cap8)
+        return eng.combine_chunks_packed(packed, slot, capsf, dirb, dbytes, tiles, counts, batch)
+
     def step(b):
+        if args.chunks:
+            return step_chunks(b)
         if args.sync_free:
             assert nh == 1
             return step_sf(b)
@@ -123,13 +168,81 @@ def main():
     prof = f.profile_read(reset=True)
     out = {"config": args.config, "shards": args.shards, "m": m, "k": k, "batch": batch,
            "shard_bytes": f.device_bytes, "route32": bool(eng.offset_dtype == torch.int32),
-           "route": "sync-free windows" if args.sync_free else ("windows" if args.windows else "contiguous"),
+           "route": "chunked windows" if args.chunks else
+                    ("sync-free windows" if args.sync_free else ("windows" if args.windows else "contiguous")),
            "ms_per_step_compute": wall * 1e3,
            "kernels_ms_per_step": {name: ms / args.steps for name, (ms, _) in prof.items()},
            "kernels_ms_sum": sum(ms for ms, _ in prof.values()) / args.steps,
            "note": "ms_per_step_compute includes the stand-in receive copies of --windows "
                    "(the exchange's job in a real run); kernels_ms_sum does not"}
     print(json.dumps(out))
+
+
+def replicated(args, pkg):
+    """Per-replica compute of the replicated step at world size R, on one GPU: every rank's
+    batch i (R x batch keys) goes in as one insert, then this rank's include? of batch i.
+    The all-gather itself is not in these numbers (it runs beside the previous step)."""
+    R = args.replicated
+    n_items, err, batch, _ = bench.CONFIGS[args.config]
+    m = pkg.Bloomfilter.optimal_m(n_items, err)
+    k = pkg.Bloomfilter.optimal_k(n_items, m)
+    dev = torch.device("cuda", 0)
+    f = pkg.Filter(m, k, device=0)
+    bench.prefill_random(f, m, k, 0, host_copy=False)
+    steps = []
+    for st in range(args.steps + 1):   # each step: R ranks' insert batches + one include? batch
+        per = [bench.make_batches(n_items, batch, r + 1000 * st, 1, dev)[0] for r in range(R)]
+        kbs, offs, base = [], [], 0
+        for (ikb, iko), _ in per:
+            nb = int(iko[-1].item())
+            kbs.append(ikb[:nb])
+            offs.append(iko[:-1] + base)
+            base += nb
+        mkb = torch.cat(kbs + [torch.zeros(16, dtype=torch.uint8, device=dev)])
+        mko = torch.cat(offs + [torch.tensor([base], dtype=torch.int64, device=dev)])
+        dg = None
+        if args.gathered == "digests":   # the words every rank's batch arrives as (hashed by its rank)
+            dg = torch.empty((R * batch, 4), dtype=torch.int32, device=dev)
+            f.hash_many_dev(mkb.data_ptr(), mko.data_ptr(), R * batch, dg.data_ptr())
+        steps.append((mkb, mko, per[0][1], dg))
+    nm = R * batch
+    out = torch.empty(batch, dtype=torch.uint8, device=dev)
+    own = torch.empty((batch, 4), dtype=torch.int32, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(s_):
+        mkb, mko, (qkb, qko), dg = s_
+        if args.gathered == "digests":   # this rank hashes its own batch; all R batches go in from words
+            f.hash_many_dev(mkb.data_ptr(), mko.data_ptr(), batch, own.data_ptr(), stream=sp)
+            f.insert_digests_dev(dg.data_ptr(), nm, d_any_new=flag.data_ptr(), stream=sp)
+        else:
+            f.insert_many_dev(mkb.data_ptr(), mko.data_ptr(), nm, d_any_new=flag.data_ptr(), stream=sp)
+        f.include_many_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), stream=sp)
+
+    step(steps[0])
+    torch.cuda.synchronize()
+    f.profile(True)
+    f.profile_read(reset=True)
+    t0 = time.perf_counter()
+    for s_ in steps[1:]:
+        step(s_)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    prof = f.profile_read(reset=True)
+    assert out.cpu().numpy()[: batch // 2].all(), "false negative"
+    one = None
+    res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered, "m": m, "k": k,
+           "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
+           "ms_per_step_compute": wall * 1e3,
+           "kernels_ms_per_step": {name: ms / args.steps for name, (ms, _) in prof.items()},
+           "kernels_ms_sum": sum(ms for ms, _ in prof.values()) / args.steps,
+           "keys_per_s_per_rank": 2 * batch / wall,
+           "note": "one replica's kernels per step at world size R; the key all-gather runs beside the "
+                   "previous step and is not included"}
+    f.close()
+    print(json.dumps(res))
+    return one
 
 
 if __name__ == "__main__":
