@@ -238,7 +238,10 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         mode = auto_mode(D.world, m, k, name)
     rf = None
     if mode == "replicated":   # every rank a whole replica: include? local, inserts all-gathered
-        rf = pkg.distributed.ReplicatedFilter(m, k, device=dev)
+        # 10B@0.01 % (k = 13): the SHA-1 words travel, so every replica skips P - 1 hash passes
+        # (tools/sim_rank.py --replicated 8: profiles/r03_sim_replicated8_10b.jsonl); elsewhere
+        # key bytes (fewer bytes on the one xGMI link of N = 2) or the OR-all-reduce
+        rf = pkg.distributed.ReplicatedFilter(m, k, device=dev, insert_mode="digests" if name == "10b" else "auto")
         f = rf.filter
         if prefill == "random":   # identical replicas: the same bits on every rank
             prefill_random(f, m, k, 0, host_copy=f.device_bytes < (4 << 30))

@@ -33,6 +33,9 @@
 // answer is the AND of the key's k bits (ruby.rb:20-30) without the early exit.
 #include "bf_device.h"
 
+#include <cmath>
+#include <cstdlib>
+
 using namespace bfdev;
 
 namespace {
@@ -46,7 +49,10 @@ namespace {
 
 constexpr int kTile = 1024;                   // lanes per workgroup of the front / mid passes
 constexpr int kStageVec = 16384 / 16;         // 16 KiB LDS key stage per 1024-key sub-tile
-constexpr uint32_t kMaxSup = 256;             // superbins (8-bit superbin in the sort tags)
+// superbins of the front pass (LDS counters; a sort tag is (superbin << 16) | rank): 512 lets
+// the plan balance the front's and bin_mid's run lengths on the 6.98 GB bitsets (plan_common)
+constexpr uint32_t kMaxSup = 512;
+constexpr uint32_t kMaxOwners = 256;          // route buckets / windows (owner x sub-range)
 constexpr uint32_t kChunkBuckets = 512;       // route sort buckets of chunked windows (window x superbin x 2^sub2)
 // <= 512 regions per superbin: the reach-capped 10B / 200B bitsets (55.8e9 bits) then take
 // 2^19-bit regions (64 KiB of LDS, two apply workgroups per CU) instead of 2^20 (one):
@@ -391,10 +397,13 @@ __global__ __launch_bounds__(kMaxBlocks) void bin_group_sum_kernel(const uint32_
 // base[i]: exclusive prefix of gsum over windows i = (superbin, group); base[N] =
 // all probes.  cb_base[i]: first chunk block of window i (ceil(size / kBlockProbes)
 // blocks each), cb_base[N] = all blocks; cb_window[b] / cb_start[b]: the window
-// and level-2 position of chunk block b.  One workgroup, kScanPer windows per lane
-// (N <= kMaxWindows; only the chunk-block prefix stays in LDS: 128 KiB).
-constexpr uint32_t kScanPer = 32;
-constexpr uint32_t kMaxWindows = 1024 * kScanPer;
+// and level-2 position of chunk block b.  One workgroup, kScanPer windows per lane, for
+// N <= kScanWindows; larger N take the hierarchical scan below (launch_scan).
+constexpr uint32_t kScanPer = 4;
+constexpr uint32_t kScanWindows = 1024 * kScanPer;
+constexpr uint32_t kLocalScanPer = 4;                 // groups per lane of bin_scan_local_kernel
+constexpr uint32_t kMaxGroups = 1024 * kLocalScanPer; // groups per superbin
+constexpr uint32_t kMaxWindows = kMaxSup * kMaxGroups;
 __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __restrict__ gsum, uint32_t N,
                                                               uint32_t* __restrict__ base,
                                                               uint32_t* __restrict__ cb_base,
@@ -402,7 +411,7 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
                                                               uint32_t* __restrict__ cb_start, uint32_t nq,
                                                               unsigned long long* __restrict__ totals) {
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_cb[kMaxWindows + 1];
+    __shared__ uint32_t s_cb[kScanWindows + 1];
     const uint32_t t = threadIdx.x;
     uint32_t v[kScanPer], cv[kScanPer], sum = 0, csum = 0;
 #pragma unroll
@@ -445,6 +454,81 @@ __global__ __launch_bounds__(1024) void bin_group_scan_kernel(const uint32_t* __
         }
         cb_window[blk] = lo;
         cb_start[blk] = base[lo] + (blk - s_cb[lo]) * kBlockProbes;   // base: this workgroup's own stores
+    }
+}
+
+// The same scan for N > kScanWindows windows, in three steps: per superbin over its groups
+// (bin_scan_local), over the superbins (bin_scan_top), then every window's offsets and chunk
+// blocks (bin_scan_fill).  stot: 2 words per superbin (its probes, its chunk blocks).
+__global__ __launch_bounds__(1024) void bin_scan_local_kernel(const uint32_t* __restrict__ gsum, uint32_t nq,
+                                                              uint32_t* __restrict__ base,
+                                                              uint32_t* __restrict__ cb_base,
+                                                              uint32_t* __restrict__ stot) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t sb = blockIdx.x, t = threadIdx.x;
+    uint32_t v[kLocalScanPer], cv[kLocalScanPer], sum = 0, csum = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kLocalScanPer; ++e) {
+        const uint32_t q = kLocalScanPer * t + e;
+        v[e] = q < nq ? gsum[(uint64_t)sb * nq + q] : 0u;
+        cv[e] = (v[e] + kBlockProbes - 1) / kBlockProbes;
+        sum += v[e];
+        csum += cv[e];
+    }
+    uint32_t total, ctotal;
+    uint32_t ex = block_excl_scan(sum, s_w, &total);
+    uint32_t cex = block_excl_scan(csum, s_w, &ctotal);
+#pragma unroll
+    for (uint32_t e = 0; e < kLocalScanPer; ++e) {
+        const uint32_t q = kLocalScanPer * t + e;
+        if (q < nq) {
+            base[(uint64_t)sb * nq + q] = ex;   // superbin-relative until bin_scan_fill
+            cb_base[(uint64_t)sb * nq + q] = cex;
+        }
+        ex += v[e];
+        cex += cv[e];
+    }
+    if (t == 0) {
+        stot[2 * sb] = total;
+        stot[2 * sb + 1] = ctotal;
+    }
+}
+
+__global__ __launch_bounds__(1024) void bin_scan_top_kernel(uint32_t* __restrict__ stot, uint32_t nsup, uint32_t N,
+                                                            uint32_t* __restrict__ base,
+                                                            uint32_t* __restrict__ cb_base) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x;
+    const uint32_t v = t < nsup ? stot[2 * t] : 0u, cv = t < nsup ? stot[2 * t + 1] : 0u;
+    uint32_t total, ctotal;
+    const uint32_t ex = block_excl_scan(v, s_w, &total);
+    const uint32_t cex = block_excl_scan(cv, s_w, &ctotal);
+    if (t < nsup) {
+        stot[2 * t] = ex;
+        stot[2 * t + 1] = cex;
+    }
+    if (t == 0) {
+        base[N] = total;
+        cb_base[N] = ctotal;
+    }
+}
+
+__global__ __launch_bounds__(256) void bin_scan_fill_kernel(const uint32_t* __restrict__ gsum, uint32_t N, uint32_t nq,
+                                                            const uint32_t* __restrict__ stot,
+                                                            uint32_t* __restrict__ base,
+                                                            uint32_t* __restrict__ cb_base,
+                                                            uint32_t* __restrict__ cb_window,
+                                                            uint32_t* __restrict__ cb_start) {
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= N) return;
+    const uint32_t sb = w / nq;
+    const uint32_t b = base[w] + stot[2 * sb], cb = cb_base[w] + stot[2 * sb + 1];
+    base[w] = b;
+    cb_base[w] = cb;
+    const uint32_t nb = (gsum[w] + kBlockProbes - 1) / kBlockProbes;
+    for (uint32_t j = 0; j < nb; ++j) {
+        cb_window[cb + j] = w;
+        cb_start[cb + j] = b + j * kBlockProbes;
     }
 }
 
@@ -524,11 +608,11 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
     uint16_t* s_key = reinterpret_cast<uint16_t*>(s_raw);
     // CHUNK: up to kChunkBuckets (window, superbin, low bits) buckets; the window route keeps
     // no per-workgroup totals (s_gcnt), which keeps the LDS within two workgroups per CU
-    constexpr uint32_t NB = CHUNK ? kChunkBuckets : kMaxSup;
-    __shared__ uint32_t s_cnt[NB], s_lbase[NB], s_gcnt[WIN ? 1 : kMaxSup];
+    constexpr uint32_t NB = CHUNK ? kChunkBuckets : kMaxOwners;
+    __shared__ uint32_t s_cnt[NB], s_lbase[NB], s_gcnt[WIN ? 1 : kMaxOwners];
     __shared__ uint32_t s_w[16];
-    __shared__ unsigned long long s_gbase[WIN ? kMaxSup : 1];
-    __shared__ uint32_t s_obase[WIN ? kMaxSup : 1];
+    __shared__ unsigned long long s_gbase[WIN ? kMaxOwners : 1];
+    __shared__ uint32_t s_obase[WIN ? kMaxOwners : 1];
     // WIN: ~128 sort buckets however few the owners, so that the LDS rank atomics do not
     // all land on P words (the owner's buckets stay consecutive: one run per owner)
     uint32_t sub_log2 = 0;
@@ -542,7 +626,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
     const uint32_t t = threadIdx.x;
     if (t < NB) s_cnt[t] = 0;
     if constexpr (!WIN)
-        if (t < kMaxSup) s_gcnt[t] = 0;
+        if (t < kMaxOwners) s_gcnt[t] = 0;
     __syncthreads();
     const uint32_t k = g.k;
     const uint32_t kpl = tile_keys / kTile;
@@ -1007,11 +1091,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
             if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
         }
     }
-    if (any_flag) {
-        const unsigned long long b = __ballot(fresh != 0);
-        if (b != 0ull && (t & 63u) == (uint32_t)__builtin_ctzll(b))
-            __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (any_flag) report_any_new(any_flag, fresh != 0);
 }
 
 // include?: the region in LDS; a probe on a 0 bit clears its key's answer.  The probe
@@ -1293,7 +1373,7 @@ __global__ __launch_bounds__(kCombineLanes) void combine_chunks_packed_kernel(
         BfChunks cg, uint32_t nwin, const unsigned long long* __restrict__ counts, uint64_t n, uint32_t tile_keys,
         uint8_t* __restrict__ out) {
     __shared__ uint8_t s_ans[2 * kTile];
-    __shared__ uint32_t s_pre[kMaxSup], s_st[kMaxSup], s_w[16];
+    __shared__ uint32_t s_pre[kMaxOwners], s_st[kMaxOwners], s_w[16];
     const uint32_t t = threadIdx.x;
     const uint64_t tile = blockIdx.x, key0 = tile * tile_keys;
     const uint32_t tk = (uint32_t)(n - key0 < tile_keys ? n - key0 : tile_keys);
@@ -1346,6 +1426,7 @@ struct Carve {
     uint32_t *level1, *level1_key, *level2, *level2_key, *gcnt, *gsum, *base, *cb_base, *cb_window, *cb_start;
     uint16_t *stab, *tabs;
     uint2* runs;   // the chunked L2-local test's window run tables
+    uint32_t* stot;   // hierarchical scan: per-superbin totals
     uint64_t bytes;
 };
 
@@ -1367,6 +1448,7 @@ Carve carve(const BfBinPlan& p, void* at0) {
     c.cb_base = reinterpret_cast<uint32_t*>(take((N + 1) * 4));
     c.cb_window = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
     c.cb_start = reinterpret_cast<uint32_t*>(take(p.max_chunks * 4));
+    c.stot = reinterpret_cast<uint32_t*>(take(2 * kMaxSup * 4));
     if (p.l2test) {   // sorts nothing: the window run tables only
         c.runs = reinterpret_cast<uint2*>(take(N * kRunsPerPass * sizeof(uint2)));
         c.bytes = off;
@@ -1377,12 +1459,27 @@ Carve carve(const BfBinPlan& p, void* at0) {
     return c;
 }
 
+// Window offsets and chunk blocks from gsum: one workgroup up to kScanWindows windows, the
+// hierarchical scan beyond.
+void launch_scan(const BfBinPlan& p, const Carve& c, hipStream_t s) {
+    const uint32_t N = p.nsup * p.ngroups;
+    if (N <= kScanWindows) {
+        hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, N, c.base, c.cb_base,
+                           c.cb_window, c.cb_start, p.ngroups, (unsigned long long*)nullptr);
+        return;
+    }
+    hipLaunchKernelGGL(bin_scan_local_kernel, dim3(p.nsup), dim3(1024), 0, s, c.gsum, p.ngroups, c.base, c.cb_base,
+                       c.stot);
+    hipLaunchKernelGGL(bin_scan_top_kernel, dim3(1), dim3(1024), 0, s, c.stot, p.nsup, N, c.base, c.cb_base);
+    hipLaunchKernelGGL(bin_scan_fill_kernel, dim3((N + 255) / 256), dim3(256), 0, s, c.gsum, N, p.ngroups, c.stot,
+                       c.base, c.cb_base, c.cb_window, c.cb_start);
+}
+
 // bin_group_sum .. bin_mid over the level-1 array a front pass wrote.
 hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c, hipStream_t s, BfMarks* mk) {
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
                        p.ngroups, c.gsum);
-    hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
-                       c.cb_base, c.cb_window, c.cb_start, p.ngroups, (unsigned long long*)nullptr);
+    launch_scan(p, c, s);
     bf_mark(mk, s, "bin_group");
     const uint32_t tiles_per_group = kGroupBlocks * p.tiles_per_block;
     if (p.with_keys)
@@ -1451,7 +1548,7 @@ uint32_t superbins(uint64_t bitset_bytes, uint32_t pref_region_log2);
 uint64_t max_tiles(uint64_t bitset_bytes, uint32_t pref_region_log2) {
     const uint32_t nsup = superbins(bitset_bytes, pref_region_log2);
     if (nsup == 0) return 0;
-    const uint64_t groups = kMaxWindows / nsup;
+    const uint64_t groups = std::min<uint64_t>(kMaxWindows / nsup, kMaxGroups);
     const uint64_t blocks = std::min<uint64_t>(kMaxFrontBlocks, groups * kGroupBlocks);
     return blocks * kMaxTilesPerBlock;
 }
@@ -1472,6 +1569,38 @@ uint64_t bf_binned_max_offsets(uint64_t bitset_bytes, uint32_t pref_region_log2)
 namespace {
 
 // n units of k probes each, tile_units per front tile.
+// Superbin size: a probe passes through two sorts, the front's (tile_probes / nsup probes per
+// tile run) and bin_mid's (kBlockProbes / 2^rel per region run); their product is fixed by the
+// region count, and the gathers of both passes (bin_mid's and bin_apply's) read those runs, so
+// the plan balances the two run lengths — among superbin counts of at least 128 (fewer LDS
+// counters make the front's rank atomics collide).  1B@1 %, 100M@0.1 %, 1M@1 %: the r02 plans;
+// the 6.98 GB bitsets (10B / 200B): 416 superbins of 256 regions (runs of 32 and 32) instead of
+// 208 of 512 (64 and 16).  BFHIP_BIN_MAX_SUP=256 gives r02's plans (A/B only).
+uint32_t max_superbins() {
+    static const uint32_t cap = [] {
+        const char* e = std::getenv("BFHIP_BIN_MAX_SUP");
+        const int v = e ? std::atoi(e) : (int)kMaxSup;
+        return (uint32_t)(v >= 16 && v <= (int)kMaxSup ? v : (int)kMaxSup);
+    }();
+    return cap;
+}
+
+uint32_t balanced_rel(uint64_t nbins, uint32_t rel_min, uint32_t tile_probes) {
+    uint32_t best = rel_min;
+    double best_gap = 1e30;
+    for (uint32_t rel = rel_min; rel <= kMaxRel; ++rel) {
+        const uint64_t nsup = (nbins + (1ull << rel) - 1) >> rel;
+        if (nsup < 128 && rel != rel_min) break;
+        const double front = (double)tile_probes / (double)nsup, mid = (double)kBlockProbes / (double)(1u << rel);
+        const double gap = std::fabs(std::log2(front / mid));
+        if (gap < best_gap) {
+            best_gap = gap;
+            best = rel;
+        }
+    }
+    return best;
+}
+
 bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_units, uint32_t pref_region_log2,
                  bool with_keys, BfBinPlan* plan) {
     const uint64_t probes = n * k;
@@ -1485,8 +1614,9 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
         if (rl == 0) break;
         const uint64_t nbins = (bits + (1ull << rl) - 1) >> rl;
         uint32_t rel = 0;
-        while (((nbins + (1ull << rel) - 1) >> rel) > kMaxSup) ++rel;
+        while (((nbins + (1ull << rel) - 1) >> rel) > max_superbins()) ++rel;
         if (rel > kMaxRel) continue;
+        rel = balanced_rel(nbins, rel, tile_units * k);
         BfBinPlan p{};
         p.region_log2 = rl;
         p.nbins = (uint32_t)nbins;
@@ -1500,7 +1630,7 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
         if (p.ntiles > (uint64_t)kMaxFrontBlocks * p.tiles_per_block) continue;
         p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
         p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
-        if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) continue;
+        if ((uint64_t)p.nsup * p.ngroups > kMaxWindows || p.ngroups > kMaxGroups) continue;
         p.probes = probes;
         p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
         p.scratch_bytes = carve(p, nullptr).bytes;
@@ -1700,7 +1830,7 @@ RouteCarve route_carve(const BfBinPlan& p, bool wide, bool with_slot, void* at0)
 // (owner, group) windows fit the one-workgroup scan.
 
 bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with_slot, BfBinPlan* plan) {
-    if (k == 0 || k > (uint32_t)kWideSlots || n == 0 || shards == 0 || shards > kMaxSup) return false;
+    if (k == 0 || k > (uint32_t)kWideSlots || n == 0 || shards == 0 || shards > kMaxOwners) return false;
     const uint64_t probes = n * k;
     if (probes >= (1ull << 32)) return false;
     BfBinPlan p{};
@@ -1713,7 +1843,7 @@ bool bf_route_plan(uint64_t n, uint32_t k, uint32_t shards, bool wide, bool with
     if (p.ntiles > (uint64_t)kMaxFrontBlocks * p.tiles_per_block) return false;
     p.nblocks = (uint32_t)((p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block);
     p.ngroups = (p.nblocks + kGroupBlocks - 1) / kGroupBlocks;
-    if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) return false;
+    if ((uint64_t)p.nsup * p.ngroups > kScanWindows) return false;   // one-workgroup scan (per-owner totals)
     p.probes = probes;
     p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
     p.scratch_bytes = route_carve(p, wide, with_slot, nullptr).bytes;
@@ -1795,7 +1925,7 @@ hipError_t bf_launch_route_windows(const BfGeom& g, const BfBinPlan& p, uint32_t
 bool bf_chunk_geometry(uint64_t shard0_bits, uint32_t nwin, uint32_t pref_region_log2, BfChunks* cg,
                        uint32_t max_buckets) {
     if (max_buckets == 0 || max_buckets > kChunkBuckets) max_buckets = kChunkBuckets;
-    if (nwin == 0 || nwin > kMaxSup) return false;
+    if (nwin == 0 || nwin > kMaxOwners) return false;
     const uint32_t rl = (pref_region_log2 >= 18 && pref_region_log2 <= 20) ? pref_region_log2 : 19u;
     uint64_t nbins0 = (shard0_bits + (1ull << rl) - 1) >> rl;
     if (nbins0 == 0) nbins0 = 1;
@@ -1838,7 +1968,7 @@ bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint3
     p.nsup = (uint32_t)((nbins + (1ull << p.rel_log2) - 1) >> p.rel_log2);
     if (p.nsup == 0 || p.nsup > (uint64_t)nh * cg.S) return false;
     p.ngroups = (uint32_t)(((uint64_t)nsrc * cg.tiles + kRunsPerPass - 1) / kRunsPerPass);
-    if ((uint64_t)p.nsup * p.ngroups > kMaxWindows) return false;
+    if ((uint64_t)p.nsup * p.ngroups > kMaxWindows || p.ngroups > kMaxGroups) return false;
     p.probes = probes;
     p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
     p.scratch_bytes = carve(p, nullptr).bytes;
@@ -1851,8 +1981,7 @@ hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn&
                             BfMarks* mk) {
     hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
                        c.gsum, (uint2*)nullptr);
-    hipLaunchKernelGGL(bin_group_scan_kernel, dim3(1), dim3(1024), 0, s, c.gsum, p.nsup * p.ngroups, c.base,
-                       c.cb_base, c.cb_window, c.cb_start, p.ngroups, (unsigned long long*)nullptr);
+    launch_scan(p, c, s);
     bf_mark(mk, s, "chunk_group");
     if (p.with_keys)
         hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
@@ -1927,7 +2056,7 @@ hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t
                                            const BfChunks& cg, uint32_t nwin, const unsigned long long* counts,
                                            uint64_t n, uint32_t tile_keys, uint8_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    if (nwin > kMaxSup || tile_keys > 2 * kTile || tile_keys == 0) return hipErrorInvalidValue;
+    if (nwin > kMaxOwners || tile_keys > 2 * kTile || tile_keys == 0) return hipErrorInvalidValue;
     const uint64_t grid = (n + tile_keys - 1) / tile_keys;
     hipLaunchKernelGGL(combine_chunks_packed_kernel, dim3((uint32_t)grid), dim3(kCombineLanes), 0, s, packed, slot16,
                        wcap, (wcap + 7) / 8, cg, nwin, counts, n, tile_keys, out);

@@ -162,11 +162,7 @@ __global__ __launch_bounds__(kLanes) void engine_kernel(BfGeom g, const uint8_t*
         }
     }
     if constexpr (OP == BF_OP_INSERT) {
-        if (any_flag) {
-            const unsigned long long b = __ballot(fresh);
-            if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
-                __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (any_flag) bfdev::report_any_new(any_flag, fresh);
     }
 }
 

@@ -186,11 +186,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
     }
 
     if constexpr (OP == BF_OP_INSERT_FLAGS) {
-        if (any_flag) {
-            const unsigned long long b = __ballot(newflag != 0);
-            if (b != 0ull && (t & 63u) == (uint32_t)__builtin_ctzll(b))
-                __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (any_flag) report_any_new(any_flag, newflag != 0);
     }
 }
 
@@ -208,11 +204,7 @@ __global__ __launch_bounds__(kBlock) void bf_digest_kernel(BfGeom g, const uint4
         digest_op<OP>(g, H, j, out8, out64, newflag, nullptr, NoSide{});
     }
     if constexpr (OP == BF_OP_INSERT_FLAGS) {
-        if (any_flag) {
-            const unsigned long long b = __ballot(newflag != 0);
-            if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
-                __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (any_flag) report_any_new(any_flag, newflag != 0);
     }
 }
 
@@ -431,11 +423,7 @@ __global__ __launch_bounds__(256) void shard_insert_kernel(uint32_t* __restrict_
             }
         }
     }
-    if constexpr (FLAGS) {
-        const unsigned long long b = __ballot(isnew != 0);
-        if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
-            __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if constexpr (FLAGS) report_any_new(any_flag, isnew != 0);
 }
 
 template <typename Off>

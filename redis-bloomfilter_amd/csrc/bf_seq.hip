@@ -108,11 +108,7 @@ __global__ __launch_bounds__(256) void seq_mark_kernel(BfGeom g, uint32_t i0, ui
         }
         if (out8) out8[j] = (uint8_t)isnew;
     }
-    if (any_flag) {
-        const unsigned long long b = __ballot(isnew != 0 && j < limit);
-        if (b != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(b))
-            __hip_atomic_fetch_or(any_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (any_flag) report_any_new(any_flag, isnew != 0 && j < limit);
 }
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }

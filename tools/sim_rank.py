@@ -50,6 +50,10 @@ def main():
     ap.add_argument("--gathered", default="keys", choices=["keys", "digests"],
                     help="replicated: what travels — key bytes (every replica hashes every batch: "
                          "ReplicatedFilter) or 16-B SHA-1 words (each key hashed once, by its own rank)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="--chunks: route the NEXT step's insert batch on a second stream while this step's "
+                         "owner kernels run (what PartitionedFilter's next_insert prefetch would do on a side "
+                         "stream); the step's wall time is what to read")
     args = ap.parse_args()
     pkg = pkgload.load()
     if args.replicated:
@@ -128,9 +132,21 @@ def main():
             rmsg = torch.cat([counts.view(P, nh), torch.zeros(P, 1, dtype=torch.int64, device=dev)], 1).contiguous()
             return recv, rdir, rmsg
 
-        send, _, counts, dirb = eng.route_chunks(ikb, iko, batch, capsf, tiles, dbytes, want_slot=False)
+        if args.overlap:   # this step's insert batch was routed during the previous step, on side
+            torch.cuda.current_stream(dev).wait_event(pre["ev"])
+            send, counts, dirb = pre["send"], pre["counts"], pre["dirb"]
+        else:
+            send, _, counts, dirb = eng.route_chunks(ikb, iko, batch, capsf, tiles, dbytes, want_slot=False)
         recv, rdir, rmsg = deliver(send, dirb, counts)
         eng.shard_insert_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1)
+        if args.overlap:   # the next step's insert route, beside this step's owner kernels
+            nb = nxt_batch[0]
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):   # a second handle: one handle orders its calls across streams
+                s_, _, c_, d_ = router.route_chunks(nb[0][0], nb[0][1], batch, capsf, tiles, dbytes, want_slot=False)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            pre.update(send=s_, counts=c_, dirb=d_, ev=ev)
         send, slot, counts, dirb = eng.route_chunks(qkb, qko, batch, capsf, tiles, dbytes)
         recv, rdir, rmsg = deliver(send, dirb, counts)
         bits = torch.empty(nh * P * capsf, dtype=torch.uint8, device=dev)
@@ -140,6 +156,11 @@ def main():
                             for h in range(nh)], dtype=torch.int64).to(dev)
         packed = eng.pack_answers(bits, seg, capsf, P * nh * cap8)
         return eng.combine_chunks_packed(packed, slot, capsf, dirb, dbytes, tiles, counts, batch)
+
+    side = torch.cuda.Stream(dev)
+    router = pkg.distributed.HipEngine(m, k, args.shards, 0, 20, dev) if args.overlap else None
+    pre = {}
+    nxt_batch = [None]
 
     def step(b):
         if args.chunks:
@@ -156,12 +177,23 @@ def main():
         bits = eng.shard_test(send)
         return eng.combine(bits, slot, batch)
 
+    if args.overlap:   # batch 0's insert route before the first step (the pipeline's fill)
+        tiles0, dbytes0 = eng.chunk_info(batch)
+        A = 12288
+        cap0 = -(-min(batch * k, batch * k // P + batch * k // (8 * P) + 4096) // A) * A
+        s_, _, c_, d_ = eng.route_chunks(batches[0][0][0], batches[0][0][1], batch, cap0, tiles0, dbytes0,
+                                         want_slot=False)
+        ev = torch.cuda.Event()
+        ev.record()
+        pre.update(send=s_, counts=c_, dirb=d_, ev=ev)
+    nxt_batch[0] = batches[1]
     step(batches[0])
     torch.cuda.synchronize()
     f.profile(True)
     f.profile_read(reset=True)
     t0 = time.perf_counter()
-    for b in batches[1:]:
+    for i, b in enumerate(batches[1:], start=1):
+        nxt_batch[0] = batches[(i + 1) % len(batches)]
         step(b)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.steps
