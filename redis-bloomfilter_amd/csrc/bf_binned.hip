@@ -33,9 +33,6 @@
 // answer is the AND of the key's k bits (ruby.rb:20-30) without the early exit.
 #include "bf_device.h"
 
-#include <cmath>
-#include <cstdlib>
-
 using namespace bfdev;
 
 namespace {
@@ -49,9 +46,10 @@ namespace {
 
 constexpr int kTile = 1024;                   // lanes per workgroup of the front / mid passes
 constexpr int kStageVec = 16384 / 16;         // 16 KiB LDS key stage per 1024-key sub-tile
-// superbins of the front pass (LDS counters; a sort tag is (superbin << 16) | rank): 512 lets
-// the plan balance the front's and bin_mid's run lengths on the 6.98 GB bitsets (plan_common)
-constexpr uint32_t kMaxSup = 512;
+// superbins of the front pass (LDS counters; a sort tag is (superbin << 16) | rank).  512 with
+// run lengths balanced between the front and bin_mid (416 superbins at 10B) measured slower:
+// 10B step 6.85 vs 6.55 ms
+constexpr uint32_t kMaxSup = 256;
 constexpr uint32_t kMaxOwners = 256;          // route buckets / windows (owner x sub-range)
 constexpr uint32_t kChunkBuckets = 512;       // route sort buckets of chunked windows (window x superbin x 2^sub2)
 // <= 512 regions per superbin: the reach-capped 10B / 200B bitsets (55.8e9 bits) then take
@@ -1569,38 +1567,6 @@ uint64_t bf_binned_max_offsets(uint64_t bitset_bytes, uint32_t pref_region_log2)
 namespace {
 
 // n units of k probes each, tile_units per front tile.
-// Superbin size: a probe passes through two sorts, the front's (tile_probes / nsup probes per
-// tile run) and bin_mid's (kBlockProbes / 2^rel per region run); their product is fixed by the
-// region count, and the gathers of both passes (bin_mid's and bin_apply's) read those runs, so
-// the plan balances the two run lengths — among superbin counts of at least 128 (fewer LDS
-// counters make the front's rank atomics collide).  1B@1 %, 100M@0.1 %, 1M@1 %: the r02 plans;
-// the 6.98 GB bitsets (10B / 200B): 416 superbins of 256 regions (runs of 32 and 32) instead of
-// 208 of 512 (64 and 16).  BFHIP_BIN_MAX_SUP=256 gives r02's plans (A/B only).
-uint32_t max_superbins() {
-    static const uint32_t cap = [] {
-        const char* e = std::getenv("BFHIP_BIN_MAX_SUP");
-        const int v = e ? std::atoi(e) : (int)kMaxSup;
-        return (uint32_t)(v >= 16 && v <= (int)kMaxSup ? v : (int)kMaxSup);
-    }();
-    return cap;
-}
-
-uint32_t balanced_rel(uint64_t nbins, uint32_t rel_min, uint32_t tile_probes) {
-    uint32_t best = rel_min;
-    double best_gap = 1e30;
-    for (uint32_t rel = rel_min; rel <= kMaxRel; ++rel) {
-        const uint64_t nsup = (nbins + (1ull << rel) - 1) >> rel;
-        if (nsup < 128 && rel != rel_min) break;
-        const double front = (double)tile_probes / (double)nsup, mid = (double)kBlockProbes / (double)(1u << rel);
-        const double gap = std::fabs(std::log2(front / mid));
-        if (gap < best_gap) {
-            best_gap = gap;
-            best = rel;
-        }
-    }
-    return best;
-}
-
 bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_units, uint32_t pref_region_log2,
                  bool with_keys, BfBinPlan* plan) {
     const uint64_t probes = n * k;
@@ -1614,9 +1580,8 @@ bool plan_common(uint64_t bitset_bytes, uint64_t n, uint32_t k, uint32_t tile_un
         if (rl == 0) break;
         const uint64_t nbins = (bits + (1ull << rl) - 1) >> rl;
         uint32_t rel = 0;
-        while (((nbins + (1ull << rel) - 1) >> rel) > max_superbins()) ++rel;
+        while (((nbins + (1ull << rel) - 1) >> rel) > kMaxSup) ++rel;
         if (rel > kMaxRel) continue;
-        rel = balanced_rel(nbins, rel, tile_units * k);
         BfBinPlan p{};
         p.region_log2 = rl;
         p.nbins = (uint32_t)nbins;
