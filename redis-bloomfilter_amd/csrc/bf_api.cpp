@@ -8,8 +8,6 @@
 #include "bf_multi.h"
 
 #include <sched.h>
-#include <sys/mman.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -342,32 +340,6 @@ int ensure_staging(bf_handle* h, uint64_t keys, uint64_t bytes, uint64_t out_byt
     return BF_OK;
 }
 
-// The caller's result buffer of a large host-pointer call is typically fresh memory (numpy
-// zeros, an FFI::MemoryPointer): its first touch page-faults, and those faults would land in
-// the result memcpy of every retired chunk, on the pipeline's critical path.  A helper thread
-// populates the pages (MADV_POPULATE_WRITE: faulted in by the kernel, contents unchanged, so
-// it may race the memcpy harmlessly) while the first chunks are staged and run.  Kernels
-// without the advice (EINVAL) just keep the old behaviour.
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
-constexpr uint64_t kPrefaultBytes = 1ull << 20;
-struct Prefault {
-    std::thread th;
-    Prefault(void* p, uint64_t bytes) {
-        if (!p || bytes < kPrefaultBytes || std::getenv("BFHIP_NO_PREFAULT")) return;
-        th = std::thread([p, bytes] {
-            const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
-            const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(pg - 1);
-            const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + pg - 1) & ~(pg - 1);
-            (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_POPULATE_WRITE);
-        });
-    }
-    ~Prefault() {
-        if (th.joinable()) th.join();
-    }
-};
-
 // Waits for a slot's previous chunk and copies its results to the caller.
 int retire_slot(bf_handle* h, Slot& s) {
     if (!s.busy) return BF_OK;
@@ -647,8 +619,6 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
 
     const bool want_flag = (op == BF_OP_INSERT_FLAGS) && any_new;
     if (want_flag) HIPCHK(h, hipMemsetAsync(h->d_flag, 0, sizeof(uint32_t), h->stream));
-    Prefault prefault(out8 ? static_cast<void*>(out8) : static_cast<void*>(out64),
-                      out8 ? n : (out64 ? n * h->k * sizeof(uint64_t) : 0));
 
     uint64_t i = 0;
     int c = 0;

@@ -33,6 +33,8 @@
 // answer is the AND of the key's k bits (ruby.rb:20-30) without the early exit.
 #include "bf_device.h"
 
+#include <cstdlib>
+
 using namespace bfdev;
 
 namespace {
@@ -1980,9 +1982,14 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
         hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
                            c.gsum, c.runs);
         bf_mark(mk, s, "chunk_group");
-        // >= kL2Grid items per superbin, so the whole grid sweeps one superbin at a time
-        const uint32_t parts = (kL2Grid + p.ngroups - 1) / p.ngroups;
-        hipLaunchKernelGGL(chunk_test_l2_kernel, dim3(kL2Grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup, p.ngroups,
+        // >= grid items per superbin, so the whole grid sweeps one superbin at a time
+        static const uint32_t grid = [] {
+            const char* e = std::getenv("BFHIP_L2_GRID");   // A/B: resident workgroups of the sweep
+            const int v = e ? std::atoi(e) : (int)kL2Grid;
+            return (uint32_t)(v >= 64 && v <= 8192 ? v : (int)kL2Grid);
+        }();
+        const uint32_t parts = (grid + p.ngroups - 1) / p.ngroups;
+        hipLaunchKernelGGL(chunk_test_l2_kernel, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup, p.ngroups,
                            parts, c.gsum, c.runs, out8);
         bf_mark(mk, s, "test_l2");
         return hipGetLastError();
