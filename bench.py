@@ -694,6 +694,20 @@ def load_traffic(workload: str, kernel: str):
 
 
 PMC_FILES = {"nstar": "pmc_r02i_nstar.json", "1m_big": "pmc_r02_1m_big.json", "10b": "pmc_r02_10b.json"}
+# rocprofv3 --kernel-trace --stats of the bench command on the round's final tree
+# (tools/rocprof_means.py over profiles/<tag>_kernel_stats.csv): each kernel's mean launch
+ROCPROF_MEANS = "rocprof_means.json"
+
+
+def load_rocprof_mean(workload: str, kernel: str):
+    """(mean ms, source) of `kernel` from the committed rocprof summary, or (None, None)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", ROCPROF_MEANS)) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    rec = (t.get(workload) or {}).get(kernel)
+    return (rec, t.get("source")) if rec else (None, None)
 
 
 def load_pmc(workload: str):
@@ -850,6 +864,7 @@ def main():
     dom_name = max(kern, key=lambda nm: kern[nm]["ms"] * kern[nm]["launches"])
     dom = kern[dom_name]
     achieved = dom["algo_bytes"] / (dom["ms"] / 1e3) if "algo_bytes" in dom else None
+    rp_ms, rp_src = load_rocprof_mean(args.config, dom_name)
     traffic = load_traffic(args.config, dom_name)
     n, p, batch, _ = CONFIGS[args.config]
     fills = None
@@ -915,7 +930,11 @@ def main():
                      # against the measured random-fill ceiling of this chip
                      "random_fill": fills,
                      "kernel_ms": dom["ms"], "timing": "HIP events on the launch stream around each kernel, "
-                                                       "inside the timed region (bf_profile)"},
+                                                       "inside the timed region (bf_profile)",
+                     # the same fraction from the committed rocprofv3 --stats mean of this kernel
+                     "kernel_ms_rocprof": rp_ms, "rocprof_source": rp_src,
+                     "frac_rocprof": (dom["algo_bytes"] / (rp_ms / 1e3) / HBM_PEAK)
+                     if rp_ms and "algo_bytes" in dom else None},
         "pmc": load_pmc(args.config),
         "cpu_baseline": cpu,
         "ops": {"insert": ins, "include": inc},

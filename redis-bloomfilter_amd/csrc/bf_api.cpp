@@ -160,13 +160,14 @@ struct bf_handle {
     uint32_t include_binned_mode = 2;   // the same policy for include?
     uint32_t shard_test_binned_mode = 2;   // ... and for the owner-side test of routed probes
     uint32_t bin_region_log2 = 19;   // preferred region (LDS image) size of the apply pass
-    // chunked windows: route sort buckets (window x owner superbin x low bits).  256 (bigger
-    // superbins, longer runs) measured 3.38-3.40 ms per P = 8 rank step against 3.44 at 512
-    // (profiles/r03_sim_chunks_P8.jsonl); BFHIP_CHUNK_BUCKETS, A/B only
-    uint32_t chunk_buckets = 256;
-    // chunked include?: 1 = the superbin-major L2-local sweep (chunk_test_l2_kernel), 0 = sort
-    // by region + region test.  The sweep measured 1.53 ms against 1.08: off
-    uint32_t chunk_test_l2 = 0;
+    // chunked windows.  The owner's include? takes the superbin-major L2-local sweep
+    // (chunk_test_l2_kernel) when the route's buckets can make superbins of <= 4 MiB (512 buckets:
+    // the north-star shards at P = 2..8): 0.89 ms against 1.08 for sort + region test, 3.22 vs
+    // 3.38 ms per P = 8 rank step.  Otherwise (8 MiB+ superbins, e.g. 200B x 8: 3.44 vs 3.11 ms)
+    // it sorts, with 256 buckets (longer runs for the owner's mid).  profiles/r03_sim_chunks_P8.jsonl.
+    // BFHIP_CHUNK_BUCKETS forces the bucket count, BFHIP_CHUNK_TEST_L2=0/1 the test (A/B only).
+    uint32_t chunk_buckets = 0;   // 0: auto
+    uint32_t chunk_test_l2 = 2;   // 2: auto
     void* d_bin_scratch = nullptr;   // digests, probe arrays and histograms of one binned launch
     uint64_t bin_scratch_cap = 0;
     uint64_t cap_keys = 0, cap_bytes = 0;   // chunk limits of the host-pointer calls (bf_config)
@@ -906,8 +907,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);
-    h->chunk_buckets = env_u32("BFHIP_CHUNK_BUCKETS", 256);
-    h->chunk_test_l2 = env_u32("BFHIP_CHUNK_TEST_L2", 0);
+    h->chunk_buckets = env_u32("BFHIP_CHUNK_BUCKETS", 0);
+    h->chunk_test_l2 = env_u32("BFHIP_CHUNK_TEST_L2", 2);
     h->include_binned_mode = env_u32("BFHIP_INCLUDE_BINNED", kDefaultIncludeBinnedMode);
     h->shard_test_binned_mode = env_u32("BFHIP_SHARD_TEST_BINNED", 2);
     *out = h;
@@ -1275,13 +1276,28 @@ int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
 namespace {
 // The chunked-window geometry of a shard handle's filter (the same on every rank: it depends
 // on the largest shard's size and the window count only).
-static bool handle_chunks(const bf_handle* h, BfChunks* cg, uint32_t* nh_out) {
+constexpr uint32_t kL2SweepMaxSupLog2 = 25;   // 4 MiB superbins: what one XCD's L2 keeps
+
+// l2 (nullable): whether the owner's include? takes the L2-local sweep with this geometry.
+static bool handle_chunks(const bf_handle* h, BfChunks* cg, uint32_t* nh_out, bool* l2 = nullptr) {
     uint32_t nh = 1;
     bf_route_window_split(h, &nh);
     const uint64_t nblocks = (h->reach + (1ull << h->block_log2) - 1) >> h->block_log2;
     const uint64_t bits0 = h->shards == 1 ? h->reach : ((nblocks + h->shards - 1) / h->shards) << h->block_log2;
     if (nh_out) *nh_out = nh;
-    return bf_chunk_geometry(bits0, h->shards * nh, h->bin_region_log2, cg, h->chunk_buckets);
+    const uint32_t nwin = h->shards * nh;
+    bool sweep = false;
+    if (h->chunk_buckets) {   // forced
+        if (!bf_chunk_geometry(bits0, nwin, h->bin_region_log2, cg, h->chunk_buckets)) return false;
+        sweep = h->chunk_test_l2 == 1 || (h->chunk_test_l2 == 2 && cg->sup_log2 <= kL2SweepMaxSupLog2);
+    } else if (h->chunk_test_l2 != 0 && bf_chunk_geometry(bits0, nwin, h->bin_region_log2, cg, 512) &&
+               (h->chunk_test_l2 == 1 || cg->sup_log2 <= kL2SweepMaxSupLog2)) {
+        sweep = true;
+    } else if (!bf_chunk_geometry(bits0, nwin, h->bin_region_log2, cg, 256)) {
+        return false;
+    }
+    if (l2) *l2 = sweep;
+    return true;
 }
 
 static uint64_t route_tile_keys(uint32_t k) { return k <= 6 ? 2048 : 1024; }   // bf_route_plan's tiles
@@ -1360,7 +1376,8 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
     if (!d_recv || !d_dir || !d_counts || (test && !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
     BfChunks cg;
     uint32_t nh = 1;
-    if (!handle_chunks(h, &cg, &nh)) return set_err(h, BF_EINVAL, "this shard count cannot take chunked windows");
+    bool sweep = false;
+    if (!handle_chunks(h, &cg, &nh, &sweep)) return set_err(h, BF_EINVAL, "this shard count cannot take chunked windows");
     int rc = check_chunk_args(h, cg, dir_bytes, tiles);
     if (rc) return rc;
     if (count_stride < nh) return set_err(h, BF_EINVAL, "count_stride %u < %u sub-ranges", count_stride, nh);
@@ -1384,7 +1401,7 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
     ci.sup_log2 = cg.sup_log2;
     BfBinPlan plan;
     const bool binned = (test ? h->shard_test_binned_mode : h->binned_mode) != 0 &&
-                        bf_chunk_plan(h->dev_bytes, cg, nh, nsrc, window_cap, test, &plan, h->chunk_test_l2 != 0) &&
+                        bf_chunk_plan(h->dev_bytes, cg, nh, nsrc, window_cap, test, &plan, sweep) &&
                         ((test ? h->shard_test_binned_mode : h->binned_mode) == 1 ||
                          (h->dev_bytes >= (64ull << 20) &&
                           (double)total * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));

@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
                                                           const uint16_t* __restrict__ tabs, uint64_t max_chunks,
                                                           uint32_t nq, uint32_t rel_log2, uint32_t dense,
                                                           uint32_t* __restrict__ any_flag,
-                                                          uint8_t* __restrict__ dirty) {
+                                                          uint8_t* __restrict__ dirty, uint32_t store_fresh) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
     constexpr uint32_t kPer = kVec / LANES;
     constexpr int kLoads = 8;
@@ -1087,6 +1087,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
             const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
                                 (msk[c].w & ~old[c].w);
             fresh |= fr;
+            if (store_fresh && dense != 2 && !fr) continue;   // every probe hit a set bit: nothing to store
             apply_store(gv + v0 + v, make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z, old[c].w | msk[c].w));
             if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
         }
@@ -1166,9 +1167,12 @@ __device__ __forceinline__ void chunk_run(const BfChunkIn& ci, uint32_t h, uint3
 // sub-range).  One workgroup per (superbin, group), one lane per chunk: coalesced table reads.
 // runs (nullable): window w = sb * nq + q's run table, (exclusive prefix of the run lengths,
 // the run's first receive index) for kRunsPerPass chunks, for chunk_test_l2_kernel.
+// istart (with runs): istart[w * parts + p] = the run holding the first probe of part p of
+// window w (the L2 sweep's items), so an item loads only its own runs.
 __global__ __launch_bounds__(kRunsPerPass) void chunk_group_sum_kernel(BfChunkIn ci, uint32_t nq,
                                                                        uint32_t* __restrict__ gsum,
-                                                                       uint2* __restrict__ runs) {
+                                                                       uint2* __restrict__ runs, uint32_t parts,
+                                                                       uint16_t* __restrict__ istart) {
     __shared__ uint32_t s_w[16];
     const uint32_t sb = blockIdx.x, q = blockIdx.y, t = threadIdx.x;
     const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
@@ -1178,7 +1182,15 @@ __global__ __launch_bounds__(kRunsPerPass) void chunk_group_sum_kernel(BfChunkIn
     uint32_t total;
     const uint32_t ex = block_excl_scan(len, s_w, &total);
     if (t == 0) gsum[sb * nq + q] = total;
-    if (runs) runs[((uint64_t)sb * nq + q) * kRunsPerPass + t] = make_uint2(ex, st);
+    if (runs) {
+        const uint64_t w = (uint64_t)sb * nq + q;
+        runs[w * kRunsPerPass + t] = make_uint2(ex, st);
+        if (len)
+            for (uint32_t p = 0; p < parts; ++p) {
+                const uint32_t f0 = (uint32_t)((uint64_t)total * p / parts);
+                if (f0 >= ex && f0 < ex + len) istart[w * parts + p] = (uint16_t)t;
+            }
+    }
 }
 
 // Owner side of a chunked include? without sorting: the probes of superbin sb stay in their
@@ -1191,11 +1203,13 @@ __global__ __launch_bounds__(kRunsPerPass) void chunk_group_sum_kernel(BfChunkIn
 // outside its superbin or past the shard answers 0.  Every live entry gets an answer.
 constexpr uint32_t kL2Lanes = 256;
 constexpr int kL2Loads = 8;
-constexpr uint32_t kL2Grid = 2048;   // 256 CUs x 8 workgroups of 4 waves: one full residency
+constexpr uint32_t kL2Grid = 1024;   // 256 CUs x 4 workgroups of 4 waves (grid A/B: 256-2048)
+constexpr uint32_t kL2MaxParts = 256;
 __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
                                                                  uint32_t nsup, uint32_t nq, uint32_t parts,
                                                                  const uint32_t* __restrict__ gsum,
                                                                  const uint2* __restrict__ runs,
+                                                                 const uint16_t* __restrict__ istart,
                                                                  uint8_t* __restrict__ out8) {
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
     const uint32_t t = threadIdx.x;
@@ -1208,10 +1222,14 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
         const uint32_t f0 = (uint32_t)((uint64_t)E * part / parts), f1 = (uint32_t)((uint64_t)E * (part + 1) / parts);
         if (f0 >= f1) continue;   // workgroup-uniform
         const uint64_t c0 = (uint64_t)q * kRunsPerPass;
-        const uint32_t nt = (uint32_t)(nch - c0 < kRunsPerPass ? nch - c0 : kRunsPerPass);
+        const uint32_t ntw = (uint32_t)(nch - c0 < kRunsPerPass ? nch - c0 : kRunsPerPass);
+        // only this item's runs: from the run holding f0 to the one holding the next part's f0
+        const uint32_t i0 = istart[(uint64_t)w * parts + part];
+        const uint32_t i1 = part + 1 < parts ? istart[(uint64_t)w * parts + part + 1] : ntw - 1;
+        const uint32_t nt = i1 - i0 + 1;
         __syncthreads();   // the previous item's readers of s_pre / s_gst are done
         for (uint32_t j = t; j < nt; j += kL2Lanes) {
-            const uint2 r = runs[(uint64_t)w * kRunsPerPass + j];
+            const uint2 r = runs[(uint64_t)w * kRunsPerPass + i0 + j];
             s_pre[j] = r.x;
             s_gst[j] = r.y;
         }
@@ -1426,6 +1444,7 @@ struct Carve {
     uint32_t *level1, *level1_key, *level2, *level2_key, *gcnt, *gsum, *base, *cb_base, *cb_window, *cb_start;
     uint16_t *stab, *tabs;
     uint2* runs;   // the chunked L2-local test's window run tables
+    uint16_t* istart;   // ... and the first run of each of its items
     uint32_t* stot;   // hierarchical scan: per-superbin totals
     uint64_t bytes;
 };
@@ -1451,6 +1470,7 @@ Carve carve(const BfBinPlan& p, void* at0) {
     c.stot = reinterpret_cast<uint32_t*>(take(2 * kMaxSup * 4));
     if (p.l2test) {   // sorts nothing: the window run tables only
         c.runs = reinterpret_cast<uint2*>(take(N * kRunsPerPass * sizeof(uint2)));
+        c.istart = reinterpret_cast<uint16_t*>(take(N * kL2MaxParts * sizeof(uint16_t)));
         c.bytes = off;
         return c;
     }
@@ -1628,6 +1648,17 @@ bool bf_binned_plan_offsets(uint64_t bitset_bytes, uint64_t count, uint32_t pref
 
 namespace {
 
+// Below the whole-region density, store only the vectors that gain a bit instead of every
+// touched one: 10B@0.01 % step 6.27 ms against 6.43 (profiles/r03m_apply_fresh.jsonl).
+// BFHIP_APPLY_FRESH=0 stores every touched vector (A/B only)
+uint32_t apply_store_fresh() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("BFHIP_APPLY_FRESH");
+        return (uint32_t)!(e && e[0] == '0');
+    }();
+    return v;
+}
+
 hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes,
                         uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
     const uint64_t nwords = bitset_bytes / 4;
@@ -1640,15 +1671,15 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
-                           p.rel_log2, dense, any_flag, g.dirty);
+                           p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
     else if (p.region_log2 == 19)
         hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag, g.dirty);
+                           any_flag, g.dirty, apply_store_fresh());
     else
         hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag, g.dirty);
+                           any_flag, g.dirty, apply_store_fresh());
     bf_mark(mk, s, "bin_apply");
     return hipGetLastError();
 }
@@ -1947,7 +1978,7 @@ namespace {
 hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn& ci, uint8_t* out8, hipStream_t s,
                             BfMarks* mk) {
     hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
-                       c.gsum, (uint2*)nullptr);
+                       c.gsum, (uint2*)nullptr, 0u, (uint16_t*)nullptr);
     launch_scan(p, c, s);
     bf_mark(mk, s, "chunk_group");
     if (p.with_keys)
@@ -1979,18 +2010,18 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
     if (!p.chunked || !p.with_keys || !out8) return hipErrorInvalidValue;
     const Carve c = carve(p, scratch);
     if (p.l2test) {   // no sort: a superbin-major sweep, probes in receive order, answers stored in place
-        hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
-                           c.gsum, c.runs);
-        bf_mark(mk, s, "chunk_group");
         // >= grid items per superbin, so the whole grid sweeps one superbin at a time
         static const uint32_t grid = [] {
             const char* e = std::getenv("BFHIP_L2_GRID");   // A/B: resident workgroups of the sweep
             const int v = e ? std::atoi(e) : (int)kL2Grid;
             return (uint32_t)(v >= 64 && v <= 8192 ? v : (int)kL2Grid);
         }();
-        const uint32_t parts = (grid + p.ngroups - 1) / p.ngroups;
+        const uint32_t parts = std::min<uint32_t>((grid + p.ngroups - 1) / p.ngroups, kL2MaxParts);
+        hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
+                           c.gsum, c.runs, parts, c.istart);
+        bf_mark(mk, s, "chunk_group");
         hipLaunchKernelGGL(chunk_test_l2_kernel, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup, p.ngroups,
-                           parts, c.gsum, c.runs, out8);
+                           parts, c.gsum, c.runs, c.istart, out8);
         bf_mark(mk, s, "test_l2");
         return hipGetLastError();
     }
