@@ -75,6 +75,7 @@ constexpr uint32_t kRunsPerPass = 1024;       // run-table entries per gather pa
 constexpr uint32_t kMidBuckets = 128;         // bin_mid sort buckets per block (>= regions per superbin)
 constexpr uint32_t kMidParts = 2;             // bin_mid workgroups per level-2 window (1 and 4: same time)
 constexpr uint32_t kApplyLanes = 1024;
+constexpr uint32_t kPipeLanes = 1024;         // bin_apply_pipe_kernel: one workgroup per CU
 
 // Exclusive prefix sum of v over the workgroup (blockDim.x a multiple of 64,
 // at most 1024 lanes); *total gets the workgroup sum.  s_w: 16 words of LDS.
@@ -982,8 +983,9 @@ __device__ __forceinline__ void for_region_probes(const uint32_t* __restrict__ c
     const uint32_t sb = r >> rel_log2, rl = r & (R - 1u);
     const uint32_t t = threadIdx.x, lanes = blockDim.x;
     const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
-    for (uint32_t p0 = bb0; p0 < bb1; p0 += kRunsPerPass) {
-        const uint32_t nt = (bb1 - p0 < kRunsPerPass) ? bb1 - p0 : kRunsPerPass;
+    const uint32_t pass = lanes < kRunsPerPass ? lanes : kRunsPerPass;   // one run-table entry per lane
+    for (uint32_t p0 = bb0; p0 < bb1; p0 += pass) {
+        const uint32_t nt = (bb1 - p0 < pass) ? bb1 - p0 : pass;
         uint32_t len = 0, st = 0;
         if (t < nt) {   // consecutive lanes, consecutive blocks: coalesced
             const uint32_t a = tabs[(uint64_t)rl * max_chunks + p0 + t];
@@ -1091,6 +1093,314 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
             apply_store(gv + v0 + v, make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z, old[c].w | msk[c].w));
             if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
         }
+    }
+    if (any_flag) report_any_new(any_flag, fresh != 0);
+}
+
+// bin_apply for dense batches (every region read whole), persistent and software-pipelined.
+// bin_apply's workgroup waits out three dependent memory round trips per region (its vectors
+// and run table, then the level-2 probes, then its stores) with two regions per CU in flight
+// (the LDS image), so the 10B / 200B apply streamed at ~3.9 TB/s.  Here each workgroup walks
+// regions r = blockIdx.x + i * G and keeps a three-stage pipeline in registers: while it ORs
+// region r's probes into the LDS image and writes r back, the vectors and the first level-2
+// step of r + G and the run table of r + 2G are already in flight.  An iteration then waits
+// only for loads issued one iteration earlier.  The prefetch loads are unconditional (clamped
+// addresses; past the last region a workgroup reloads its last one), so the compiler's
+// in-order vmcnt waits for older values leave the younger prefetches outstanding.  Two LDS
+// run-table buffers alternate between r and r + G, the register buffers by unrolling the
+// region loop twice (a register copy would wait for the stores just issued).
+constexpr int kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+template <uint32_t RLOG2, uint32_t LANES>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) void bin_apply_pipe_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
+                                                               uint32_t nbins, const uint32_t* __restrict__ level2,
+                                                               const uint32_t* __restrict__ cb_base,
+                                                               const uint32_t* __restrict__ cb_start,
+                                                               const uint16_t* __restrict__ tabs, uint64_t max_chunks,
+                                                               uint32_t nq, uint32_t rel_log2, uint32_t dense,
+                                                               uint32_t* __restrict__ any_flag,
+                                                               uint8_t* __restrict__ dirty, uint32_t store_fresh) {
+    constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
+    constexpr uint32_t kPer = kVec / LANES;
+    constexpr int kLoads = 8;
+    constexpr uint32_t kPass = LANES < kRunsPerPass ? LANES : kRunsPerPass;   // run-table entries per pass
+    static_assert(kPer * LANES == kVec, "region must tile the workgroup");
+    __shared__ uint4 s_mask4[kVec];
+    __shared__ uint32_t s_pre[2][kPass], s_gst[2][kPass], s_w[16];
+    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
+    const uint32_t t = threadIdx.x;
+    const uint32_t R = 1u << rel_log2;
+    const uint64_t nvec = nwords / 4;
+    uint4* gv = reinterpret_cast<uint4*>(bits);
+    const uint32_t G = gridDim.x;
+    const uint32_t span = kLoads * 64u, step = span * (LANES >> 6);
+    if (blockIdx.x >= nbins) return;   // workgroup-uniform
+    const uint32_t last = blockIdx.x + (nbins - 1 - blockIdx.x) / G * G;   // this workgroup's last region
+    auto clampr = [&](uint32_t q) { return q < last ? q : last; };
+
+    // The run-table row of region q for its first pass (lane t: chunk block bb0 + t).
+    struct Tab { uint32_t a, b, cs; };
+    auto load_tab = [&](uint32_t q) {
+        const uint32_t sb = q >> rel_log2, rl = q & (R - 1u);
+        const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
+        const uint32_t nt = bb1 - bb0;
+        const uint64_t j = nt ? bb0 + (t < nt ? t : nt - 1u) : 0u;
+        Tab x;
+        x.a = tabs[(uint64_t)rl * max_chunks + j];
+        x.b = tabs[(uint64_t)(rl + 1) * max_chunks + j];
+        x.cs = cb_start[j];
+        return x;
+    };
+    // Scans a run-table pass into LDS buffer bi; returns the pass's probe count (uniform).
+    // Contains barriers.
+    auto scan = [&](uint32_t nt, uint32_t len, uint32_t st, uint32_t bi) {
+        uint32_t E;
+        const uint32_t ex = block_excl_scan(t < nt ? len : 0u, s_w, &E);
+        if (t < nt) {
+            s_pre[bi][t] = ex;
+            s_gst[bi][t] = st;
+        }
+        __syncthreads();
+        return E;
+    };
+    auto pass_nt = [&](uint32_t q) {
+        const uint32_t sb = q >> rel_log2;
+        const uint32_t n = cb_base[(sb + 1) * nq] - cb_base[sb * nq];
+        return n < kPass ? n : kPass;
+    };
+    // Level-2 values of step fb of the pass in buffer bi.  Every load issues (entry 0 stands in
+    // past the pass's E probes), so the number of loads in flight is static; mark() skips them.
+    auto load_l2 = [&](uint32_t bi, uint32_t nt, uint32_t E, uint32_t fb, uint32_t* l) {
+        const uint32_t fw = fb + (t >> 6) * span;
+        uint32_t i = (nt && fw < E) ? run_of(s_pre[bi], nt, fw) : 0u;
+#pragma unroll
+        for (int c = 0; c < kLoads; ++c) {
+            const uint32_t f = fw + c * 64 + (t & 63u);
+            uint32_t idx = 0;
+            if (f < E) {
+                while (i + 1 < nt && s_pre[bi][i + 1] <= f) ++i;
+                idx = s_gst[bi][i] + (f - s_pre[bi][i]);
+            }
+            l[c] = level2[idx];
+        }
+    };
+    auto mark = [&](const uint32_t* l, uint32_t E, uint32_t fb) {
+        const uint32_t fw = fb + (t >> 6) * span;
+#pragma unroll
+        for (int c = 0; c < kLoads; ++c)
+            if (fw + c * 64 + (t & 63u) < E) atomicOr(s_mask + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
+    };
+    auto load_vecs = [&](uint32_t q, uint4* vo) {
+        const uint64_t v0 = (uint64_t)q * kVec;
+#pragma unroll
+        for (uint32_t c = 0; c < kPer; ++c) {
+            const uint64_t v = v0 + c * LANES + t;
+            vo[c] = apply_load(gv + (v < nvec ? v : nvec - 1));
+        }
+    };
+
+    uint32_t fresh = 0;
+    // Region r: its vectors (cur), first level-2 step (lv), first-pass table (LDS buffer bi,
+    // E probes over nt blocks) are in flight or ready; r + G's run-table row (tn) is in flight.
+    // Issues r + G's step / vectors into (nlv, nxt), r + 2G's row into tnn, and returns r + G's E.
+    auto region = [&](uint32_t r, uint32_t bi, uint32_t nt, uint32_t E, const uint4* cur, const uint32_t* lv,
+                      const Tab& tn, uint4* nxt, uint32_t* nlv, Tab& tnn, uint32_t& ntn) {
+        const uint32_t rn = clampr(r + G);
+        // stage 1: r + G's table -> LDS buffer bi ^ 1 (its row was issued an iteration ago)
+        ntn = pass_nt(rn);
+        const uint32_t En = scan(ntn, tn.b - tn.a, tn.cs + tn.a, bi ^ 1u);
+        // stage 2: issue r + 2G's row, r + G's first level-2 step and its vectors
+        tnn = load_tab(clampr(r + 2 * G));
+        load_l2(bi ^ 1u, ntn, En, 0, nlv);
+        load_vecs(rn, nxt);
+        // stage 3: r's probes into the image (lv waited: issued before everything above)
+        mark(lv, E, 0);
+        // The rare paths below end each trip with vmcnt(0) (they wait for their loads anyway), so
+        // at their exits the compiler's wait state is the main path's: no full wait joins it.
+        for (uint32_t fb = step; fb < E; fb += step) {   // regions of more than one step
+            uint32_t l[kLoads];
+            load_l2(bi, nt, E, fb, l);
+            mark(l, E, fb);
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        }
+        const uint32_t sb = r >> rel_log2, rl = r & (R - 1u);
+        const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
+        for (uint32_t p0 = bb0 + kPass; p0 < bb1; p0 += kPass) {   // superbins of more than kPass blocks
+            const uint32_t pn = (bb1 - p0 < kPass) ? bb1 - p0 : kPass;
+            uint32_t len = 0, st = 0;
+            if (t < pn) {
+                const uint32_t a = tabs[(uint64_t)rl * max_chunks + p0 + t];
+                len = tabs[(uint64_t)(rl + 1) * max_chunks + p0 + t] - a;
+                st = cb_start[p0 + t] + a;
+            }
+            __syncthreads();   // every lane is past its reads of buffer bi
+            const uint32_t Ep = scan(pn, len, st, bi);
+            for (uint32_t fb = 0; fb < Ep; fb += step) {
+                uint32_t l[kLoads];
+                load_l2(bi, pn, Ep, fb, l);
+                mark(l, Ep, fb);
+            }
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        }
+        __syncthreads();   // the image is complete
+        // OR the image into the region; each lane then zeroes the mask vectors it read
+        const uint64_t v0 = (uint64_t)r * kVec;
+#pragma unroll
+        for (uint32_t c = 0; c < kPer; ++c) {
+            const uint32_t v = c * LANES + t;
+            const uint4 m = s_mask4[v];
+            s_mask4[v] = make_uint4(0, 0, 0, 0);
+            if (v0 + v < nvec && (dense == 2 || (m.x | m.y | m.z | m.w))) {
+                const uint32_t fr = (m.x & ~cur[c].x) | (m.y & ~cur[c].y) | (m.z & ~cur[c].z) | (m.w & ~cur[c].w);
+                fresh |= fr;
+                if (store_fresh && dense != 2 && !fr) continue;   // every probe hit a set bit: nothing to store
+                apply_store(gv + v0 + v, make_uint4(cur[c].x | m.x, cur[c].y | m.y, cur[c].z | m.z, cur[c].w | m.w));
+                if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
+            }
+        }
+        return En;
+    };
+
+    // prologue: region blockIdx.x's table, first step and vectors; the next region's row
+    uint32_t r = blockIdx.x;
+    for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
+    uint4 bufA[kPer], bufB[kPer];
+    uint32_t lA[kLoads], lB[kLoads];
+    Tab tA, tB;
+    uint32_t ntA, ntB, EA, EB;
+    {
+        const Tab t0 = load_tab(r);
+        ntA = pass_nt(r);
+        EA = scan(ntA, t0.b - t0.a, t0.cs + t0.a, 0u);
+        tA = load_tab(clampr(r + G));
+        load_l2(0u, ntA, EA, 0, lA);
+        load_vecs(r, bufA);
+    }
+    for (;; r += 2 * G) {
+        EB = region(r, 0u, ntA, EA, bufA, lA, tA, bufB, lB, tB, ntB);
+        if (r + G >= nbins) break;
+        EA = region(r + G, 1u, ntB, EB, bufB, lB, tB, bufA, lA, tA, ntA);
+        if (r + 2 * G >= nbins) break;
+    }
+    if (any_flag) report_any_new(any_flag, fresh != 0);
+}
+
+// bin_apply for dense batches, persistent with the run table one region ahead: two workgroups
+// per CU walk regions r = blockIdx.x + i * G.  An iteration issues r's vectors, scans r's run
+// table (its row was loaded an iteration earlier), issues r + G's row and r's level-2 loads,
+// then ORs and stores: one dependent round trip per region (vectors and level-2 loads in
+// flight together), where bin_apply waits out three (row, level 2, stores before exit).
+template <uint32_t RLOG2, uint32_t LANES>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) void bin_apply_tab_kernel(
+    uint32_t* __restrict__ bits, uint64_t nwords, uint32_t nbins, const uint32_t* __restrict__ level2,
+    const uint32_t* __restrict__ cb_base, const uint32_t* __restrict__ cb_start, const uint16_t* __restrict__ tabs,
+    uint64_t max_chunks, uint32_t nq, uint32_t rel_log2, uint32_t dense, uint32_t* __restrict__ any_flag,
+    uint8_t* __restrict__ dirty, uint32_t store_fresh) {
+    constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
+    constexpr uint32_t kPer = kVec / LANES;
+    constexpr int kLoads = 8;
+    constexpr uint32_t kPass = LANES < kRunsPerPass ? LANES : kRunsPerPass;   // run-table entries per pass
+    static_assert(kPer * LANES == kVec, "region must tile the workgroup");
+    __shared__ uint4 s_mask4[kVec];
+    __shared__ uint32_t s_pre[kPass], s_gst[kPass], s_w[16];
+    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
+    const uint32_t t = threadIdx.x;
+    const uint32_t R = 1u << rel_log2;
+    const uint64_t nvec = nwords / 4;
+    uint4* gv = reinterpret_cast<uint4*>(bits);
+    const uint32_t G = gridDim.x;
+    const uint32_t span = kLoads * 64u, step = span * (LANES >> 6);
+    if (blockIdx.x >= nbins) return;   // workgroup-uniform
+    const uint32_t last = blockIdx.x + (nbins - 1 - blockIdx.x) / G * G;
+
+    auto load_row = [&](uint32_t q, uint32_t& len, uint32_t& st) {   // first-pass row of region q
+        const uint32_t sb = q >> rel_log2, rl = q & (R - 1u);
+        const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
+        const uint32_t nt = bb1 - bb0;
+        const uint64_t j = nt ? bb0 + (t < nt ? t : nt - 1u) : 0u;
+        const uint32_t a = tabs[(uint64_t)rl * max_chunks + j];
+        const uint32_t b = tabs[(uint64_t)(rl + 1) * max_chunks + j];
+        const uint32_t cs = cb_start[j];
+        return [=, &len, &st]() { len = b - a; st = cs + a; };   // run once the loads are needed
+    };
+    auto scan = [&](uint32_t nt, uint32_t len, uint32_t st) {
+        uint32_t E;
+        const uint32_t ex = block_excl_scan(t < nt ? len : 0u, s_w, &E);
+        if (t < nt) {
+            s_pre[t] = ex;
+            s_gst[t] = st;
+        }
+        __syncthreads();
+        return E;
+    };
+    auto steps = [&](uint32_t nt, uint32_t E) {   // every probe of the pass into the image
+        for (uint32_t fb = 0; fb < E; fb += step) {
+            const uint32_t fw = fb + (t >> 6) * span;
+            uint32_t i = (nt && fw < E) ? run_of(s_pre, nt, fw) : 0u;
+            uint32_t l[kLoads];
+#pragma unroll
+            for (int c = 0; c < kLoads; ++c) {
+                const uint32_t f = fw + c * 64 + (t & 63u);
+                uint32_t idx = 0xFFFFFFFFu;
+                if (f < E) {
+                    while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
+                    idx = s_gst[i] + (f - s_pre[i]);
+                }
+                l[c] = idx != 0xFFFFFFFFu ? level2[idx] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int c = 0; c < kLoads; ++c)
+                if (l[c] != 0xFFFFFFFFu) atomicOr(s_mask + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
+        }
+    };
+
+    for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
+    uint32_t clen, cst;
+    load_row(blockIdx.x, clen, cst)();
+    uint32_t fresh = 0;
+    for (uint32_t r = blockIdx.x;; r += G) {
+        const uint64_t v0 = (uint64_t)r * kVec;
+        uint4 cur[kPer];
+#pragma unroll
+        for (uint32_t c = 0; c < kPer; ++c) {
+            const uint64_t v = v0 + c * LANES + t;
+            cur[c] = apply_load(gv + (v < nvec ? v : nvec - 1));
+        }
+        const uint32_t sb = r >> rel_log2, rl = r & (R - 1u);
+        const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
+        const uint32_t nt = (bb1 - bb0 < kPass) ? bb1 - bb0 : kPass;
+        const uint32_t E = scan(nt, clen, cst);
+        uint32_t nlen, nst;
+        auto finish_row = load_row(r + G <= last ? r + G : last, nlen, nst);
+        steps(nt, E);
+        finish_row();   // the row's loads preceded the level-2 loads just waited for
+        clen = nlen;
+        cst = nst;
+        for (uint32_t p0 = bb0 + kPass; p0 < bb1; p0 += kPass) {   // superbins of more than kPass blocks
+            const uint32_t pn = (bb1 - p0 < kPass) ? bb1 - p0 : kPass;
+            uint32_t len = 0, st = 0;
+            if (t < pn) {
+                const uint32_t a = tabs[(uint64_t)rl * max_chunks + p0 + t];
+                len = tabs[(uint64_t)(rl + 1) * max_chunks + p0 + t] - a;
+                st = cb_start[p0 + t] + a;
+            }
+            __syncthreads();   // every lane is past its reads of the table
+            steps(pn, scan(pn, len, st));
+        }
+        __syncthreads();   // the image is complete
+#pragma unroll
+        for (uint32_t c = 0; c < kPer; ++c) {
+            const uint32_t v = c * LANES + t;
+            const uint4 m = s_mask4[v];
+            s_mask4[v] = make_uint4(0, 0, 0, 0);
+            if (v0 + v < nvec && (dense == 2 || (m.x | m.y | m.z | m.w))) {
+                const uint32_t fr = (m.x & ~cur[c].x) | (m.y & ~cur[c].y) | (m.z & ~cur[c].z) | (m.w & ~cur[c].w);
+                fresh |= fr;
+                if (store_fresh && dense != 2 && !fr) continue;   // every probe hit a set bit: nothing to store
+                apply_store(gv + v0 + v, make_uint4(cur[c].x | m.x, cur[c].y | m.y, cur[c].z | m.z, cur[c].w | m.w));
+                if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
+            }
+        }
+        if (r == last) break;
     }
     if (any_flag) report_any_new(any_flag, fresh != 0);
 }
@@ -1659,6 +1969,31 @@ uint32_t apply_store_fresh() {
     return v;
 }
 
+// Workgroups of the persistent dense apply (bin_apply_pipe_kernel): one per CU (an LDS image
+// plus two run-table buffers; 4 waves per SIMD for its register pipeline).  BFHIP_APPLY_PIPE_GRID=n overrides it; 0 takes bin_apply_kernel (A/B).
+uint32_t apply_pipe_grid() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("BFHIP_APPLY_PIPE_GRID");
+        if (e && e[0]) return (uint32_t)std::strtoul(e, nullptr, 10);
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (uint32_t)cus;
+    }();
+    return v;
+}
+
+// Dense apply form: 1 bin_apply_pipe_kernel, 2 bin_apply_tab_kernel, 0 bin_apply_kernel
+// (BFHIP_APPLY_FORM, A/B)
+uint32_t apply_form() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("BFHIP_APPLY_FORM");
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
+    return v;
+}
+
 hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes,
                         uint32_t* any_flag, hipStream_t s, BfMarks* mk) {
     const uint64_t nwords = bitset_bytes / 4;
@@ -1668,7 +2003,17 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     // ms) and 10B@0.01 % (4 / line, 1: 2.81 -> 2.65 ms; writing whole lines there: 2.81)
     const uint64_t vecs = (uint64_t)p.nbins << (p.region_log2 - 7);
     const uint32_t dense = p.probes >= vecs ? 2u : (p.probes >= vecs / 8 ? 1u : 0u);
-    if (p.region_log2 == 18)
+    const uint32_t pg = apply_pipe_grid();
+    const uint32_t form = apply_form();
+    if (dense && pg && p.region_log2 == 19 && form == 1) {   // 2^20-bit regions: one image per CU, not pipelined
+        hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes>), dim3(std::min<uint32_t>(p.nbins, pg)),
+                           dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
+                           p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
+    } else if (dense && pg && p.region_log2 == 19 && form == 2) {
+        hipLaunchKernelGGL((bin_apply_tab_kernel<19, kApplyLanes / 2>), dim3(std::min<uint32_t>(p.nbins, 2 * pg)),
+                           dim3(kApplyLanes / 2), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
+                           p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
+    } else if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
                            p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());

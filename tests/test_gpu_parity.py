@@ -295,10 +295,11 @@ def test_device_api_torch(pkg, oracle):
 
 @pytest.mark.parametrize("mode", ["0", "1"])
 @pytest.mark.parametrize("m,k,n", [(95851, 6, 20_000), (9585058, 6, 300_000), (1437758757, 10, 200_000),
-                                   (2**32 + 17, 7, 100_000)])
+                                   (2**32 + 17, 7, 100_000), (95851, 6, 1_500_000)])
 def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
     """BFHIP_INSERT_BINNED / BFHIP_INCLUDE_BINNED = 1 force the binned (front/mid/apply|test)
-    insert and include?; 0 the direct kernels."""
+    insert and include?; 0 the direct kernels.  1.5M keys into one region: a superbin of more
+    than one run-table pass (> 1024 chunk blocks) and a region of many probe steps."""
     monkeypatch.setenv("BFHIP_INSERT_BINNED", mode)
     monkeypatch.setenv("BFHIP_INCLUDE_BINNED", mode)
     rng = np.random.default_rng(RNG_SEED + 7)
