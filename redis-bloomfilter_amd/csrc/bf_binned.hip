@@ -1985,13 +1985,16 @@ uint32_t apply_pipe_grid() {
 }
 
 // Dense apply form: 1 bin_apply_pipe_kernel, 2 bin_apply_tab_kernel, 0 bin_apply_kernel
-// (BFHIP_APPLY_FORM, A/B)
-uint32_t apply_form() {
+// (BFHIP_APPLY_FORM, A/B).  By default a batch dense enough to rewrite whole regions (dense 2,
+// the north-star step: 0.52 -> 0.474 ms) takes the pipelined form; a line-dense one (the 10B
+// step, ~4 probes per line) keeps bin_apply (2.40 ms against 2.97 pipelined at one workgroup
+// per CU: profiles/r03p_apply_pipe.jsonl).
+uint32_t apply_form(uint32_t dense) {
     static const uint32_t v = [] {
         const char* e = std::getenv("BFHIP_APPLY_FORM");
-        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 255u;
     }();
-    return v;
+    return v != 255u ? v : (dense == 2 ? 1u : 0u);
 }
 
 hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uint64_t bitset_bytes,
@@ -2004,7 +2007,7 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     const uint64_t vecs = (uint64_t)p.nbins << (p.region_log2 - 7);
     const uint32_t dense = p.probes >= vecs ? 2u : (p.probes >= vecs / 8 ? 1u : 0u);
     const uint32_t pg = apply_pipe_grid();
-    const uint32_t form = apply_form();
+    const uint32_t form = apply_form(dense);
     if (dense && pg && p.region_log2 == 19 && form == 1) {   // 2^20-bit regions: one image per CU, not pipelined
         hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes>), dim3(std::min<uint32_t>(p.nbins, pg)),
                            dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
