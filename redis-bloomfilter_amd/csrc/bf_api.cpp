@@ -127,7 +127,8 @@ struct Slot {
     uint8_t*  d_out = nullptr;
     uint64_t  cap_bytes = 0, cap_keys = 0, out_cap = 0;
     hipEvent_t h2d = nullptr;      // the chunk's inputs are on the device (copy stream)
-    hipEvent_t done = nullptr;     // the chunk's kernels and result copy are done (compute stream)
+    hipEvent_t done = nullptr;     // the chunk's kernels and result copy are done
+    hipEvent_t op = nullptr;       // the chunk's kernels are done (compute stream; its D2H waits for it)
     // pending result copy-out
     bool      busy = false;
     uint8_t*  user_out = nullptr;
@@ -174,6 +175,7 @@ struct bf_handle {
     Slot slot[kSlots];
     bool staging_ready = false;
     hipStream_t copy_stream = nullptr;      // H2D of the host-pointer pipeline
+    hipStream_t d2h_stream = nullptr;       // ... and its result copies (PCIe is full duplex)
     HostPool pool;
     uint32_t* d_flag = nullptr;
     unsigned long long* d_scan = nullptr;
@@ -297,6 +299,7 @@ int free_staging(bf_handle* h) {
         if (s.d_out) (void)hipFree(s.d_out);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.h2d) (void)hipEventDestroy(s.h2d);
+        if (s.op) (void)hipEventDestroy(s.op);
         s = Slot{};
     }
     h->staging_ready = false;
@@ -323,6 +326,7 @@ int ensure_staging(bf_handle* h, uint64_t keys, uint64_t bytes, uint64_t out_byt
                    co = std::max(want_out, cur.out_cap);
     free_staging(h);
     if (!h->copy_stream) HIPCHK(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    if (!h->d2h_stream) HIPCHK(h, hipStreamCreateWithFlags(&h->d2h_stream, hipStreamNonBlocking));
     for (Slot& s : h->slot) {
         HIPCHK(h, hipHostMalloc((void**)&s.h_keys, cb + 16, hipHostMallocDefault));
         HIPCHK(h, hipHostMalloc((void**)&s.h_off, (ck + 1) * sizeof(uint32_t), hipHostMallocDefault));
@@ -333,6 +337,7 @@ int ensure_staging(bf_handle* h, uint64_t keys, uint64_t bytes, uint64_t out_byt
         HIPCHK(h, hipMalloc((void**)&s.d_out, co));
         HIPCHK(h, hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming));
         HIPCHK(h, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIPCHK(h, hipEventCreateWithFlags(&s.op, hipEventDisableTiming));
         s.cap_keys = ck;
         s.cap_bytes = cb;
         s.out_cap = co;
@@ -670,8 +675,16 @@ int run_host(bf_handle* h, BfOp op, const uint8_t* keys, const uint64_t* offsets
             s.out_bytes = cn * h->k * sizeof(uint64_t);
             s.user_out = reinterpret_cast<uint8_t*>(out64 + i * h->k);
         }
-        if (s.out_bytes) HIPCHK(h, hipMemcpyAsync(s.h_out, s.d_out, s.out_bytes, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipEventRecord(s.done, h->stream));
+        if (s.out_bytes) {
+            // the result copy runs on its own stream, so chunk c + 1's kernels do not queue
+            // behind chunk c's D2H (include?: 1 B per key back while the next keys go in)
+            HIPCHK(h, hipEventRecord(s.op, h->stream));
+            HIPCHK(h, hipStreamWaitEvent(h->d2h_stream, s.op, 0));
+            HIPCHK(h, hipMemcpyAsync(s.h_out, s.d_out, s.out_bytes, hipMemcpyDeviceToHost, h->d2h_stream));
+            HIPCHK(h, hipEventRecord(s.done, h->d2h_stream));
+        } else {
+            HIPCHK(h, hipEventRecord(s.done, h->stream));
+        }
         s.busy = true;
         i = j;
         ++c;
@@ -944,6 +957,7 @@ int bf_destroy(bf_handle* h) {
             for (hipEvent_t e : mk.ev) (void)hipEventDestroy(e);
         if (h->order_ev) (void)hipEventDestroy(h->order_ev);
         if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
+        if (h->d2h_stream) (void)hipStreamDestroy(h->d2h_stream);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
