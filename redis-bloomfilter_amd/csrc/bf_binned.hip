@@ -1085,14 +1085,23 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
 #pragma unroll
     for (uint32_t c = 0; c < kPer; ++c) {
         const uint32_t v = c * LANES + t;
-        if (v0 + v < nvec && (dense == 2 || (msk[c].x | msk[c].y | msk[c].z | msk[c].w))) {
-            const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
-                                (msk[c].w & ~old[c].w);
-            fresh |= fr;
-            if (store_fresh && dense != 2 && !fr) continue;   // every probe hit a set bit: nothing to store
+        // fr: the bits this vector gains (0 for an untouched one: its mask is 0)
+        const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
+                            (msk[c].w & ~old[c].w);
+        // store_fresh 2 (line-dense batches, every vector loaded): a 64-B sector is written whole
+        // when any of its 4 vectors (4 consecutive lanes) gains a bit — whole-sector writes
+        // instead of 32-B partial ones
+        const uint32_t fr4 = fr | __shfl_xor(fr, 1) | __shfl_xor(fr, 2);
+        fresh |= fr;
+        if (v0 + v >= nvec) continue;
+        bool st;
+        if (dense == 2) st = true;
+        else if (store_fresh == 2 && dense == 1) st = fr4 != 0u;
+        else if (store_fresh) st = fr != 0u;   // every probe hit a set bit: nothing to store
+        else st = (msk[c].x | msk[c].y | msk[c].z | msk[c].w) != 0u;
+        if (st)
             apply_store(gv + v0 + v, make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z, old[c].w | msk[c].w));
-            if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
-        }
+        if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
     }
     if (any_flag) report_any_new(any_flag, fresh != 0);
 }
@@ -1284,127 +1293,6 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     if (any_flag) report_any_new(any_flag, fresh != 0);
 }
 
-// bin_apply for dense batches, persistent with the run table one region ahead: two workgroups
-// per CU walk regions r = blockIdx.x + i * G.  An iteration issues r's vectors, scans r's run
-// table (its row was loaded an iteration earlier), issues r + G's row and r's level-2 loads,
-// then ORs and stores: one dependent round trip per region (vectors and level-2 loads in
-// flight together), where bin_apply waits out three (row, level 2, stores before exit).
-template <uint32_t RLOG2, uint32_t LANES>
-__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) void bin_apply_tab_kernel(
-    uint32_t* __restrict__ bits, uint64_t nwords, uint32_t nbins, const uint32_t* __restrict__ level2,
-    const uint32_t* __restrict__ cb_base, const uint32_t* __restrict__ cb_start, const uint16_t* __restrict__ tabs,
-    uint64_t max_chunks, uint32_t nq, uint32_t rel_log2, uint32_t dense, uint32_t* __restrict__ any_flag,
-    uint8_t* __restrict__ dirty, uint32_t store_fresh) {
-    constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
-    constexpr uint32_t kPer = kVec / LANES;
-    constexpr int kLoads = 8;
-    constexpr uint32_t kPass = LANES < kRunsPerPass ? LANES : kRunsPerPass;   // run-table entries per pass
-    static_assert(kPer * LANES == kVec, "region must tile the workgroup");
-    __shared__ uint4 s_mask4[kVec];
-    __shared__ uint32_t s_pre[kPass], s_gst[kPass], s_w[16];
-    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
-    const uint32_t t = threadIdx.x;
-    const uint32_t R = 1u << rel_log2;
-    const uint64_t nvec = nwords / 4;
-    uint4* gv = reinterpret_cast<uint4*>(bits);
-    const uint32_t G = gridDim.x;
-    const uint32_t span = kLoads * 64u, step = span * (LANES >> 6);
-    if (blockIdx.x >= nbins) return;   // workgroup-uniform
-    const uint32_t last = blockIdx.x + (nbins - 1 - blockIdx.x) / G * G;
-
-    auto load_row = [&](uint32_t q, uint32_t& len, uint32_t& st) {   // first-pass row of region q
-        const uint32_t sb = q >> rel_log2, rl = q & (R - 1u);
-        const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
-        const uint32_t nt = bb1 - bb0;
-        const uint64_t j = nt ? bb0 + (t < nt ? t : nt - 1u) : 0u;
-        const uint32_t a = tabs[(uint64_t)rl * max_chunks + j];
-        const uint32_t b = tabs[(uint64_t)(rl + 1) * max_chunks + j];
-        const uint32_t cs = cb_start[j];
-        return [=, &len, &st]() { len = b - a; st = cs + a; };   // run once the loads are needed
-    };
-    auto scan = [&](uint32_t nt, uint32_t len, uint32_t st) {
-        uint32_t E;
-        const uint32_t ex = block_excl_scan(t < nt ? len : 0u, s_w, &E);
-        if (t < nt) {
-            s_pre[t] = ex;
-            s_gst[t] = st;
-        }
-        __syncthreads();
-        return E;
-    };
-    auto steps = [&](uint32_t nt, uint32_t E) {   // every probe of the pass into the image
-        for (uint32_t fb = 0; fb < E; fb += step) {
-            const uint32_t fw = fb + (t >> 6) * span;
-            uint32_t i = (nt && fw < E) ? run_of(s_pre, nt, fw) : 0u;
-            uint32_t l[kLoads];
-#pragma unroll
-            for (int c = 0; c < kLoads; ++c) {
-                const uint32_t f = fw + c * 64 + (t & 63u);
-                uint32_t idx = 0xFFFFFFFFu;
-                if (f < E) {
-                    while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
-                    idx = s_gst[i] + (f - s_pre[i]);
-                }
-                l[c] = idx != 0xFFFFFFFFu ? level2[idx] : 0xFFFFFFFFu;
-            }
-#pragma unroll
-            for (int c = 0; c < kLoads; ++c)
-                if (l[c] != 0xFFFFFFFFu) atomicOr(s_mask + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
-        }
-    };
-
-    for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
-    uint32_t clen, cst;
-    load_row(blockIdx.x, clen, cst)();
-    uint32_t fresh = 0;
-    for (uint32_t r = blockIdx.x;; r += G) {
-        const uint64_t v0 = (uint64_t)r * kVec;
-        uint4 cur[kPer];
-#pragma unroll
-        for (uint32_t c = 0; c < kPer; ++c) {
-            const uint64_t v = v0 + c * LANES + t;
-            cur[c] = apply_load(gv + (v < nvec ? v : nvec - 1));
-        }
-        const uint32_t sb = r >> rel_log2, rl = r & (R - 1u);
-        const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
-        const uint32_t nt = (bb1 - bb0 < kPass) ? bb1 - bb0 : kPass;
-        const uint32_t E = scan(nt, clen, cst);
-        uint32_t nlen, nst;
-        auto finish_row = load_row(r + G <= last ? r + G : last, nlen, nst);
-        steps(nt, E);
-        finish_row();   // the row's loads preceded the level-2 loads just waited for
-        clen = nlen;
-        cst = nst;
-        for (uint32_t p0 = bb0 + kPass; p0 < bb1; p0 += kPass) {   // superbins of more than kPass blocks
-            const uint32_t pn = (bb1 - p0 < kPass) ? bb1 - p0 : kPass;
-            uint32_t len = 0, st = 0;
-            if (t < pn) {
-                const uint32_t a = tabs[(uint64_t)rl * max_chunks + p0 + t];
-                len = tabs[(uint64_t)(rl + 1) * max_chunks + p0 + t] - a;
-                st = cb_start[p0 + t] + a;
-            }
-            __syncthreads();   // every lane is past its reads of the table
-            steps(pn, scan(pn, len, st));
-        }
-        __syncthreads();   // the image is complete
-#pragma unroll
-        for (uint32_t c = 0; c < kPer; ++c) {
-            const uint32_t v = c * LANES + t;
-            const uint4 m = s_mask4[v];
-            s_mask4[v] = make_uint4(0, 0, 0, 0);
-            if (v0 + v < nvec && (dense == 2 || (m.x | m.y | m.z | m.w))) {
-                const uint32_t fr = (m.x & ~cur[c].x) | (m.y & ~cur[c].y) | (m.z & ~cur[c].z) | (m.w & ~cur[c].w);
-                fresh |= fr;
-                if (store_fresh && dense != 2 && !fr) continue;   // every probe hit a set bit: nothing to store
-                apply_store(gv + v0 + v, make_uint4(cur[c].x | m.x, cur[c].y | m.y, cur[c].z | m.z, cur[c].w | m.w));
-                if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
-            }
-        }
-        if (r == last) break;
-    }
-    if (any_flag) report_any_new(any_flag, fresh != 0);
-}
-
 // include?: the region in LDS; a probe on a 0 bit clears its key's answer.  The probe
 // streams and the region are read non-temporally, so that the scattered answer bytes keep
 // their lines in the caches (0.745 -> 0.691 ms at P = 8).
@@ -1422,7 +1310,8 @@ __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restr
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
     const uint32_t* s_bits = reinterpret_cast<const uint32_t*>(s_bits4);
     const uint32_t t = threadIdx.x;
-    const uint64_t v0 = (uint64_t)blockIdx.x * kVec;
+    const uint32_t r = blockIdx.x;
+    const uint64_t v0 = (uint64_t)r * kVec;
     const uint64_t nvec = nwords / 4;
     typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
     const nt_u32x4* gn = reinterpret_cast<const nt_u32x4*>(bits);
@@ -1432,7 +1321,7 @@ __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restr
         s_bits4[v] = make_uint4(x.x, x.y, x.z, x.w);
     }
     __syncthreads();
-    for_region_probes<kLoads>(cb_base, cb_start, tabs, max_chunks, blockIdx.x, nq, rel_log2, s_pre, s_gst, s_w,
+    for_region_probes<kLoads>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
         [&](const uint32_t* idx) {
             uint32_t l[kLoads], key[kLoads];
 #pragma unroll
@@ -1964,7 +1853,7 @@ namespace {
 uint32_t apply_store_fresh() {
     static const uint32_t v = [] {
         const char* e = std::getenv("BFHIP_APPLY_FRESH");
-        return (uint32_t)!(e && e[0] == '0');
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
     }();
     return v;
 }
@@ -1984,11 +1873,11 @@ uint32_t apply_pipe_grid() {
     return v;
 }
 
-// Dense apply form: 1 bin_apply_pipe_kernel, 2 bin_apply_tab_kernel, 0 bin_apply_kernel
-// (BFHIP_APPLY_FORM, A/B).  By default a batch dense enough to rewrite whole regions (dense 2,
+// Dense apply form: 1 bin_apply_pipe_kernel, 0 bin_apply_kernel (BFHIP_APPLY_FORM, A/B).  By default a batch dense enough to rewrite whole regions (dense 2,
 // the north-star step: 0.52 -> 0.474 ms) takes the pipelined form; a line-dense one (the 10B
 // step, ~4 probes per line) keeps bin_apply (2.40 ms against 2.97 pipelined at one workgroup
-// per CU: profiles/r03p_apply_pipe.jsonl).
+// per CU: profiles/r03p_apply_pipe.jsonl; a two-workgroup-per-CU form with only the run table
+// prefetched measured 2.44: the 10B apply is not bound by its dependent round trips).
 uint32_t apply_form(uint32_t dense) {
     static const uint32_t v = [] {
         const char* e = std::getenv("BFHIP_APPLY_FORM");
@@ -2011,10 +1900,6 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     if (dense && pg && p.region_log2 == 19 && form == 1) {   // 2^20-bit regions: one image per CU, not pipelined
         hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes>), dim3(std::min<uint32_t>(p.nbins, pg)),
                            dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
-                           p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
-    } else if (dense && pg && p.region_log2 == 19 && form == 2) {
-        hipLaunchKernelGGL((bin_apply_tab_kernel<19, kApplyLanes / 2>), dim3(std::min<uint32_t>(p.nbins, 2 * pg)),
-                           dim3(kApplyLanes / 2), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
                            p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
     } else if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
