@@ -1088,15 +1088,12 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
         // fr: the bits this vector gains (0 for an untouched one: its mask is 0)
         const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
                             (msk[c].w & ~old[c].w);
-        // store_fresh 2 (line-dense batches, every vector loaded): a 64-B sector is written whole
-        // when any of its 4 vectors (4 consecutive lanes) gains a bit — whole-sector writes
-        // instead of 32-B partial ones
-        const uint32_t fr4 = fr | __shfl_xor(fr, 1) | __shfl_xor(fr, 2);
         fresh |= fr;
         if (v0 + v >= nvec) continue;
+        // (writing whole 64-B sectors when any of their vectors gains a bit, instead of 32-B
+        // partial writes, measured 2.459 vs 2.448 ms at 10B: profiles/r03t_apply_ab.jsonl)
         bool st;
         if (dense == 2) st = true;
-        else if (store_fresh == 2 && dense == 1) st = fr4 != 0u;
         else if (store_fresh) st = fr != 0u;   // every probe hit a set bit: nothing to store
         else st = (msk[c].x | msk[c].y | msk[c].z | msk[c].w) != 0u;
         if (st)
@@ -1853,7 +1850,7 @@ namespace {
 uint32_t apply_store_fresh() {
     static const uint32_t v = [] {
         const char* e = std::getenv("BFHIP_APPLY_FRESH");
-        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+        return (uint32_t)!(e && e[0] == '0');
     }();
     return v;
 }

@@ -13,3 +13,4 @@ for i in 1 2; do
 done
 export BFHIP_APPLY_FRESH=2
 bash tools/pmc_passes.sh 10b r03t_10b wr
+timeout -k 10 180 python tools/cu_mask_probe.py > gpurun_out/cu_mask_${TAG}.jsonl 2> gpurun_out/cu_mask_${TAG}.err || exit 1
