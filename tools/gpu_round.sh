@@ -9,7 +9,7 @@ shift
 STEPS=${*:-tests smoke bench prof pmc}
 for st in $STEPS; do
     case $st in
-        tests) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
                    ${PYTEST_EXTRA:-} > gpurun_out/tests_${TAG}.log 2>&1 ;;
         smoke) timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
         bench) timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
