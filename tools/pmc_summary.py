@@ -29,7 +29,7 @@ KERNELS = {
     "bin_front_digest": re.compile(r"bin_front_kernel<true>"),
     "bin_front_wide": re.compile(r"bin_front_wide_kernel"),
     "bin_mid": re.compile(r"bin_mid_kernel"),
-    "bin_apply": re.compile(r"bin_apply_kernel"),
+    "bin_apply": re.compile(r"bin_apply_(pipe_)?kernel"),
     "bin_test": re.compile(r"bin_test_kernel"),
 }
 FULL_BATCH = ("bf_keys_kernel",)   # grid = one lane per key: keep full-batch launches only

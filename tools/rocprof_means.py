@@ -16,7 +16,7 @@ NAMES = {
     "bin_front_digest": r"bin_front_kernel<true>",
     "bin_front": r"bin_front_kernel<false>",
     "bin_mid": r"bin_mid_kernel",
-    "bin_apply": r"bin_apply_kernel",
+    "bin_apply": r"bin_apply_(pipe_)?kernel",
 }
 
 
