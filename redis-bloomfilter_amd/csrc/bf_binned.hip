@@ -1410,10 +1410,19 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
     const uint32_t t = threadIdx.x;
     const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles;
-    const uint64_t items = (uint64_t)nsup * nq * parts;
-    for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const uint32_t w = (uint32_t)(it / parts), part = (uint32_t)(it - (uint64_t)w * parts);
-        const uint32_t sb = w / nq, q = w - sb * nq;
+    // XCD-local sweep: workgroup b runs on XCD b % 8 (round-robin dispatch; the grid is a
+    // multiple of 8), and XCD x sweeps superbins x, x + 8, ..., its gridDim / 8 workgroups
+    // sharing each superbin's items.  So each XCD's L2 holds one superbin, where a sweep of the
+    // whole grid over one superbin made every XCD fetch the same lines (tools/probe_xcd.hip is
+    // this layout: 178 G probes/s at 4 MiB per XCD).
+    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
+    const uint64_t per_sb = (uint64_t)nq * parts;
+    const uint64_t items = (uint64_t)((nsup + 7u - xcd) >> 3) * per_sb;   // this XCD's superbins
+    for (uint64_t k = blockIdx.x >> 3; k < items; k += g8) {
+        const uint32_t sb = xcd + 8u * (uint32_t)(k / per_sb);
+        const uint64_t kk = k - (uint64_t)(k / per_sb) * per_sb;
+        const uint32_t q = (uint32_t)(kk / parts), part = (uint32_t)(kk - (uint64_t)q * parts);
+        const uint32_t w = sb * nq + q;
         const uint32_t E = gsum[w];
         const uint32_t f0 = (uint32_t)((uint64_t)E * part / parts), f1 = (uint32_t)((uint64_t)E * (part + 1) / parts);
         if (f0 >= f1) continue;   // workgroup-uniform
@@ -1894,7 +1903,9 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     const uint32_t dense = p.probes >= vecs ? 2u : (p.probes >= vecs / 8 ? 1u : 0u);
     const uint32_t pg = apply_pipe_grid();
     const uint32_t form = apply_form(dense);
-    if (dense && pg && p.region_log2 == 19 && form == 1) {   // 2^20-bit regions: one image per CU, not pipelined
+    // the pipeline pays off over many regions per workgroup: a 150 MB shard (2288 regions, 9
+    // per workgroup) measured 0.206 pipelined against 0.164 ms (P = 8 owner insert)
+    if (dense && pg && p.region_log2 == 19 && form == 1 && p.nbins >= 16 * pg) {   // 2^20-bit regions: not pipelined
         hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes>), dim3(std::min<uint32_t>(p.nbins, pg)),
                            dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
                            p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
@@ -2240,13 +2251,14 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
     if (!p.chunked || !p.with_keys || !out8) return hipErrorInvalidValue;
     const Carve c = carve(p, scratch);
     if (p.l2test) {   // no sort: a superbin-major sweep, probes in receive order, answers stored in place
-        // >= grid items per superbin, so the whole grid sweeps one superbin at a time
+        // each XCD sweeps its own superbins, >= grid / 8 items each (chunk_test_l2_kernel)
         static const uint32_t grid = [] {
             const char* e = std::getenv("BFHIP_L2_GRID");   // A/B: resident workgroups of the sweep
             const int v = e ? std::atoi(e) : (int)kL2Grid;
-            return (uint32_t)(v >= 64 && v <= 8192 ? v : (int)kL2Grid);
+            return (uint32_t)(v >= 64 && v <= 8192 ? v : (int)kL2Grid) & ~7u;   // whole XCD groups
         }();
-        const uint32_t parts = std::min<uint32_t>((grid + p.ngroups - 1) / p.ngroups, kL2MaxParts);
+        // each XCD's grid / 8 workgroups share a superbin's items: at least one item each
+        const uint32_t parts = std::min<uint32_t>((grid / 8 + p.ngroups - 1) / p.ngroups, kL2MaxParts);
         hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
                            c.gsum, c.runs, parts, c.istart);
         bf_mark(mk, s, "chunk_group");
