@@ -847,6 +847,32 @@ __global__ __launch_bounds__(kTile) void route_gather_kernel(const uint32_t* __r
     }
 }
 
+// bin_mid's workgroup order.  grouped: workgroup b runs on XCD x = b % 8, and superbin sb's
+// nq * kMidParts workgroups all run on XCD sb % 8 in (group, part) order, so the partial-line
+// stores of its region run table rows (tabs[region][block], one u16 per block) merge in one L2
+// instead of eight (10B: 26.9M -> 16.3M write requests, bin_mid 0.656 -> 0.633 ms).  (Each XCD
+// on one contiguous eighth of the superbins instead: 1.14 ms — the XCDs must sweep the same
+// address neighbourhood, as in bin_apply)  Otherwise b = w * kMidParts + part.
+// Returns sb (>= nsup: a spare workgroup of mid_grid).
+__device__ __forceinline__ uint32_t mid_superbin(uint32_t nsup, uint32_t nq, bool grouped, uint32_t* q,
+                                                 uint32_t* part) {
+    if (!grouped) {
+        const uint32_t w = blockIdx.x / kMidParts;
+        *part = blockIdx.x - w * kMidParts;
+        *q = w % nq;
+        return w / nq;
+    }
+    const uint32_t wpsb = nq * kMidParts, xi = blockIdx.x >> 3;
+    const uint32_t i = xi / wpsb, wq = xi - i * wpsb;
+    *q = wq / kMidParts;
+    *part = wq - *q * kMidParts;
+    return (blockIdx.x & 7u) + 8u * i;
+}
+__host__ __device__ inline bool mid_grouped(uint32_t nsup) { return nsup >= 64; }
+uint32_t mid_grid(uint32_t nsup, uint32_t nq) {
+    return mid_grouped(nsup) ? 8u * ((nsup + 7u) / 8u) * nq * kMidParts : nsup * nq * kMidParts;
+}
+
 // One workgroup per (window, part): window w = (superbin sb, group q)
 // concatenates superbin sb's runs from the group's tiles in tile order; it is
 // cut into chunk blocks of kBlockProbes, and part p of kMidParts takes an equal
@@ -868,8 +894,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ uint32_t s_sorted[kBlockProbes];
     __shared__ uint32_t s_key[KEYS ? kBlockProbes : 1];
     const uint32_t t = threadIdx.x;
-    const uint32_t w = blockIdx.x / kMidParts, part = blockIdx.x - w * kMidParts;
-    const uint32_t sb = w / nq, q = w - sb * nq;
+    uint32_t w_q, w_part;
+    const uint32_t sb = mid_superbin(nsup, nq, mid_grouped(nsup), &w_q, &w_part);   // XCD-grouped
+    if (sb >= nsup) return;   // workgroup-uniform: the grid is rounded up to whole XCD rows
+    const uint32_t q = w_q, part = w_part;
+    const uint32_t w = sb * nq + q;
     const uint32_t wbase = base[w];
     const uint32_t E = base[w + 1] - wbase;
     const uint32_t nblk = (E + kBlockProbes - 1) / kBlockProbes;
@@ -1478,7 +1507,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
 // each probe's position is its index in the receive buffer (no level-1 key array).
 template <bool KEYS>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
+void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
                            const uint32_t* __restrict__ base, const uint32_t* __restrict__ cb_base,
                            uint64_t max_chunks, uint16_t* __restrict__ tabs, uint32_t* __restrict__ level2,
                            uint32_t* __restrict__ level2_key, uint8_t* __restrict__ out8) {
@@ -1488,8 +1517,12 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nq, uint32_t region_log2, uint
     __shared__ uint32_t s_sorted[kBlockProbes];
     __shared__ uint32_t s_key[KEYS ? kBlockProbes : 1];
     const uint32_t t = threadIdx.x;
-    const uint32_t w = blockIdx.x / kMidParts, part = blockIdx.x - w * kMidParts;
-    const uint32_t sb = w / nq, q = w - sb * nq;
+    uint32_t w_q, w_part;
+    // linear order: the owner's few superbins (36 at P = 8) would leave XCDs unevenly loaded
+    // grouped (0.405 vs 0.381 ms)
+    const uint32_t sb = mid_superbin(nsup, nq, false, &w_q, &w_part);
+    const uint32_t q = w_q, part = w_part;
+    const uint32_t w = sb * nq + q;
     const uint32_t wbase = base[w];
     const uint32_t E = base[w + 1] - wbase;
     const uint32_t nblk = (E + kBlockProbes - 1) / kBlockProbes;
@@ -1708,12 +1741,12 @@ hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c
     bf_mark(mk, s, "bin_group");
     const uint32_t tiles_per_group = kGroupBlocks * p.tiles_per_block;
     if (p.with_keys)
-        hipLaunchKernelGGL(bin_mid_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, c.level1,
+        hipLaunchKernelGGL(bin_mid_kernel<true>, dim3(mid_grid(p.nsup, p.ngroups)), dim3(kTile), 0, s, c.level1,
                            c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
     else
-        hipLaunchKernelGGL(bin_mid_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, c.level1,
+        hipLaunchKernelGGL(bin_mid_kernel<false>, dim3(mid_grid(p.nsup, p.ngroups)), dim3(kTile), 0, s, c.level1,
                            c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
@@ -2224,11 +2257,11 @@ hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn&
     bf_mark(mk, s, "chunk_group");
     if (p.with_keys)
         hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
-                           p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key, out8);
     else
         hipLaunchKernelGGL(bin_mid_chunks_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
-                           p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key, out8);
     bf_mark(mk, s, p.with_keys ? "mid_chunks_keys" : "mid_chunks");
     return hipGetLastError();
