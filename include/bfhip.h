@@ -337,7 +337,14 @@ int  bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t
  *                           + i] for the live entries i.
  * bf_combine_chunks_packed_dev  requester: the include? answers from window w's answer bits
  *                           at d_packed + w*ceil(window_cap/8), through this rank's own
- *                           route directory and slots. */
+ *                           route directory and slots.
+ * bf_route_chunks_digests_dev   bf_route_chunks_dev from the keys' SHA-1 words (16-byte
+ *                           aligned uint32[4] per key, as bf_hash_many_dev writes them).
+ * bf_shard_test_chunks_hash_dev bf_shard_test_chunks_dev that also writes the SHA-1 words of
+ *                           another key batch (this rank's next include? batch) to
+ *                           d_next_digests: the owner test is latency-bound, so its waves hash
+ *                           between their probe rounds (ruby.rb:41-47 per key, as
+ *                           bf_hash_many_dev; the next step then routes from the words). */
 int  bf_route_chunk_info(const bf_handle* h, uint64_t n_bound, uint64_t* tiles, uint64_t* dir_bytes,
                          uint32_t* superbins /* nullable: the owner superbins per window */);
 int  bf_route_chunks_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
@@ -353,6 +360,15 @@ int  bf_shard_test_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t win
 int  bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint16_t* d_slot16,
                                   uint64_t window_cap, const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
                                   const uint64_t* d_counts /* nwin */, uint64_t n, uint8_t* d_out, void* stream);
+int  bf_route_chunks_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n,
+                                 uint32_t* d_send, uint16_t* d_slot16 /* nullable */, uint64_t window_cap,
+                                 uint64_t* d_counts, uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
+                                 void* stream);
+int  bf_shard_test_chunks_hash_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                                   const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
+                                   const uint64_t* d_counts, uint32_t count_stride, uint8_t* d_bits,
+                                   const uint8_t* d_next_keys, const uint64_t* d_next_offsets, uint64_t n_next,
+                                   uint32_t* d_next_digests, void* stream);
 int  bf_shard_insert_dev(bf_handle* h, const void* d_local /* uint64 or uint32 (ROUTE32) */, uint64_t count,
                          uint32_t* d_any_new /* nullable */, void* stream);
 int  bf_shard_test_dev(bf_handle* h, const void* d_local, uint64_t count, uint8_t* d_bits,

@@ -114,6 +114,9 @@ SIGNATURES = {
     "bf_route_chunks_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp]),
     "bf_shard_insert_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
     "bf_shard_test_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
+    "bf_route_chunks_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp]),
+    "bf_shard_test_chunks_hash_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp,
+                                                     _vp, _vp, _u64, _vp, _vp]),
     "bf_combine_chunks_packed_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _u64, _vp, _u64, _vp, _vp]),
     "bf_shard_export": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_shard_import": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
@@ -507,6 +510,13 @@ class Filter:
                                              int(window_cap), d_counts, d_dir, int(dir_bytes), int(tiles),
                                              self._s(stream)), self._h)
 
+    def route_chunks_digests_dev(self, d_digests: int, n: int, d_send: int, d_slot16: int, window_cap: int,
+                                 d_counts: int, d_dir: int, dir_bytes: int, tiles: int, stream=None) -> None:
+        """route_chunks_dev from the keys' SHA-1 words (hash_many_dev's output)."""
+        _check(self._lib.bf_route_chunks_digests_dev(self.handle, d_digests, int(n), d_send, d_slot16 or None,
+                                                     int(window_cap), d_counts, d_dir, int(dir_bytes), int(tiles),
+                                                     self._s(stream)), self._h)
+
     def shard_insert_chunks_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int, tiles: int,
                                 d_counts: int, count_stride: int, d_any_new: int = 0, stream=None) -> None:
         _check(self._lib.bf_shard_insert_chunks_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
@@ -518,6 +528,15 @@ class Filter:
         _check(self._lib.bf_shard_test_chunks_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
                                                   int(dir_bytes), int(tiles), d_counts, int(count_stride), d_bits,
                                                   self._s(stream)), self._h)
+
+    def shard_test_chunks_hash_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int,
+                                   tiles: int, d_counts: int, count_stride: int, d_bits: int, d_next_keys: int,
+                                   d_next_offsets: int, n_next: int, d_next_digests: int, stream=None) -> None:
+        """shard_test_chunks_dev that also hashes another key batch (SHA-1 words to d_next_digests)."""
+        _check(self._lib.bf_shard_test_chunks_hash_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
+                                                       int(dir_bytes), int(tiles), d_counts, int(count_stride), d_bits,
+                                                       d_next_keys or None, d_next_offsets or None, int(n_next),
+                                                       d_next_digests or None, self._s(stream)), self._h)
 
     def combine_chunks_packed_dev(self, d_packed: int, d_slot16: int, window_cap: int, d_dir: int, dir_bytes: int,
                                   tiles: int, d_counts: int, n: int, d_out: int, stream=None) -> None:

@@ -1337,13 +1337,17 @@ int bf_route_chunk_info(const bf_handle* h, uint64_t n_bound, uint64_t* tiles, u
     return BF_OK;
 }
 
-int bf_route_chunks_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
-                        uint32_t* d_send, uint16_t* d_slot16, uint64_t window_cap, uint64_t* d_counts, uint8_t* d_dir,
-                        uint64_t dir_bytes, uint64_t tiles, void* stream) {
+namespace {
+// dig: d_key_bytes holds n SHA-1 word quadruples (d_offsets unused).
+int route_chunks_impl(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n, bool dig,
+                      uint32_t* d_send, uint16_t* d_slot16, uint64_t window_cap, uint64_t* d_counts, uint8_t* d_dir,
+                      uint64_t dir_bytes, uint64_t tiles, void* stream) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (!d_counts || !d_dir) return set_err(h, BF_EINVAL, "d_counts / d_dir is NULL");
-    if (n && (!d_key_bytes || !d_offsets || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (n && (!d_key_bytes || (!dig && !d_offsets) || !d_send)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (dig && n && (reinterpret_cast<uintptr_t>(d_key_bytes) & 15u))
+        return set_err(h, BF_EINVAL, "d_digests must be 16-byte aligned");
     const uint64_t probes = n * h->k;
     if (n && probes / n != h->k) return set_err(h, BF_EINVAL, "n*k overflows");
     if (probes >= (1ull << 32)) return set_err(h, BF_EINVAL, "n*k must be < 2^32 per call");
@@ -1373,20 +1377,40 @@ int bf_route_chunks_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
     cg.dir_bytes = dir_bytes;
     cg.tiles = tiles;
     uint64_t bias = 0;
-    const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
+    const uint8_t* k16 = n ? (dig ? d_key_bytes : align_keys(d_key_bytes, &bias)) : nullptr;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_route_chunks(h->g, plan, nh, cg, k16, d_offsets, bias, n, d_send, d_slot16, window_cap,
-                                     reinterpret_cast<unsigned long long*>(d_counts), s, mk));
+                                     reinterpret_cast<unsigned long long*>(d_counts), s, mk, dig));
     return BF_OK;
+}
+}  // namespace
+
+int bf_route_chunks_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                        uint32_t* d_send, uint16_t* d_slot16, uint64_t window_cap, uint64_t* d_counts, uint8_t* d_dir,
+                        uint64_t dir_bytes, uint64_t tiles, void* stream) {
+    return route_chunks_impl(h, d_key_bytes, d_offsets, n, false, d_send, d_slot16, window_cap, d_counts, d_dir,
+                             dir_bytes, tiles, stream);
+}
+
+int bf_route_chunks_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint32_t* d_send,
+                                uint16_t* d_slot16, uint64_t window_cap, uint64_t* d_counts, uint8_t* d_dir,
+                                uint64_t dir_bytes, uint64_t tiles, void* stream) {
+    return route_chunks_impl(h, reinterpret_cast<const uint8_t*>(d_digests), nullptr, n, true, d_send, d_slot16,
+                             window_cap, d_counts, d_dir, dir_bytes, tiles, stream);
 }
 
 namespace {
+// side (test only): a key batch [keys, offsets, n) whose SHA-1 words go to side_dig (nullable).
 static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc, const uint8_t* d_dir,
                       uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts, uint32_t count_stride,
-                      uint32_t* d_any_new, uint8_t* d_bits, bool test, void* stream) {
+                      uint32_t* d_any_new, uint8_t* d_bits, bool test, void* stream,
+                      const uint8_t* side_keys = nullptr, const uint64_t* side_offsets = nullptr, uint64_t side_n = 0,
+                      uint32_t* side_dig = nullptr) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
-    if (!nsrc || !window_cap) return BF_OK;
+    if (side_n && (!side_keys || !side_offsets || !side_dig)) return set_err(h, BF_EINVAL, "NULL side-hash pointer");
+    if (!nsrc || !window_cap)
+        return side_n ? bf_hash_many_dev(h, side_keys, side_offsets, side_n, side_dig, stream) : BF_OK;
     if (!d_recv || !d_dir || !d_counts || (test && !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
     BfChunks cg;
     uint32_t nh = 1;
@@ -1428,7 +1452,7 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
                       : bf_shard_insert_windows_dev(h, rw, window_cap, nsrc, cw, count_stride, hi, d_any_new, stream);
             if (rc) return rc;
         }
-        return BF_OK;
+        return side_n ? bf_hash_many_dev(h, side_keys, side_offsets, side_n, side_dig, stream) : BF_OK;
     }
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
@@ -1437,8 +1461,15 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
     hipStream_t s = so.s;
     if ((rc = ensure_scratch(h, plan.scratch_bytes))) return rc;
     BfMarks* mk = prof_begin(h, s);
+    BfSideHash side;
+    if (side_n) {
+        side.keys16 = align_keys(side_keys, &side.bias);
+        side.offsets = side_offsets;
+        side.n = side_n;
+        side.dig = reinterpret_cast<uint4*>(side_dig);
+    }
     if (test)
-        HIPCHK(h, bf_launch_shard_test_chunks(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_bits, s, mk));
+        HIPCHK(h, bf_launch_shard_test_chunks(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_bits, s, mk, side));
     else
         HIPCHK(h, bf_launch_shard_insert_chunks(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_any_new, s, mk));
     return BF_OK;
@@ -1457,6 +1488,15 @@ int bf_shard_test_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t wind
                              uint32_t count_stride, uint8_t* d_bits, void* stream) {
     return shard_chunks_impl(h, d_recv, window_cap, nsrc, d_dir, dir_bytes, tiles, d_counts, count_stride, nullptr,
                              d_bits, true, stream);
+}
+
+int bf_shard_test_chunks_hash_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                                  const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                                  uint32_t count_stride, uint8_t* d_bits, const uint8_t* d_next_keys,
+                                  const uint64_t* d_next_offsets, uint64_t n_next, uint32_t* d_next_digests,
+                                  void* stream) {
+    return shard_chunks_impl(h, d_recv, window_cap, nsrc, d_dir, dir_bytes, tiles, d_counts, count_stride, nullptr,
+                             d_bits, true, stream, d_next_keys, d_next_offsets, n_next, d_next_digests);
 }
 
 int bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint16_t* d_slot16, uint64_t window_cap,

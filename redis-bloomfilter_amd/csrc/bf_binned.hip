@@ -585,7 +585,7 @@ __device__ __forceinline__ uint32_t wave_agg_rank(bool live, uint32_t owner, uin
 // and the tile records its chunk in the window's directory: the run's place in the window
 // and its superbin run table (BfChunks).  The owner then reads the received windows as a
 // level-1 array of chunks and skips its own front (sort) pass; slots are u16, tile-relative.
-template <bool WIDE, bool SLOT, int SLOTS, bool WIN, bool CHUNK = false>
+template <bool WIDE, bool SLOT, int SLOTS, bool WIN, bool CHUNK = false, bool DIG = false>
 __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __restrict__ keys16,
                                                  const uint64_t* __restrict__ offsets, uint64_t bias,
                                                  uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
@@ -638,6 +638,11 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         const uint64_t key0 = tile * tile_keys;
         const uint32_t tk = (uint32_t)((n - key0) < (uint64_t)tile_keys ? (n - key0) : tile_keys);
         uint4 H0 = make_uint4(0, 0, 0, 0), H1 = make_uint4(0, 0, 0, 0);
+        if constexpr (DIG) {   // the keys' SHA-1 words, hashed earlier (bf_route_chunks_digests_dev)
+            const uint4* dg = reinterpret_cast<const uint4*>(keys16);
+            if (t < tk) H0 = dg[key0 + t];
+            if (kTile + t < tk) H1 = dg[key0 + kTile + t];
+        } else {
         for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off, s_stage,
             [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
                 uint32_t H[5];
@@ -651,6 +656,7 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                     sha1_any<decltype(staged)::value>(src, s, L, H);
                     H1 = make_uint4(H[0], H[1], H[2], H[3]);
                 });
+        }
         }
         const bool live0 = t < tk;
         const bool live1 = kpl == 2 && kTile + t < tk;
@@ -775,16 +781,16 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         void* __restrict__ wsend, uint32_t* __restrict__ wslot, uint32_t nh
 #define BF_ROUTE_FRONT_PASS \
     g, keys16, offsets, bias, n, tile_keys, tiles_per_block, P, lo1, hi1, key1, stab, gcnt, wcap, wcounts, wsend, wslot, nh
-template <bool WIDE, bool SLOT, int SLOTS, bool WIN, bool CHUNK = false>
+template <bool WIDE, bool SLOT, int SLOTS, bool WIN, bool CHUNK = false, bool DIG = false>
 __global__ __launch_bounds__(kTile) void route_front_kernel(BF_ROUTE_FRONT_ARGS, BfChunks cg) {
-    route_front_body<WIDE, SLOT, SLOTS, WIN, CHUNK>(BF_ROUTE_FRONT_PASS, cg);
+    route_front_body<WIDE, SLOT, SLOTS, WIN, CHUNK, DIG>(BF_ROUTE_FRONT_PASS, cg);
 }
 // 32-bit offsets (shards of <= 2^32 bits): 76 KiB of LDS with or without slots, so two
 // workgroups per CU at 8 waves per SIMD, as bin_front
-template <bool SLOT, bool WIN, bool CHUNK = false>
+template <bool SLOT, bool WIN, bool CHUNK = false, bool DIG = false>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void route_front32_kernel(BF_ROUTE_FRONT_ARGS, BfChunks cg) {
-    route_front_body<false, SLOT, kSlots, WIN, CHUNK>(BF_ROUTE_FRONT_PASS, cg);
+    route_front_body<false, SLOT, kSlots, WIN, CHUNK, DIG>(BF_ROUTE_FRONT_PASS, cg);
 }
 #undef BF_ROUTE_FRONT_PASS
 #undef BF_ROUTE_FRONT_ARGS
@@ -1435,9 +1441,29 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
                                                                  const uint32_t* __restrict__ gsum,
                                                                  const uint2* __restrict__ runs,
                                                                  const uint16_t* __restrict__ istart,
-                                                                 uint8_t* __restrict__ out8) {
+                                                                 uint8_t* __restrict__ out8, BfSideHash sh) {
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
     const uint32_t t = threadIdx.x;
+    // Side job (sh.n > 0): SHA-1 words of another batch, one key per lane in tiles of kL2Lanes
+    // keys; tile T belongs to workgroup T % gridDim and is hashed at the top of one of its items
+    // (spread evenly), so hashing waves overlap other waves' probe latency, as the single-GPU
+    // include? kernel hashes the next insert batch (bf_include_hash_kernel).
+    const uint64_t sh_tiles = (sh.n + kL2Lanes - 1) / kL2Lanes;
+    const uint64_t sh_mine = sh_tiles > blockIdx.x ? (sh_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+    uint64_t sh_done = 0;
+    auto side_hash = [&](uint64_t upto) {   // this workgroup's tiles [sh_done, upto)
+        for (; sh_done < upto; ++sh_done) {
+            const uint64_t j = (blockIdx.x + sh_done * gridDim.x) * kL2Lanes + t;
+            if (j < sh.n) {
+                const uint64_t ks = sh.offsets[j] + sh.bias, ke = sh.offsets[j + 1] + sh.bias;
+                const uint64_t kbase = ks & ~(uint64_t)3;
+                uint32_t H[5];
+                sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks - kbase),
+                         (uint32_t)(ke - ks), H);
+                sh.dig[j] = make_uint4(H[0], H[1], H[2], H[3]);
+            }
+        }
+    };
     const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles;
     // XCD-local sweep: workgroup b runs on XCD b % 8 (round-robin dispatch; the grid is a
     // multiple of 8), and XCD x sweeps superbins x, x + 8, ..., its gridDim / 8 workgroups
@@ -1447,7 +1473,11 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
     const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
     const uint64_t per_sb = (uint64_t)nq * parts;
     const uint64_t items = (uint64_t)((nsup + 7u - xcd) >> 3) * per_sb;   // this XCD's superbins
-    for (uint64_t k = blockIdx.x >> 3; k < items; k += g8) {
+    const uint64_t k0 = blockIdx.x >> 3;
+    const uint64_t my_items = items > k0 ? (items - 1 - k0) / g8 + 1 : 0;
+    uint64_t ii = 0;
+    for (uint64_t k = k0; k < items; k += g8, ++ii) {
+        if (sh.n) side_hash((ii + 1) * sh_mine / my_items);
         const uint32_t sb = xcd + 8u * (uint32_t)(k / per_sb);
         const uint64_t kk = k - (uint64_t)(k / per_sb) * per_sb;
         const uint32_t q = (uint32_t)(kk / parts), part = (uint32_t)(kk - (uint64_t)q * parts);
@@ -1498,6 +1528,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
                 }
         }
     }
+    if (sh.n) side_hash(sh_mine);
 }
 
 // bin_mid over chunked windows: window w = (superbin sb, chunk group q) concatenates sb's runs
@@ -2280,7 +2311,7 @@ hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, ui
 
 hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,
-                                       BfMarks* mk) {
+                                       BfMarks* mk, const BfSideHash& side) {
     if (!p.chunked || !p.with_keys || !out8) return hipErrorInvalidValue;
     const Carve c = carve(p, scratch);
     if (p.l2test) {   // no sort: a superbin-major sweep, probes in receive order, answers stored in place
@@ -2296,9 +2327,14 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
                            c.gsum, c.runs, parts, c.istart);
         bf_mark(mk, s, "chunk_group");
         hipLaunchKernelGGL(chunk_test_l2_kernel, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup, p.ngroups,
-                           parts, c.gsum, c.runs, c.istart, out8);
-        bf_mark(mk, s, "test_l2");
+                           parts, c.gsum, c.runs, c.istart, out8, side);
+        bf_mark(mk, s, side.n ? "test_l2_hash" : "test_l2");
         return hipGetLastError();
+    }
+    if (side.n) {   // the sorted test has no latency to hide: hash in a pass of its own
+        hipError_t e = bf_launch_keys(BF_OP_HASH, g, side.keys16, side.offsets, side.bias, side.n, nullptr,
+                                      reinterpret_cast<uint64_t*>(side.dig), nullptr, s);
+        if (e != hipSuccess) return e;
     }
     hipError_t e = hipMemsetAsync(out8, 1, p.probes, s);   // every entry's answer starts true
     if (e != hipSuccess) return e;
@@ -2309,7 +2345,7 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
 hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const BfChunks& cg,
                                   const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                   void* send, uint16_t* slot16, uint64_t wcap, unsigned long long* counts,
-                                  hipStream_t s, BfMarks* mk) {
+                                  hipStream_t s, BfMarks* mk, bool dig) {
     hipError_t e;
     if ((e = hipMemsetAsync(counts, 0, (uint64_t)p.nsup * sizeof(unsigned long long), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(cg.dir, 0, (uint64_t)p.nsup * cg.dir_bytes, s)) != hipSuccess) return e;
@@ -2319,14 +2355,21 @@ hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t 
     hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,      \
                        p.tiles_per_block, p.nsup, nullptr, nullptr, nullptr, nullptr, nullptr, wcap, counts, send, \
                        slot, nh, cg)
-    if (g.k > (uint32_t)kSlots) {
+    if (dig) {
+        if (g.k > (uint32_t)kSlots) {
+            if (slot16) BF_ROUTE_CH((route_front_kernel<false, true, kWideSlots, true, true, true>));
+            else BF_ROUTE_CH((route_front_kernel<false, false, kWideSlots, true, true, true>));
+        }
+        else if (slot16) BF_ROUTE_CH((route_front32_kernel<true, true, true, true>));
+        else BF_ROUTE_CH((route_front32_kernel<false, true, true, true>));
+    } else if (g.k > (uint32_t)kSlots) {
         if (slot16) BF_ROUTE_CH((route_front_kernel<false, true, kWideSlots, true, true>));
         else BF_ROUTE_CH((route_front_kernel<false, false, kWideSlots, true, true>));
     }
     else if (slot16) BF_ROUTE_CH((route_front32_kernel<true, true, true>));
     else BF_ROUTE_CH((route_front32_kernel<false, true, true>));
 #undef BF_ROUTE_CH
-    bf_mark(mk, s, slot16 ? "route_chunks_slot" : "route_chunks");
+    bf_mark(mk, s, slot16 ? (dig ? "route_chunks_slot_dig" : "route_chunks_slot") : (dig ? "route_chunks_dig" : "route_chunks"));
     return hipGetLastError();
 }
 

@@ -199,15 +199,25 @@ bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint3
 hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                          const BfChunkIn& ci, void* scratch, uint32_t* any_flag, hipStream_t s,
                                          BfMarks* marks = nullptr);
+// A side job for the owner test: the SHA-1 words of another key batch (a requester's next
+// include? batch), hashed by the L2 sweep's workgroups between their items (keys16 aligned
+// down to 16 B, bias = the dropped bytes; n = 0: none).
+struct BfSideHash {
+    const uint8_t* keys16 = nullptr;
+    const uint64_t* offsets = nullptr;
+    uint64_t bias = 0, n = 0;
+    uint4* dig = nullptr;
+};
 hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,
-                                       BfMarks* marks = nullptr);
+                                       BfMarks* marks = nullptr, const BfSideHash& side = BfSideHash{});
 // Requester side: the window route with directories (cg.dir zeroed here first; slot16
 // nullable: tile-relative key indices).
+// dig: keys16 holds the keys' SHA-1 words (uint4 per key; offsets unused) instead of key bytes.
 hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const BfChunks& cg,
                                   const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                   void* send, uint16_t* slot16, uint64_t wcap, unsigned long long* counts,
-                                  hipStream_t s, BfMarks* marks = nullptr);
+                                  hipStream_t s, BfMarks* marks = nullptr, bool dig = false);
 // out[j] = AND over every window's chunk of j's tile of the packed answer bits (window w at
 // packed + w * ceil(wcap / 8)); one workgroup per route tile, answers gathered in LDS.
 hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t* slot16, uint64_t wcap,

@@ -241,10 +241,22 @@ class HipEngine:
             send.fill_(self.poison)
             if slot is not None:
                 slot.fill_(0)
-        self.filter.route_chunks_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
-                                     slot.data_ptr() if want_slot else 0, cap, counts.data_ptr(), dirb.data_ptr(),
-                                     dir_bytes, tiles, stream=self._stream())
+        if kb is not None and ko is None:   # kb: the keys' SHA-1 words (hash_keys / shard_test_chunks(next=))
+            self.filter.route_chunks_digests_dev(kb.data_ptr(), n, send.data_ptr(), slot.data_ptr() if want_slot else 0,
+                                                 cap, counts.data_ptr(), dirb.data_ptr(), dir_bytes, tiles,
+                                                 stream=self._stream())
+        else:
+            self.filter.route_chunks_dev(kb.data_ptr(), ko.data_ptr(), n, send.data_ptr(),
+                                         slot.data_ptr() if want_slot else 0, cap, counts.data_ptr(), dirb.data_ptr(),
+                                         dir_bytes, tiles, stream=self._stream())
         return send, slot, counts, dirb
+
+    def hash_keys(self, kb: torch.Tensor, ko: torch.Tensor, n: int, out: torch.Tensor = None) -> torch.Tensor:
+        """The keys' SHA-1 words (n x 4 int32), route_chunks' digest input."""
+        dig = out if out is not None else torch.empty((max(n, 1), 4), dtype=torch.int32, device=self.device)
+        if n:
+            self.filter.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, dig.data_ptr(), stream=self._stream())
+        return dig
 
     def shard_insert_chunks(self, recv: torch.Tensor, cap: int, nsrc: int, rdir: torch.Tensor, dir_bytes: int,
                             tiles: int, counts: torch.Tensor, cstride: int) -> None:
@@ -254,7 +266,14 @@ class HipEngine:
                                             counts.data_ptr(), cstride, stream=self._stream())
 
     def shard_test_chunks(self, recv: torch.Tensor, cap: int, nsrc: int, rdir: torch.Tensor, dir_bytes: int,
-                          tiles: int, counts: torch.Tensor, cstride: int, out: torch.Tensor) -> None:
+                          tiles: int, counts: torch.Tensor, cstride: int, out: torch.Tensor, nxt=None) -> None:
+        """nxt = (kb, ko, n, dig): the owner test's waves also hash that batch into dig (n x 4 int32)."""
+        if nxt is not None and nxt[2]:
+            kb, ko, n, dig = nxt
+            self.filter.shard_test_chunks_hash_dev(recv.data_ptr(), cap, nsrc, rdir.data_ptr(), dir_bytes, tiles,
+                                                   counts.data_ptr(), cstride, out.data_ptr(), kb.data_ptr(),
+                                                   ko.data_ptr(), n, dig.data_ptr(), stream=self._stream())
+            return
         self.filter.shard_test_chunks_dev(recv.data_ptr(), cap, nsrc, rdir.data_ptr(), dir_bytes, tiles,
                                           counts.data_ptr(), cstride, out.data_ptr(), stream=self._stream())
 

@@ -182,7 +182,9 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     with P shards simulated on one GPU and the exchange done by copies: every window holds
     exactly its owner's (key, local offset) pairs, the directories partition each window into
     one run per route tile, the owners' shards rebuild the oracle's Redis string and the
-    requesters' answers equal the oracle's include?.  owner: "direct" = the direct kernels over
+    requesters' answers equal the oracle's include? (odd ranks route their include? batch from
+    SHA-1 words; every owner test also hashes a side batch, whose words equal hash_many's).
+    owner: "direct" = the direct kernels over
     the same windows; "sorted" = the binned pass straight off the chunks (bin_mid, then the
     region apply / test); "l2" = the binned insert and the superbin-major L2-local test."""
     import torch
@@ -208,11 +210,16 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     rng = np.random.default_rng(23)
     per_rank = [["c%d-%d" % (r, int(v)) for v in rng.integers(0, 10**12, n)] for r in range(P)]
 
-    def route_all(batches, want_slot):
+    def route_all(batches, want_slot, dig=False):
+        """dig: odd ranks route from their keys' SHA-1 words (bf_route_chunks_digests_dev)."""
         out = []
         for r in range(P):
             kb, ko, nn, buf, offs = dev_batch(pkg, torch, batches[r])
-            out.append(shards[r].route_chunks(kb, ko, nn, cap, tiles, dbytes, want_slot=want_slot) + (buf, offs))
+            if dig and r % 2:
+                out.append(shards[r].route_chunks(shards[r].hash_keys(kb, ko, nn), None, nn, cap, tiles, dbytes,
+                                                  want_slot=want_slot) + (buf, offs))
+            else:
+                out.append(shards[r].route_chunks(kb, ko, nn, cap, tiles, dbytes, want_slot=want_slot) + (buf, offs))
         torch.cuda.synchronize()
         return out
 
@@ -273,13 +280,19 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     # include?: members of two ranks + fresh keys per requester
     probes = [per_rank[r][: n // 3] + per_rank[(r + 1) % P][: n // 3] + ["fresh%d-%d" % (r, i) for i in range(n // 3)]
               for r in range(P)]
-    qs = route_all(probes, want_slot=True)
+    qs = route_all(probes, want_slot=True, dig=True)
+    for r in range(1, P, 2):
+        check_route(*qs[r][:4], qs[r][4], qs[r][5])
     cap8 = (cap + 7) // 8
     answers = []
     for o in range(P):
         recv, rdir, rmsg = deliver(qs, o)
         out = torch.zeros(nh * P * cap, dtype=torch.uint8, device=dev)
-        shards[o].shard_test_chunks(recv, cap, P, rdir, dbytes, tiles, rmsg, nh + 1, out)
+        # the owner test also hashes a side batch (a requester's next include? batch)
+        skb, sko, sn, _, _ = dev_batch(pkg, torch, per_rank[o][: 3001 + 97 * o])
+        sdig = torch.full((sn, 4), -1, dtype=torch.int32, device=dev)
+        shards[o].shard_test_chunks(recv, cap, P, rdir, dbytes, tiles, rmsg, nh + 1, out, nxt=(skb, sko, sn, sdig))
+        torch.testing.assert_close(sdig, shards[o].hash_keys(skb, sko, sn), rtol=0, atol=0)
         answers.append(out)
     for r in range(P):
         back = torch.zeros(nwin * cap8, dtype=torch.uint8, device=dev)

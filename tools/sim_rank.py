@@ -50,6 +50,13 @@ def main():
     ap.add_argument("--gathered", default="keys", choices=["keys", "digests"],
                     help="replicated: what travels — key bytes (every replica hashes every batch: "
                          "ReplicatedFilter) or 16-B SHA-1 words (each key hashed once, by its own rank)")
+    ap.add_argument("--dig", action="store_true",
+                    help="--chunks: route the include? batch from SHA-1 words that the previous step's owner "
+                         "test hashed between its probe rounds (bf_shard_test_chunks_hash_dev + "
+                         "bf_route_chunks_digests_dev)")
+    ap.add_argument("--dig-side", action="store_true",
+                    help="--chunks --dig, but the next include? batch is hashed by bf_hash_many_dev on a second "
+                         "stream (a second handle) beside the owner test, not inside it; read the wall time")
     ap.add_argument("--overlap", action="store_true",
                     help="--chunks: route the NEXT step's insert batch on a second stream while this step's "
                          "owner kernels run (what PartitionedFilter's next_insert prefetch would do on a side "
@@ -147,10 +154,30 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record(side)
             pre.update(send=s_, counts=c_, dirb=d_, ev=ev)
-        send, slot, counts, dirb = eng.route_chunks(qkb, qko, batch, capsf, tiles, dbytes)
+        if args.dig:   # this step's include? batch was hashed by the previous step's owner test
+            send, slot, counts, dirb = eng.route_chunks(digs["cur"], None, batch, capsf, tiles, dbytes)
+        else:
+            send, slot, counts, dirb = eng.route_chunks(qkb, qko, batch, capsf, tiles, dbytes)
         recv, rdir, rmsg = deliver(send, dirb, counts)
         bits = torch.empty(nh * P * capsf, dtype=torch.uint8, device=dev)
-        eng.shard_test_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1, bits)
+        nxt = None
+        if args.dig:   # ... and this one hashes the next step's
+            nq = nxt_batch[0][1]
+            nd = digs["spare"]
+            nxt = (nq[0], nq[1], batch, nd)
+            if args.dig_side:   # on a second stream, beside the test
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    hasher.hash_many_dev(nq[0].data_ptr(), nq[1].data_ptr(), batch, nd.data_ptr(),
+                                         stream=side.cuda_stream)
+                    hev = torch.cuda.Event()
+                    hev.record(side)
+                nxt = None
+        eng.shard_test_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1, bits, nxt=nxt)
+        if args.dig:
+            if args.dig_side:
+                torch.cuda.current_stream(dev).wait_event(hev)
+            digs["spare"], digs["cur"] = digs["cur"], nd
         cap8 = (capsf + 7) // 8
         seg = torch.tensor([[(h * P + src) * capsf, capsf, (src * nh + h) * cap8] for src in range(P)
                             for h in range(nh)], dtype=torch.int64).to(dev)
@@ -161,6 +188,11 @@ def main():
     router = pkg.distributed.HipEngine(m, k, args.shards, 0, 20, dev) if args.overlap else None
     pre = {}
     nxt_batch = [None]
+    digs = {}
+    hasher = pkg.Filter(1 << 20, k, device=0) if args.dig_side else None   # hash_many needs a handle
+    if args.dig:   # batch 0's include? words before the first step (the pipeline's fill)
+        digs["cur"] = eng.hash_keys(batches[0][1][0], batches[0][1][1], batch)
+        digs["spare"] = torch.empty_like(digs["cur"])
 
     def step(b):
         if args.chunks:
