@@ -243,6 +243,18 @@ __global__ __launch_bounds__(kTile) void bin_front_wide_kernel(BfGeom g, const u
                                           level1, level1_key, stab, gcnt, out8);
 }
 
+// ... from SHA-1 words (the pipelined insert at k > 12: 10B / 200B): no key stage, so 67 KiB
+// of LDS, and capped at 64 VGPRs for two workgroups per CU
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void bin_front_wide_dig_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
+                               uint64_t bias, uint64_t n, uint32_t tile_keys, uint32_t tiles_per_block,
+                               uint32_t sup_log2, uint32_t nsup, uint32_t* __restrict__ level1,
+                               uint32_t* __restrict__ level1_key, uint16_t* __restrict__ stab,
+                               uint32_t* __restrict__ gcnt, uint8_t* __restrict__ out8) {
+    bin_front_body<false, kWideSlots, true>(g, keys16, offsets, bias, n, tile_keys, tiles_per_block, sup_log2, nsup,
+                                            level1, level1_key, stab, gcnt, out8);
+}
+
 // include?: key indices ride along (123 KiB of LDS: one workgroup per CU)
 __global__ __launch_bounds__(kTile)
 void bin_front_keys_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
@@ -1793,7 +1805,15 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
     const uint32_t sup_log2 = p.region_log2 + p.rel_log2;
     if (dig) {
         if (p.with_keys) return hipErrorInvalidValue;
-        if (g.k > (uint32_t)kSlots)
+        static const bool wide2 = [] {   // A/B: BFHIP_FRONT_WIDE2=0 takes one workgroup per CU
+            const char* e = std::getenv("BFHIP_FRONT_WIDE2");
+            return !(e && e[0] == '0');
+        }();
+        if (g.k > (uint32_t)kSlots && wide2)
+            hipLaunchKernelGGL(bin_front_wide_dig_kernel, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias,
+                               n, p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1, c.level1_key, c.stab,
+                               c.gcnt, out8);
+        else if (g.k > (uint32_t)kSlots)
             hipLaunchKernelGGL((bin_front_wide_kernel<false, true>), dim3(p.nblocks), dim3(kTile), 0, s, g, keys16,
                                offsets, bias, n, p.tile_keys, p.tiles_per_block, sup_log2, p.nsup, c.level1,
                                c.level1_key, c.stab, c.gcnt, out8);

@@ -27,7 +27,7 @@ KERNELS = {
     "bf_keys_kernel<HASH>": re.compile(r"bf_keys_kernel<5>"),
     "bin_front": re.compile(r"bin_front_kernel<false>"),
     "bin_front_digest": re.compile(r"bin_front_kernel<true>"),
-    "bin_front_wide": re.compile(r"bin_front_wide_kernel"),
+    "bin_front_wide": re.compile(r"bin_front_wide_(dig_)?kernel"),
     "bin_mid": re.compile(r"bin_mid_kernel"),
     "bin_apply": re.compile(r"bin_apply_(pipe_)?kernel"),
     "bin_test": re.compile(r"bin_test_kernel"),
