@@ -693,7 +693,7 @@ def load_traffic(workload: str, kernel: str):
     return rec.get("hbm_bytes_per_launch") if isinstance(rec, dict) else None
 
 
-PMC_FILES = {"nstar": "pmc_r03n_nstar.json", "1m_big": "pmc_r02_1m_big.json", "10b": "pmc_r02_10b.json"}
+PMC_FILES = {"nstar": "pmc_r03f_nstar.json", "1m_big": "pmc_r02_1m_big.json", "10b": "pmc_r03r_10b.json"}
 # rocprofv3 --kernel-trace --stats of the bench command on the round's final tree
 # (tools/rocprof_means.py over profiles/<tag>_kernel_stats.csv): each kernel's mean launch
 ROCPROF_MEANS = "rocprof_means.json"
