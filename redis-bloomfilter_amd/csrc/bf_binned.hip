@@ -1455,24 +1455,44 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
                                                                  const uint16_t* __restrict__ istart,
                                                                  uint8_t* __restrict__ out8, BfSideHash sh) {
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
+    constexpr uint32_t kSideVec = 256;   // 4 KiB key stage: a tile of 256 keys of <= ~16 B each
+    __shared__ uint64_t s_soff[kL2Lanes + 1];
+    __shared__ uint4 s_sstage[kSideVec + kStageSlackVec];
     const uint32_t t = threadIdx.x;
     // Side job (sh.n > 0): SHA-1 words of another batch, one key per lane in tiles of kL2Lanes
     // keys; tile T belongs to workgroup T % gridDim and is hashed at the top of one of its items
     // (spread evenly), so hashing waves overlap other waves' probe latency, as the single-GPU
-    // include? kernel hashes the next insert batch (bf_include_hash_kernel).
+    // include? kernel hashes the next insert batch (bf_include_hash_kernel).  A tile's key bytes
+    // are staged into LDS with one coalesced pass (a tile past the stage reads from global).
     const uint64_t sh_tiles = (sh.n + kL2Lanes - 1) / kL2Lanes;
     const uint64_t sh_mine = sh_tiles > blockIdx.x ? (sh_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
     uint64_t sh_done = 0;
-    auto side_hash = [&](uint64_t upto) {   // this workgroup's tiles [sh_done, upto)
+    auto side_hash = [&](uint64_t upto) {   // this workgroup's tiles [sh_done, upto); has barriers
         for (; sh_done < upto; ++sh_done) {
-            const uint64_t j = (blockIdx.x + sh_done * gridDim.x) * kL2Lanes + t;
-            if (j < sh.n) {
-                const uint64_t ks = sh.offsets[j] + sh.bias, ke = sh.offsets[j + 1] + sh.bias;
-                const uint64_t kbase = ks & ~(uint64_t)3;
+            const uint64_t j0 = (blockIdx.x + sh_done * gridDim.x) * kL2Lanes;
+            const uint32_t cnt = (uint32_t)(sh.n - j0 < kL2Lanes ? sh.n - j0 : kL2Lanes);
+            __syncthreads();   // the previous tile's readers of the stage are done
+            if (t < cnt) s_soff[t] = sh.offsets[j0 + t] + sh.bias;
+            if (t == 0) s_soff[cnt] = sh.offsets[j0 + cnt] + sh.bias;
+            __syncthreads();
+            const uint64_t abase = s_soff[0] & ~(uint64_t)15;
+            const uint64_t nvec = (s_soff[cnt] - abase + 15) >> 4;
+            const bool staged = nvec <= kSideVec;   // workgroup-uniform
+            if (staged) {
+                const uint4* gv = reinterpret_cast<const uint4*>(sh.keys16 + abase);
+                for (uint32_t v = t; v < (uint32_t)nvec; v += kL2Lanes) s_sstage[v] = gv[v];
+            }
+            __syncthreads();
+            if (t < cnt) {
+                const uint64_t ks = s_soff[t], L = s_soff[t + 1] - ks;
                 uint32_t H[5];
-                sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks - kbase),
-                         (uint32_t)(ke - ks), H);
-                sh.dig[j] = make_uint4(H[0], H[1], H[2], H[3]);
+                if (staged) {
+                    sha1_key_staged(reinterpret_cast<const uint32_t*>(s_sstage), (uint32_t)(ks - abase), (uint32_t)L, H);
+                } else {
+                    const uint64_t kbase = ks & ~(uint64_t)3;
+                    sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks - kbase), (uint32_t)L, H);
+                }
+                sh.dig[j0 + t] = make_uint4(H[0], H[1], H[2], H[3]);
             }
         }
     };
