@@ -1448,6 +1448,7 @@ constexpr uint32_t kL2Lanes = 256;
 constexpr int kL2Loads = 8;
 constexpr uint32_t kL2Grid = 1024;   // 256 CUs x 4 workgroups of 4 waves (grid A/B: 256-2048)
 constexpr uint32_t kL2MaxParts = 256;
+template <bool SIDE>
 __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
                                                                  uint32_t nsup, uint32_t nq, uint32_t parts,
                                                                  const uint32_t* __restrict__ gsum,
@@ -1509,7 +1510,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
     const uint64_t my_items = items > k0 ? (items - 1 - k0) / g8 + 1 : 0;
     uint64_t ii = 0;
     for (uint64_t k = k0; k < items; k += g8, ++ii) {
-        if (sh.n) side_hash((ii + 1) * sh_mine / my_items);
+        if constexpr (SIDE) side_hash((ii + 1) * sh_mine / my_items);
         const uint32_t sb = xcd + 8u * (uint32_t)(k / per_sb);
         const uint64_t kk = k - (uint64_t)(k / per_sb) * per_sb;
         const uint32_t q = (uint32_t)(kk / parts), part = (uint32_t)(kk - (uint64_t)q * parts);
@@ -1560,7 +1561,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
                 }
         }
     }
-    if (sh.n) side_hash(sh_mine);
+    if constexpr (SIDE) side_hash(sh_mine);
 }
 
 // bin_mid over chunked windows: window w = (superbin sb, chunk group q) concatenates sb's runs
@@ -2366,8 +2367,12 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
         hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
                            c.gsum, c.runs, parts, c.istart);
         bf_mark(mk, s, "chunk_group");
-        hipLaunchKernelGGL(chunk_test_l2_kernel, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup, p.ngroups,
-                           parts, c.gsum, c.runs, c.istart, out8, side);
+        if (side.n)
+            hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
+                               p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+        else
+            hipLaunchKernelGGL(chunk_test_l2_kernel<false>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
+                               p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         bf_mark(mk, s, side.n ? "test_l2_hash" : "test_l2");
         return hipGetLastError();
     }
