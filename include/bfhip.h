@@ -337,7 +337,13 @@ int  bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t
  *                           + i] for the live entries i.
  * bf_combine_chunks_packed_dev  requester: the include? answers from window w's answer bits
  *                           at d_packed + w*ceil(window_cap/8), through this rank's own
- *                           route directory and slots.
+ *                           route directory and slots.  A window whose count exceeds
+ *                           window_cap (overflowed: its entries were never all written, so the
+ *                           owner skipped it) contributes no answers, and the keys routed
+ *                           there answer 1: after ANY overflow on ANY rank the combined answers
+ *                           are false positives the caller must discard and recompute through
+ *                           a re-route (distributed.py replays the step through the synced
+ *                           exchange).  The same holds for bf_combine_windows[_packed]_dev.
  * bf_route_chunks_digests_dev   bf_route_chunks_dev from the keys' SHA-1 words (16-byte
  *                           aligned uint32[4] per key, as bf_hash_many_dev writes them).
  * bf_shard_test_chunks_hash_dev bf_shard_test_chunks_dev that also writes the SHA-1 words of

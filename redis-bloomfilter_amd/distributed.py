@@ -442,6 +442,11 @@ class PartitionedFilter:
         # skips its sort pass; BFHIP_CHUNKS=0 keeps the plain windows
         self.chunks = bool(chunks and self.sync_free and hasattr(engine, "route_chunks")
                            and os.environ.get("BFHIP_CHUNKS", "1") != "0")
+        # a shard count whose windows have no chunk geometry (P * nh past the directory's
+        # window limit, e.g. the k = 13 filters at P = 6) takes the plain sync-free windows;
+        # the geometry depends only on the shard layout, so every rank decides the same
+        if self.chunks and engine.chunk_info(1) is None:
+            self.chunks = False
         self._chunk_geo = {}
         # The sync-free windows are sized from a batch bound every rank agrees on, never from
         # the rank's own n: ranks that size them from different n would post p2p messages of
@@ -810,12 +815,17 @@ class PartitionedFilter:
         call must then pass that same batch as (ikb, iko, ni)."""
         pend = self._pending
         if pend is not None and not (pend["kb"] is ikb and pend["n"] == ni):
-            # the prefetched batch is already routed and sent: complete it (it was announced
-            # as the next insert) before refusing the call, so no rank drops it
-            self.drain_prefetch()
-            raise ArgumentError("insert_include_dev: the insert batch differs from the prefetched next_insert "
-                                "(the prefetched batch was inserted)")
+            # Refused without touching the prefetch: completing it here would run collectives
+            # (an overflow replay, the bound agreement) on this rank alone while the others go
+            # on into their exchanges, and the job would hang.  Every rank must call
+            # drain_prefetch() (collective) to complete the prefetched batch.
+            raise ArgumentError("insert_include_dev: the insert batch differs from the prefetched next_insert; "
+                                "call drain_prefetch() on every rank")
         self._pending = None
+        if self.sync_free and self._sf_n is None:
+            # the first sync-free call agrees on the bound from every batch it will route, so an
+            # include? (or prefetched) batch larger than the insert batch does not overflow
+            self._agree_batch(max(ni, nq, next_insert[2] if next_insert is not None else 0))
         if self.sync_free:
             # route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test |
             # send(back) | combine, all enqueued before the host waits for anything
@@ -836,7 +846,9 @@ class PartitionedFilter:
         return self._insert_include_synced(ikb, iko, ni, qkb, qko, nq)
 
     def drain_prefetch(self) -> None:
-        """Complete a prefetched next_insert that no call will consume: its batch is inserted."""
+        """Complete a prefetched next_insert that no call will consume: its batch is inserted.
+        Collective: every rank must call it at the same point (an overflowed prefetch is
+        replayed through the synced exchange and the bound agreed again)."""
         pend, self._pending = self._pending, None
         if pend is not None:
             self._sf_flag(pend)

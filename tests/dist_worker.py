@@ -110,6 +110,106 @@ def replicated_case(rank, P, cfg, dev):
     return ok
 
 
+class _DevBytes:
+    """Raw device bytes (a filter's bitset) as a torch tensor, without a copy."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+def sparse_bits(orc, keys, m, k):
+    """The Redis string of inserting `keys` into an empty (m, k) filter, as (nonzero byte
+    positions, their bytes), from the oracle's offsets alone: a 6.98 GB string need not be
+    built to be compared, since an insert only ever sets bits (ruby.rb:57-60)."""
+    kb, ko = O.pack_keys(keys)
+    idx = np.unique(orc.indexes_many(kb, ko, m, k).reshape(-1))
+    pos = (idx >> np.uint64(3)).astype(np.int64)
+    mask = (np.uint64(0x80) >> (idx & np.uint64(7))).astype(np.uint8)
+    starts = np.flatnonzero(np.concatenate([[True], pos[1:] != pos[:-1]]))
+    return pos[starts], np.bitwise_or.reduceat(mask, starts), idx
+
+
+def device_sparse(f):
+    """(nonzero byte positions, bytes) of a filter's device bitset, found on the device."""
+    torch.cuda.synchronize()
+    ptr, nbytes = f.device_bits()
+    t = torch.as_tensor(_DevBytes(ptr, nbytes), device="cuda")
+    nz = torch.nonzero(t).view(-1)
+    return nz.cpu().numpy(), t[nz].cpu().numpy()
+
+
+def sparse_include(orc, set_idx, probe, m, k):
+    """The oracle's include? answers over a filter whose set bits are `set_idx` (sorted)."""
+    pb, po = O.pack_keys(probe)
+    idx = orc.indexes_many(pb, po, m, k).reshape(len(probe), k)
+    return np.isin(idx, set_idx).all(axis=1)
+
+
+def replicated_big_case(rank, P, cfg, dev):
+    """BASELINE configs[3] (10B@0.01 %, 6.98 GB reachable, replicated on every rank, key
+    batches sharded) through the forms bench.py --config 10b runs: the "digests" insert (each
+    rank hashes its own batch once, the SHA-1 words are all-gathered, every replica inserts all
+    of them from words as one binned insert), both through insert_many and through the
+    pipelined sizes_start / gather_start(sizes=) / insert_gathered sequence, plus uneven
+    batches; the "gather" form for comparison.  Every replica's bitset must equal the oracle's
+    over all ranks' keys (compared sparsely, ruby.rb:57-63) and its include? answers the
+    oracle's (ruby.rb:20-30)."""
+    m, k, n = cfg["m"], cfg["k"], cfg["n"]
+    orc = O.COracle()
+    keys = [["q%d-%d" % (r, int(v)) for v in np.random.default_rng([cfg["seed"], r]).integers(0, 10**9, n)]
+            for r in range(P)]
+    all_keys = [x for ks in keys for x in ks]
+    want_pos, want_val, set_idx = sparse_bits(orc, all_keys, m, k)
+    probe = all_keys[rank::P] + ["fresh-%d-%d" % (rank, i) for i in range(n)]
+    want_inc = sparse_include(orc, set_idx, probe, m, k)
+    ok = True
+
+    def same(rf, wp, wv):
+        gp, gv = device_sparse(rf.filter)
+        return bool(np.array_equal(gp, wp) and np.array_equal(gv, wv))
+
+    for mode in ("digests", "gather"):
+        rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
+        rf.insert_many(keys[rank])
+        ok = ok and rf.last_insert_mode == mode and same(rf, want_pos, want_val)
+        ok = ok and bool((rf.include_many(probe) == want_inc).all())
+        rf.close()
+        if not ok:
+            print("rank %d replicated 10B mode %s MISMATCH" % (rank, mode), flush=True)
+    # bench.py's pipelined step: batch i+1's sizes all-gathered one batch ahead, its words
+    # gathered beside batch i's insert, then every rank's batch as one insert from words
+    third = n // 3
+    parts = [keys[rank][:third], keys[rank][third: 2 * third], keys[rank][2 * third:]]
+    bt = [D._device_batch(p, dev) for p in parts]
+    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="digests")
+    szp = {0: rf.sizes_start(*bt[0]), 1: rf.sizes_start(*bt[1])}
+    gpend = {0: rf.gather_start(*bt[0], sizes=szp.pop(0))}
+    for i in range(3):
+        st = gpend.pop(i)
+        if i + 1 < 3:
+            gpend[i + 1] = rf.gather_start(*bt[i + 1], sizes=szp.pop(i + 1))
+        if i + 2 < 3:
+            szp[i + 2] = rf.sizes_start(*bt[i + 2])
+        rf.insert_gathered(st)
+    ok = ok and rf.last_insert_mode == "digests" and same(rf, want_pos, want_val)
+    ok = ok and bool((rf.include_many(probe) == want_inc).all())
+    rf.close()
+    if not ok:
+        print("rank %d replicated 10B pipelined MISMATCH" % rank, flush=True)
+    # uneven batches (rank r brings n - 50 r keys; the last rank none): the gathered words
+    # are padded to the largest batch and the padding rows cut out before the insert
+    cut = [n - 50 * r if r != P - 1 else 0 for r in range(P)]
+    sub = [x for r in range(P) for x in keys[r][:cut[r]]]
+    up, uv, _ = sparse_bits(orc, sub, m, k)
+    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="digests")
+    rf.insert_many(keys[rank][:cut[rank]])
+    ok = ok and same(rf, up, uv)
+    rf.close()
+    if not ok:
+        print("rank %d replicated 10B uneven MISMATCH" % rank, flush=True)
+    return ok
+
+
 def uneven_case(rank, P, cfg, dev, make_engine):
     """Ranks that bring batches of different sizes (the sync-free windows must
     not be sized from a rank's own n), one rank bringing none, and a later batch past the
@@ -171,7 +271,8 @@ def uneven_case(rank, P, cfg, dev, make_engine):
     if not ok:
         print("rank %d uneven MISMATCH: replays %d agreed %s bound %s" % (rank, pf.replays, agreed, pf._sf_n),
               flush=True)
-    # a pending prefetch blocks the whole-filter calls, and a mismatched consume still inserts it
+    # a pending prefetch blocks the whole-filter calls; a mismatched consume is refused and
+    # leaves the prefetch pending (no rank runs a collective alone) until every rank drains it
     pf.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2))
     try:
         pf.clear()
@@ -183,6 +284,8 @@ def uneven_case(rank, P, cfg, dev, make_engine):
         ok = False
     except pkg.ArgumentError:
         pass
+    ok = ok and pf._pending is not None
+    pf.drain_prefetch()
     ok = ok and pf._pending is None
     pf.clear()
     pf.close()
@@ -195,8 +298,9 @@ def main():
     cfg = json.loads(os.environ["BF_DIST_CFG"])
     hip = cfg.get("engine") == "hip"
     dev = torch.device("cuda", 0) if hip else None
-    if cfg.get("case") == "replicated":
-        flag = torch.tensor([1 if replicated_case(rank, P, cfg, dev) else 0])
+    if cfg.get("case") in ("replicated", "replicated_big"):
+        fn = replicated_case if cfg["case"] == "replicated" else replicated_big_case
+        flag = torch.tensor([1 if fn(rank, P, cfg, dev) else 0])
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if rank == 0:
             print("DIST_RESULT", "ok" if flag.item() == 1 else "fail", flush=True)
@@ -266,6 +370,12 @@ def main():
     pf3 = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
     got3 = pf3.insert_include(mine, probe)
     same_shard = bool(np.array_equal(pf3.engine.shard_export(), pf.engine.shard_export()))
+    # the first overlapped call agrees on its bound from both batches (the include? batch is
+    # the larger here), so nothing overflows; cfg "chunks": whether this shard count takes
+    # chunked windows (P * nh past the directory limit falls back to plain windows)
+    same_shard = same_shard and pf3.replays == 0 and pf3.chunks == cfg.get("chunks", pf3.chunks)
+    if not same_shard:
+        print("rank %d pf3: replays %d chunks %s" % (rank, pf3.replays, pf3.chunks), flush=True)
     shard_sha = hashlib.sha1(pf.engine.shard_export().tobytes()).hexdigest()
     del pf, pf3
     # the same step through the contiguous route (windows off), and with every window

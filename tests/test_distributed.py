@@ -104,3 +104,28 @@ def test_ownership_map_properties(pkg):
     data = data.rstrip(b"\0")
     parts = [D.split_shard(data, 3, s, 5000 * 8, 7) for s in range(3)]
     assert D.interleave_shards(parts, 5000 * 8, 7) == data
+
+
+def test_sparse_checker_matches_dense_oracle():
+    """The sparse comparison the 10B x 8 replicated GPU test uses (dist_worker.sparse_bits /
+    sparse_include) equals the dense oracle's Redis string and include? answers."""
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dist_worker as W
+    import oracle as O
+    orc = O.COracle()
+    for m, k in ((95851, 6), (9585058, 6), (191701167547, 13)):
+        keys = ["s%d" % i for i in range(700)]
+        pos, val, idx = W.sparse_bits(orc, keys, m, k)
+        probe = keys[::5] + ["n%d" % i for i in range(300)]
+        got_inc = W.sparse_include(orc, idx, probe, m, k)
+        if m < 10**8:
+            bits = orc.new_bitset(m, k)
+            kb, ko = O.pack_keys(keys)
+            orc.insert_many(bits, m, k, kb, ko)
+            s = np.frombuffer(orc.redis_string(bits), np.uint8)
+            nz = np.flatnonzero(s)
+            assert np.array_equal(nz, pos) and np.array_equal(s[nz], val)
+            pb, po = O.pack_keys(probe)
+            assert np.array_equal(orc.include_many(bits, m, k, pb, po).astype(bool), got_inc)
+        assert got_inc[: len(keys[::5])].all()

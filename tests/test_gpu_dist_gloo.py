@@ -45,9 +45,12 @@ def torchrun(world, script, args=(), env_extra=None, timeout=240):
     (2, 191701167547, 13, 20),      # 10B@0.01 %: shards past 2^32 bits (nh > 1, uint64 routes)
     (8, 9585058377, 6, 20),         # the north-star filter over eight owners
     (8, 3834023350947, 13, 20),     # BASELINE configs[4]: 200B@0.01 % partitioned x8 (nh = 2)
+    (6, 3834023350947, 13, 20),     # P * nh = 18 windows: no chunk geometry, plain sync-free windows
 ])
 def test_partitioned_hip_multirank(world, m, k, block_log2):
     cfg = {"m": m, "k": k, "block_log2": block_log2, "n": 800, "seed": 11, "engine": "hip"}
+    if world == 6:
+        cfg["chunks"] = False   # falls back to plain windows, no replays
     out = torchrun(world, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
                    timeout=280)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
@@ -97,6 +100,19 @@ def test_replicated_hip_multirank(world):
     assert "DIST_RESULT ok" in out.stdout
 
 
+@pytest.mark.timeout(300)
+def test_replicated_hip_10b_x8():
+    """BASELINE configs[3]: 10B@0.01 % (m = 191,701,167,547, k = 13, 6.98 GB reachable)
+    replicated on 8 ranks, key batches sharded, through the digests insert and the pipelined
+    sizes_start / gather_start / insert_gathered sequence bench.py --config 10b runs; every
+    replica checked against the oracle (ruby.rb:57-63, compared by nonzero bytes)."""
+    cfg = {"case": "replicated_big", "m": 191701167547, "k": 13, "n": 1500, "seed": 7, "engine": "hip"}
+    out = torchrun(8, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
+                   timeout=280)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
 def test_or_allreduce_device_tensors():
     cfg = {"case": "or_allreduce", "engine": "hip"}
     out = torchrun(3, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
@@ -111,6 +127,7 @@ def test_or_allreduce_device_tensors():
     (4, "1m_big", "partitioned"),   # N >= 4 (auto)
     (2, "nstar", "replicated"),     # the north-star filter at N = 2 (auto: gather insert)
     (4, "nstar", "partitioned"),    # ... and at N = 4
+    (2, "10b", "replicated"),       # BASELINE configs[3]'s layout: digests insert, 6.98 GB replicas
 ])
 def test_bench_multirank_rehearsal(world, config, layout):
     """bench.py's N > 1 step, launched as the driver launches it (torch.distributed.run),
