@@ -184,6 +184,34 @@ int  bf_include_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n,
 int  bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                          uint8_t* d_out, const uint8_t* d_next_key_bytes, const uint64_t* d_next_offsets,
                          uint64_t n_next, uint32_t* d_next_digests, void* stream);
+/* ---- Replicated inserts from region sets (ruby.rb:57-63 on every replica of a replicated
+ *      filter; BASELINE configs[3]'s "replicated on 8 GPUs, key batches sharded").  Each rank
+ *      sorts ITS OWN batch by filter region once and encodes it; the encoded batches of all
+ *      ranks travel (an all-gather of fixed-size buffers); every replica ORs all of them in
+ *      with one pass over its bitset and no sort.  Per region the encoding is the set of
+ *      distinct region-local offsets the batch probes, as an Elias-Fano set (~log2(region bits
+ *      / offsets) + 2 bits per offset: about the size of the keys' SHA-1 words).  The bitset
+ *      after bf_insert_region_sets_dev of every rank's sets equals the one after inserting
+ *      every rank's keys (OR is idempotent and commutative).
+ *   bf_region_sets_capacity  bytes a set buffer needs for any batch of <= n keys (a bound,
+ *                            the same on every handle of this m and k: size the all-gather)
+ *   bf_encode_region_sets_dev / _digests_dev   keys (or their SHA-1 words) -> d_sets
+ *                            (sets_bytes >= the capacity; 16-byte aligned; the filter is not
+ *                            modified).  n = 0 writes an empty set buffer.
+ *   bf_insert_region_sets_dev  nsrc set buffers at d_sets + s * stride_bytes (each written by
+ *                            an encode on a handle of the same m and k) ORed into the filter;
+ *                            probes_hint = the probes they hold (sum of n * k: picks the apply's
+ *                            density form, never the result); d_any_new as bf_insert_many_dev;
+ *                            d_status (nullable) gets 1 ORed in when a buffer's header does not
+ *                            match this filter (that buffer is skipped). */
+int  bf_region_sets_capacity(const bf_handle* h, uint64_t n, uint64_t* bytes);
+int  bf_encode_region_sets_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                               uint32_t* d_sets, uint64_t sets_bytes, void* stream);
+int  bf_encode_region_sets_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint32_t* d_sets,
+                                       uint64_t sets_bytes, void* stream);
+int  bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t stride_bytes, uint32_t nsrc,
+                               uint64_t probes_hint, uint32_t* d_any_new /* nullable */,
+                               uint32_t* d_status /* nullable */, void* stream);
 /* The device bitset (Redis byte order, device_bytes long, zero past the reachable prefix). */
 int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
 /* How an insert batch of n keys will run (no launch): *binned = 1 for the binned

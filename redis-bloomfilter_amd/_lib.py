@@ -87,6 +87,10 @@ SIGNATURES = {
     "bf_insert_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp, _vp]),
     "bf_include_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp]),
     "bf_include_hash_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_region_sets_capacity": (ctypes.c_int, [_vp, _u64, _u64p]),
+    "bf_encode_region_sets_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _vp]),
+    "bf_encode_region_sets_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
+    "bf_insert_region_sets_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _u64, _vp, _vp, _vp]),
     "bf_insert_plan": (ctypes.c_int, [_vp, _u64, _u32p, _u64p]),
     "bf_track_dirty": (ctypes.c_int, [_vp, _u32]),
     "bf_dirty_ranges": (ctypes.c_int, [_vp, _u64p, _u32, _u32p, _u64p, _u32]),
@@ -437,6 +441,30 @@ class Filter:
         _check(self._lib.bf_include_hash_dev(self.handle, d_keys, d_offsets, int(n), d_out, d_next_keys or None,
                                              d_next_offsets or None, int(n_next), d_next_digests or None,
                                              self._s(stream)), self._h)
+
+    # -- replicated inserts from region sets (include/bfhip.h): encode once per rank, OR in everywhere
+    def region_sets_capacity(self, n: int) -> int:
+        """Bytes a region-set buffer needs for any batch of <= n keys (the same on every
+        handle of this m and k)."""
+        b = ctypes.c_uint64()
+        _check(self._lib.bf_region_sets_capacity(self.handle, int(n), ctypes.byref(b)), self._h)
+        return int(b.value)
+
+    def encode_region_sets_dev(self, d_keys: int, d_offsets: int, n: int, d_sets: int, sets_bytes: int,
+                               stream=None) -> None:
+        _check(self._lib.bf_encode_region_sets_dev(self.handle, d_keys or None, d_offsets or None, int(n), d_sets,
+                                                   int(sets_bytes), self._s(stream)), self._h)
+
+    def encode_region_sets_digests_dev(self, d_digests: int, n: int, d_sets: int, sets_bytes: int,
+                                       stream=None) -> None:
+        _check(self._lib.bf_encode_region_sets_digests_dev(self.handle, d_digests or None, int(n), d_sets,
+                                                           int(sets_bytes), self._s(stream)), self._h)
+
+    def insert_region_sets_dev(self, d_sets: int, stride_bytes: int, nsrc: int, probes_hint: int,
+                               d_any_new: int = 0, d_status: int = 0, stream=None) -> None:
+        _check(self._lib.bf_insert_region_sets_dev(self.handle, d_sets, int(stride_bytes), int(nsrc),
+                                                   int(probes_hint), d_any_new or None, d_status or None,
+                                                   self._s(stream)), self._h)
 
     def _s(self, stream):
         if stream is None:

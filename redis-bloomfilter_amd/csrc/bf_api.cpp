@@ -1878,6 +1878,86 @@ int bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
     return BF_OK;
 }
 
+// ---- replicated inserts from region sets (include/bfhip.h) ----
+int bf_region_sets_capacity(const bf_handle* h, uint64_t n, uint64_t* bytes) {
+    if (!h || h->multi || !bytes) return BF_EINVAL;
+    *bytes = bf_sets_capacity_bytes(h->dev_bytes, h->bin_region_log2, n, h->k);
+    return *bytes ? BF_OK : BF_EINVAL;
+}
+
+namespace {
+int encode_sets(bf_handle* h, const uint8_t* d_keys, const uint64_t* d_offsets, uint64_t n, bool dig,
+                uint32_t* d_sets, uint64_t sets_bytes, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (!d_sets || (reinterpret_cast<uintptr_t>(d_sets) & 15u)) return set_err(h, BF_EINVAL, "d_sets must be 16-byte aligned");
+    if (n && (!d_keys || (!dig && !d_offsets))) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (dig && n && (reinterpret_cast<uintptr_t>(d_keys) & 15u)) return set_err(h, BF_EINVAL, "d_digests must be 16-byte aligned");
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter");
+    if (h->engine != BF_ENGINE_RUBY) return set_err(h, BF_EINVAL, "region sets carry the ruby driver's derivation only");
+    uint32_t rl = 0, nbins = 0;
+    if (!bf_sets_geometry(h->dev_bytes, h->bin_region_log2, &rl, &nbins))
+        return set_err(h, BF_EINVAL, "this filter's regions cannot take region sets");
+    const uint64_t need = bf_sets_capacity_bytes(h->dev_bytes, h->bin_region_log2, n, h->k);
+    if (sets_bytes < need)
+        return set_err(h, BF_EINVAL, "sets_bytes %llu < bf_region_sets_capacity %llu", (unsigned long long)sets_bytes,
+                       (unsigned long long)need);
+    BfBinPlan plan{};
+    plan.region_log2 = rl;
+    plan.nbins = nbins;
+    if (n && (!bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, false, &plan) || plan.region_log2 != rl))
+        return set_err(h, BF_EINVAL, "a batch of %llu keys does not sort in one pass (at most %llu keys per set buffer)",
+                       (unsigned long long)n,
+                       (unsigned long long)bf_binned_max_keys(h->k, h->dev_bytes, h->bin_region_log2));
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    if (n) {
+        int rc = ensure_scratch(h, plan.scratch_bytes);
+        if (rc) return rc;
+    }
+    uint64_t bias = 0;
+    const uint8_t* k16 = (n && !dig) ? align_keys(d_keys, &bias) : d_keys;
+    BfMarks* mk = n ? prof_begin(h, so.s) : nullptr;
+    HIPCHK(h, bf_launch_encode_sets(h->g, plan, h->dev_bytes, k16, d_offsets, bias, n, dig, h->d_bin_scratch, d_sets,
+                                    std::min<uint64_t>(sets_bytes / 4, 0xFFFFFFFFull), so.s, mk));
+    return BF_OK;
+}
+}  // namespace
+
+int bf_encode_region_sets_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                              uint32_t* d_sets, uint64_t sets_bytes, void* stream) {
+    return encode_sets(h, d_key_bytes, d_offsets, n, false, d_sets, sets_bytes, stream);
+}
+
+int bf_encode_region_sets_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_t n, uint32_t* d_sets,
+                                      uint64_t sets_bytes, void* stream) {
+    return encode_sets(h, reinterpret_cast<const uint8_t*>(d_digests), nullptr, n, true, d_sets, sets_bytes, stream);
+}
+
+int bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t stride_bytes, uint32_t nsrc,
+                              uint64_t probes_hint, uint32_t* d_any_new, uint32_t* d_status, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (nsrc == 0) return BF_OK;
+    if (!d_sets || (reinterpret_cast<uintptr_t>(d_sets) & 15u) || (stride_bytes & 15u))
+        return set_err(h, BF_EINVAL, "d_sets and stride_bytes must be 16-byte aligned");
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter");
+    uint32_t rl = 0, nbins = 0;
+    if (!bf_sets_geometry(h->dev_bytes, h->bin_region_log2, &rl, &nbins))
+        return set_err(h, BF_EINVAL, "this filter's regions cannot take region sets");
+    if (stride_bytes < 4 * (nbins + 4ull)) return set_err(h, BF_EINVAL, "stride_bytes below a set buffer's header");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    BfMarks* mk = prof_begin(h, so.s);
+    HIPCHK(h, bf_launch_insert_sets(h->g, h->dev_bytes, rl, nbins, d_sets, stride_bytes / 4, nsrc, probes_hint,
+                                    d_any_new, d_status, so.s, mk));
+    return BF_OK;
+}
+
 int bf_stream(bf_handle* h, void** stream) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h || !stream) return BF_EINVAL;

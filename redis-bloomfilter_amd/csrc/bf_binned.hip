@@ -33,6 +33,8 @@
 // answer is the AND of the key's k bits (ruby.rb:20-30) without the early exit.
 #include "bf_device.h"
 
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 using namespace bfdev;
@@ -2426,5 +2428,353 @@ hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t
     const uint64_t grid = (n + tile_keys - 1) / tile_keys;
     hipLaunchKernelGGL(combine_chunks_packed_kernel, dim3((uint32_t)grid), dim3(kCombineLanes), 0, s, packed, slot16,
                        wcap, (wcap + 7) / 8, cg, nwin, counts, n, tile_keys, out);
+    return hipGetLastError();
+}
+
+// ---- replicated inserts from region sets (BASELINE configs[3]'s layout) --------
+//
+// A replicated filter must OR every rank's batch into every replica.  Shipping SHA-1 words
+// (16 B per key, 9.8 bits per probe at k = 13) is compact, but then every replica sorts all
+// P batches' probes by region (the 8 x 2^24-key merged insert at 10B spends 8.8 of its 16.5 ms
+// in bin_front + bin_mid, identical on every replica).  Here each rank sorts ITS OWN batch
+// once (bin_front .. bin_mid) and encodes, per region, the set of distinct region-local offsets
+// its probes hit as an Elias-Fano set: with n offsets in a region of U bits, l = floor(log2(U /
+// n)) low bits of each offset in a packed array, then the high parts in unary (offset i sets
+// bit (x_i >> l) + i of the upper bitmap): n (l + 1) + U / 2^l bits, ~ log2(U / n) + 2 bits per
+// offset, about the SHA-1 words' size (sorted offsets carry no more entropy than that).  A
+// region whose set would exceed U bits is written as its bitmap.  Every replica then ORs all
+// ranks' sets in ONE pass over the bitset (sets_apply_kernel), with no sort at all.
+//
+// A set buffer (uint32 words): [0] magic "BFRS", [1] region_log2, [2] regions R, [3] words used
+// (a cursor; the encode's regions claim their place with one atomic each, so the sets' order
+// in the buffer is arbitrary), [4 + r] region r's first word (0: no offsets), sets from
+// sets_first_word(R).  A set: word 0 = n | (l << 24) (l = 31: bitmap), then ceil(n l / 32)
+// words of low bits (offset i's at bit i l, LSB first), then ceil((n + (U >> l)) / 32) words of
+// the upper bitmap; a bitmap set is the region's U / 32 words in the bitset's own word layout.
+namespace {
+constexpr uint32_t kSetsMagic = 0x53524642u;   // "BFRS"
+constexpr uint32_t kSetsHdr = 4;
+constexpr uint32_t kSetsBitmap = 31u;
+constexpr uint32_t kMaxSetSrc = 16;            // sources per sets_apply launch
+__host__ __device__ inline uint64_t sets_first_word(uint32_t nbins) {
+    return ((uint64_t)kSetsHdr + nbins + 63) & ~(uint64_t)63;
+}
+// bit j of the result <-> region offset 32 w + j (the bitset's word w holds offset 32 w + j at
+// bit j ^ 7: Redis byte order); an involution
+__device__ __forceinline__ uint32_t offset_order(uint32_t w) { return __builtin_bswap32(__builtin_bitreverse32(w)); }
+
+__global__ void sets_header_kernel(uint32_t* __restrict__ out, uint32_t rl, uint32_t nbins, uint32_t zero_offs) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        out[0] = kSetsMagic;
+        out[1] = rl;
+        out[2] = nbins;
+        out[3] = (uint32_t)sets_first_word(nbins);
+    }
+    if (zero_offs && i < nbins) out[kSetsHdr + i] = 0;
+}
+
+// One workgroup per region: the region's probes (level 2, as bin_apply gathers them) into an
+// LDS bitmap, then each lane's WPL consecutive words -> its offsets in ascending order (their
+// ranks from one workgroup scan), the set built in the same LDS (the bitmap words are in
+// registers by then) and copied out.  72 KiB of LDS at 2^19-bit regions: two workgroups per CU.
+template <uint32_t RLOG2, uint32_t LANES>
+__global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __restrict__ level2,
+                                                            const uint32_t* __restrict__ cb_base,
+                                                            const uint32_t* __restrict__ cb_start,
+                                                            const uint16_t* __restrict__ tabs, uint64_t max_chunks,
+                                                            uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
+                                                            uint32_t cap_words) {
+    constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
+    static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
+    __shared__ uint4 s_m4[NW / 4];
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
+    __shared__ uint32_t s_start;
+    uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
+    const uint32_t t = threadIdx.x, r = blockIdx.x;
+    for (uint32_t v = t; v < NW / 4; v += LANES) s_m4[v] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for_region_probes<8>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
+        [&](const uint32_t* idx) {
+            uint32_t l[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) l[c] = idx[c] != 0xFFFFFFFFu ? level2[idx[c]] : 0xFFFFFFFFu;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (l[c] != 0xFFFFFFFFu) atomicOr(s_m + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
+        });
+    uint32_t wv[WPL];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < WPL / 4; ++q) {
+        const uint4 v = s_m4[t * (WPL / 4) + q];
+        wv[4 * q + 0] = offset_order(v.x);
+        wv[4 * q + 1] = offset_order(v.y);
+        wv[4 * q + 2] = offset_order(v.z);
+        wv[4 * q + 3] = offset_order(v.w);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < WPL; ++j) cnt += __popc(wv[j]);
+    uint32_t n;
+    const uint32_t base = block_excl_scan(cnt, s_w, &n);   // its barriers: every lane has read s_m
+    uint32_t l = 0, lw = 0, uw = 0, words = 0;
+    bool bitmap = false;
+    if (n) {
+        l = 31u - __clz(U / n);
+        bitmap = (uint64_t)n * l + n + (U >> l) > U;
+        lw = (n * l + 31u) / 32u;
+        uw = (n + (U >> l) + 31u) / 32u;
+        words = 1u + (bitmap ? NW : lw + uw);
+    }
+    if (t == 0) {
+        uint32_t st = 0;
+        if (n) {
+            st = atomicAdd(out + 3, words);
+            // past the capacity (bf_sets_capacity_bytes bounds every batch, so never): the
+            // region is not written, and out[3] > capacity tells the reader
+            if ((uint64_t)st + words > cap_words) st = 0;
+        }
+        s_start = st;
+        out[kSetsHdr + r] = st;
+    }
+    __syncthreads();
+    const uint32_t st = s_start;
+    if (st == 0) return;   // workgroup-uniform
+    uint32_t* o = out + st;
+    if (bitmap) {   // the LDS bitmap is still intact
+        if (t == 0) o[0] = n | (kSetsBitmap << 24);
+        for (uint32_t v = t; v < NW; v += LANES) o[1 + v] = s_m[v];
+        return;
+    }
+    for (uint32_t v = t; v < lw + uw; v += LANES) s_m[v] = 0;
+    __syncthreads();
+    const uint32_t lmask = (1u << l) - 1u;   // l <= RLOG2 < 32
+    uint32_t i = base;
+#pragma unroll
+    for (uint32_t j = 0; j < WPL; ++j) {
+        uint32_t w = wv[j];
+        const uint32_t x0 = (t * WPL + j) * 32u;
+        while (w) {
+            const uint32_t x = x0 + (uint32_t)__builtin_ctz(w);
+            w &= w - 1u;
+            if (l) {
+                const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
+                atomicOr(s_m + wi, lo << sh);
+                if (sh + l > 32u) atomicOr(s_m + wi + 1, lo >> (32u - sh));
+            }
+            const uint32_t u = lw * 32u + (x >> l) + i;
+            atomicOr(s_m + (u >> 5), 1u << (u & 31u));
+            ++i;
+        }
+    }
+    __syncthreads();
+    if (t == 0) o[0] = n | (l << 24);
+    for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
+}
+
+// One workgroup per region: every source's set for the region ORed into an LDS image (bitmap
+// sets word by word; Elias-Fano sets decoded one pass of LANES upper-bitmap words at a time
+// across all sources: an offset's rank in its set is its rank among all sources' upper bits
+// minus the offsets of the sources before it), then bin_apply's read-OR-write of the region.
+// A source whose header does not match (magic, region geometry, capacity) is skipped and
+// flagged in *status.
+template <uint32_t RLOG2, uint32_t LANES>
+__global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
+                                                           const uint32_t* __restrict__ sets, uint64_t stride_words,
+                                                           uint32_t nsrc, uint32_t nbins, uint32_t dense,
+                                                           uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
+                                                           uint32_t store_fresh, uint32_t* __restrict__ status) {
+    constexpr uint32_t kVec = 1u << (RLOG2 - 7);
+    constexpr uint32_t kPer = kVec / LANES;
+    constexpr uint32_t U = 1u << RLOG2, NW = U / 32;
+    static_assert(kPer * LANES == kVec, "region must tile the workgroup");
+    __shared__ uint4 s_mask4[kVec];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_st[kMaxSetSrc], s_hdr[kMaxSetSrc], s_uw0[kMaxSetSrc + 1], s_np[kMaxSetSrc + 1];
+    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
+    const uint32_t t = threadIdx.x;
+    const uint32_t r = blockIdx.x;
+    const uint64_t v0 = (uint64_t)r * kVec;
+    const uint64_t nvec = nwords / 4;
+    uint4* gv = reinterpret_cast<uint4*>(bits);
+    uint4 old[kPer];
+#pragma unroll
+    for (uint32_t c = 0; c < kPer; ++c) {
+        const uint32_t v = c * LANES + t;
+        old[c] = make_uint4(0, 0, 0, 0);
+        if (dense && v0 + v < nvec) old[c] = apply_load(gv + v0 + v);
+    }
+    for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
+    if (t < nsrc) {   // source t's set for this region
+        const uint32_t* S = sets + (uint64_t)t * stride_words;
+        uint32_t st = 0, hdr = 0;
+        if (S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] <= stride_words) {
+            st = S[kSetsHdr + r];
+            if (st) hdr = S[st];
+        } else if (status) {
+            atomicOr(status, 1u);
+        }
+        s_st[t] = st;
+        s_hdr[t] = hdr;
+    }
+    __syncthreads();
+    if (t == 0) {   // upper-bitmap words and offsets of the Elias-Fano sources before each source
+        uint32_t a = 0, np = 0;
+        for (uint32_t s = 0; s < nsrc; ++s) {
+            s_uw0[s] = a;
+            s_np[s] = np;
+            const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
+            if (s_st[s] && l != kSetsBitmap) {
+                a += (n + (U >> l) + 31u) / 32u;
+                np += n;
+            }
+        }
+        s_uw0[nsrc] = a;
+        s_np[nsrc] = np;
+    }
+    __syncthreads();
+    for (uint32_t s = 0; s < nsrc; ++s) {   // bitmap sets
+        if (!s_st[s] || (s_hdr[s] >> 24) != kSetsBitmap) continue;   // workgroup-uniform
+        const uint32_t* B = sets + (uint64_t)s * stride_words + s_st[s] + 1;
+        for (uint32_t v = t; v < NW; v += LANES) {
+            const uint32_t x = B[v];
+            if (x) atomicOr(s_mask + v, x);
+        }
+    }
+    const uint32_t TW = s_uw0[nsrc];
+    uint32_t carry = 0;
+    for (uint32_t g0 = 0; g0 < TW; g0 += LANES) {   // Elias-Fano sets
+        const uint32_t g = g0 + t;
+        uint32_t word = 0, s = 0;
+        if (g < TW) {
+            while (s + 1 < nsrc && s_uw0[s + 1] <= g) ++s;
+            const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
+            word = sets[(uint64_t)s * stride_words + s_st[s] + 1 + (n * l + 31u) / 32u + (g - s_uw0[s])];
+        }
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);
+        if (word) {
+            const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
+            const uint32_t* lows = sets + (uint64_t)s * stride_words + s_st[s] + 1;
+            const uint32_t lmask = (1u << l) - 1u;
+            uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
+            const uint32_t p0 = (g - s_uw0[s]) * 32u;
+            (void)n;
+            while (word) {
+                const uint32_t p = p0 + (uint32_t)__builtin_ctz(word);
+                word &= word - 1u;
+                uint32_t lo = 0;
+                if (l) {
+                    const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u;
+                    uint64_t two = lows[wi];
+                    if (sh + l > 32u) two |= (uint64_t)lows[wi + 1] << 32;
+                    lo = (uint32_t)(two >> sh) & lmask;
+                }
+                const uint32_t x = ((p - i) << l) | lo;
+                if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
+                ++i;
+            }
+        }
+        carry += tot;
+    }
+    __syncthreads();
+    uint4 msk[kPer];
+#pragma unroll
+    for (uint32_t c = 0; c < kPer; ++c) {
+        const uint32_t v = c * LANES + t;
+        msk[c] = s_mask4[v];
+        if (!dense && v0 + v < nvec && (msk[c].x | msk[c].y | msk[c].z | msk[c].w)) old[c] = apply_load(gv + v0 + v);
+    }
+    uint32_t fresh = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kPer; ++c) {
+        const uint32_t v = c * LANES + t;
+        const uint32_t fr = (msk[c].x & ~old[c].x) | (msk[c].y & ~old[c].y) | (msk[c].z & ~old[c].z) |
+                            (msk[c].w & ~old[c].w);
+        fresh |= fr;
+        if (v0 + v >= nvec) continue;
+        bool stv;
+        if (dense == 2) stv = true;
+        else if (store_fresh) stv = fr != 0u;
+        else stv = (msk[c].x | msk[c].y | msk[c].z | msk[c].w) != 0u;
+        if (stv)
+            apply_store(gv + v0 + v, make_uint4(old[c].x | msk[c].x, old[c].y | msk[c].y, old[c].z | msk[c].z,
+                                                old[c].w | msk[c].w));
+        if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
+    }
+    if (any_flag) report_any_new(any_flag, fresh != 0);
+}
+}  // namespace
+
+bool bf_sets_geometry(uint64_t bitset_bytes, uint32_t pref_region_log2, uint32_t* region_log2, uint32_t* nbins) {
+    BfBinPlan p{};
+    if (!plan_common(bitset_bytes, 1, 1, 1, pref_region_log2, false, &p)) return false;
+    if (p.region_log2 != 18 && p.region_log2 != 19) return false;   // the encode's LDS holds <= 2^19 bits
+    *region_log2 = p.region_log2;
+    *nbins = p.nbins;
+    return true;
+}
+
+uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2, uint64_t n, uint32_t k) {
+    uint32_t rl = 0, R = 0;
+    if (!bf_sets_geometry(bitset_bytes, pref_region_log2, &rl, &R)) return 0;
+    // n k probes hit at most N = n k distinct offsets.  A set of n_r offsets takes < n_r
+    // (log2(U / n_r) + 3) bits (l <= log2(U / n_r), U >> l < 2 n_r), concave in n_r, so over R
+    // regions the total peaks at an even split: N (log2(U R / N) + 3); a bitmap set (U bits)
+    // is taken only below its Elias-Fano size.  Plus 3 words of header and padding per region.
+    const double U = (double)(1ull << rl), N = (double)n * (double)k;
+    double bitsum = 0.0;
+    if (N > 0) bitsum = std::min(N * (std::log2(U * R / N) + 3.0), U * R) * 1.01 + 4096.0;
+    const uint64_t words = sets_first_word(R) + 3ull * R + (uint64_t)(bitsum / 32.0) + 64;
+    return words * 4;
+}
+
+hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,
+                                 const uint64_t* offsets, uint64_t bias, uint64_t n, bool dig, void* scratch,
+                                 uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* mk) {
+    (void)bitset_bytes;
+    if (cap_words >= (1ull << 32)) return hipErrorInvalidValue;
+    const uint32_t hgrid = n ? 1u : (uint32_t)((p.nbins + 255) / 256);
+    hipLaunchKernelGGL(sets_header_kernel, dim3(hgrid), dim3(256), 0, s, out, p.region_log2, p.nbins, n ? 0u : 1u);
+    if (n == 0) return hipGetLastError();
+    if (p.with_keys) return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, nullptr, s, mk, dig);
+    if (e != hipSuccess) return e;
+    if (p.region_log2 == 19)
+        hipLaunchKernelGGL((sets_encode_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, c.level2,
+                           c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, (uint32_t)cap_words);
+    else if (p.region_log2 == 18)
+        hipLaunchKernelGGL((sets_encode_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
+                           c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out,
+                           (uint32_t)cap_words);
+    else
+        return hipErrorInvalidValue;
+    bf_mark(mk, s, "sets_encode");
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_t region_log2, uint32_t nbins,
+                                 const uint32_t* sets, uint64_t stride_words, uint32_t nsrc, uint64_t probes_hint,
+                                 uint32_t* any_flag, uint32_t* status, hipStream_t s, BfMarks* mk) {
+    if (nsrc == 0) return hipSuccess;
+    const uint64_t nwords = bitset_bytes / 4;
+    const uint64_t vecs = (uint64_t)nbins << (region_log2 - 7);
+    const uint32_t dense = probes_hint >= vecs ? 2u : (probes_hint >= vecs / 8 ? 1u : 0u);
+    for (uint32_t s0 = 0; s0 < nsrc; s0 += kMaxSetSrc) {
+        const uint32_t ns = std::min<uint32_t>(kMaxSetSrc, nsrc - s0);
+        const uint32_t* src = sets + (uint64_t)s0 * stride_words;
+        if (region_log2 == 19)
+            hipLaunchKernelGGL((sets_apply_kernel<19, kApplyLanes>), dim3(nbins), dim3(kApplyLanes), 0, s, g.bits,
+                               nwords, src, stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(),
+                               status);
+        else if (region_log2 == 18)
+            hipLaunchKernelGGL((sets_apply_kernel<18, kApplyLanes / 2>), dim3(nbins), dim3(kApplyLanes / 2), 0, s,
+                               g.bits, nwords, src, stride_words, ns, nbins, dense, any_flag, g.dirty,
+                               apply_store_fresh(), status);
+        else
+            return hipErrorInvalidValue;
+    }
+    bf_mark(mk, s, "sets_apply");
     return hipGetLastError();
 }

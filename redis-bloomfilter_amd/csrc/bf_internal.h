@@ -177,6 +177,20 @@ hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_
                                     const uint8_t* keys16, const uint64_t* offsets, uint64_t bias, uint64_t n,
                                     void* scratch, uint8_t* out8, hipStream_t s, BfMarks* marks = nullptr);
 
+// Replicated inserts from region sets (bf_binned.hip): every rank encodes its own
+// batch once as per-region Elias-Fano sets of the offsets it probes; every replica ORs all
+// ranks' sets in with one pass over the bitset.  Geometry: the regions a bitset of this size
+// takes (region_log2 18 or 19; false otherwise).  Capacity: a bound on the set buffer of any
+// batch of n keys.  The encode's plan (bf_binned_plan) must have the geometry's region size.
+bool bf_sets_geometry(uint64_t bitset_bytes, uint32_t pref_region_log2, uint32_t* region_log2, uint32_t* nbins);
+uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2, uint64_t n, uint32_t k);
+hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,
+                                 const uint64_t* offsets, uint64_t bias, uint64_t n, bool dig, void* scratch,
+                                 uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* marks = nullptr);
+hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_t region_log2, uint32_t nbins,
+                                 const uint32_t* sets, uint64_t stride_words, uint32_t nsrc, uint64_t probes_hint,
+                                 uint32_t* any_flag, uint32_t* status, hipStream_t s, BfMarks* marks = nullptr);
+
 // Exact sequential per-key results (bf_seq.hip): batches of at most
 // bf_seq_chunk_keys(k) keys, scratch of bf_seq_scratch_bytes(n, k).  Probe
 // indices i0 .. i0+k-1 (0 for the ruby driver, 1 for the Lua scripts).

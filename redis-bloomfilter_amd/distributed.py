@@ -1028,13 +1028,19 @@ class ReplicatedFilter:
     * ``"digests"``: (i) with every key hashed once, by its own rank: the 16-B SHA-1 words
       (``ruby.rb:42-47``'s h[0..3]) are all-gathered and every replica inserts all of them
       from words (no hash pass) — 16 B per key on the wire instead of ~L + 1, and P - 1
-      fewer SHA-1 passes per replica (``tools/sim_rank.py --replicated P --gathered``).
+      fewer SHA-1 passes per replica (``tools/sim_rank.py --replicated P --gathered``);
+    * ``"sets"``: (i) with every batch also SORTED once, by its own rank: each rank encodes its
+      batch as per-region Elias-Fano sets of the offsets it probes
+      (``bf_encode_region_sets_dev``, about the SHA-1 words' size on the wire), the fixed-size
+      set buffers are all-gathered, and every replica ORs all of them in with one pass over
+      its bitset and no sort (``bf_insert_region_sets_dev``): a replica's insert work no
+      longer repeats every other rank's sort.
 
     ``insert_mode="auto"`` takes (ii) when the bitset is small next to the gathered batches
     (2 * bitset bytes < all ranks' key bytes + lengths), e.g. the 1M@1 % filter (1.2 MB)
     against 2^24-key batches, and (i) otherwise, e.g. the north-star filter (1.2 GB)."""
 
-    MODES = ("auto", "gather", "or", "digests")
+    MODES = ("auto", "gather", "or", "digests", "sets")
 
     def __init__(self, m: int, k: int, group=None, device=None, insert_mode: str = "auto"):
         if insert_mode not in self.MODES:
@@ -1114,6 +1120,15 @@ class ReplicatedFilter:
             mode = "or" if 2 * self.filter.device_bytes < gather_bytes else "gather"
         if mode == "or":
             return dict(mode="or", kb=kb, ko=ko, n=n)
+        if mode == "sets":   # this rank sorts and encodes its batch once; the region sets travel
+            max_n = max(max(sz[1] for sz in all_sizes), 1)
+            cap = self.filter.region_sets_capacity(max_n)   # the same on every rank: one gather size
+            mine = torch.empty(cap // 4, dtype=torch.int32, device=self.device)
+            self.filter.encode_region_sets_dev(kb.data_ptr() if n else 0, ko.data_ptr() if n else 0, n,
+                                               mine.data_ptr(), cap, stream=self._stream())
+            gs = torch.empty(self.P * (cap // 4), dtype=torch.int32, device=self.device)
+            works = [_all_gather_into_tensor(gs, mine, group=self.group, async_op=True)]
+            return dict(mode="sets", kb=kb, ko=ko, n=n, gs=gs, send=mine, works=works, sizes=all_sizes, cap=cap)
         if mode == "digests":   # this rank hashes its batch once; the words travel
             max_n = max(max(sz[1] for sz in all_sizes), 1)
             mine = torch.zeros((max_n, 4), dtype=torch.int32, device=self.device)
@@ -1149,6 +1164,12 @@ class ReplicatedFilter:
             return
         for w in st["works"]:
             w.wait()
+        if st["mode"] == "sets":   # every rank's sets ORed in by one pass over the bitset
+            probes = sum(sz[1] for sz in st["sizes"]) * self.k
+            if probes:
+                self.filter.insert_region_sets_dev(st["gs"].data_ptr(), st["cap"], self.P, probes,
+                                                   stream=self._stream())
+            return
         if st["mode"] == "digests":   # every rank's words as ONE insert (padding rows cut out)
             counts = [sz[1] for sz in st["sizes"]]
             mx = st["max_n"]

@@ -66,7 +66,7 @@ def replicated_case(rank, P, cfg, dev):
     pb, po = O.pack_keys(probe)
     want = orc.include_many(bits, m, k, pb, po).astype(bool)
     ok = True
-    for mode in ("gather", "or", "digests"):
+    for mode in ("gather", "or", "digests", "sets"):
         rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
         rf.insert_many(keys[rank])
         ok = ok and rf.last_insert_mode == mode and rf.export_redis() == want_s
@@ -77,7 +77,7 @@ def replicated_case(rank, P, cfg, dev):
     half = len(keys[rank]) // 2
     kb1, ko1, n1 = D._device_batch(keys[rank][:half], dev)
     kb2, ko2, n2 = D._device_batch(keys[rank][half:], dev)
-    for mode in ("gather", "or", "digests"):
+    for mode in ("gather", "or", "digests", "sets"):
         rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
         st1 = rf.gather_start(kb1, ko1, n1)
         st2 = rf.gather_start(kb2, ko2, n2)
@@ -92,7 +92,7 @@ def replicated_case(rank, P, cfg, dev):
     ub = orc.new_bitset(m, k)
     orc.insert_many(ub, m, k, sb_, so_)
     want_u = orc.redis_string(ub)
-    for mode in ("gather", "or", "digests"):
+    for mode in ("gather", "or", "digests", "sets"):
         rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
         rf.insert_many(keys[rank][:cut[rank]])
         ok = ok and rf.export_redis() == want_u
@@ -168,7 +168,7 @@ def replicated_big_case(rank, P, cfg, dev):
         gp, gv = device_sparse(rf.filter)
         return bool(np.array_equal(gp, wp) and np.array_equal(gv, wv))
 
-    for mode in ("digests", "gather"):
+    for mode in ("digests", "sets", "gather"):
         rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
         rf.insert_many(keys[rank])
         ok = ok and rf.last_insert_mode == mode and same(rf, want_pos, want_val)
@@ -181,30 +181,32 @@ def replicated_big_case(rank, P, cfg, dev):
     third = n // 3
     parts = [keys[rank][:third], keys[rank][third: 2 * third], keys[rank][2 * third:]]
     bt = [D._device_batch(p, dev) for p in parts]
-    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="digests")
-    szp = {0: rf.sizes_start(*bt[0]), 1: rf.sizes_start(*bt[1])}
-    gpend = {0: rf.gather_start(*bt[0], sizes=szp.pop(0))}
-    for i in range(3):
-        st = gpend.pop(i)
-        if i + 1 < 3:
-            gpend[i + 1] = rf.gather_start(*bt[i + 1], sizes=szp.pop(i + 1))
-        if i + 2 < 3:
-            szp[i + 2] = rf.sizes_start(*bt[i + 2])
-        rf.insert_gathered(st)
-    ok = ok and rf.last_insert_mode == "digests" and same(rf, want_pos, want_val)
-    ok = ok and bool((rf.include_many(probe) == want_inc).all())
-    rf.close()
-    if not ok:
-        print("rank %d replicated 10B pipelined MISMATCH" % rank, flush=True)
+    for mode in ("digests", "sets"):
+        rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
+        szp = {0: rf.sizes_start(*bt[0]), 1: rf.sizes_start(*bt[1])}
+        gpend = {0: rf.gather_start(*bt[0], sizes=szp.pop(0))}
+        for i in range(3):
+            st = gpend.pop(i)
+            if i + 1 < 3:
+                gpend[i + 1] = rf.gather_start(*bt[i + 1], sizes=szp.pop(i + 1))
+            if i + 2 < 3:
+                szp[i + 2] = rf.sizes_start(*bt[i + 2])
+            rf.insert_gathered(st)
+        ok = ok and rf.last_insert_mode == mode and same(rf, want_pos, want_val)
+        ok = ok and bool((rf.include_many(probe) == want_inc).all())
+        rf.close()
+        if not ok:
+            print("rank %d replicated 10B pipelined %s MISMATCH" % (rank, mode), flush=True)
     # uneven batches (rank r brings n - 50 r keys; the last rank none): the gathered words
     # are padded to the largest batch and the padding rows cut out before the insert
     cut = [n - 50 * r if r != P - 1 else 0 for r in range(P)]
     sub = [x for r in range(P) for x in keys[r][:cut[r]]]
     up, uv, _ = sparse_bits(orc, sub, m, k)
-    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="digests")
-    rf.insert_many(keys[rank][:cut[rank]])
-    ok = ok and same(rf, up, uv)
-    rf.close()
+    for mode in ("digests", "sets"):
+        rf = D.ReplicatedFilter(m, k, device=dev, insert_mode=mode)
+        rf.insert_many(keys[rank][:cut[rank]])
+        ok = ok and same(rf, up, uv)
+        rf.close()
     if not ok:
         print("rank %d replicated 10B uneven MISMATCH" % rank, flush=True)
     return ok

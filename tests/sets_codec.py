@@ -1,0 +1,69 @@
+"""Host-side reader of the region-set buffers bf_encode_region_sets_dev writes (include/bfhip.h)
+— TEST INFRASTRUCTURE: it decodes a buffer independently of the device decoder, so the
+tests can check the encoding itself against the oracle's offsets (ruby.rb:41-55).
+
+Layout (uint32 words): [0] "BFRS", [1] region_log2, [2] regions R, [3] words used, [4 + r]
+region r's first word (0: empty); a set is n | (l << 24), then ceil(n l / 32) words of low
+bits (offset i's l bits at bit i l, LSB first) and ceil((n + (U >> l)) / 32) words of the upper
+bitmap (offset i sets bit (x_i >> l) + i); l = 31: the region's bitmap in the bitset's own
+word layout (offset x at bit (x & 31) ^ 7 of word x >> 5)."""
+import numpy as np
+
+MAGIC = 0x53524642
+
+
+def header(words: np.ndarray):
+    return int(words[0]), int(words[1]), int(words[2]), int(words[3])
+
+
+def decode(buf) -> dict:
+    """{region: sorted uint64 array of region-local offsets} of one set buffer."""
+    w = np.frombuffer(bytes(buf), dtype=np.uint32) if not isinstance(buf, np.ndarray) else buf.view(np.uint32)
+    magic, rl, R, used = header(w)
+    assert magic == MAGIC, "not a region-set buffer"
+    assert used <= len(w), "set buffer overflowed its capacity"
+    U = 1 << rl
+    out = {}
+    for r in range(R):
+        st = int(w[4 + r])
+        if st == 0:
+            continue
+        hdr = int(w[st])
+        n, l = hdr & 0xFFFFFF, hdr >> 24
+        if l == 31:
+            bm = w[st + 1: st + 1 + U // 32]
+            bits = np.unpackbits(bm.view(np.uint8), bitorder="big")   # byte-major, MSB first = Redis order
+            xs = np.flatnonzero(bits).astype(np.uint64)
+            assert len(xs) == n, "bitmap set: count mismatch"
+            out[r] = xs
+            continue
+        lw = (n * l + 31) // 32
+        uw = (n + (U >> l) + 31) // 32
+        lows_w = w[st + 1: st + 1 + lw]
+        up_w = w[st + 1 + lw: st + 1 + lw + uw]
+        up = np.unpackbits(up_w.view(np.uint8), bitorder="little")
+        pos = np.flatnonzero(up)
+        assert len(pos) == n, "upper bitmap: %d ones for %d offsets" % (len(pos), n)
+        high = pos - np.arange(n)
+        if l:
+            lb = np.unpackbits(lows_w.view(np.uint8), bitorder="little")[: n * l].reshape(n, l)
+            lows = (lb.astype(np.uint64) << np.arange(l, dtype=np.uint64)).sum(axis=1)
+        else:
+            lows = np.zeros(n, np.uint64)
+        xs = (high.astype(np.uint64) << np.uint64(l)) | lows
+        assert np.all(np.diff(xs.astype(np.int64)) > 0), "offsets not strictly ascending"
+        out[r] = xs
+    return out
+
+
+def expected(idx: np.ndarray, region_log2: int) -> dict:
+    """{region: sorted distinct region-local offsets} of a batch's probe offsets."""
+    u = np.unique(np.asarray(idx, dtype=np.uint64).reshape(-1))
+    reg = (u >> np.uint64(region_log2)).astype(np.int64)
+    loc = u & np.uint64((1 << region_log2) - 1)
+    out = {}
+    if len(u):
+        cut = np.flatnonzero(np.diff(reg)) + 1
+        for part_r, part_x in zip(np.split(reg, cut), np.split(loc, cut)):
+            out[int(part_r[0])] = part_x
+    return out

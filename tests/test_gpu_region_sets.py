@@ -1,0 +1,193 @@
+"""Replicated inserts from region sets (include/bfhip.h: bf_region_sets_capacity,
+bf_encode_region_sets_dev / _digests_dev, bf_insert_region_sets_dev) against the oracle.
+
+* the encoding itself: every region's decoded set (tests/sets_codec.py, a host reader
+  independent of the device decoder) equals the distinct offsets the oracle derives for the
+  batch (ruby.rb:41-55), in Elias-Fano and bitmap form, at 2^19- and 2^18-bit regions;
+* the insert: the sets of several batches ORed into a filter give the bitset inserting all of
+  their keys gives (ruby.rb:57-63), on an empty and a prefilled filter, with any_new as the
+  reference's !found (ruby.rb:61); a foreign buffer is skipped and flagged."""
+import numpy as np
+import pytest
+
+import sets_codec
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED + 404
+
+
+def _dev(torch, buf, offs):
+    kb = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).cuda()
+    ko = torch.from_numpy(offs.view(np.int64)).cuda()
+    return kb, ko
+
+
+def _keys(pkg, rng, n, tag="s"):
+    return pkg.keys.pack(["%s%d" % (tag, int(v)) for v in rng.integers(0, 10**12, size=n)])
+
+
+def _encode(torch, f, buf, offs, digests=False, cap=None):
+    n = len(offs) - 1
+    cap = cap or f.region_sets_capacity(n)
+    sets = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+    if n and digests:
+        kb, ko = _dev(torch, buf, offs)
+        dig = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        f.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, dig.data_ptr(), stream=0)
+        f.encode_region_sets_digests_dev(dig.data_ptr(), n, sets.data_ptr(), cap, stream=0)
+    elif n:
+        kb, ko = _dev(torch, buf, offs)
+        f.encode_region_sets_dev(kb.data_ptr(), ko.data_ptr(), n, sets.data_ptr(), cap, stream=0)
+    else:
+        f.encode_region_sets_dev(0, 0, 0, sets.data_ptr(), cap, stream=0)
+    torch.cuda.synchronize()
+    return sets
+
+
+def _nonzero_bytes(torch, f):
+    torch.cuda.synchronize()
+    ptr, nbytes = f.device_bits()
+
+    class _B:
+        __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+    t = torch.as_tensor(_B(), device="cuda")
+    nz = torch.nonzero(t).view(-1)
+    return nz.cpu().numpy(), t[nz].cpu().numpy()
+
+
+def _want_sparse(idx):
+    u = np.unique(np.asarray(idx, np.uint64).reshape(-1))
+    pos = (u >> np.uint64(3)).astype(np.int64)
+    mask = (np.uint64(0x80) >> (u & np.uint64(7))).astype(np.uint8)
+    if not len(u):
+        return pos, mask
+    st = np.flatnonzero(np.concatenate([[True], pos[1:] != pos[:-1]]))
+    return pos[st], np.bitwise_or.reduceat(mask, st)
+
+
+@pytest.mark.parametrize("rl", ["19", "18"])
+@pytest.mark.parametrize("m,k,n", [
+    (9585058, 6, 40_000),           # 1M@1 %: 19 regions, dense (bitmap and low-l sets)
+    (1437758757, 10, 20_000),       # 100M@0.1 %: sparse, large l
+    (9585058377, 6, 200_000),       # the north-star filter
+    (191701167547, 13, 100_000),    # 10B@0.01 % (reach-capped 6.98 GB): 106k regions
+])
+def test_encoded_sets_equal_oracle_offsets(pkg, oracle, monkeypatch, rl, m, k, n):
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("BFHIP_BIN_REGION_LOG2", rl)
+    rng = np.random.default_rng(SEED + k + int(rl))
+    buf, offs = _keys(pkg, rng, n)
+    want = sets_codec.expected(oracle.indexes_many(buf, offs, m, k), int(rl))
+    with pkg.Filter(m, k) as f:
+        for digests in (False, True):
+            sets = _encode(torch, f, buf, offs, digests=digests)
+            words = sets.cpu().numpy().view(np.uint32)
+            magic, got_rl, R, used = sets_codec.header(words)
+            assert (magic, got_rl) == (sets_codec.MAGIC, int(rl)) and used <= len(words)
+            got = sets_codec.decode(words)
+            assert sorted(got) == sorted(want)
+            for r in want:
+                np.testing.assert_array_equal(got[r], want[r])
+
+
+def test_bitmap_and_empty_sets(pkg, oracle):
+    """A region hit by most of its offsets is written as its bitmap; an empty batch is a valid
+    empty buffer (every region absent)."""
+    torch = pytest.importorskip("torch")
+    m, k = 1 << 20, 6   # two 2^19-bit regions
+    rng = np.random.default_rng(SEED)
+    buf, offs = _keys(pkg, rng, 300_000)
+    with pkg.Filter(m, k) as f:
+        words = _encode(torch, f, buf, offs).cpu().numpy().view(np.uint32)
+        hdrs = [int(words[int(words[4 + r])]) >> 24 for r in range(2)]
+        assert hdrs == [31, 31]
+        want = sets_codec.expected(oracle.indexes_many(buf, offs, m, k), 19)
+        got = sets_codec.decode(words)
+        for r in want:
+            np.testing.assert_array_equal(got[r], want[r])
+        empty = _encode(torch, f, buf[:0], offs[:1]).cpu().numpy().view(np.uint32)
+        assert sets_codec.decode(empty) == {}
+
+
+@pytest.mark.parametrize("m,k,n", [
+    (9585058, 6, 30_000),
+    (1437758757, 10, 30_000),
+    (9585058377, 6, 100_000),
+    (191701167547, 13, 60_000),
+])
+def test_insert_sets_equals_inserting_the_keys(pkg, oracle, m, k, n):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(SEED + 7 * k)
+    batches = [_keys(pkg, rng, n, "a"), _keys(pkg, rng, n // 3, "b"), _keys(pkg, rng, 0, "c"), _keys(pkg, rng, n, "d")]
+    with pkg.Filter(m, k) as f:
+        cap = max(f.region_sets_capacity(len(o) - 1) for _, o in batches)
+        sets = torch.cat([_encode(torch, f, b, o, cap=cap) for b, o in batches])
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        probes = sum(len(o) - 1 for _, o in batches) * k
+        f.insert_region_sets_dev(sets.data_ptr(), cap, len(batches), probes, d_any_new=flag.data_ptr(),
+                                 d_status=status.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(flag.item()) == 1 and int(status.item()) == 0
+        idx = np.concatenate([oracle.indexes_many(b, o, m, k).reshape(-1) for b, o in batches])
+        got_p, got_v = _nonzero_bytes(torch, f)
+        want_p, want_v = _want_sparse(idx)
+        np.testing.assert_array_equal(got_p, want_p)
+        np.testing.assert_array_equal(got_v, want_v)
+        # the same sets again change nothing: any_new stays 0 (every probe hits a set bit)
+        flag.zero_()
+        f.insert_region_sets_dev(sets.data_ptr(), cap, len(batches), probes, d_any_new=flag.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(flag.item()) == 0
+
+
+@pytest.mark.parametrize("m,k", [(9585058, 6), (9585058377, 6)])
+def test_insert_sets_into_prefilled_filter_and_include(pkg, oracle, m, k):
+    """OR into a filter already holding bits (a Redis string imported), then include? answers
+    and the exported string equal the oracle's insert of the same keys into that string."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(SEED + 99)
+    pre_b, pre_o = _keys(pkg, rng, 20_000, "p")
+    batches = [_keys(pkg, rng, 25_000, "x%d" % s) for s in range(5)]
+    with pkg.Filter(m, k) as f:
+        f.insert_many(pre_b, pre_o)
+        cap = f.region_sets_capacity(25_000)
+        sets = torch.cat([_encode(torch, f, b, o, cap=cap) for b, o in batches])
+        f.insert_region_sets_dev(sets.data_ptr(), cap, len(batches), 5 * 25_000 * k, stream=0)
+        torch.cuda.synchronize()
+        probe_b, probe_o = _keys(pkg, rng, 5_000, "x2")
+        got_inc = f.include_many(probe_b, probe_o)
+        got_s = f.export_redis() if m < 10**8 else None
+    if m < 10**8:
+        bits = oracle.new_bitset(m, k)
+        oracle.insert_many(bits, m, k, pre_b, pre_o)
+        for b, o in batches:
+            oracle.insert_many(bits, m, k, b, o)
+        assert got_s == oracle.redis_string(bits)
+        np.testing.assert_array_equal(got_inc, oracle.include_many(bits, m, k, probe_b, probe_o))
+    else:
+        idx = np.concatenate([oracle.indexes_many(b, o, m, k).reshape(-1) for b, o in [(pre_b, pre_o)] + batches])
+        pidx = oracle.indexes_many(probe_b, probe_o, m, k)
+        want = np.isin(pidx, np.unique(idx)).all(axis=1)
+        np.testing.assert_array_equal(got_inc.astype(bool), want)
+
+
+def test_foreign_set_buffer_is_skipped(pkg):
+    """A buffer encoded for another filter size does not match this filter's regions: it is
+    skipped (no bit set) and d_status flags it; the ABI refuses a short capacity."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(SEED + 5)
+    buf, offs = _keys(pkg, rng, 10_000)
+    with pkg.Filter(1437758757, 10) as other, pkg.Filter(9585058, 6) as f:
+        sets = _encode(torch, other, buf, offs)
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        cap = sets.numel() * 4
+        f.insert_region_sets_dev(sets.data_ptr(), cap, 1, 60_000, d_status=status.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(status.item()) == 1 and f.export_redis() == b""
+        kb, ko = _dev(torch, buf, offs)
+        small = torch.zeros(64, dtype=torch.int32, device="cuda")
+        with pytest.raises(pkg.ArgumentError):
+            f.encode_region_sets_dev(kb.data_ptr(), ko.data_ptr(), 10_000, small.data_ptr(), 256, stream=0)

@@ -47,9 +47,11 @@ def main():
                     help="R > 0: one replica's step of the replicated layout at world size R (BASELINE "
                          "configs[3]): ONE merged insert of every rank's batch (R x batch keys) into the whole "
                          "filter, then this rank's include? batch")
-    ap.add_argument("--gathered", default="keys", choices=["keys", "digests"],
+    ap.add_argument("--gathered", default="keys", choices=["keys", "digests", "sets"],
                     help="replicated: what travels — key bytes (every replica hashes every batch: "
-                         "ReplicatedFilter) or 16-B SHA-1 words (each key hashed once, by its own rank)")
+                         "ReplicatedFilter), 16-B SHA-1 words (each key hashed once, by its own rank), or "
+                         "region sets (each batch hashed, sorted and encoded once, by its own rank; every "
+                         "replica ORs all R ranks' sets in without sorting)")
     ap.add_argument("--dig", action="store_true",
                     help="--chunks: route the include? batch from SHA-1 words that the previous step's owner "
                          "test hashed between its probe rounds (bf_shard_test_chunks_hash_dev + "
@@ -268,6 +270,14 @@ def replicated(args, pkg):
         if args.gathered == "digests":   # the words every rank's batch arrives as (hashed by its rank)
             dg = torch.empty((R * batch, 4), dtype=torch.int32, device=dev)
             f.hash_many_dev(mkb.data_ptr(), mko.data_ptr(), R * batch, dg.data_ptr())
+        elif args.gathered == "sets":   # what the all-gather delivers: every rank's set buffer (rank 0 = own,
+            # re-encoded inside the timed step)
+            cap = f.region_sets_capacity(batch)
+            dg = torch.empty(R * (cap // 4), dtype=torch.int32, device=dev)
+            for r, ((ikb, iko), _) in enumerate(per):
+                f.encode_region_sets_dev(ikb.data_ptr(), iko.data_ptr(), batch, dg[r * (cap // 4):].data_ptr(), cap)
+            torch.cuda.synchronize()
+            mkb, mko = per[0][0]   # own batch's keys
         steps.append((mkb, mko, per[0][1], dg))
     nm = R * batch
     out = torch.empty(batch, dtype=torch.uint8, device=dev)
@@ -275,9 +285,14 @@ def replicated(args, pkg):
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     sp = torch.cuda.current_stream(dev).cuda_stream
 
+    cap_sets = f.region_sets_capacity(batch) if args.gathered == "sets" else 0
+
     def step(s_):
         mkb, mko, (qkb, qko), dg = s_
-        if args.gathered == "digests":   # this rank hashes its own batch; all R batches go in from words
+        if args.gathered == "sets":   # own batch sorted + encoded (into rank 0's slot), then all R sets in
+            f.encode_region_sets_dev(mkb.data_ptr(), mko.data_ptr(), batch, dg.data_ptr(), cap_sets, stream=sp)
+            f.insert_region_sets_dev(dg.data_ptr(), cap_sets, R, R * batch * k, d_any_new=flag.data_ptr(), stream=sp)
+        elif args.gathered == "digests":   # this rank hashes its own batch; all R batches go in from words
             f.hash_many_dev(mkb.data_ptr(), mko.data_ptr(), batch, own.data_ptr(), stream=sp)
             f.insert_digests_dev(dg.data_ptr(), nm, d_any_new=flag.data_ptr(), stream=sp)
         else:
@@ -298,6 +313,9 @@ def replicated(args, pkg):
     one = None
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered, "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
+           "gathered_bytes_per_rank": (cap_sets if args.gathered == "sets" else
+                                       batch * 16 if args.gathered == "digests" else None),
+           "sets_used_bytes_per_rank": int(steps[-1][3][3].item()) * 4 if args.gathered == "sets" else None,
            "ms_per_step_compute": wall * 1e3,
            "kernels_ms_per_step": {name: ms / args.steps for name, (ms, _) in prof.items()},
            "kernels_ms_sum": sum(ms for ms, _ in prof.values()) / args.steps,
