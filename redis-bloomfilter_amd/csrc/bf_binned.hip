@@ -1080,6 +1080,19 @@ __device__ __forceinline__ void apply_store(uint4* p, uint4 v) {
     __builtin_nontemporal_store(x, reinterpret_cast<apply_u32x4*>(p));
 }
 
+// Workgroup b's region.  xg > 1: xg consecutive regions on one XCD (workgroups b, b + 8, ...
+// b + 8 (xg - 1) run on XCD b % 8 at about the same time), so the level-2 lines two
+// neighbouring regions' runs share are fetched into one L2 once instead of into two; every XCD
+// still sweeps the same 8 xg-region neighbourhood (a contiguous eighth per XCD measured
+// slower).  A tail of fewer than 8 xg regions keeps the identity map.
+__device__ __forceinline__ uint32_t apply_region(uint32_t b, uint32_t nb, uint32_t xg) {
+    if (xg <= 1) return b;
+    const uint32_t span = 8u * xg, full = nb - nb % span;
+    if (b >= full) return b;
+    const uint32_t w = b % span;
+    return b - w + (w & 7u) * xg + (w >> 3);
+}
+
 template <uint32_t RLOG2, uint32_t LANES>
 __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
                                                           const uint32_t* __restrict__ level2,
@@ -1088,7 +1101,8 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
                                                           const uint16_t* __restrict__ tabs, uint64_t max_chunks,
                                                           uint32_t nq, uint32_t rel_log2, uint32_t dense,
                                                           uint32_t* __restrict__ any_flag,
-                                                          uint8_t* __restrict__ dirty, uint32_t store_fresh) {
+                                                          uint8_t* __restrict__ dirty, uint32_t store_fresh,
+                                                          uint32_t xg) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
     constexpr uint32_t kPer = kVec / LANES;
     constexpr int kLoads = 8;
@@ -1097,7 +1111,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
-    const uint32_t r = blockIdx.x;
+    const uint32_t r = apply_region(blockIdx.x, gridDim.x, xg);
     const uint64_t v0 = (uint64_t)r * kVec;
     const uint64_t nvec = nwords / 4;
     uint4* gv = reinterpret_cast<uint4*>(bits);
@@ -1971,6 +1985,15 @@ uint32_t apply_store_fresh() {
     return v;
 }
 
+// bin_apply's regions per XCD group (apply_region): BFHIP_APPLY_XG, A/B.
+uint32_t apply_xcd_group() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("BFHIP_APPLY_XG");
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
+    return v;
+}
+
 // Workgroups of the persistent dense apply (bin_apply_pipe_kernel): one per CU (an LDS image
 // plus two run-table buffers; 4 waves per SIMD for its register pipeline).  BFHIP_APPLY_PIPE_GRID=n overrides it; 0 takes bin_apply_kernel (A/B).
 uint32_t apply_pipe_grid() {
@@ -2019,15 +2042,15 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     } else if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
-                           p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
+                           p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh(), apply_xcd_group());
     else if (p.region_log2 == 19)
         hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag, g.dirty, apply_store_fresh());
+                           any_flag, g.dirty, apply_store_fresh(), apply_xcd_group());
     else
         hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag, g.dirty, apply_store_fresh());
+                           any_flag, g.dirty, apply_store_fresh(), apply_xcd_group());
     bf_mark(mk, s, "bin_apply");
     return hipGetLastError();
 }
@@ -2653,22 +2676,33 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         }
         uint32_t tot;
         const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);
-        if (word) {
+        if (word) {   // ~16 offsets: their low bits are consecutive, read through a 3-word window
             const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
             const uint32_t* lows = sets + (uint64_t)s * stride_words + s_st[s] + 1;
             const uint32_t lmask = (1u << l) - 1u;
             uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
             const uint32_t p0 = (g - s_uw0[s]) * 32u;
-            (void)n;
+            const uint32_t lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
+            uint32_t wi = (i * l) >> 5;
+            uint32_t a = 0, b = 0, c = 0;
+            if (l) {   // loaded together, one word ahead of use
+                a = lows[wi];
+                b = lows[min(wi + 1u, lim)];
+                c = lows[min(wi + 2u, lim)];
+            }
             while (word) {
                 const uint32_t p = p0 + (uint32_t)__builtin_ctz(word);
                 word &= word - 1u;
                 uint32_t lo = 0;
                 if (l) {
-                    const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u;
-                    uint64_t two = lows[wi];
-                    if (sh + l > 32u) two |= (uint64_t)lows[wi + 1] << 32;
-                    lo = (uint32_t)(two >> sh) & lmask;
+                    const uint32_t bp = i * l;
+                    while ((bp >> 5) != wi) {
+                        a = b;
+                        b = c;
+                        ++wi;
+                        c = lows[min(wi + 2u, lim)];
+                    }
+                    lo = (uint32_t)(((uint64_t)b << 32 | a) >> (bp & 31u)) & lmask;
                 }
                 const uint32_t x = ((p - i) << l) | lo;
                 if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
