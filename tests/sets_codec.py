@@ -67,3 +67,48 @@ def expected(idx: np.ndarray, region_log2: int) -> dict:
         for part_r, part_x in zip(np.split(reg, cut), np.split(loc, cut)):
             out[int(part_r[0])] = part_x
     return out
+
+
+def encode(sets: dict, region_log2: int, nregions: int) -> np.ndarray:
+    """A set buffer holding `sets` ({region: sorted distinct offsets}), laid out as the device
+    encode lays it out (regions in index order; the device's order is arbitrary)."""
+    U = 1 << region_log2
+    first = (4 + nregions + 63) // 64 * 64
+    words = [0] * first
+    words[0], words[1], words[2] = MAGIC, region_log2, nregions
+    for r in range(nregions):
+        xs = np.asarray(sets.get(r, []), dtype=np.uint64)
+        n = len(xs)
+        if n == 0:
+            continue
+        words[4 + r] = len(words)
+        l = int(np.floor(np.log2(U // n))) if n else 0
+        if n * l + n + (U >> l) > U:   # bitmap
+            bits = np.zeros(U, np.uint8)
+            bits[xs.astype(np.int64)] = 1
+            words.append(n | (31 << 24))
+            words.extend(np.packbits(bits, bitorder="big").view(np.uint32).tolist())
+            continue
+        lw = (n * l + 31) // 32
+        uw = (n + (U >> l) + 31) // 32
+        lowbits = np.zeros(lw * 32, np.uint8)
+        if l:
+            lo = xs & np.uint64((1 << l) - 1)
+            lowbits[: n * l] = ((lo[:, None] >> np.arange(l, dtype=np.uint64)) & np.uint64(1)).astype(np.uint8).reshape(-1)
+        up = np.zeros(uw * 32, np.uint8)
+        up[(xs >> np.uint64(l)).astype(np.int64) + np.arange(n)] = 1
+        words.append(n | (l << 24))
+        words.extend(np.packbits(lowbits, bitorder="little").view(np.uint32).tolist())
+        words.extend(np.packbits(up, bitorder="little").view(np.uint32).tolist())
+    words[3] = len(words)
+    return np.asarray(words, dtype=np.uint32)
+
+
+def capacity_words(bitset_bytes: int, region_log2: int, n_keys: int, k: int) -> int:
+    """bf_sets_capacity_bytes / 4 (bf_binned.hip), restated for the host tests."""
+    R = -(-(bitset_bytes * 8) // (1 << region_log2))
+    U, N = float(1 << region_log2), float(n_keys * k)
+    bits = 0.0
+    if N > 0:
+        bits = min(N * (np.log2(U * R / N) + 3.0), U * R) * 1.01 + 4096.0
+    return (4 + R + 63) // 64 * 64 + 3 * R + int(bits / 32.0) + 64
