@@ -761,8 +761,11 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         const uint64_t seg = key0 * k;
         const uint32_t tp = tk * k;
         if constexpr (WIN) {
+            // the window of sorted entry j: one search for the lane's first entry, then forward
+            // steps (its entries are kTile apart, a window holds ~tp / P of them)
+            uint32_t o = run_of(s_obase, P, t < tp ? t : 0u);
             for (uint32_t j = t; j < tp; j += kTile) {
-                const uint32_t o = run_of(s_obase, P, j);
+                while (o + 1u < P && s_obase[o + 1u] <= j) ++o;
                 const unsigned long long gb = s_gbase[o];   // the run's place in owner o's window
                 if (gb != ~0ull) {
                     const uint64_t d = gb + (j - s_obase[o]);
