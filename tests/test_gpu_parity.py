@@ -315,8 +315,13 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
         assert f.export_redis() == s
 
 
-@pytest.mark.parametrize("rl", ["18", "19", "20"])
-@pytest.mark.parametrize("case", ["dup", "tiny", "long", "k12", "k13", "k16", "nstar"])
+# Every case at the default 2^19-bit regions; the 2^18 / 2^20 templates (512-lane apply / test,
+# 128 KiB LDS images) on the cheap cases, and the 10B filter at 2^20 (at 2^18 it takes 2^19)
+EDGE_CASES = ([("19", c) for c in ("dup", "tiny", "long", "k12", "k13", "k16", "nstar")] +
+              [("18", c) for c in ("dup", "long", "k12")] + [("20", c) for c in ("dup", "long", "k12", "k13")])
+
+
+@pytest.mark.parametrize("rl,case", EDGE_CASES)
 def test_binned_edge_cases(pkg, oracle, monkeypatch, rl, case):
     """Forced binned insert and include? on shapes that stress their partition passes: one key repeated
     (every probe in <= k regions, one superbin run per tile holding thousands of probes),
