@@ -204,6 +204,13 @@ def prefill_random(f, m: int, k: int, rank: int, host_copy: bool = True):
     return host
 
 
+# The replicated layout's insert form per config (ReplicatedFilter insert_mode; "auto" picks
+# key bytes or the OR-all-reduce by size).  10B@0.01 % (k = 13): the SHA-1 words travel, so
+# every replica skips P - 1 hash passes (tools/sim_rank.py --replicated 8:
+# profiles/r03_sim_replicated8_10b.jsonl).
+REPLICATED_INSERT = {"10b": "digests"}
+
+
 def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
     """single at N = 1.  BASELINE's own layouts for its multi-GPU configs: 10b (configs[3],
     "10B keys replicated on 8 GPUs, key batches sharded") replicated, 200b (configs[4])
@@ -225,7 +232,8 @@ def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
 
 
 def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=False, mode: str = "auto",
-                overlap: bool = True, pipeline: bool = False, comm_prefetch: bool = False):
+                overlap: bool = True, pipeline: bool = False, comm_prefetch: bool = False,
+                replicated_insert: str = "auto"):
     n, p, batch, prefill = CONFIGS[name]
     B = pkg.Bloomfilter
     m = B.optimal_m(n, p)
@@ -238,10 +246,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         mode = auto_mode(D.world, m, k, name)
     rf = None
     if mode == "replicated":   # every rank a whole replica: include? local, inserts all-gathered
-        # 10B@0.01 % (k = 13): the SHA-1 words travel, so every replica skips P - 1 hash passes
-        # (tools/sim_rank.py --replicated 8: profiles/r03_sim_replicated8_10b.jsonl); elsewhere
-        # key bytes (fewer bytes on the one xGMI link of N = 2) or the OR-all-reduce
-        rf = pkg.distributed.ReplicatedFilter(m, k, device=dev, insert_mode="digests" if name == "10b" else "auto")
+        if replicated_insert == "auto":
+            replicated_insert = REPLICATED_INSERT.get(name, "auto")
+        rf = pkg.distributed.ReplicatedFilter(m, k, device=dev, insert_mode=replicated_insert)
         f = rf.filter
         if prefill == "random":   # identical replicas: the same bits on every rank
             prefill_random(f, m, k, 0, host_copy=f.device_bytes < (4 << 30))
@@ -838,6 +845,9 @@ def main():
                     help="1 = exchange the next step's insert batch during this step (replicated: gather "
                          "its keys, then insert every rank's batch as one insert; partitioned: route and "
                          "send its probes beside this step's owner kernels); 0 = within the step")
+    ap.add_argument("--replicated-insert", default="auto", choices=["auto", "gather", "or", "digests", "sets"],
+                    help="replicated layout: what every rank's insert batch travels as (ReplicatedFilter "
+                         "insert_mode); auto: the per-config choice REPLICATED_INSERT, else by size")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL) is the measured path; gloo rehearses N > 1 with host-staged "
                          "exchanges, several ranks per GPU allowed (not a performance number)")
@@ -862,7 +872,7 @@ def main():
     pkg = pkgload.load()
     main_res, data = time_config(pkg, D, args.config, args.steps, args.warmup, want_host=(D.world == 1 and not args.no_host_api),
                                   mode=args.mode, overlap=not args.no_overlap, pipeline=bool(args.pipeline),
-                                  comm_prefetch=bool(args.comm_prefetch))
+                                  comm_prefetch=bool(args.comm_prefetch), replicated_insert=args.replicated_insert)
     secondary = {}
     if D.world == 1 and not args.no_secondary:
         # 1m_big: the L2-resident 1M@1 % filter at 2^24-key batches (hash-bound; 1m's 2^20-key
