@@ -2471,10 +2471,12 @@ hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t
 // region whose set would exceed U bits is written as its bitmap.  Every replica then ORs all
 // ranks' sets in ONE pass over the bitset (sets_apply_kernel), with no sort at all.
 //
-// A set buffer (uint32 words): [0] magic "BFRS", [1] region_log2, [2] regions R, [3] words used
-// (a cursor; the encode's regions claim their place with one atomic each, so the sets' order
-// in the buffer is arbitrary), [4 + r] region r's first word (0: no offsets), sets from
-// sets_first_word(R).  A set: word 0 = n | (l << 24) (l = 31: bitmap), then ceil(n l / 32)
+// A set buffer (uint32 words): [0] magic "BFRS", [1] region_log2, [2] regions R, [3] words
+// reserved, [4 + r] region r's first word (0: no offsets), sets from sets_first_word(R) in
+// region order.  Region r's place is reserved before the encode (sets_size_kernel +
+// sets_place_kernel): its probe count E_r from the level-2 run tables bounds its set at
+// sets_region_words(E_r) words, so the encode needs no allocator and the layout is a function
+// of the batch alone.  A set: word 0 = n | (l << 24) (l = 31: bitmap), then ceil(n l / 32)
 // words of low bits (offset i's at bit i l, LSB first), then ceil((n + (U >> l)) / 32) words of
 // the upper bitmap; a bitmap set is the region's U / 32 words in the bitset's own word layout.
 namespace {
@@ -2489,7 +2491,8 @@ __host__ __device__ inline uint64_t sets_first_word(uint32_t nbins) {
 // bit j ^ 7: Redis byte order); an involution
 __device__ __forceinline__ uint32_t offset_order(uint32_t w) { return __builtin_bswap32(__builtin_bitreverse32(w)); }
 
-__global__ void sets_header_kernel(uint32_t* __restrict__ out, uint32_t rl, uint32_t nbins, uint32_t zero_offs) {
+// An empty batch's buffer: the header and every region absent.
+__global__ void sets_header_kernel(uint32_t* __restrict__ out, uint32_t rl, uint32_t nbins) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) {
         out[0] = kSetsMagic;
@@ -2497,7 +2500,62 @@ __global__ void sets_header_kernel(uint32_t* __restrict__ out, uint32_t rl, uint
         out[2] = nbins;
         out[3] = (uint32_t)sets_first_word(nbins);
     }
-    if (zero_offs && i < nbins) out[kSetsHdr + i] = 0;
+    if (i < nbins) out[kSetsHdr + i] = 0;
+}
+
+// A bound on the words of the set of a region its batch probes E times: the set has n <= E
+// offsets and takes < n (log2(U / n) + 3) bits (l <= log2(U / n), U >> l < 2 n), increasing in
+// n, or U bits as a bitmap (only when that is smaller); + a header word and two words of
+// padding.  bf_sets_capacity_bytes bounds the sum over the regions (concave in E).
+__device__ __forceinline__ uint32_t sets_region_words(uint32_t E, uint32_t U) {
+    if (E == 0) return 0;
+    const double e = (double)min(E, U), bits = e * (__log2f((float)((double)U / e)) + 3.01);
+    return 4u + (uint32_t)((bits < (double)U ? bits : (double)U) / 32.0);
+}
+
+// Per superbin: region r's probe count E_r = sum over the superbin's level-2 blocks of its run
+// length (a telescoping sum of the [region][block] run-start rows), its set's reserved words
+// into out[4 + r] (sets_place_kernel turns them into places).
+__global__ __launch_bounds__(1024) void sets_size_kernel(const uint16_t* __restrict__ tabs,
+                                                         const uint32_t* __restrict__ cb_base, uint64_t max_chunks,
+                                                         uint32_t nq, uint32_t rel_log2, uint32_t nbins, uint32_t U,
+                                                         uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_row[(1u << kMaxRel) + 1];
+    const uint32_t sb = blockIdx.x, t = threadIdx.x, R = 1u << rel_log2;
+    const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
+    if (t <= R) {
+        uint32_t sum = 0;
+        const uint16_t* row = tabs + (uint64_t)t * max_chunks;
+        for (uint32_t b = bb0; b < bb1; ++b) sum += row[b];
+        s_row[t] = sum;
+    }
+    __syncthreads();
+    const uint32_t r = sb * R + t;
+    if (t < R && r < nbins) out[kSetsHdr + r] = sets_region_words(s_row[t + 1] - s_row[t], U);
+}
+
+// One workgroup: the reserved words -> every region's first word (0 for an empty one), the
+// header, and [3] = the words reserved in all (> cap_words cannot happen within the capacity;
+// the encode then writes no region past cap_words).
+__global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__ out, uint32_t rl, uint32_t nbins) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nbins + 1023u) / 1024u, r0 = t * per, r1 = min(r0 + per, nbins);
+    uint64_t mine = 0;
+    for (uint32_t r = r0; r < r1; ++r) mine += out[kSetsHdr + r];
+    uint32_t total;   // < 2^32 words: the capacity is checked on the host
+    uint32_t at = (uint32_t)sets_first_word(nbins) + block_excl_scan((uint32_t)mine, s_w, &total);
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint32_t w = out[kSetsHdr + r];
+        out[kSetsHdr + r] = w ? at : 0u;
+        at += w;
+    }
+    if (t == 0) {
+        out[0] = kSetsMagic;
+        out[1] = rl;
+        out[2] = nbins;
+        out[3] = (uint32_t)sets_first_word(nbins) + total;
+    }
 }
 
 // One workgroup per region: the region's probes (level 2, as bin_apply gathers them) into an
@@ -2515,9 +2573,10 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
     __shared__ uint4 s_m4[NW / 4];
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
-    __shared__ uint32_t s_start;
     uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
     const uint32_t t = threadIdx.x, r = blockIdx.x;
+    const uint32_t st = out[kSetsHdr + r];   // reserved by sets_place_kernel; 0: no probes
+    if (st == 0) return;                     // workgroup-uniform
     for (uint32_t v = t; v < NW / 4; v += LANES) s_m4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     for_region_probes<8>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
@@ -2552,20 +2611,9 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         uw = (n + (U >> l) + 31u) / 32u;
         words = 1u + (bitmap ? NW : lw + uw);
     }
-    if (t == 0) {
-        uint32_t st = 0;
-        if (n) {
-            st = atomicAdd(out + 3, words);
-            // past the capacity (bf_sets_capacity_bytes bounds every batch, so never): the
-            // region is not written, and out[3] > capacity tells the reader
-            if ((uint64_t)st + words > cap_words) st = 0;
-        }
-        s_start = st;
-        out[kSetsHdr + r] = st;
-    }
-    __syncthreads();
-    const uint32_t st = s_start;
-    if (st == 0) return;   // workgroup-uniform
+    // past the capacity (bf_sets_capacity_bytes bounds every batch, so never): not written,
+    // and out[3] > capacity tells the reader
+    if ((uint64_t)st + words > cap_words) return;   // workgroup-uniform
     uint32_t* o = out + st;
     if (bitmap) {   // the LDS bitmap is still intact
         if (t == 0) o[0] = n | (kSetsBitmap << 24);
@@ -2758,11 +2806,12 @@ uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2
     // n k probes hit at most N = n k distinct offsets.  A set of n_r offsets takes < n_r
     // (log2(U / n_r) + 3) bits (l <= log2(U / n_r), U >> l < 2 n_r), concave in n_r, so over R
     // regions the total peaks at an even split: N (log2(U R / N) + 3); a bitmap set (U bits)
-    // is taken only below its Elias-Fano size.  Plus 3 words of header and padding per region.
-    const double U = (double)(1ull << rl), N = (double)n * (double)k;
+    // is taken only below its Elias-Fano size.  Plus 4 words of header and padding per region
+    // (sets_region_words: the places reserved per region before the encode).
+    const double U = (double)(1ull << rl), N = std::min((double)n * (double)k, U * R);
     double bitsum = 0.0;
-    if (N > 0) bitsum = std::min(N * (std::log2(U * R / N) + 3.0), U * R) * 1.01 + 4096.0;
-    const uint64_t words = sets_first_word(R) + 3ull * R + (uint64_t)(bitsum / 32.0) + 64;
+    if (N > 0) bitsum = std::min(N * (std::log2(U * R / N) + 3.01), U * R) * 1.01 + 4096.0;
+    const uint64_t words = sets_first_word(R) + 4ull * R + (uint64_t)(bitsum / 32.0) + 64;
     return words * 4;
 }
 
@@ -2771,13 +2820,17 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
                                  uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* mk) {
     (void)bitset_bytes;
     if (cap_words >= (1ull << 32)) return hipErrorInvalidValue;
-    const uint32_t hgrid = n ? 1u : (uint32_t)((p.nbins + 255) / 256);
-    hipLaunchKernelGGL(sets_header_kernel, dim3(hgrid), dim3(256), 0, s, out, p.region_log2, p.nbins, n ? 0u : 1u);
-    if (n == 0) return hipGetLastError();
+    if (n == 0) {
+        hipLaunchKernelGGL(sets_header_kernel, dim3((p.nbins + 255) / 256), dim3(256), 0, s, out, p.region_log2, p.nbins);
+        return hipGetLastError();
+    }
     if (p.with_keys) return hipErrorInvalidValue;
     const Carve c = carve(p, scratch);
     hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, nullptr, s, mk, dig);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sets_size_kernel, dim3(p.nsup), dim3(1024), 0, s, c.tabs, c.cb_base, p.max_chunks, p.ngroups,
+                       p.rel_log2, p.nbins, 1u << p.region_log2, out);
+    hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, out, p.region_log2, p.nbins);
     if (p.region_log2 == 19)
         hipLaunchKernelGGL((sets_encode_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, c.level2,
                            c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, (uint32_t)cap_words);

@@ -107,8 +107,9 @@ def encode(sets: dict, region_log2: int, nregions: int) -> np.ndarray:
 def capacity_words(bitset_bytes: int, region_log2: int, n_keys: int, k: int) -> int:
     """bf_sets_capacity_bytes / 4 (bf_binned.hip), restated for the host tests."""
     R = -(-(bitset_bytes * 8) // (1 << region_log2))
-    U, N = float(1 << region_log2), float(n_keys * k)
+    U = float(1 << region_log2)
+    N = min(float(n_keys * k), U * R)
     bits = 0.0
     if N > 0:
-        bits = min(N * (np.log2(U * R / N) + 3.0), U * R) * 1.01 + 4096.0
-    return (4 + R + 63) // 64 * 64 + 3 * R + int(bits / 32.0) + 64
+        bits = min(N * (np.log2(U * R / N) + 3.01), U * R) * 1.01 + 4096.0
+    return (4 + R + 63) // 64 * 64 + 4 * R + int(bits / 32.0) + 64
