@@ -901,7 +901,9 @@ uint32_t mid_grid(uint32_t nsup, uint32_t nq) {
 // cut into chunk blocks of kBlockProbes, and part p of kMidParts takes an equal
 // share of them.  The run table is built once; each block's loads are issued
 // while the previous block is sorted and written.
-template <bool KEYS>
+// DEEP: the loads run two blocks ahead instead of one (the stall counters show bin_mid parked
+// on memory for 0.60 of its cycles: one block of sorting does not cover a block's load).
+template <bool KEYS, bool DEEP = false>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void bin_mid_kernel(const uint32_t* __restrict__ level1,
                                                         const uint32_t* __restrict__ level1_key,
                                                         const uint16_t* __restrict__ stab, uint64_t ntiles,
@@ -973,7 +975,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
     };
     uint32_t lv[kChunkPerLane], kv[kChunkPerLane];
+    uint32_t plv[kChunkPerLane], pkv[kChunkPerLane];   // DEEP: block c + 1, loaded an iteration ago
     load(c_lo * kBlockProbes, lv, kv);
+    if constexpr (DEEP)
+        if (c_lo + 1 < c_hi) load((c_lo + 1) * kBlockProbes, plv, pkv);
+    constexpr uint32_t kAhead = DEEP ? 2u : 1u;
     for (uint32_t c = c_lo; c < c_hi; ++c) {
         const uint32_t f0 = c * kBlockProbes;
         const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
@@ -989,7 +995,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
         uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
-        if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
+        if (c + kAhead < c_hi) load(f0 + kAhead * kBlockProbes, nlv, nkv);   // a later block in flight
         __syncthreads();
         const uint32_t cn = t < NB ? s_cnt[t] : 0u;
         const uint32_t cex = block_excl_scan(cn, s_w, nullptr);   // its barriers order the s_cnt reads first
@@ -1014,8 +1020,15 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (c + 1 < c_hi) {
 #pragma unroll
             for (int u = 0; u < kChunkPerLane; ++u) {
-                lv[u] = nlv[u];
-                kv[u] = nkv[u];
+                if constexpr (DEEP) {
+                    lv[u] = plv[u];
+                    kv[u] = pkv[u];
+                    plv[u] = nlv[u];
+                    pkv[u] = nkv[u];
+                } else {
+                    lv[u] = nlv[u];
+                    kv[u] = nkv[u];
+                }
             }
         }
     }
@@ -1588,7 +1601,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
 // The received entries are window-local offsets: an entry outside its superbin or past the
 // shard is dropped (KEYS: answered 0), so peer data never addresses outside the bitset.  KEYS:
 // each probe's position is its index in the receive buffer (no level-1 key array).
-template <bool KEYS>
+template <bool KEYS, bool DEEP = false>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
                            const uint32_t* __restrict__ base, const uint32_t* __restrict__ cb_base,
@@ -1654,7 +1667,11 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
         }
     };
     uint32_t lv[kChunkPerLane], kv[kChunkPerLane];
+    uint32_t plv[kChunkPerLane], pkv[kChunkPerLane];   // DEEP: block c + 1, loaded an iteration ago
     load(c_lo * kBlockProbes, lv, kv);
+    if constexpr (DEEP)
+        if (c_lo + 1 < c_hi) load((c_lo + 1) * kBlockProbes, plv, pkv);
+    constexpr uint32_t kAhead = DEEP ? 2u : 1u;
     for (uint32_t c = c_lo; c < c_hi; ++c) {
         const uint32_t f0 = c * kBlockProbes;
         const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
@@ -1670,7 +1687,7 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
             }
         }
         uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
-        if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
+        if (c + kAhead < c_hi) load(f0 + kAhead * kBlockProbes, nlv, nkv);   // a later block in flight
         __syncthreads();
         const uint32_t cn = t < NB ? s_cnt[t] : 0u;
         const uint32_t cex = block_excl_scan(cn, s_w, nullptr);
@@ -1695,8 +1712,15 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
         if (c + 1 < c_hi) {
 #pragma unroll
             for (int u = 0; u < kChunkPerLane; ++u) {
-                lv[u] = nlv[u];
-                kv[u] = nkv[u];
+                if constexpr (DEEP) {
+                    lv[u] = plv[u];
+                    kv[u] = pkv[u];
+                    plv[u] = nlv[u];
+                    pkv[u] = nkv[u];
+                } else {
+                    lv[u] = nlv[u];
+                    kv[u] = nkv[u];
+                }
             }
         }
     }
@@ -1816,6 +1840,15 @@ void launch_scan(const BfBinPlan& p, const Carve& c, hipStream_t s) {
                        c.base, c.cb_base, c.cb_window, c.cb_start);
 }
 
+// bin_mid's load depth (blocks in flight ahead of the one it sorts): BFHIP_MID_DEPTH, A/B.
+uint32_t mid_depth() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("BFHIP_MID_DEPTH");
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
+    return v;
+}
+
 // bin_group_sum .. bin_mid over the level-1 array a front pass wrote.
 hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c, hipStream_t s, BfMarks* mk) {
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
@@ -1826,6 +1859,11 @@ hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c
     if (p.with_keys)
         hipLaunchKernelGGL(bin_mid_kernel<true>, dim3(mid_grid(p.nsup, p.ngroups)), dim3(kTile), 0, s, c.level1,
                            c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
+                           p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
+                           c.level2_key);
+    else if (mid_depth() == 2)
+        hipLaunchKernelGGL((bin_mid_kernel<false, true>), dim3(mid_grid(p.nsup, p.ngroups)), dim3(kTile), 0, s,
+                           c.level1, c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
     else

@@ -11,6 +11,13 @@ bash tools/gpu_round.sh r04a repl || exit $?
 for xg in 1 2 4 1 2 4; do
     BFHIP_APPLY_XG=$xg timeout -k 10 150 python bench.py --config 10b --steps 10 --warmup 3 --no-secondary \
         --no-cpu-baseline --no-host-api --no-reference-shapes > gpurun_out/ab_xg${xg}_r04a.json 2>/dev/null || exit $?
-    cat gpurun_out/ab_xg${xg}_r04a.json >> gpurun_out/ab_xg_r04a.jsonl
+    (echo -n "{\"xg\": $xg, \"line\": "; cat gpurun_out/ab_xg${xg}_r04a.json; echo "}") >> gpurun_out/ab_xg_r04a.jsonl
+done
+for cfg in nstar 10b; do
+    for d in 1 2 1 2; do
+        BFHIP_MID_DEPTH=$d timeout -k 10 150 python bench.py --config $cfg --steps 10 --warmup 3 --no-secondary \
+            --no-cpu-baseline --no-host-api --no-reference-shapes > gpurun_out/ab_mid_r04a.json 2>/dev/null || exit $?
+        (echo -n "{\"depth\": $d, \"line\": "; cat gpurun_out/ab_mid_r04a.json; echo "}") >> gpurun_out/ab_mid_r04a.jsonl
+    done
 done
 bash tools/gpu_round.sh r04a bench
