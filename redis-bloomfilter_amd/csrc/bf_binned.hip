@@ -2397,6 +2397,10 @@ hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn&
         hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
                            p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key, out8);
+    else if (mid_depth() == 2)
+        hipLaunchKernelGGL((bin_mid_chunks_kernel<false, true>), dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0,
+                           s, ci, p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs,
+                           c.level2, c.level2_key, out8);
     else
         hipLaunchKernelGGL(bin_mid_chunks_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
                            p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
