@@ -2854,7 +2854,7 @@ uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2
     double bitsum = 0.0;
     if (N > 0) bitsum = std::min(N * (std::log2(U * R / N) + 3.01), U * R) * 1.01 + 4096.0;
     const uint64_t words = sets_first_word(R) + 4ull * R + (uint64_t)(bitsum / 32.0) + 64;
-    return words * 4;
+    return ((words + 63) & ~63ull) * 4;   // whole 256-B units: buffers laid end to end stay aligned
 }
 
 hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,

@@ -112,4 +112,5 @@ def capacity_words(bitset_bytes: int, region_log2: int, n_keys: int, k: int) -> 
     bits = 0.0
     if N > 0:
         bits = min(N * (np.log2(U * R / N) + 3.01), U * R) * 1.01 + 4096.0
-    return (4 + R + 63) // 64 * 64 + 4 * R + int(bits / 32.0) + 64
+    words = (4 + R + 63) // 64 * 64 + 4 * R + int(bits / 32.0) + 64
+    return (words + 63) // 64 * 64
