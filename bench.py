@@ -268,6 +268,10 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     out = torch.empty(batch, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream   # 0 = the null stream torch uses by default
+    # replicated "sets" insert, pipelined: batch i+2's SHA-1 words come out of step i's include?
+    # kernel (bf_include_hash_dev, as the single-GPU step), step i+1 encodes them into region sets
+    # (no hash pass) and all-gathers them beside its own work, step i+2 ORs every rank's sets in
+    rpipe = pipeline and rf is not None and comm_prefetch and rf.insert_mode == "sets"
     pipeline = pipeline and mode == "single"
     if pipeline:
         # Pipelined steps (include/bfhip.h, bf_include_hash_dev): step i inserts batch i from
@@ -290,6 +294,17 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     comm_prefetch_flag = comm_prefetch
     comm_prefetch = comm_prefetch and rf is not None
     gpend, rstep, szp = {}, [0], {}
+    rdig = {}
+
+    def rdigs(b: int) -> torch.Tensor:   # batch b's SHA-1 words (a ring of three buffers)
+        if b % 3 not in rdig:
+            rdig[b % 3] = torch.empty((batch, 4), dtype=torch.int32, device=dev)
+        return rdig[b % 3]
+
+    if rpipe:   # the pipeline's fill: batches 0 and 1 hashed before the timed region
+        for b in (0, 1):
+            kb_, ko_ = batches[b % len(batches)][0]
+            f.hash_many_dev(kb_.data_ptr(), ko_.data_ptr(), batch, rdigs(b).data_ptr(), stream=sp)
 
     # Every timed insert asks for any_new, the reference's !found that drives EXPIRE
     # (ruby.rb:61-62): one pre-zeroed flag word per step, so no memset joins the step.
@@ -309,9 +324,10 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             # the sizes of batch i+2 are all-gathered now, so step i+1's gather_start reads them
             # from pinned memory without waiting for the kernels in flight
             i, L = rstep[0], len(batches)
-            st = gpend.pop(i % L, None) or rf.gather_start(ikb, iko, batch)
+            st = gpend.pop(i % L, None) or rf.gather_start(ikb, iko, batch, digests=rdigs(i) if rpipe else None)
             nxt = (i + 1) % L
-            gpend[nxt] = rf.gather_start(*batches[nxt][0], batch, sizes=szp.pop(nxt, None))
+            gpend[nxt] = rf.gather_start(*batches[nxt][0], batch, sizes=szp.pop(nxt, None),
+                                         digests=rdigs(i + 1) if rpipe else None)
             szp[(i + 2) % L] = rf.sizes_start(*batches[(i + 2) % L][0], batch)
             rf.insert_gathered(st)
             rstep[0] = i + 1
@@ -330,6 +346,11 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             f.include_hash_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), nkb.data_ptr(), nko.data_ptr(),
                                batch, digs[(i + 1) % 2].data_ptr(), stream=sp)
             step_no[0] = i + 1
+        elif rpipe:   # include? of batch i with batch i+2's SHA-1 fused in
+            i = rstep[0] - 1
+            nkb, nko = batches[(i + 2) % len(batches)][0]
+            f.include_hash_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), nkb.data_ptr(), nko.data_ptr(),
+                               batch, rdigs(i + 2).data_ptr(), stream=sp)
         elif rf is not None:
             out.copy_(rf.include_many_dev(pkb, pko, batch))
         elif pf is None:
@@ -438,7 +459,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             kt["algo_bytes"] = algo[name]
             kt["GBps"] = algo[name] / (kt["ms"] / 1e3) / 1e9
     res = {
-        "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3), "pipelined": pipeline,
+        "m": m, "k": k, "batch": batch, "mean_key_bytes": round(Lmean, 3), "pipelined": pipeline or rpipe,
         "wall_s": wall, "steps": steps,
         "keys_per_s": 2 * batch * D.world * steps / wall,
         "insert": {"op_ms": ins_ms, "keys_per_s": batch / (ins_ms / 1e3),

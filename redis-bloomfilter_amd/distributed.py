@@ -1092,7 +1092,8 @@ class ReplicatedFilter:
             ev.record()
         return dict(host=host, ev=ev, lens=lens, n=n)
 
-    def gather_start(self, kb: torch.Tensor, ko: torch.Tensor, n: int, sizes: Optional[dict] = None) -> dict:
+    def gather_start(self, kb: torch.Tensor, ko: torch.Tensor, n: int, sizes: Optional[dict] = None,
+                     digests: Optional[torch.Tensor] = None) -> dict:
         """Enqueue the all-gather of this rank's batch (collective: every rank calls it, in
         the same order); ``insert_gathered`` finishes it.  Between the two the gather runs on
         the process group's stream beside whatever the caller enqueues — e.g. the previous
@@ -1100,7 +1101,9 @@ class ReplicatedFilter:
         sizes come from ``sizes`` (a ``sizes_start`` of this batch issued earlier: the host
         waits only for that small all-gather's event) or from a sizes_start made here (the
         host then waits for everything enqueued before it).  In "or" mode nothing travels
-        here; ``insert_gathered`` inserts and OR-all-reduces."""
+        here; ``insert_gathered`` inserts and OR-all-reduces.  ``digests`` ("sets" mode): the
+        batch's SHA-1 words, already computed (e.g. by a fused include?+hash kernel), so the
+        encode skips its hash pass."""
         if sizes is None:
             sizes = self.sizes_start(kb, ko, n)
         if sizes["n"] != n:
@@ -1124,8 +1127,12 @@ class ReplicatedFilter:
             max_n = max(max(sz[1] for sz in all_sizes), 1)
             cap = self.filter.region_sets_capacity(max_n)   # the same on every rank: one gather size
             mine = torch.empty(cap // 4, dtype=torch.int32, device=self.device)
-            self.filter.encode_region_sets_dev(kb.data_ptr() if n else 0, ko.data_ptr() if n else 0, n,
-                                               mine.data_ptr(), cap, stream=self._stream())
+            if digests is not None and n:
+                self.filter.encode_region_sets_digests_dev(digests.data_ptr(), n, mine.data_ptr(), cap,
+                                                           stream=self._stream())
+            else:
+                self.filter.encode_region_sets_dev(kb.data_ptr() if n else 0, ko.data_ptr() if n else 0, n,
+                                                   mine.data_ptr(), cap, stream=self._stream())
             gs = torch.empty(self.P * (cap // 4), dtype=torch.int32, device=self.device)
             works = [_all_gather_into_tensor(gs, mine, group=self.group, async_op=True)]
             return dict(mode="sets", kb=kb, ko=ko, n=n, gs=gs, send=mine, works=works, sizes=all_sizes, cap=cap)

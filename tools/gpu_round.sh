@@ -30,11 +30,11 @@ for st in $STEPS; do
                    GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv \
                    -d gpurun_out/pmc_${TAG}_P8_valu -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
                    > gpurun_out/pmc_${TAG}_P8_valu.log 2>&1 ;;
-        repl)  for g in digests sets; do
+        repl)  for g in digests sets "sets --fused-hash"; do
                    timeout -k 10 240 python tools/sim_rank.py --replicated 8 --config 10b --gathered $g --steps 3 \
                        >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
                done &&
-               for g in keys sets; do
+               for g in keys sets "sets --fused-hash"; do
                    timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered $g --steps 5 \
                        >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
                done ;;

@@ -52,6 +52,10 @@ def main():
                          "ReplicatedFilter), 16-B SHA-1 words (each key hashed once, by its own rank), or "
                          "region sets (each batch hashed, sorted and encoded once, by its own rank; every "
                          "replica ORs all R ranks' sets in without sorting)")
+    ap.add_argument("--fused-hash", action="store_true",
+                    help="--replicated --gathered sets: the own batch's SHA-1 words come out of the previous "
+                         "step's include? kernel (bf_include_hash_dev) and the encode starts from them "
+                         "(bench.py's pipelined replicated step)")
     ap.add_argument("--dig", action="store_true",
                     help="--chunks: route the include? batch from SHA-1 words that the previous step's owner "
                          "test hashed between its probe rounds (bf_shard_test_chunks_hash_dev + "
@@ -287,8 +291,15 @@ def replicated(args, pkg):
 
     cap_sets = f.region_sets_capacity(batch) if args.gathered == "sets" else 0
 
-    def step(s_):
+    def step(s_, nxt_=None):
         mkb, mko, (qkb, qko), dg = s_
+        if args.gathered == "sets" and args.fused_hash:   # own words from the previous include? kernel
+            f.encode_region_sets_digests_dev(own.data_ptr(), batch, dg.data_ptr(), cap_sets, stream=sp)
+            f.insert_region_sets_dev(dg.data_ptr(), cap_sets, R, R * batch * k, d_any_new=flag.data_ptr(), stream=sp)
+            nkb, nko = nxt_[0], nxt_[1]   # the next step's own batch, hashed here
+            f.include_hash_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), nkb.data_ptr(), nko.data_ptr(),
+                               batch, own.data_ptr(), stream=sp)
+            return
         if args.gathered == "sets":   # own batch sorted + encoded (into rank 0's slot), then all R sets in
             f.encode_region_sets_dev(mkb.data_ptr(), mko.data_ptr(), batch, dg.data_ptr(), cap_sets, stream=sp)
             f.insert_region_sets_dev(dg.data_ptr(), cap_sets, R, R * batch * k, d_any_new=flag.data_ptr(), stream=sp)
@@ -299,19 +310,22 @@ def replicated(args, pkg):
             f.insert_many_dev(mkb.data_ptr(), mko.data_ptr(), nm, d_any_new=flag.data_ptr(), stream=sp)
         f.include_many_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), stream=sp)
 
-    step(steps[0])
+    if args.fused_hash:   # the pipeline's fill: the first step's own words
+        f.hash_many_dev(steps[0][0].data_ptr(), steps[0][1].data_ptr(), batch, own.data_ptr(), stream=sp)
+    step(steps[0], steps[1 % len(steps)])
     torch.cuda.synchronize()
     f.profile(True)
     f.profile_read(reset=True)
     t0 = time.perf_counter()
-    for s_ in steps[1:]:
-        step(s_)
+    for j, s_ in enumerate(steps[1:], start=1):
+        step(s_, steps[(j + 1) % len(steps)])
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.steps
     prof = f.profile_read(reset=True)
     assert out.cpu().numpy()[: batch // 2].all(), "false negative"
     one = None
-    res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered, "m": m, "k": k,
+    res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
+           "fused_hash": bool(args.fused_hash), "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
            "gathered_bytes_per_rank": (cap_sets if args.gathered == "sets" else
                                        batch * 16 if args.gathered == "digests" else None),
