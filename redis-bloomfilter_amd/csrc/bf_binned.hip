@@ -901,9 +901,7 @@ uint32_t mid_grid(uint32_t nsup, uint32_t nq) {
 // cut into chunk blocks of kBlockProbes, and part p of kMidParts takes an equal
 // share of them.  The run table is built once; each block's loads are issued
 // while the previous block is sorted and written.
-// DEEP: the loads run two blocks ahead instead of one (the stall counters show bin_mid parked
-// on memory for 0.60 of its cycles: one block of sorting does not cover a block's load).
-template <bool KEYS, bool DEEP = false>
+template <bool KEYS>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void bin_mid_kernel(const uint32_t* __restrict__ level1,
                                                         const uint32_t* __restrict__ level1_key,
                                                         const uint16_t* __restrict__ stab, uint64_t ntiles,
@@ -975,11 +973,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
     };
     uint32_t lv[kChunkPerLane], kv[kChunkPerLane];
-    uint32_t plv[kChunkPerLane], pkv[kChunkPerLane];   // DEEP: block c + 1, loaded an iteration ago
     load(c_lo * kBlockProbes, lv, kv);
-    if constexpr (DEEP)
-        if (c_lo + 1 < c_hi) load((c_lo + 1) * kBlockProbes, plv, pkv);
-    constexpr uint32_t kAhead = DEEP ? 2u : 1u;
     for (uint32_t c = c_lo; c < c_hi; ++c) {
         const uint32_t f0 = c * kBlockProbes;
         const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
@@ -995,7 +989,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             }
         }
         uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
-        if (c + kAhead < c_hi) load(f0 + kAhead * kBlockProbes, nlv, nkv);   // a later block in flight
+        if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
         __syncthreads();
         const uint32_t cn = t < NB ? s_cnt[t] : 0u;
         const uint32_t cex = block_excl_scan(cn, s_w, nullptr);   // its barriers order the s_cnt reads first
@@ -1020,15 +1014,8 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         if (c + 1 < c_hi) {
 #pragma unroll
             for (int u = 0; u < kChunkPerLane; ++u) {
-                if constexpr (DEEP) {
-                    lv[u] = plv[u];
-                    kv[u] = pkv[u];
-                    plv[u] = nlv[u];
-                    pkv[u] = nkv[u];
-                } else {
-                    lv[u] = nlv[u];
-                    kv[u] = nkv[u];
-                }
+                lv[u] = nlv[u];
+                kv[u] = nkv[u];
             }
         }
     }
@@ -1601,7 +1588,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
 // The received entries are window-local offsets: an entry outside its superbin or past the
 // shard is dropped (KEYS: answered 0), so peer data never addresses outside the bitset.  KEYS:
 // each probe's position is its index in the receive buffer (no level-1 key array).
-template <bool KEYS, bool DEEP = false>
+template <bool KEYS>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
                            const uint32_t* __restrict__ base, const uint32_t* __restrict__ cb_base,
@@ -1667,11 +1654,7 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
         }
     };
     uint32_t lv[kChunkPerLane], kv[kChunkPerLane];
-    uint32_t plv[kChunkPerLane], pkv[kChunkPerLane];   // DEEP: block c + 1, loaded an iteration ago
     load(c_lo * kBlockProbes, lv, kv);
-    if constexpr (DEEP)
-        if (c_lo + 1 < c_hi) load((c_lo + 1) * kBlockProbes, plv, pkv);
-    constexpr uint32_t kAhead = DEEP ? 2u : 1u;
     for (uint32_t c = c_lo; c < c_hi; ++c) {
         const uint32_t f0 = c * kBlockProbes;
         const uint32_t f1 = (E - f0 < kBlockProbes) ? E : f0 + kBlockProbes;
@@ -1687,7 +1670,7 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
             }
         }
         uint32_t nlv[kChunkPerLane], nkv[kChunkPerLane];
-        if (c + kAhead < c_hi) load(f0 + kAhead * kBlockProbes, nlv, nkv);   // a later block in flight
+        if (c + 1 < c_hi) load(f0 + kBlockProbes, nlv, nkv);   // next block in flight
         __syncthreads();
         const uint32_t cn = t < NB ? s_cnt[t] : 0u;
         const uint32_t cex = block_excl_scan(cn, s_w, nullptr);
@@ -1712,15 +1695,8 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
         if (c + 1 < c_hi) {
 #pragma unroll
             for (int u = 0; u < kChunkPerLane; ++u) {
-                if constexpr (DEEP) {
-                    lv[u] = plv[u];
-                    kv[u] = pkv[u];
-                    plv[u] = nlv[u];
-                    pkv[u] = nkv[u];
-                } else {
-                    lv[u] = nlv[u];
-                    kv[u] = nkv[u];
-                }
+                lv[u] = nlv[u];
+                kv[u] = nkv[u];
             }
         }
     }
@@ -1840,15 +1816,6 @@ void launch_scan(const BfBinPlan& p, const Carve& c, hipStream_t s) {
                        c.base, c.cb_base, c.cb_window, c.cb_start);
 }
 
-// bin_mid's load depth (blocks in flight ahead of the one it sorts): BFHIP_MID_DEPTH, A/B.
-uint32_t mid_depth() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("BFHIP_MID_DEPTH");
-        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
-    }();
-    return v;
-}
-
 // bin_group_sum .. bin_mid over the level-1 array a front pass wrote.
 hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c, hipStream_t s, BfMarks* mk) {
     hipLaunchKernelGGL(bin_group_sum_kernel, dim3(p.nsup), dim3(kMaxBlocks), 0, s, c.gcnt, p.nblocks, p.nsup,
@@ -1859,11 +1826,6 @@ hipError_t launch_groups_mid(const BfGeom& g, const BfBinPlan& p, const Carve& c
     if (p.with_keys)
         hipLaunchKernelGGL(bin_mid_kernel<true>, dim3(mid_grid(p.nsup, p.ngroups)), dim3(kTile), 0, s, c.level1,
                            c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
-                           p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
-                           c.level2_key);
-    else if (mid_depth() == 2)
-        hipLaunchKernelGGL((bin_mid_kernel<false, true>), dim3(mid_grid(p.nsup, p.ngroups)), dim3(kTile), 0, s,
-                           c.level1, c.level1_key, c.stab, p.ntiles, p.tile_probes, tiles_per_group, p.nsup, p.ngroups,
                            p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key);
     else
@@ -2026,11 +1988,12 @@ uint32_t apply_store_fresh() {
     return v;
 }
 
-// bin_apply's regions per XCD group (apply_region): BFHIP_APPLY_XG, A/B.
+// bin_apply's regions per XCD group (apply_region): 2 measured 2.394 / 2.395 ms against 2.423 /
+// 2.431 (1) and 2.409 / 2.401 (4) at 10B (profiles/r04a_ab_xg.jsonl).  BFHIP_APPLY_XG overrides.
 uint32_t apply_xcd_group() {
     static const uint32_t v = [] {
         const char* e = std::getenv("BFHIP_APPLY_XG");
-        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
     }();
     return v;
 }
@@ -2397,10 +2360,6 @@ hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn&
         hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
                            p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
                            c.level2_key, out8);
-    else if (mid_depth() == 2)
-        hipLaunchKernelGGL((bin_mid_chunks_kernel<false, true>), dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0,
-                           s, ci, p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs,
-                           c.level2, c.level2_key, out8);
     else
         hipLaunchKernelGGL(bin_mid_chunks_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
                            p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
@@ -2556,13 +2515,15 @@ __device__ __forceinline__ uint32_t sets_region_words(uint32_t E, uint32_t U) {
 }
 
 // Per superbin: region r's probe count E_r = sum over the superbin's level-2 blocks of its run
-// length (a telescoping sum of the [region][block] run-start rows), its set's reserved words
-// into out[4 + r] (sets_place_kernel turns them into places).
+// length (a telescoping sum of the [region][block] run-start rows) -> its set's reserved words,
+// their exclusive prefix inside the superbin into out[4 + r] (bit 31: the region has probes),
+// and the superbin's total into sb_tot[sb] (sets_place_kernel scans those).
 __global__ __launch_bounds__(1024) void sets_size_kernel(const uint16_t* __restrict__ tabs,
                                                          const uint32_t* __restrict__ cb_base, uint64_t max_chunks,
                                                          uint32_t nq, uint32_t rel_log2, uint32_t nbins, uint32_t U,
-                                                         uint32_t* __restrict__ out) {
+                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ sb_tot) {
     __shared__ uint32_t s_row[(1u << kMaxRel) + 1];
+    __shared__ uint32_t s_w[16];
     const uint32_t sb = blockIdx.x, t = threadIdx.x, R = 1u << rel_log2;
     const uint32_t bb0 = cb_base[sb * nq], bb1 = cb_base[(sb + 1) * nq];
     if (t <= R) {
@@ -2573,30 +2534,30 @@ __global__ __launch_bounds__(1024) void sets_size_kernel(const uint16_t* __restr
     }
     __syncthreads();
     const uint32_t r = sb * R + t;
-    if (t < R && r < nbins) out[kSetsHdr + r] = sets_region_words(s_row[t + 1] - s_row[t], U);
+    const uint32_t w = (t < R && r < nbins) ? sets_region_words(s_row[t + 1] - s_row[t], U) : 0u;
+    uint32_t total;
+    const uint32_t lp = block_excl_scan(w, s_w, &total);
+    if (t < R && r < nbins) out[kSetsHdr + r] = w ? (lp | 0x80000000u) : 0u;
+    if (t == 0) sb_tot[sb] = total;
 }
 
-// One workgroup: the reserved words -> every region's first word (0 for an empty one), the
-// header, and [3] = the words reserved in all (> cap_words cannot happen within the capacity;
+// One workgroup: each superbin's first word (sets from sets_first_word(R), superbins in order)
+// into sb_tot, and the header; [3] = the words reserved in all (> the capacity cannot happen;
 // the encode then writes no region past cap_words).
-__global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__ out, uint32_t rl, uint32_t nbins) {
+__global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__ out, uint32_t* __restrict__ sb_tot,
+                                                          uint32_t nsup, uint32_t rl, uint32_t nbins) {
     __shared__ uint32_t s_w[16];
     const uint32_t t = threadIdx.x;
-    const uint32_t per = (nbins + 1023u) / 1024u, r0 = t * per, r1 = min(r0 + per, nbins);
-    uint64_t mine = 0;
-    for (uint32_t r = r0; r < r1; ++r) mine += out[kSetsHdr + r];
-    uint32_t total;   // < 2^32 words: the capacity is checked on the host
-    uint32_t at = (uint32_t)sets_first_word(nbins) + block_excl_scan((uint32_t)mine, s_w, &total);
-    for (uint32_t r = r0; r < r1; ++r) {
-        const uint32_t w = out[kSetsHdr + r];
-        out[kSetsHdr + r] = w ? at : 0u;
-        at += w;
-    }
+    const uint32_t v = t < nsup ? sb_tot[t] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(v, s_w, &total);
+    const uint32_t first = (uint32_t)sets_first_word(nbins);
+    if (t < nsup) sb_tot[t] = first + ex;
     if (t == 0) {
         out[0] = kSetsMagic;
         out[1] = rl;
         out[2] = nbins;
-        out[3] = (uint32_t)sets_first_word(nbins) + total;
+        out[3] = first + total;
     }
 }
 
@@ -2610,17 +2571,20 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
                                                             const uint32_t* __restrict__ cb_start,
                                                             const uint16_t* __restrict__ tabs, uint64_t max_chunks,
                                                             uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
-                                                            uint32_t cap_words) {
+                                                            const uint32_t* __restrict__ sb_first, uint32_t cap_words) {
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
     static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
     __shared__ uint4 s_m4[NW / 4];
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
     uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
     const uint32_t t = threadIdx.x, r = blockIdx.x;
-    const uint32_t st = out[kSetsHdr + r];   // reserved by sets_place_kernel; 0: no probes
-    if (st == 0) return;                     // workgroup-uniform
+    // the region's reserved place: its superbin's first word + its prefix in the superbin
+    // (sets_size_kernel / sets_place_kernel); loaded while the LDS image is cleared
+    const uint32_t rv = out[kSetsHdr + r], sbf = sb_first[r >> rel_log2];
     for (uint32_t v = t; v < NW / 4; v += LANES) s_m4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    if (!(rv & 0x80000000u)) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
+    const uint32_t st = sbf + (rv & 0x7FFFFFFFu);
     for_region_probes<8>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
         [&](const uint32_t* idx) {
             uint32_t l[8];
@@ -2655,7 +2619,9 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     }
     // past the capacity (bf_sets_capacity_bytes bounds every batch, so never): not written,
     // and out[3] > capacity tells the reader
-    if ((uint64_t)st + words > cap_words) return;   // workgroup-uniform
+    const bool fits = (uint64_t)st + words <= cap_words;
+    if (t == 0) out[kSetsHdr + r] = fits ? st : 0u;   // every lane read rv before the barriers above
+    if (!fits) return;   // workgroup-uniform
     uint32_t* o = out + st;
     if (bitmap) {   // the LDS bitmap is still intact
         if (t == 0) o[0] = n | (kSetsBitmap << 24);
@@ -2870,15 +2836,17 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
     const Carve c = carve(p, scratch);
     hipError_t e = launch_partition(g, p, c, keys16, offsets, bias, n, nullptr, s, mk, dig);
     if (e != hipSuccess) return e;
+    // c.stot (the hierarchical scan's superbin totals) is free once bin_mid has run
     hipLaunchKernelGGL(sets_size_kernel, dim3(p.nsup), dim3(1024), 0, s, c.tabs, c.cb_base, p.max_chunks, p.ngroups,
-                       p.rel_log2, p.nbins, 1u << p.region_log2, out);
-    hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, out, p.region_log2, p.nbins);
+                       p.rel_log2, p.nbins, 1u << p.region_log2, out, c.stot);
+    hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, out, c.stot, p.nsup, p.region_log2, p.nbins);
     if (p.region_log2 == 19)
         hipLaunchKernelGGL((sets_encode_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, c.level2,
-                           c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, (uint32_t)cap_words);
+                           c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot,
+                           (uint32_t)cap_words);
     else if (p.region_log2 == 18)
         hipLaunchKernelGGL((sets_encode_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
-                           c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out,
+                           c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot,
                            (uint32_t)cap_words);
     else
         return hipErrorInvalidValue;

@@ -134,8 +134,12 @@ def device_sparse(f):
     torch.cuda.synchronize()
     ptr, nbytes = f.device_bits()
     t = torch.as_tensor(_DevBytes(ptr, nbytes), device="cuda")
-    nz = torch.nonzero(t).view(-1)
-    return nz.cpu().numpy(), t[nz].cpu().numpy()
+    pos, val = [], []
+    for a in range(0, nbytes, 1 << 28):   # torch.nonzero's scratch grows with its input: 256 MiB pieces
+        nz = torch.nonzero(t[a: a + (1 << 28)]).view(-1) + a
+        pos.append(nz.cpu().numpy())
+        val.append(t[nz].cpu().numpy())
+    return np.concatenate(pos), np.concatenate(val)
 
 
 def sparse_include(orc, set_idx, probe, m, k):

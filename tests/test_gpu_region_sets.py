@@ -53,8 +53,12 @@ def _nonzero_bytes(torch, f):
         __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
 
     t = torch.as_tensor(_B(), device="cuda")
-    nz = torch.nonzero(t).view(-1)
-    return nz.cpu().numpy(), t[nz].cpu().numpy()
+    pos, val = [], []
+    for a in range(0, nbytes, 1 << 28):   # torch.nonzero's scratch grows with its input: 256 MiB pieces
+        nz = torch.nonzero(t[a: a + (1 << 28)]).view(-1) + a
+        pos.append(nz.cpu().numpy())
+        val.append(t[nz].cpu().numpy())
+    return np.concatenate(pos), np.concatenate(val)
 
 
 def _want_sparse(idx):
