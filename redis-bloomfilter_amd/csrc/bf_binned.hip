@@ -2473,8 +2473,8 @@ hipError_t bf_launch_combine_chunks_packed(const uint8_t* packed, const uint16_t
 // ranks' sets in ONE pass over the bitset (sets_apply_kernel), with no sort at all.
 //
 // A set buffer (uint32 words): [0] magic "BFRS", [1] region_log2, [2] regions R, [3] words
-// reserved, [4 + r] region r's first word (0: no offsets), sets from sets_first_word(R) in
-// region order.  Region r's place is reserved before the encode (sets_size_kernel +
+// reserved, [4 + r] region r's first word (0: no offsets), [4 + R + r] its set's header word,
+// sets from sets_first_word(R) in region order.  Region r's place is reserved before the encode (sets_size_kernel +
 // sets_place_kernel): its probe count E_r from the level-2 run tables bounds its set at
 // sets_region_words(E_r) words, so the encode needs no allocator and the layout is a function
 // of the batch alone.  A set: word 0 = n | (l << 24) (l = 31: bitmap), then ceil(n l / 32)
@@ -2485,8 +2485,10 @@ constexpr uint32_t kSetsMagic = 0x53524642u;   // "BFRS"
 constexpr uint32_t kSetsHdr = 4;
 constexpr uint32_t kSetsBitmap = 31u;
 constexpr uint32_t kMaxSetSrc = 16;            // sources per sets_apply launch
+// [4, 4 + R): each region's first word; [4 + R, 4 + 2R): each region's set header (so a
+// reader gets both in one round trip); the sets from sets_first_word(R)
 __host__ __device__ inline uint64_t sets_first_word(uint32_t nbins) {
-    return ((uint64_t)kSetsHdr + nbins + 63) & ~(uint64_t)63;
+    return ((uint64_t)kSetsHdr + 2ull * nbins + 63) & ~(uint64_t)63;
 }
 // bit j of the result <-> region offset 32 w + j (the bitset's word w holds offset 32 w + j at
 // bit j ^ 7: Redis byte order); an involution
@@ -2501,7 +2503,10 @@ __global__ void sets_header_kernel(uint32_t* __restrict__ out, uint32_t rl, uint
         out[2] = nbins;
         out[3] = (uint32_t)sets_first_word(nbins);
     }
-    if (i < nbins) out[kSetsHdr + i] = 0;
+    if (i < nbins) {
+        out[kSetsHdr + i] = 0;
+        out[kSetsHdr + nbins + i] = 0;
+    }
 }
 
 // A bound on the words of the set of a region its batch probes E times: the set has n <= E
@@ -2537,7 +2542,10 @@ __global__ __launch_bounds__(1024) void sets_size_kernel(const uint16_t* __restr
     const uint32_t w = (t < R && r < nbins) ? sets_region_words(s_row[t + 1] - s_row[t], U) : 0u;
     uint32_t total;
     const uint32_t lp = block_excl_scan(w, s_w, &total);
-    if (t < R && r < nbins) out[kSetsHdr + r] = w ? (lp | 0x80000000u) : 0u;
+    if (t < R && r < nbins) {
+        out[kSetsHdr + r] = w ? (lp | 0x80000000u) : 0u;
+        if (!w) out[kSetsHdr + nbins + r] = 0u;   // the encode writes the others
+    }
     if (t == 0) sb_tot[sb] = total;
 }
 
@@ -2620,7 +2628,10 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     // past the capacity (bf_sets_capacity_bytes bounds every batch, so never): not written,
     // and out[3] > capacity tells the reader
     const bool fits = (uint64_t)st + words <= cap_words;
-    if (t == 0) out[kSetsHdr + r] = fits ? st : 0u;   // every lane read rv before the barriers above
+    if (t == 0) {   // every lane read rv before the barriers above
+        out[kSetsHdr + r] = fits ? st : 0u;
+        out[kSetsHdr + gridDim.x + r] = fits ? n | ((bitmap ? kSetsBitmap : l) << 24) : 0u;
+    }
     if (!fits) return;   // workgroup-uniform
     uint32_t* o = out + st;
     if (bitmap) {   // the LDS bitmap is still intact
@@ -2628,9 +2639,17 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         for (uint32_t v = t; v < NW; v += LANES) o[1 + v] = s_m[v];
         return;
     }
-    for (uint32_t v = t; v < lw + uw; v += LANES) s_m[v] = 0;
-    __syncthreads();
     const uint32_t lmask = (1u << l) - 1u;   // l <= RLOG2 < 32
+    if (t == 0) o[0] = n | (l << 24);
+    // n <= NW: the offsets are compacted in rank order into the LDS the bitmap held (its words
+    // are in registers by now), then every output word is built by one lane from the offsets it
+    // covers: plain coalesced stores, no staging image, no atomics.  More offsets than that:
+    // the set is assembled in that LDS by atomics and copied out.
+    const bool compact = n <= NW;   // workgroup-uniform
+    if (!compact) {
+        for (uint32_t v = t; v < lw + uw; v += LANES) s_m[v] = 0;
+        __syncthreads();
+    }
     uint32_t i = base;
 #pragma unroll
     for (uint32_t j = 0; j < WPL; ++j) {
@@ -2639,19 +2658,50 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         while (w) {
             const uint32_t x = x0 + (uint32_t)__builtin_ctz(w);
             w &= w - 1u;
-            if (l) {
-                const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
-                atomicOr(s_m + wi, lo << sh);
-                if (sh + l > 32u) atomicOr(s_m + wi + 1, lo >> (32u - sh));
+            if (compact) {
+                s_m[i] = x;
+            } else {
+                if (l) {
+                    const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
+                    atomicOr(s_m + wi, lo << sh);
+                    if (sh + l > 32u) atomicOr(s_m + wi + 1, lo >> (32u - sh));
+                }
+                const uint32_t u = lw * 32u + (x >> l) + i;
+                atomicOr(s_m + (u >> 5), 1u << (u & 31u));
             }
-            const uint32_t u = lw * 32u + (x >> l) + i;
-            atomicOr(s_m + (u >> 5), 1u << (u & 31u));
             ++i;
         }
     }
     __syncthreads();
-    if (t == 0) o[0] = n | (l << 24);
-    for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
+    if (!compact) {
+        for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
+        return;
+    }
+    for (uint32_t wi = t; wi < lw; wi += LANES) {   // low bits: offsets floor(32 wi / l) ..
+        const uint32_t b0 = wi * 32u;
+        uint32_t word = 0;
+        for (uint32_t e = b0 / l; e < n && e * l < b0 + 32u; ++e) {
+            const uint32_t lo = s_m[e] & lmask;
+            const int32_t sh = (int32_t)(e * l) - (int32_t)b0;   // the field's start in this word
+            word |= sh >= 0 ? (lo << sh) : (lo >> (uint32_t)(-sh));
+        }
+        o[1 + wi] = word;
+    }
+    for (uint32_t ui = t; ui < uw; ui += LANES) {   // upper bitmap: f(e) = (x_e >> l) + e ascends
+        const uint32_t p0 = ui * 32u;
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((s_m[mid] >> l) + mid < p0) lo = mid + 1u; else hi = mid;
+        }
+        uint32_t word = 0;
+        for (uint32_t e = lo; e < n; ++e) {
+            const uint32_t pe = (s_m[e] >> l) + e;
+            if (pe >= p0 + 32u) break;
+            word |= 1u << (pe - p0);
+        }
+        o[1 + lw + ui] = word;
+    }
 }
 
 // One workgroup per region: every source's set for the region ORed into an LDS image (bitmap
@@ -2692,7 +2742,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         uint32_t st = 0, hdr = 0;
         if (S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] <= stride_words) {
             st = S[kSetsHdr + r];
-            if (st) hdr = S[st];
+            hdr = S[kSetsHdr + nbins + r];   // beside the place: one round trip
         } else if (status) {
             atomicOr(status, 1u);
         }
@@ -2819,7 +2869,7 @@ uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2
     const double U = (double)(1ull << rl), N = std::min((double)n * (double)k, U * R);
     double bitsum = 0.0;
     if (N > 0) bitsum = std::min(N * (std::log2(U * R / N) + 3.01), U * R) * 1.01 + 4096.0;
-    const uint64_t words = sets_first_word(R) + 4ull * R + (uint64_t)(bitsum / 32.0) + 64;
+    const uint64_t words = sets_first_word(R) + 4ull * R + (uint64_t)(bitsum / 32.0) + 64;   // (first word: 2R tables)
     return ((words + 63) & ~63ull) * 4;   // whole 256-B units: buffers laid end to end stay aligned
 }
 

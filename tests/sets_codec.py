@@ -3,7 +3,7 @@
 tests can check the encoding itself against the oracle's offsets (ruby.rb:41-55).
 
 Layout (uint32 words): [0] "BFRS", [1] region_log2, [2] regions R, [3] words used, [4 + r]
-region r's first word (0: empty); a set is n | (l << 24), then ceil(n l / 32) words of low
+region r's first word (0: empty), [4 + R + r] its set's header word; a set is n | (l << 24), then ceil(n l / 32) words of low
 bits (offset i's l bits at bit i l, LSB first) and ceil((n + (U >> l)) / 32) words of the upper
 bitmap (offset i sets bit (x_i >> l) + i); l = 31: the region's bitmap in the bitset's own
 word layout (offset x at bit (x & 31) ^ 7 of word x >> 5)."""
@@ -27,8 +27,10 @@ def decode(buf) -> dict:
     for r in range(R):
         st = int(w[4 + r])
         if st == 0:
+            assert int(w[4 + R + r]) == 0, "empty region with a header"
             continue
         hdr = int(w[st])
+        assert int(w[4 + R + r]) == hdr, "header table disagrees with the set"
         n, l = hdr & 0xFFFFFF, hdr >> 24
         if l == 31:
             bm = w[st + 1: st + 1 + U // 32]
@@ -73,7 +75,7 @@ def encode(sets: dict, region_log2: int, nregions: int) -> np.ndarray:
     """A set buffer holding `sets` ({region: sorted distinct offsets}), laid out as the device
     encode lays it out (regions in index order; the device's order is arbitrary)."""
     U = 1 << region_log2
-    first = (4 + nregions + 63) // 64 * 64
+    first = (4 + 2 * nregions + 63) // 64 * 64
     words = [0] * first
     words[0], words[1], words[2] = MAGIC, region_log2, nregions
     for r in range(nregions):
@@ -86,6 +88,7 @@ def encode(sets: dict, region_log2: int, nregions: int) -> np.ndarray:
         if n * l + n + (U >> l) > U:   # bitmap
             bits = np.zeros(U, np.uint8)
             bits[xs.astype(np.int64)] = 1
+            words[4 + nregions + r] = n | (31 << 24)
             words.append(n | (31 << 24))
             words.extend(np.packbits(bits, bitorder="big").view(np.uint32).tolist())
             continue
@@ -97,6 +100,7 @@ def encode(sets: dict, region_log2: int, nregions: int) -> np.ndarray:
             lowbits[: n * l] = ((lo[:, None] >> np.arange(l, dtype=np.uint64)) & np.uint64(1)).astype(np.uint8).reshape(-1)
         up = np.zeros(uw * 32, np.uint8)
         up[(xs >> np.uint64(l)).astype(np.int64) + np.arange(n)] = 1
+        words[4 + nregions + r] = n | (l << 24)
         words.append(n | (l << 24))
         words.extend(np.packbits(lowbits, bitorder="little").view(np.uint32).tolist())
         words.extend(np.packbits(up, bitorder="little").view(np.uint32).tolist())
@@ -112,5 +116,5 @@ def capacity_words(bitset_bytes: int, region_log2: int, n_keys: int, k: int) -> 
     bits = 0.0
     if N > 0:
         bits = min(N * (np.log2(U * R / N) + 3.01), U * R) * 1.01 + 4096.0
-    words = (4 + R + 63) // 64 * 64 + 4 * R + int(bits / 32.0) + 64
+    words = (4 + 2 * R + 63) // 64 * 64 + 4 * R + int(bits / 32.0) + 64
     return (words + 63) // 64 * 64

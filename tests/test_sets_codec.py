@@ -39,6 +39,6 @@ def test_capacity_bounds_even_batches(n_keys, k, bitset):
     n = max(1, min(U, int(round(per))))
     rng = np.random.default_rng(1)
     xs = np.sort(rng.choice(U, size=n, replace=False)).astype(np.uint64)
-    one = len(sets_codec.encode({0: xs}, rl, 1)) - (4 + 1 + 63) // 64 * 64
-    need = (4 + R + 63) // 64 * 64 + one * min(R, n_keys * k)
+    one = len(sets_codec.encode({0: xs}, rl, 1)) - (4 + 2 + 63) // 64 * 64
+    need = (4 + 2 * R + 63) // 64 * 64 + one * min(R, n_keys * k)
     assert need <= sets_codec.capacity_words(bitset, rl, n_keys, k)
