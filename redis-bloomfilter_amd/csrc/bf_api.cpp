@@ -759,6 +759,7 @@ int bf_indexes(const uint8_t* key, uint64_t len, uint64_t m_bits, uint32_t k, ui
     g.nomod = (m_bits > (uint64_t)k * 0xFFFFFFFFull) ? 1u : 0u;
     g.mod_f32 = (m_bits >= (1ull << 17)) ? 1u : 0u;
     g.inv_m_f = (float)(1.0 / (double)m_bits);
+    g.mod_sub = bf_mod_sub(m_bits, (uint64_t)k * 0xFFFFFFFFull);
     g.shards = 1;
     g.inv_shards = 1.0;
     const uint64_t kb = round_up(len + 16, 16);
@@ -913,6 +914,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.nomod = (m_bits > maxval) ? 1u : 0u;
     h->g.mod_f32 = (m_bits >= (1ull << 17)) ? 1u : 0u;
     h->g.inv_m_f = (float)(1.0 / (double)m_bits);
+    // BFHIP_MOD_SUB=0: the float-estimate modulo everywhere (A/B)
+    h->g.mod_sub = env_u32("BFHIP_MOD_SUB", 1) ? bf_mod_sub(m_bits, (uint64_t)k * 0xFFFFFFFFull) : 0u;
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
     h->g.inv_shards = 1.0 / (double)h->shards;

@@ -2579,7 +2579,8 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
                                                             const uint32_t* __restrict__ cb_start,
                                                             const uint16_t* __restrict__ tabs, uint64_t max_chunks,
                                                             uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
-                                                            const uint32_t* __restrict__ sb_first, uint32_t cap_words) {
+                                                            const uint32_t* __restrict__ sb_first, uint32_t cap_words,
+                                                            uint32_t stop) {
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
     static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
     __shared__ uint4 s_m4[NW / 4];
@@ -2591,7 +2592,7 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     const uint32_t rv = out[kSetsHdr + r], sbf = sb_first[r >> rel_log2];
     for (uint32_t v = t; v < NW / 4; v += LANES) s_m4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    if (!(rv & 0x80000000u)) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
+    if (!(rv & 0x80000000u) || stop == 3) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
     const uint32_t st = sbf + (rv & 0x7FFFFFFFu);
     for_region_probes<8>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
         [&](const uint32_t* idx) {
@@ -2602,6 +2603,7 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
             for (int c = 0; c < 8; ++c)
                 if (l[c] != 0xFFFFFFFFu) atomicOr(s_m + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
         });
+    if (stop == 2) return;   // (A/B: where the time goes; BFHIP_SETS_STOP)
     uint32_t wv[WPL];
     uint32_t cnt = 0;
 #pragma unroll
@@ -2634,6 +2636,7 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     }
     if (!fits) return;   // workgroup-uniform
     uint32_t* o = out + st;
+    if (stop == 1) return;
     if (bitmap) {   // the LDS bitmap is still intact
         if (t == 0) o[0] = n | (kSetsBitmap << 24);
         for (uint32_t v = t; v < NW; v += LANES) o[1 + v] = s_m[v];
@@ -2849,6 +2852,18 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
 }
 }  // namespace
 
+namespace {
+// A/B only (BFHIP_SETS_STOP): the encode stops after its probe pass (2), before writing the set
+// (1), or at once (3); the output is then incomplete.  0: the whole encode.
+uint32_t sets_stop() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("BFHIP_SETS_STOP");
+        return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    }();
+    return v;
+}
+}  // namespace
+
 bool bf_sets_geometry(uint64_t bitset_bytes, uint32_t pref_region_log2, uint32_t* region_log2, uint32_t* nbins) {
     BfBinPlan p{};
     if (!plan_common(bitset_bytes, 1, 1, 1, pref_region_log2, false, &p)) return false;
@@ -2893,11 +2908,11 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
     if (p.region_log2 == 19)
         hipLaunchKernelGGL((sets_encode_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, c.level2,
                            c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot,
-                           (uint32_t)cap_words);
+                           (uint32_t)cap_words, sets_stop());
     else if (p.region_log2 == 18)
         hipLaunchKernelGGL((sets_encode_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot,
-                           (uint32_t)cap_words);
+                           (uint32_t)cap_words, sets_stop());
     else
         return hipErrorInvalidValue;
     bf_mark(mk, s, "sets_encode");

@@ -148,6 +148,13 @@ __device__ __forceinline__ uint64_t probe_offset(const BfGeom& g, uint32_t h0, u
     const uint32_t b = (((i + (i & 1u)) & 3u) >> 1) ? h3 : h2;
     const uint64_t v = (uint64_t)a + (uint64_t)i * (uint64_t)b;  // < k * 2^32: exact
     if (g.nomod) return v;
+    if (g.mod_sub) {   // v < (mod_sub + 1) m: conditional subtractions, no estimate
+        uint64_t r = v;
+#pragma unroll
+        for (uint32_t j = 0; j < 3u; ++j)
+            if (j < g.mod_sub) r = r >= g.m ? r - g.m : r;
+        return r;
+    }
     if (g.mod_f32) {
         // m >= 2^17 (set at create): q = v/m < 2^21 (v < 2^38), and a float32 estimate
         // (relative error <= 2^-22) is off by at most one after truncation; the remainder

@@ -12,6 +12,9 @@ struct BfGeom {
     uint32_t  nomod;   // 1 iff m > k*(2^32-1): every derived offset is already < m
     uint32_t  mod_f32; // 1 iff m >= 2^17: the quotient is estimated in float32 (else float64)
     float     inv_m_f; // (float)(1.0 / m)
+    uint32_t  mod_sub; // 1..3: every derived offset v <= vmax is below (mod_sub + 1) m, so v mod m
+                       // is at most mod_sub conditional subtractions (the north-star m ~ 2.2 x 2^32:
+                       // 2); 0: the float-estimate paths (bf_mod_sub)
     uint32_t  shards;  // partitioned filters: shard count P (1 = whole filter)
     uint32_t  block_log2;  // ownership block = 2^block_log2 bits, owner = block % P
     double    inv_shards;  // 1.0 / P, for the division-free block -> (owner, local block) map
@@ -34,6 +37,13 @@ struct BfGeom {
     uint64_t  flip_cap;
     uint64_t  flip_tag;     // ORed into every reported offset (the Lua layout: layer << 58)
 };
+
+// BfGeom::mod_sub for a modulus m and the largest value the derivation reaches (ruby.rb:51:
+// k (2^32 - 1); the Lua scripts' i = 1..k: (k + 1) (2^32 - 1)).
+inline uint32_t bf_mod_sub(uint64_t m, uint64_t vmax) {
+    const uint64_t q = vmax / m;
+    return q <= 3 ? (uint32_t)q : 0u;
+}
 
 constexpr uint32_t kDirtyShiftBits = 19;   // dirty-tracking block: 2^19 bits = BF_DIRTY_BLOCK_BYTES of the string
 

@@ -169,6 +169,7 @@ int ensure_layer(bf_lua* h, uint32_t n) {
         g.nomod = m > (uint64_t)(k + 1) * 0xFFFFFFFFull ? 1u : 0u;   // probes i = 1..k: v <= (k+1)(2^32-1)
         g.mod_f32 = m >= (1ull << 17) ? 1u : 0u;
         g.inv_m_f = (float)(1.0 / (double)m);
+        g.mod_sub = bf_mod_sub(m, (uint64_t)(k + 1) * 0xFFFFFFFFull);
         g.shards = 1;
         g.inv_shards = 1.0;
         g.block_log2 = 20;
