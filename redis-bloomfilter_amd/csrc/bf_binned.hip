@@ -676,9 +676,12 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
         const bool live1 = kpl == 2 && kTile + t < tk;
         uint32_t tag[SLOTS], lo[SLOTS];
         uint8_t hi[SLOTS];
+        // keys per lane as a compile-time constant (as bin_front_body): each slot's i is one
+        auto probes = [&](auto kplc) {
+        constexpr uint32_t KPL = decltype(kplc)::value;
 #pragma unroll
         for (int q = 0; q < SLOTS; ++q) {
-            const bool second = kpl == 2 && q >= (int)kTwoKeys;
+            const bool second = KPL == 2 && q >= (int)kTwoKeys;
             const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
             const bool live = i < k && (second ? live1 : live0);
             tag[q] = 0xFFFFFFFFu;
@@ -711,6 +714,9 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 tag[q] = (owner << 16) | atomicAdd(s_cnt + owner, 1u);
             }
         }
+        };
+        if (kpl == 2) probes(std::integral_constant<uint32_t, 2>{});
+        else probes(std::integral_constant<uint32_t, 1>{});
         __syncthreads();
         const uint32_t c = t < NB ? s_cnt[t] : 0u;
         const uint32_t ex = block_excl_scan(c, s_w, nullptr);
