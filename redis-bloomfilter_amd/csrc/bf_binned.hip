@@ -84,21 +84,11 @@ constexpr uint32_t kPipeLanes = 1024;         // bin_apply_pipe_kernel: one work
 // Contains barriers: every lane must call it.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= (uint32_t)off) x += y;
-    }
+    const uint32_t x = wave_incl_scan(v);
     if (lane == 63u) s_w[wid] = x;
     __syncthreads();
     if (wid == 0) {
-        uint32_t s = lane < nw ? s_w[lane] : 0u;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const uint32_t y = __shfl_up(s, off);
-            if (lane >= (uint32_t)off) s += y;
-        }
+        const uint32_t s = wave_incl_scan(lane < nw ? s_w[lane] : 0u);
         if (lane < nw) s_w[lane] = s;   // inclusive wave totals
     }
     __syncthreads();

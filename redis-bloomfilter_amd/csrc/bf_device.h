@@ -88,6 +88,21 @@ __device__ __forceinline__ void sha1_key(Src src, uint32_t s, uint32_t L, uint32
     }
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS round trips, as
+// __shfl_up's ds_bpermute takes): four row shifts inside each 16-lane row, then the row ends
+// broadcast into the rows above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and
+// 3; gfx9-family DPP).  A lane whose source is shifted out or masked keeps 0.  Every lane of the
+// wave must be active (block_excl_scan's contract).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
