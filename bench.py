@@ -205,10 +205,11 @@ def prefill_random(f, m: int, k: int, rank: int, host_copy: bool = True):
 
 
 # The replicated layout's insert form per config (ReplicatedFilter insert_mode; "auto" picks
-# key bytes or the OR-all-reduce by size).  10B@0.01 % (k = 13): the SHA-1 words travel, so
-# every replica skips P - 1 hash passes (tools/sim_rank.py --replicated 8:
-# profiles/r03_sim_replicated8_10b.jsonl).
-REPLICATED_INSERT = {"10b": "digests"}
+# key bytes or the OR-all-reduce by size).  10B@0.01 % (BASELINE configs[3], k = 13): region
+# sets — each rank sorts and encodes its own batch once, every replica ORs all ranks' sets in
+# one pass: one replica's step 17.8 -> 12.5 ms against the SHA-1 words form on the same box
+# (tools/sim_rank.py --replicated 8: profiles/r04b_sim_replicated.jsonl).
+REPLICATED_INSERT = {"10b": "sets"}
 
 
 def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
