@@ -2481,6 +2481,7 @@ constexpr uint32_t kSetsMagic = 0x53524642u;   // "BFRS"
 constexpr uint32_t kSetsHdr = 4;
 constexpr uint32_t kSetsBitmap = 31u;
 constexpr uint32_t kMaxSetSrc = 16;            // sources per sets_apply launch
+constexpr uint32_t kLowsStage = 3840;           // low-bit words sets_apply stages in LDS (15 KB: two 2^19-bit workgroups per CU)
 // [4, 4 + R): each region's first word; [4 + R, 4 + 2R): each region's set header (so a
 // reader gets both in one round trip); the sets from sets_first_word(R)
 __host__ __device__ inline uint64_t sets_first_word(uint32_t nbins) {
@@ -2722,6 +2723,8 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     __shared__ uint4 s_mask4[kVec];
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_st[kMaxSetSrc], s_hdr[kMaxSetSrc], s_uw0[kMaxSetSrc + 1], s_np[kMaxSetSrc + 1];
+    __shared__ uint32_t s_lw0[kMaxSetSrc + 1];
+    __shared__ uint32_t s_lows[kLowsStage + 1];   // every Elias-Fano source's low-bit words, back to back
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
     const uint32_t r = blockIdx.x;
@@ -2749,21 +2752,37 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         s_hdr[t] = hdr;
     }
     __syncthreads();
-    if (t == 0) {   // upper-bitmap words and offsets of the Elias-Fano sources before each source
-        uint32_t a = 0, np = 0;
+    if (t == 0) {   // upper-bitmap words, low-bit words and offsets of the Elias-Fano sources before each source
+        uint32_t a = 0, np = 0, lw = 0;
         for (uint32_t s = 0; s < nsrc; ++s) {
             s_uw0[s] = a;
             s_np[s] = np;
+            s_lw0[s] = lw;
             const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
             if (s_st[s] && l != kSetsBitmap) {
                 a += (n + (U >> l) + 31u) / 32u;
                 np += n;
+                lw += (n * l + 31u) / 32u;
             }
         }
         s_uw0[nsrc] = a;
         s_np[nsrc] = np;
+        s_lw0[nsrc] = lw;
     }
     __syncthreads();
+    // The low bits are read in offset order, a word or two per offset: staged once into LDS,
+    // coalesced, instead of a dependent global load per offset.  Sets too big for the stage
+    // (dense regions, many sources) read them from global memory.
+    const uint32_t TL = s_lw0[nsrc];
+    const bool staged = TL <= kLowsStage;   // workgroup-uniform
+    if (staged) {
+        uint32_t s = 0;
+        for (uint32_t q = t; q < TL; q += LANES) {
+            while (s_lw0[s + 1] <= q) ++s;
+            s_lows[q] = sets[(uint64_t)s * stride_words + s_st[s] + 1 + (q - s_lw0[s])];
+        }
+        if (t == 0) s_lows[TL] = 0;   // the word past the last source's lows: read, masked off
+    }
     for (uint32_t s = 0; s < nsrc; ++s) {   // bitmap sets
         if (!s_st[s] || (s_hdr[s] >> 24) != kSetsBitmap) continue;   // workgroup-uniform
         const uint32_t* B = sets + (uint64_t)s * stride_words + s_st[s] + 1;
@@ -2783,32 +2802,28 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
             word = sets[(uint64_t)s * stride_words + s_st[s] + 1 + (n * l + 31u) / 32u + (g - s_uw0[s])];
         }
         uint32_t tot;
-        const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);
-        if (word) {   // ~16 offsets: their low bits are consecutive, read through a 3-word window
+        const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);   // (its barriers also order the staging)
+        if (word) {   // ~16 offsets: their low bits are consecutive
             const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
             const uint32_t* lows = sets + (uint64_t)s * stride_words + s_st[s] + 1;
+            const uint32_t* slows = s_lows + s_lw0[s];
             const uint32_t lmask = (1u << l) - 1u;
             uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
             const uint32_t p0 = (g - s_uw0[s]) * 32u;
             const uint32_t lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
-            uint32_t wi = (i * l) >> 5;
-            uint32_t a = 0, b = 0, c = 0;
-            if (l) {   // loaded together, one word ahead of use
-                a = lows[wi];
-                b = lows[min(wi + 1u, lim)];
-                c = lows[min(wi + 2u, lim)];
-            }
             while (word) {
                 const uint32_t p = p0 + (uint32_t)__builtin_ctz(word);
                 word &= word - 1u;
                 uint32_t lo = 0;
                 if (l) {
-                    const uint32_t bp = i * l;
-                    while ((bp >> 5) != wi) {
-                        a = b;
-                        b = c;
-                        ++wi;
-                        c = lows[min(wi + 2u, lim)];
+                    const uint32_t bp = i * l, wi = bp >> 5;
+                    uint32_t a, b;
+                    if (staged) {
+                        a = slows[wi];
+                        b = slows[wi + 1u];
+                    } else {
+                        a = lows[wi];
+                        b = lows[min(wi + 1u, lim)];
                     }
                     lo = (uint32_t)(((uint64_t)b << 32 | a) >> (bp & 31u)) & lmask;
                 }

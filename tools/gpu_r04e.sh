@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 TAG=${1:-r04e}
 # parity first: the modulo and route changes touch every offset
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_distributed.py tests/test_gpu_digests.py \
+timeout -k 10 560 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_distributed.py tests/test_gpu_digests.py tests/test_gpu_region_sets.py \
     -x -q --timeout 200 --timeout-method thread > gpurun_out/tests_${TAG}_parity.log 2>&1 || exit $?
 for st in 0 1 2 3; do
     BFHIP_SETS_STOP=$st timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 \
