@@ -1,42 +1,95 @@
 #!/bin/bash
-# Full GPU-box pass: every -m gpu test, smoke(), the driver's bench command, a kernel-trace
-# profile of the bench, and the PMC passes (tools/pmc_passes.sh).
+# GPU-box passes, one script for every round (no per-round one-off scripts).
 # Run from the repo root: gpurun -- bash tools/gpu_round.sh <tag> [steps...]
-#   steps: tests smoke bench prof pmc (default: all); also simP8 (the P = 8 per-rank step:
-#   time + stall/LDS + VALU counters), repl (one replica's step of the replicated 10B x 8 and
-#   north-star x 2 layouts, per insert form)
+#   tests      every -m gpu test (PYTEST_EXTRA adds flags, e.g. --durations=100)
+#   parity     the parity files alone: parity, distributed primitives, digests, region sets
+#   sets       region-set tests + the replicated / region-set multi-rank gloo cases
+#   smoke      __graft_entry__.smoke()
+#   bench      the driver's bench command (--gpus 1 --steps 20 --warmup 5)
+#   bench10b / bench200b / bench100m   the other single-GPU configs
+#   prof       kernel trace (rocprofv3 --kernel-trace --stats) of a short bench run
+#   pmc        the PMC passes of tools/pmc_passes.sh on the north-star bench
+#   simP8      the P = 8 per-rank step (tools/sim_rank.py): time + stall/LDS + VALU counters
+#   simP8t     the P = 8 per-rank step, time only
+#   repl       one replica's step of the replicated 10B x 8 and north-star x 2 layouts, per
+#              insert form
+#   replprof   kernel trace of the 10B x 8 region-set replica step
+#   replpmc    stall/LDS + VALU counters of the 10B x 8 region-set replica step
+#   ab         an A/B over one environment variable: AB_VAR, AB_VALUES (interleaved, e.g.
+#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, repl10b}; lines appended to
+#              gpurun_out/ab_${AB_VAR}_<tag>.jsonl
+# Default: tests smoke bench prof pmc.  Every GPU step runs under its own time limit; a failing
+# step ends the script (no further GPU work after a fault, abort or time limit).
 export TMPDIR=/tmp
 TAG=${1:-round}
 shift
 STEPS=${*:-tests smoke bench prof pmc}
+NOEXTRA="--no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes"
+STALL="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS"
+VALU="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_SALU"
+PYT="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
+
+ab_cmd() {   # one A/B line's command, stdout = its JSON
+    case $1 in
+        nstar|10b|200b) timeout -k 10 150 python bench.py --config $1 --steps 10 --warmup 3 $NOEXTRA 2>/dev/null ;;
+        simP8)   timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 2>/dev/null ;;
+        repl10b) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 2>/dev/null ;;
+        *) echo "unknown AB_CMD $1" >&2; return 2 ;;
+    esac
+}
+
 for st in $STEPS; do
     case $st in
-        tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-                   ${PYTEST_EXTRA:-} > gpurun_out/tests_${TAG}.log 2>&1 ;;
-        smoke) timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
-        bench) timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
-                   > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
-        prof)  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- \
-                   python bench.py --steps 5 --warmup 2 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes \
-                   > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/bench_prof_${TAG}.err ;;
-        pmc)   bash tools/pmc_passes.sh nstar ${TAG}_nstar ;;
-        simP8) timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 \
-                   > gpurun_out/sim_P8_${TAG}.json 2> gpurun_out/sim_P8_${TAG}.err &&
-               timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-                   SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS --output-format csv \
-                   -d gpurun_out/pmc_${TAG}_P8_stall -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
-                   > gpurun_out/pmc_${TAG}_P8_stall.log 2>&1 &&
-               timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES \
-                   GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv \
-                   -d gpurun_out/pmc_${TAG}_P8_valu -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
-                   > gpurun_out/pmc_${TAG}_P8_valu.log 2>&1 ;;
-        repl)  for g in digests sets "sets --fused-hash"; do
-                   timeout -k 10 240 python tools/sim_rank.py --replicated 8 --config 10b --gathered $g --steps 3 \
-                       >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
-               done &&
-               for g in keys sets "sets --fused-hash"; do
-                   timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered $g --steps 5 \
-                       >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
-               done ;;
+        tests)  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+                    ${PYTEST_EXTRA:-} > gpurun_out/tests_${TAG}.log 2>&1 ;;
+        parity) timeout -k 10 560 $PYT tests/test_gpu_parity.py tests/test_gpu_distributed.py tests/test_gpu_digests.py \
+                    tests/test_gpu_region_sets.py > gpurun_out/tests_${TAG}_parity.log 2>&1 ;;
+        sets)   timeout -k 10 300 $PYT tests/test_gpu_region_sets.py tests/test_gpu_dist_gloo.py -k "sets or replicated" \
+                    > gpurun_out/tests_${TAG}_sets.log 2>&1 ;;
+        smoke)  timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
+        bench)  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
+                    > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
+        bench10b|bench200b|bench100m)
+                timeout -k 10 300 python bench.py --config ${st#bench} --steps 20 --warmup 5 $NOEXTRA \
+                    > gpurun_out/bench_${st#bench}_${TAG}.json 2> gpurun_out/bench_${st#bench}_${TAG}.err ;;
+        prof)   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- \
+                    python bench.py --steps 5 --warmup 2 $NOEXTRA \
+                    > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/bench_prof_${TAG}.err ;;
+        pmc)    bash tools/pmc_passes.sh nstar ${TAG}_nstar ;;
+        simP8t) timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 \
+                    > gpurun_out/sim_P8_${TAG}.json 2> gpurun_out/sim_P8_${TAG}.err ;;
+        simP8)  timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 \
+                    > gpurun_out/sim_P8_${TAG}.json 2> gpurun_out/sim_P8_${TAG}.err &&
+                timeout -s KILL 120 rocprofv3 --pmc $STALL --output-format csv \
+                    -d gpurun_out/pmc_${TAG}_P8_stall -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
+                    > gpurun_out/pmc_${TAG}_P8_stall.log 2>&1 &&
+                timeout -s KILL 120 rocprofv3 --pmc $VALU --output-format csv \
+                    -d gpurun_out/pmc_${TAG}_P8_valu -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
+                    > gpurun_out/pmc_${TAG}_P8_valu.log 2>&1 ;;
+        repl)   for g in digests sets "sets --fused-hash"; do
+                    timeout -k 10 240 python tools/sim_rank.py --replicated 8 --config 10b --gathered $g --steps 3 \
+                        >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
+                done &&
+                for g in keys sets "sets --fused-hash"; do
+                    timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered $g --steps 5 \
+                        >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
+                done ;;
+        replprof)
+                timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sets_${TAG} -o run -- \
+                    python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash --steps 3 \
+                    > gpurun_out/prof_sets_${TAG}.json 2>/dev/null ;;
+        replpmc)
+                timeout -s KILL 150 rocprofv3 --pmc $STALL --output-format csv -d gpurun_out/pmc_${TAG}_sets_1 -o run -- \
+                    python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 1 \
+                    > gpurun_out/pmc_${TAG}_sets_1.log 2>&1 &&
+                timeout -s KILL 150 rocprofv3 --pmc $VALU --output-format csv -d gpurun_out/pmc_${TAG}_sets_2 -o run -- \
+                    python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 1 \
+                    > gpurun_out/pmc_${TAG}_sets_2.log 2>&1 ;;
+        ab)     for v in ${AB_VALUES:?}; do
+                    line=$(export "${AB_VAR:?}=$v"; ab_cmd "${AB_CMD:?}") || exit $?
+                    echo "{\"var\": \"$AB_VAR\", \"value\": \"$v\", \"cmd\": \"$AB_CMD\", \"line\": $line}" \
+                        >> gpurun_out/ab_${AB_VAR}_${TAG}.jsonl
+                done ;;
+        *)      echo "unknown step $st"; exit 2 ;;
     esac || { echo "step $st failed: $?"; exit 1; }
 done
