@@ -2568,12 +2568,8 @@ __global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__
 
 // One workgroup per region: the region's probes (level 2, as bin_apply gathers them) into an
 // LDS bitmap, then each lane's WPL consecutive words -> its offsets in ascending order (their
-// ranks from one workgroup scan).  A set of at most U / 128 offsets (l >= 7: at most
-// U * 9 / 4096 words) is assembled in its own small LDS stage while the bitmap stays intact:
-// each lane walks only its non-zero words, one offset per trip, and ORs the offset's low bits
-// and upper bit into the stage; the stage is then copied out.  Larger sets are assembled in the
-// bitmap's LDS (its words in registers by then).  69 KiB of LDS at 2^19-bit regions: two
-// workgroups per CU.
+// ranks from one workgroup scan), the set built in the same LDS (the bitmap words are in
+// registers by then) and copied out.  72 KiB of LDS at 2^19-bit regions: two workgroups per CU.
 template <uint32_t RLOG2, uint32_t LANES>
 __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __restrict__ level2,
                                                             const uint32_t* __restrict__ cb_base,
@@ -2583,10 +2579,8 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
                                                             const uint32_t* __restrict__ sb_first, uint32_t cap_words,
                                                             uint32_t stop) {
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
-    constexpr uint32_t NSMALL = U / 128, SSTAGE = NSMALL * 9 / 32 + 2;   // n <= NSMALL: l >= 7
-    static_assert(WPL * LANES == NW && WPL % 4 == 0 && WPL <= 32, "region words must tile the lanes in vectors");
+    static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
     __shared__ uint4 s_m4[NW / 4];
-    __shared__ uint32_t s_set[SSTAGE];
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
     uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
     const uint32_t t = threadIdx.x, r = blockIdx.x;
@@ -2594,9 +2588,12 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     // (sets_size_kernel / sets_place_kernel); loaded while the LDS image is cleared
     const uint32_t rv = out[kSetsHdr + r], sbf = sb_first[r >> rel_log2];
     for (uint32_t v = t; v < NW / 4; v += LANES) s_m4[v] = make_uint4(0, 0, 0, 0);
-    for (uint32_t v = t; v < SSTAGE; v += LANES) s_set[v] = 0;
     __syncthreads();
-    if (!(rv & 0x80000000u) || stop == 3) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
+    if (!(rv & 0x80000000u)) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
+    if (stop == 3) {   // (A/B: where the time goes; BFHIP_SETS_STOP) the region left absent
+        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;   // every lane read rv before the barrier
+        return;
+    }
     const uint32_t st = sbf + (rv & 0x7FFFFFFFu);
     for_region_probes<8>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
         [&](const uint32_t* idx) {
@@ -2607,23 +2604,22 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
             for (int c = 0; c < 8; ++c)
                 if (l[c] != 0xFFFFFFFFu) atomicOr(s_m + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
         });
-    if (stop == 2) return;   // (A/B: where the time goes; BFHIP_SETS_STOP)
+    if (stop == 2) {   // (A/B)
+        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
+        return;
+    }
     uint32_t wv[WPL];
-    uint32_t cnt = 0, nz = 0;   // nz: bit j <-> the lane's word j has offsets
+    uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t q = 0; q < WPL / 4; ++q) {
         const uint4 v = s_m4[t * (WPL / 4) + q];
-        wv[4 * q + 0] = v.x;
-        wv[4 * q + 1] = v.y;
-        wv[4 * q + 2] = v.z;
-        wv[4 * q + 3] = v.w;
+        wv[4 * q + 0] = offset_order(v.x);
+        wv[4 * q + 1] = offset_order(v.y);
+        wv[4 * q + 2] = offset_order(v.z);
+        wv[4 * q + 3] = offset_order(v.w);
     }
 #pragma unroll
-    for (uint32_t j = 0; j < WPL; ++j) {
-        const uint32_t c = __popc(wv[j]);
-        cnt += c;
-        nz |= min(c, 1u) << j;
-    }
+    for (uint32_t j = 0; j < WPL; ++j) cnt += __popc(wv[j]);
     uint32_t n;
     const uint32_t base = block_excl_scan(cnt, s_w, &n);   // its barriers: every lane has read s_m
     uint32_t l = 0, lw = 0, uw = 0, words = 0;
@@ -2652,51 +2648,67 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     }
     const uint32_t lmask = (1u << l) - 1u;   // l <= RLOG2 < 32
     if (t == 0) o[0] = n | (l << 24);
-    const uint32_t lw32 = lw * 32u;
-    if (n <= NSMALL) {   // workgroup-uniform
-        uint32_t i = base, w = 0, x0 = 0;
-        while (w | nz) {   // one offset per trip
-            if (!w) {
-                const uint32_t j = (uint32_t)__builtin_ctz(nz);
-                nz &= nz - 1u;
-                w = offset_order(s_m[t * WPL + j]);
-                x0 = (t * WPL + j) * 32u;
-            }
-            const uint32_t x = x0 + (uint32_t)__builtin_ctz(w);
-            w &= w - 1u;
-            const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
-            atomicOr(s_set + wi, lo << sh);
-            if (sh + l > 32u) atomicOr(s_set + wi + 1, lo >> (32u - sh));
-            const uint32_t u = lw32 + (x >> l) + i;
-            atomicOr(s_set + (u >> 5), 1u << (u & 31u));
-            ++i;
-        }
+    // n <= NW: the offsets are compacted in rank order into the LDS the bitmap held (its words
+    // are in registers by now), then every output word is built by one lane from the offsets it
+    // covers: plain coalesced stores, no staging image, no atomics.  More offsets than that:
+    // the set is assembled in that LDS by atomics and copied out.
+    const bool compact = n <= NW;   // workgroup-uniform
+    if (!compact) {
+        for (uint32_t v = t; v < lw + uw; v += LANES) s_m[v] = 0;
         __syncthreads();
-        for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_set[v];
-        return;
     }
-    for (uint32_t v = t; v < lw + uw; v += LANES) s_m[v] = 0;   // every lane's words are in wv
-    __syncthreads();
     uint32_t i = base;
 #pragma unroll
     for (uint32_t j = 0; j < WPL; ++j) {
-        uint32_t w = offset_order(wv[j]);
+        uint32_t w = wv[j];
         const uint32_t x0 = (t * WPL + j) * 32u;
         while (w) {
             const uint32_t x = x0 + (uint32_t)__builtin_ctz(w);
             w &= w - 1u;
-            if (l) {
-                const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
-                atomicOr(s_m + wi, lo << sh);
-                if (sh + l > 32u) atomicOr(s_m + wi + 1, lo >> (32u - sh));
+            if (compact) {
+                s_m[i] = x;
+            } else {
+                if (l) {
+                    const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
+                    atomicOr(s_m + wi, lo << sh);
+                    if (sh + l > 32u) atomicOr(s_m + wi + 1, lo >> (32u - sh));
+                }
+                const uint32_t u = lw * 32u + (x >> l) + i;
+                atomicOr(s_m + (u >> 5), 1u << (u & 31u));
             }
-            const uint32_t u = lw32 + (x >> l) + i;
-            atomicOr(s_m + (u >> 5), 1u << (u & 31u));
             ++i;
         }
     }
     __syncthreads();
-    for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
+    if (!compact) {
+        for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
+        return;
+    }
+    for (uint32_t wi = t; wi < lw; wi += LANES) {   // low bits: offsets floor(32 wi / l) ..
+        const uint32_t b0 = wi * 32u;
+        uint32_t word = 0;
+        for (uint32_t e = b0 / l; e < n && e * l < b0 + 32u; ++e) {
+            const uint32_t lo = s_m[e] & lmask;
+            const int32_t sh = (int32_t)(e * l) - (int32_t)b0;   // the field's start in this word
+            word |= sh >= 0 ? (lo << sh) : (lo >> (uint32_t)(-sh));
+        }
+        o[1 + wi] = word;
+    }
+    for (uint32_t ui = t; ui < uw; ui += LANES) {   // upper bitmap: f(e) = (x_e >> l) + e ascends
+        const uint32_t p0 = ui * 32u;
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((s_m[mid] >> l) + mid < p0) lo = mid + 1u; else hi = mid;
+        }
+        uint32_t word = 0;
+        for (uint32_t e = lo; e < n; ++e) {
+            const uint32_t pe = (s_m[e] >> l) + e;
+            if (pe >= p0 + 32u) break;
+            word |= 1u << (pe - p0);
+        }
+        o[1 + lw + ui] = word;
+    }
 }
 
 // One workgroup per region: every source's set for the region ORed into an LDS image (bitmap
@@ -2737,12 +2749,21 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     if (t < nsrc) {   // source t's set for this region
         const uint32_t* S = sets + (uint64_t)t * stride_words;
         uint32_t st = 0, hdr = 0;
-        if (S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] <= stride_words) {
+        bool ok = S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] <= stride_words;
+        if (ok) {
             st = S[kSetsHdr + r];
             hdr = S[kSetsHdr + nbins + r];   // beside the place: one round trip
-        } else if (status) {
-            atomicOr(status, 1u);
+            if (st) {   // the set must lie inside the buffer: a damaged entry is skipped, not read
+                const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
+                const bool shape = n && n <= U && (l == kSetsBitmap || l < RLOG2);
+                const uint64_t need = !shape ? 0 : 1ull + (l == kSetsBitmap ? NW : (n * l + 31u) / 32u + (n + (U >> l) + 31u) / 32u);
+                if (!shape || (uint64_t)st + need > stride_words) {
+                    ok = false;
+                    st = hdr = 0;
+                }
+            }
         }
+        if (!ok && status) atomicOr(status, 1u);
         s_st[t] = st;
         s_hdr[t] = hdr;
     }

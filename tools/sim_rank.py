@@ -322,7 +322,8 @@ def replicated(args, pkg):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.steps
     prof = f.profile_read(reset=True)
-    assert out.cpu().numpy()[: batch // 2].all(), "false negative"
+    if os.environ.get("BFHIP_SETS_STOP", "0") == "0":   # (the encode stop-point A/B writes no sets)
+        assert out.cpu().numpy()[: batch // 2].all(), "false negative"
     one = None
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
            "fused_hash": bool(args.fused_hash), "m": m, "k": k,
