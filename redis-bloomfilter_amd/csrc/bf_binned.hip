@@ -2482,6 +2482,7 @@ constexpr uint32_t kSetsHdr = 4;
 constexpr uint32_t kSetsBitmap = 31u;
 constexpr uint32_t kMaxSetSrc = 16;            // sources per sets_apply launch
 constexpr uint32_t kLowsStage = 3840;           // low-bit words sets_apply stages in LDS (15 KB: two 2^19-bit workgroups per CU)
+constexpr uint32_t kLowsStageBig = 12288;       // ... 48 KB: one workgroup per CU (BFHIP_SETS_STAGE=2)
 // [4, 4 + R): each region's first word; [4 + R, 4 + 2R): each region's set header (so a
 // reader gets both in one round trip); the sets from sets_first_word(R)
 __host__ __device__ inline uint64_t sets_first_word(uint32_t nbins) {
@@ -2717,7 +2718,7 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
 // minus the offsets of the sources before it), then bin_apply's read-OR-write of the region.
 // A source whose header does not match (magic, region geometry, capacity) is skipped and
 // flagged in *status.
-template <uint32_t RLOG2, uint32_t LANES>
+template <uint32_t RLOG2, uint32_t LANES, uint32_t STAGE>
 __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
                                                            const uint32_t* __restrict__ sets, uint64_t stride_words,
                                                            uint32_t nsrc, uint32_t nbins, uint32_t dense,
@@ -2731,7 +2732,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_st[kMaxSetSrc], s_hdr[kMaxSetSrc], s_uw0[kMaxSetSrc + 1], s_np[kMaxSetSrc + 1];
     __shared__ uint32_t s_lw0[kMaxSetSrc + 1];
-    __shared__ uint32_t s_lows[kLowsStage + 1];   // every Elias-Fano source's low-bit words, back to back
+    __shared__ uint32_t s_lows[STAGE + 1];   // every Elias-Fano source's low-bit words, back to back
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
     const uint32_t r = blockIdx.x;
@@ -2790,7 +2791,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     // coalesced, instead of a dependent global load per offset.  Sets too big for the stage
     // (dense regions, many sources) read them from global memory.
     const uint32_t TL = s_lw0[nsrc];
-    const bool staged = TL <= kLowsStage;   // workgroup-uniform
+    const bool staged = STAGE && TL <= STAGE;   // workgroup-uniform
     if (staged) {
         uint32_t s = 0;
         for (uint32_t q = t; q < TL; q += LANES) {
@@ -2953,19 +2954,28 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
     const uint64_t nwords = bitset_bytes / 4;
     const uint64_t vecs = (uint64_t)nbins << (region_log2 - 7);
     const uint32_t dense = probes_hint >= vecs ? 2u : (probes_hint >= vecs / 8 ? 1u : 0u);
+    // low-bit stage: 1 (default) 15 KB, two workgroups per CU; 2: 48 KB, one; 0: none (A/B)
+    static const uint32_t stage = [] {
+        const char* e = std::getenv("BFHIP_SETS_STAGE");
+        return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
     for (uint32_t s0 = 0; s0 < nsrc; s0 += kMaxSetSrc) {
         const uint32_t ns = std::min<uint32_t>(kMaxSetSrc, nsrc - s0);
         const uint32_t* src = sets + (uint64_t)s0 * stride_words;
-        if (region_log2 == 19)
-            hipLaunchKernelGGL((sets_apply_kernel<19, kApplyLanes>), dim3(nbins), dim3(kApplyLanes), 0, s, g.bits,
-                               nwords, src, stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(),
-                               status);
-        else if (region_log2 == 18)
-            hipLaunchKernelGGL((sets_apply_kernel<18, kApplyLanes / 2>), dim3(nbins), dim3(kApplyLanes / 2), 0, s,
-                               g.bits, nwords, src, stride_words, ns, nbins, dense, any_flag, g.dirty,
-                               apply_store_fresh(), status);
-        else
+#define BF_SETS_APPLY(RL, LN, ST)                                                                              \
+    hipLaunchKernelGGL((sets_apply_kernel<RL, LN, ST>), dim3(nbins), dim3(LN), 0, s, g.bits, nwords, src,       \
+                       stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status)
+        if (region_log2 == 19) {
+            if (stage == 2) BF_SETS_APPLY(19, kApplyLanes, kLowsStageBig);
+            else if (stage == 0) BF_SETS_APPLY(19, kApplyLanes, 0);
+            else BF_SETS_APPLY(19, kApplyLanes, kLowsStage);
+        } else if (region_log2 == 18) {
+            if (stage == 0) BF_SETS_APPLY(18, kApplyLanes / 2, 0);
+            else BF_SETS_APPLY(18, kApplyLanes / 2, kLowsStage);
+        } else {
             return hipErrorInvalidValue;
+        }
+#undef BF_SETS_APPLY
     }
     bf_mark(mk, s, "sets_apply");
     return hipGetLastError();
