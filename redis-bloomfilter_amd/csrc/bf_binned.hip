@@ -2756,7 +2756,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
             hdr = S[kSetsHdr + nbins + r];   // beside the place: one round trip
             if (st) {   // the set must lie inside the buffer: a damaged entry is skipped, not read
                 const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
-                const bool shape = n && n <= U && (l == kSetsBitmap || l < RLOG2);
+                const bool shape = n && n <= U && (l == kSetsBitmap || l <= RLOG2);
                 const uint64_t need = !shape ? 0 : 1ull + (l == kSetsBitmap ? NW : (n * l + 31u) / 32u + (n + (U >> l) + 31u) / 32u);
                 if (!shape || (uint64_t)st + need > stride_words) {
                     ok = false;
