@@ -2641,7 +2641,10 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     }
     if (!fits) return;   // workgroup-uniform
     uint32_t* o = out + st;
-    if (stop == 1) return;
+    if (stop == 1) {   // (A/B) the region left absent, so no reader decodes the unwritten set
+        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
+        return;
+    }
     if (bitmap) {   // the LDS bitmap is still intact
         if (t == 0) o[0] = n | (kSetsBitmap << 24);
         for (uint32_t v = t; v < NW; v += LANES) o[1 + v] = s_m[v];
@@ -2835,11 +2838,11 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
                 if (l) {
                     const uint32_t bp = i * l, wi = bp >> 5;
                     uint32_t a, b;
-                    if (staged) {
-                        a = slows[wi];
-                        b = slows[wi + 1u];
+                    if (staged) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
+                        a = slows[min(wi, lim)];
+                        b = slows[min(wi, lim) + 1u];
                     } else {
-                        a = lows[wi];
+                        a = lows[min(wi, lim)];
                         b = lows[min(wi + 1u, lim)];
                     }
                     lo = (uint32_t)(((uint64_t)b << 32 | a) >> (bp & 31u)) & lmask;

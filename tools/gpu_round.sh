@@ -31,9 +31,9 @@ PYT="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
 
 ab_cmd() {   # one A/B line's command, stdout = its JSON
     case $1 in
-        nstar|10b|200b) timeout -k 10 150 python bench.py --config $1 --steps 10 --warmup 3 $NOEXTRA 2>/dev/null ;;
-        simP8)   timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 2>/dev/null ;;
-        repl10b) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 2>/dev/null ;;
+        nstar|10b|200b) timeout -k 10 150 python bench.py --config $1 --steps 10 --warmup 3 $NOEXTRA 2>>"$ABERR" ;;
+        simP8)   timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 2>>"$ABERR" ;;
+        repl10b) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 2>>"$ABERR" ;;
         *) echo "unknown AB_CMD $1" >&2; return 2 ;;
     esac
 }
@@ -85,7 +85,8 @@ for st in $STEPS; do
                 timeout -s KILL 150 rocprofv3 --pmc $VALU --output-format csv -d gpurun_out/pmc_${TAG}_sets_2 -o run -- \
                     python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 1 \
                     > gpurun_out/pmc_${TAG}_sets_2.log 2>&1 ;;
-        ab)     for v in ${AB_VALUES:?}; do
+        ab)     ABERR=gpurun_out/ab_${AB_VAR}_${TAG}.err
+                for v in ${AB_VALUES:?}; do
                     line=$(export "${AB_VAR:?}=$v"; ab_cmd "${AB_CMD:?}") || exit $?
                     echo "{\"var\": \"$AB_VAR\", \"value\": \"$v\", \"cmd\": \"$AB_CMD\", \"line\": $line}" \
                         >> gpurun_out/ab_${AB_VAR}_${TAG}.jsonl
