@@ -2571,7 +2571,7 @@ __global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__
 // LDS bitmap, then each lane's WPL consecutive words -> its offsets in ascending order (their
 // ranks from one workgroup scan), the set built in the same LDS (the bitmap words are in
 // registers by then) and copied out.  72 KiB of LDS at 2^19-bit regions: two workgroups per CU.
-template <uint32_t RLOG2, uint32_t LANES>
+template <uint32_t RLOG2, uint32_t LANES, int LOADS>
 __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __restrict__ level2,
                                                             const uint32_t* __restrict__ cb_base,
                                                             const uint32_t* __restrict__ cb_start,
@@ -2581,9 +2581,16 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
                                                             uint32_t stop) {
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
     static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
+    // the gather's run table, then the upper bitmap of a compacted set (n <= NW, l >= 5: at
+    // most (NW + U / 32) / 32 + 1 words)
+    constexpr uint32_t UPW = (NW + U / 32) / 32 + 2;
+    constexpr uint32_t kRunLds = 2 * kRunsPerPass > UPW ? 2 * kRunsPerPass : UPW;
     __shared__ uint4 s_m4[NW / 4];
-    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
+    __shared__ uint32_t s_runs[kRunLds], s_w[16];
     uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
+    uint32_t* s_pre = s_runs;
+    uint32_t* s_gst = s_runs + kRunsPerPass;
+    uint32_t* s_up = s_runs;
     const uint32_t t = threadIdx.x, r = blockIdx.x;
     // the region's reserved place: its superbin's first word + its prefix in the superbin
     // (sets_size_kernel / sets_place_kernel); loaded while the LDS image is cleared
@@ -2596,19 +2603,24 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         return;
     }
     const uint32_t st = sbf + (rv & 0x7FFFFFFFu);
-    for_region_probes<8>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
+    // LOADS level-2 loads per lane and step: a region's ~2k probes over all 16 waves (2), or
+    // over 4 of them with more loads in flight each (8)
+    for_region_probes<LOADS>(cb_base, cb_start, tabs, max_chunks, r, nq, rel_log2, s_pre, s_gst, s_w,
         [&](const uint32_t* idx) {
-            uint32_t l[8];
+            uint32_t l[LOADS];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) l[c] = idx[c] != 0xFFFFFFFFu ? level2[idx[c]] : 0xFFFFFFFFu;
+            for (int c = 0; c < LOADS; ++c) l[c] = idx[c] != 0xFFFFFFFFu ? level2[idx[c]] : 0xFFFFFFFFu;
 #pragma unroll
-            for (int c = 0; c < 8; ++c)
+            for (int c = 0; c < LOADS; ++c)
                 if (l[c] != 0xFFFFFFFFu) atomicOr(s_m + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
         });
     if (stop == 2) {   // (A/B)
         if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
         return;
     }
+    // the run table is dead (for_region_probes ends on a barrier); the scan's barriers below
+    // order these stores before the upper bitmap's first atomic
+    for (uint32_t v = t; v < UPW; v += LANES) s_up[v] = 0;
     uint32_t wv[WPL];
     uint32_t cnt = 0;
 #pragma unroll
@@ -2669,8 +2681,10 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         while (w) {
             const uint32_t x = x0 + (uint32_t)__builtin_ctz(w);
             w &= w - 1u;
-            if (compact) {
+            if (compact) {   // the offset in rank order, and its upper-bitmap bit
                 s_m[i] = x;
+                const uint32_t u = (x >> l) + i;
+                atomicOr(s_up + (u >> 5), 1u << (u & 31u));
             } else {
                 if (l) {
                     const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
@@ -2688,31 +2702,19 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
         return;
     }
+    // floor(b / l) as a multiply-high: b < 2^24, so ceil(2^32 / l) is exact for l <= 31
+    const uint32_t mg = l ? 0xFFFFFFFFu / l + 1u : 0u;
     for (uint32_t wi = t; wi < lw; wi += LANES) {   // low bits: offsets floor(32 wi / l) ..
         const uint32_t b0 = wi * 32u;
         uint32_t word = 0;
-        for (uint32_t e = b0 / l; e < n && e * l < b0 + 32u; ++e) {
+        for (uint32_t e = __umulhi(b0, mg); e < n && e * l < b0 + 32u; ++e) {
             const uint32_t lo = s_m[e] & lmask;
             const int32_t sh = (int32_t)(e * l) - (int32_t)b0;   // the field's start in this word
             word |= sh >= 0 ? (lo << sh) : (lo >> (uint32_t)(-sh));
         }
         o[1 + wi] = word;
     }
-    for (uint32_t ui = t; ui < uw; ui += LANES) {   // upper bitmap: f(e) = (x_e >> l) + e ascends
-        const uint32_t p0 = ui * 32u;
-        uint32_t lo = 0, hi = n;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if ((s_m[mid] >> l) + mid < p0) lo = mid + 1u; else hi = mid;
-        }
-        uint32_t word = 0;
-        for (uint32_t e = lo; e < n; ++e) {
-            const uint32_t pe = (s_m[e] >> l) + e;
-            if (pe >= p0 + 32u) break;
-            word |= 1u << (pe - p0);
-        }
-        o[1 + lw + ui] = word;
-    }
+    for (uint32_t ui = t; ui < uw; ui += LANES) o[1 + lw + ui] = s_up[ui];   // built during the compaction
 }
 
 // One workgroup per region: every source's set for the region ORed into an LDS image (bitmap
@@ -2936,16 +2938,28 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
     hipLaunchKernelGGL(sets_size_kernel, dim3(p.nsup), dim3(1024), 0, s, c.tabs, c.cb_base, p.max_chunks, p.ngroups,
                        p.rel_log2, p.nbins, 1u << p.region_log2, out, c.stot);
     hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, out, c.stot, p.nsup, p.region_log2, p.nbins);
-    if (p.region_log2 == 19)
-        hipLaunchKernelGGL((sets_encode_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, c.level2,
-                           c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot,
-                           (uint32_t)cap_words, sets_stop());
-    else if (p.region_log2 == 18)
-        hipLaunchKernelGGL((sets_encode_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
-                           c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot,
-                           (uint32_t)cap_words, sets_stop());
-    else
+    // level-2 loads per lane and gather step (BFHIP_SETS_ENC_LOADS A/B: 2, 4, 8)
+    static const int loads = [] {
+        const char* e = std::getenv("BFHIP_SETS_ENC_LOADS");
+        const int v = e && *e ? std::atoi(e) : 2;
+        return v == 8 || v == 4 ? v : 2;
+    }();
+#define BF_SETS_ENCODE(RL, LN, LD)                                                                              \
+    hipLaunchKernelGGL((sets_encode_kernel<RL, LN, LD>), dim3(p.nbins), dim3(LN), 0, s, c.level2, c.cb_base,    \
+                       c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot, (uint32_t)cap_words, \
+                       sets_stop())
+    if (p.region_log2 == 19) {
+        if (loads == 8) BF_SETS_ENCODE(19, kApplyLanes, 8);
+        else if (loads == 4) BF_SETS_ENCODE(19, kApplyLanes, 4);
+        else BF_SETS_ENCODE(19, kApplyLanes, 2);
+    } else if (p.region_log2 == 18) {
+        if (loads == 8) BF_SETS_ENCODE(18, kApplyLanes / 2, 8);
+        else if (loads == 4) BF_SETS_ENCODE(18, kApplyLanes / 2, 4);
+        else BF_SETS_ENCODE(18, kApplyLanes / 2, 2);
+    } else {
         return hipErrorInvalidValue;
+    }
+#undef BF_SETS_ENCODE
     bf_mark(mk, s, "sets_encode");
     return hipGetLastError();
 }

@@ -22,9 +22,14 @@ def dev_batch(pkg, torch, keys):
     return kb, ko, len(offs) - 1, buf, offs
 
 
-@pytest.mark.parametrize("binned", ["0", "1"])
-@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20),
-                                     (3834023350947, 13, 8, 20)])   # 200B@0.01 % over 8 GPUs (BASELINE configs[4])
+# both owner forms (direct / binned) on the small and north-star filters; the 10B and 200B
+# filters (the slow cases) once each, on the form their owners take
+@pytest.mark.parametrize("m,k,P,b,binned", [
+    (95851, 6, 3, 10, "0"), (95851, 6, 3, 10, "1"),
+    (9585058377, 6, 8, 20, "0"), (9585058377, 6, 8, 20, "1"),
+    (191701167547, 13, 4, 20, "1"),
+    (3834023350947, 13, 8, 20, "0"),   # 200B@0.01 % over 8 GPUs (BASELINE configs[4])
+])
 def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
     """binned=1 forces the owner-side binned insert (offsets front pass + region apply) and
     binned shard test, and takes the wave-aggregated owner ranks in the route; 0 the direct
@@ -98,7 +103,7 @@ def test_simulated_partition(pkg, oracle, monkeypatch, m, k, P, b, binned):
 
 
 @pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (191701167547, 13, 4, 20),
-                                     (9585058377, 6, 2, 20), (191701167547, 13, 1, 20),
+                                     (9585058377, 6, 2, 20),
                                      (3834023350947, 13, 8, 20)])   # 200B at P = 8: nh = 2
 def test_route_windows(pkg, oracle, m, k, P, b):
     """bf_route_windows_dev: window w = s*nh + hi holds exactly owner s's (key, local offset)
@@ -173,10 +178,15 @@ def test_route_windows(pkg, oracle, m, k, P, b):
     e.close()
 
 
-@pytest.mark.parametrize("owner", ["direct", "sorted", "l2"])
-@pytest.mark.parametrize("m,k,P,b", [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (9585058377, 6, 2, 20),
-                                     (191701167547, 13, 4, 20), (9585058377, 6, 1, 20),
-                                     (3834023350947, 13, 8, 20)])   # 200B x8: nh = 2
+# every owner form on the small and north-star filters; the 10B x 4 and 200B x 8 filters (the
+# slow cases) on one form each: the L2 sweep, and the sorted test their owners take
+@pytest.mark.parametrize("m,k,P,b,owner", [
+    *[(m_, k_, P_, b_, o) for (m_, k_, P_, b_) in [(95851, 6, 3, 10), (9585058377, 6, 8, 20), (9585058377, 6, 2, 20),
+                                                   (9585058377, 6, 1, 20)]
+      for o in ("direct", "sorted", "l2")],
+    (191701167547, 13, 4, 20, "l2"),
+    (3834023350947, 13, 8, 20, "sorted"),   # 200B x8: nh = 2
+])
 def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     """bf_route_chunks_dev + the owner ops over chunked windows + bf_combine_chunks_packed_dev,
     with P shards simulated on one GPU and the exchange done by copies: every window holds
