@@ -1092,7 +1092,7 @@ __device__ __forceinline__ uint32_t apply_region(uint32_t b, uint32_t nb, uint32
     return b - w + (w & 7u) * xg + (w >> 3);
 }
 
-template <uint32_t RLOG2, uint32_t LANES>
+template <uint32_t RLOG2, uint32_t LANES, int LOADS = 8>
 __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
                                                           const uint32_t* __restrict__ level2,
                                                           const uint32_t* __restrict__ cb_base,
@@ -1104,7 +1104,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
                                                           uint32_t xg) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
     constexpr uint32_t kPer = kVec / LANES;
-    constexpr int kLoads = 8;
+    constexpr int kLoads = LOADS;   // level-2 loads per lane and gather step (BFHIP_APPLY_LOADS)
     static_assert(kPer * LANES == kVec, "region must tile the workgroup");
     __shared__ uint4 s_mask4[kVec];
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
@@ -2043,10 +2043,23 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
                            p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh(), apply_xcd_group());
-    else if (p.region_log2 == 19)
-        hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
-                           nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
-                           any_flag, g.dirty, apply_store_fresh(), apply_xcd_group());
+    else if (p.region_log2 == 19) {
+        // a region's probes over all 16 waves (2 loads per lane and step) or over fewer waves
+        // with more loads in flight each (8)
+        static const int loads = [] {
+            const char* e = std::getenv("BFHIP_APPLY_LOADS");
+            const int v = e && *e ? std::atoi(e) : 8;
+            return v == 2 || v == 4 ? v : 8;
+        }();
+#define BF_APPLY19(LD)                                                                                          \
+    hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes, LD>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits, \
+                       nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense, \
+                       any_flag, g.dirty, apply_store_fresh(), apply_xcd_group())
+        if (loads == 2) BF_APPLY19(2);
+        else if (loads == 4) BF_APPLY19(4);
+        else BF_APPLY19(8);
+#undef BF_APPLY19
+    }
     else
         hipLaunchKernelGGL((bin_apply_kernel<20, kApplyLanes>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
                            nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense,
