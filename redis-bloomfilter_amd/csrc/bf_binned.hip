@@ -1178,7 +1178,7 @@ __global__ __launch_bounds__(LANES) void bin_apply_kernel(uint32_t* __restrict__
 // run-table buffers alternate between r and r + G, the register buffers by unrolling the
 // region loop twice (a register copy would wait for the stores just issued).
 constexpr int kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
-template <uint32_t RLOG2, uint32_t LANES>
+template <uint32_t RLOG2, uint32_t LANES, int LOADS = 8>
 __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) void bin_apply_pipe_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
                                                                uint32_t nbins, const uint32_t* __restrict__ level2,
                                                                const uint32_t* __restrict__ cb_base,
@@ -1189,7 +1189,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
                                                                uint8_t* __restrict__ dirty, uint32_t store_fresh) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);   // 16-B vectors per region
     constexpr uint32_t kPer = kVec / LANES;
-    constexpr int kLoads = 8;
+    constexpr int kLoads = LOADS;   // (BFHIP_APPLY_PIPE_LOADS A/B)
     constexpr uint32_t kPass = LANES < kRunsPerPass ? LANES : kRunsPerPass;   // run-table entries per pass
     static_assert(kPer * LANES == kVec, "region must tile the workgroup");
     __shared__ uint4 s_mask4[kVec];
@@ -2036,21 +2036,32 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     // the pipeline pays off over many regions per workgroup: a 150 MB shard (2288 regions, 9
     // per workgroup) measured 0.206 pipelined against 0.164 ms (P = 8 owner insert)
     if (dense && pg && p.region_log2 == 19 && form == 1 && p.nbins >= 16 * pg) {   // 2^20-bit regions: not pipelined
-        hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes>), dim3(std::min<uint32_t>(p.nbins, pg)),
-                           dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,
-                           p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh());
+        static const int pl = [] {
+            const char* e = std::getenv("BFHIP_APPLY_PIPE_LOADS");
+            return e && *e && std::atoi(e) == 4 ? 4 : 8;
+        }();
+#define BF_APPLY_PIPE(LD)                                                                                         \
+    hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes, LD>), dim3(std::min<uint32_t>(p.nbins, pg)),         \
+                       dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,   \
+                       p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh())
+        if (pl == 4) BF_APPLY_PIPE(4);
+        else BF_APPLY_PIPE(8);
+#undef BF_APPLY_PIPE
     } else if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
                            g.bits, nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
                            p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh(), apply_xcd_group());
     else if (p.region_log2 == 19) {
-        // a region's probes over all 16 waves (2 loads per lane and step) or over fewer waves
-        // with more loads in flight each (8)
-        static const int loads = [] {
+        // level-2 loads per lane and gather step: a region's probes over all 16 waves (2) when
+        // it has at most 16 x 64 x 4 of them, else fewer waves with more loads in flight each
+        // (8).  10B@0.01 % (~2k probes per region): 2.37 -> 2.25 ms; a P = 8 owner's insert
+        // (~44k per region): 0.16 ms at 8 against 0.23 at 2 (profiles/r04i_ab_apply_loads.jsonl)
+        static const int forced = [] {
             const char* e = std::getenv("BFHIP_APPLY_LOADS");
-            const int v = e && *e ? std::atoi(e) : 8;
-            return v == 2 || v == 4 ? v : 8;
+            const int v = e && *e ? std::atoi(e) : 0;
+            return v == 2 || v == 4 || v == 8 ? v : 0;
         }();
+        const int loads = forced ? forced : (p.probes <= (uint64_t)p.nbins * 4096u ? 2 : 8);
 #define BF_APPLY19(LD)                                                                                          \
     hipLaunchKernelGGL((bin_apply_kernel<19, kApplyLanes, LD>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits, \
                        nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense, \
