@@ -2776,9 +2776,9 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         if (dense && v0 + v < nvec) old[c] = apply_load(gv + v0 + v);
     }
     for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
+    uint32_t st = 0, hdr = 0;
     if (t < nsrc) {   // source t's set for this region
         const uint32_t* S = sets + (uint64_t)t * stride_words;
-        uint32_t st = 0, hdr = 0;
         bool ok = S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] <= stride_words;
         if (ok) {
             st = S[kSetsHdr + r];
@@ -2797,34 +2797,37 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         s_st[t] = st;
         s_hdr[t] = hdr;
     }
-    __syncthreads();
-    if (t == 0) {   // upper-bitmap words, low-bit words and offsets of the Elias-Fano sources before each source
-        uint32_t a = 0, np = 0, lw = 0;
-        for (uint32_t s = 0; s < nsrc; ++s) {
-            s_uw0[s] = a;
-            s_np[s] = np;
-            s_lw0[s] = lw;
-            const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
-            if (s_st[s] && l != kSetsBitmap) {
-                a += (n + (U >> l) + 31u) / 32u;
-                np += n;
-                lw += (n * l + 31u) / 32u;
-            }
+    if (t < 64) {   // wave 0 (nsrc <= 16): upper-bitmap words, offsets and low-bit words of the
+                    // Elias-Fano sources before each source, as three wave scans
+        const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
+        const bool ef = st && l != kSetsBitmap;   // (st = 0 past nsrc)
+        const uint32_t ua = ef ? (n + (U >> l) + 31u) / 32u : 0u, nn = ef ? n : 0u, ll = ef ? (n * l + 31u) / 32u : 0u;
+        const uint32_t ia = wave_incl_scan(ua), in = wave_incl_scan(nn), il = wave_incl_scan(ll);
+        if (t <= nsrc) {
+            s_uw0[t] = ia - ua;
+            s_np[t] = in - nn;
+            s_lw0[t] = il - ll;
         }
-        s_uw0[nsrc] = a;
-        s_np[nsrc] = np;
-        s_lw0[nsrc] = lw;
     }
     __syncthreads();
+    // the source of word q of a table of per-source starts (sources with no words are skipped)
+    // (a binary search: the last source whose start is <= q; four dependent LDS reads)
+    static_assert(kMaxSetSrc == 16, "source_of searches 16 sources");
+    auto source_of = [&](const uint32_t* starts, uint32_t q) {
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t step = kMaxSetSrc / 2; step; step >>= 1)
+            if (s + step < nsrc && starts[s + step] <= q) s += step;
+        return s;
+    };
     // The low bits are read in offset order, a word or two per offset: staged once into LDS,
     // coalesced, instead of a dependent global load per offset.  Sets too big for the stage
     // (dense regions, many sources) read them from global memory.
     const uint32_t TL = s_lw0[nsrc];
     const bool staged = STAGE && TL <= STAGE;   // workgroup-uniform
     if (staged) {
-        uint32_t s = 0;
         for (uint32_t q = t; q < TL; q += LANES) {
-            while (s_lw0[s + 1] <= q) ++s;
+            const uint32_t s = source_of(s_lw0, q);
             s_lows[q] = sets[(uint64_t)s * stride_words + s_st[s] + 1 + (q - s_lw0[s])];
         }
         if (t == 0) s_lows[TL] = 0;   // the word past the last source's lows: read, masked off
@@ -2843,7 +2846,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         const uint32_t g = g0 + t;
         uint32_t word = 0, s = 0;
         if (g < TW) {
-            while (s + 1 < nsrc && s_uw0[s + 1] <= g) ++s;
+            s = source_of(s_uw0, g);
             const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
             word = sets[(uint64_t)s * stride_words + s_st[s] + 1 + (n * l + 31u) / 32u + (g - s_uw0[s])];
         }
