@@ -739,18 +739,21 @@ def reference_shapes(pkg, per_key_ops: int = 20000, words_n: int = 10000, flat_i
 
 
 def load_traffic(workload: str, kernel: str):
-    """PMC-measured HBM bytes per launch of `kernel` (profiles/pmc_traffic.json, tools/pmc_summary.py)."""
+    """(PMC-measured HBM bytes per launch of `kernel`, the PMC summary they come from)
+    (profiles/pmc_traffic.json, tools/pmc_summary.py), or (None, None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            t = json.load(fh).get(workload) or {}
+            doc = json.load(fh)
     except (OSError, ValueError):
-        return None
-    rec = t.get(kernel)
-    return rec.get("hbm_bytes_per_launch") if isinstance(rec, dict) else None
+        return None, None
+    rec = (doc.get(workload) or {}).get(kernel)
+    if not isinstance(rec, dict) or rec.get("hbm_bytes_per_launch") is None:
+        return None, None
+    return rec["hbm_bytes_per_launch"], doc.get("source")
 
 
-PMC_FILES = {"nstar": "pmc_r03f_nstar.json", "1m_big": "pmc_r02_1m_big.json", "10b": "pmc_r03r_10b.json"}
+PMC_FILES = {"nstar": "pmc_r04z_nstar.json", "1m_big": "pmc_r02_1m_big.json", "10b": "pmc_r03r_10b.json"}
 # rocprofv3 --kernel-trace --stats of the bench command on the round's final tree
 # (tools/rocprof_means.py over profiles/<tag>_kernel_stats.csv): each kernel's mean launch
 ROCPROF_MEANS = "rocprof_means.json"
@@ -925,7 +928,7 @@ def main():
     dom = kern[dom_name]
     achieved = dom["algo_bytes"] / (dom["ms"] / 1e3) if "algo_bytes" in dom else None
     rp_ms, rp_src = load_rocprof_mean(args.config, dom_name)
-    traffic = load_traffic(args.config, dom_name)
+    traffic, traffic_src = load_traffic(args.config, dom_name)
     n, p, batch, _ = CONFIGS[args.config]
     fills = None
     if dom_name in ("include_hash_kernel", "bf_keys_kernel<INCLUDE>"):
@@ -979,7 +982,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom_name,
                      "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK if achieved else None,
-                     "traffic": traffic,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      # the PMC-measured fabric bytes per launch over the same launch time: what
                      # the kernel actually moves (128 B line fills; SURVEY's 64 B granule model
                      # undercounts them and overcounts the early exit's skipped probes)
