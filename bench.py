@@ -718,6 +718,20 @@ def reference_shapes(pkg, per_key_ops: int = 20000, words_n: int = 10000, flat_i
     hits = np.empty(len(qkeys), np.uint8)
     t_inc, inc_all = med(lambda: drv.filter.include_many(qb, qo, out=hits))
     assert any_new and bool(np.all(hits[:half])), "100m_sync: an inserted key answered false"
+    # what bounds these calls: the host side copies every key byte and offset into pinned
+    # staging (16 threads) before the H2D; the same bytes copied by 16 host threads here
+    host_bytes = int(io[-1]) + 4 * (len(ikeys) + 1)
+    src = np.asarray(ib).view(np.uint8)[: int(io[-1])]
+    dst = np.empty_like(src)
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = np.linspace(0, len(src), 17).astype(np.int64)
+
+    def pcopy():
+        with ThreadPoolExecutor(16) as ex:
+            list(ex.map(lambda a: np.copyto(dst[cuts[a]:cuts[a + 1]], src[cuts[a]:cuts[a + 1]]), range(16)))
+
+    pcopy()
+    t_copy, _ = med(pcopy, 3)
     assert r.get("bench-100m") == drv.to_redis_string(), "100m_sync: Redis string differs from the device"
     out["100m_sync"] = {"bits": bf.options["bits"], "hashes": bf.options["hashes"], "keys": len(ikeys),
                         "host_pack_keys_per_s": len(ikeys) / t_pack,
@@ -727,6 +741,9 @@ def reference_shapes(pkg, per_key_ops: int = 20000, words_n: int = 10000, flat_i
                         "insert_ms_calls": [round(x * 1e3, 2) for x in ins_all],
                         "include_ms_calls": [round(x * 1e3, 2) for x in inc_all],
                         "first_insert_keys_per_s": len(ikeys) / t_first,
+                        "host_bytes_per_call": host_bytes,
+                        "host_bytes_GBps_insert": host_bytes / t_ins / 1e9,
+                        "host_memcpy_GBps_16_threads": len(src) / t_copy / 1e9,
                         "redis_string_bytes": slen, "synced_bytes": sent,
                         "export_GBps": sent / t_export / 1e9, "sync_s": t_sync,
                         "sync_GBps": sent / t_sync / 1e9,
