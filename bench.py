@@ -208,8 +208,11 @@ def prefill_random(f, m: int, k: int, rank: int, host_copy: bool = True):
 # key bytes or the OR-all-reduce by size).  10B@0.01 % (BASELINE configs[3], k = 13): region
 # sets — each rank sorts and encodes its own batch once, every replica ORs all ranks' sets in
 # one pass: one replica's step 17.8 -> 12.5 ms against the SHA-1 words form on the same box
-# (tools/sim_rank.py --replicated 8: profiles/r04b_sim_replicated.jsonl).
-REPLICATED_INSERT = {"10b": "sets"}
+# (tools/sim_rank.py --replicated 8: profiles/r04b_sim_replicated.jsonl).  The north-star
+# filter at N = 2 (the driver's N = 2 layout) too: 3.35 ms per replica step against 3.54 for the
+# key gather, and 122 MB on the wire per rank against ~168 MB of key bytes
+# (profiles/r04k_sim_replicated.jsonl, r04e_sim_replicated.jsonl).
+REPLICATED_INSERT = {"10b": "sets", "nstar": "sets"}
 
 
 def auto_mode(world: int, m: int, k: int, config: str = "nstar") -> str:
