@@ -1463,7 +1463,7 @@ constexpr uint32_t kL2Lanes = 256;
 constexpr int kL2Loads = 8;
 constexpr uint32_t kL2Grid = 1024;   // 256 CUs x 4 workgroups of 4 waves (grid A/B: 256-2048)
 constexpr uint32_t kL2MaxParts = 256;
-template <bool SIDE>
+template <bool SIDE, bool WALK = true>
 __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
                                                                  uint32_t nsup, uint32_t nq, uint32_t parts,
                                                                  const uint32_t* __restrict__ gsum,
@@ -1550,13 +1550,23 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
         const uint64_t hoff = (uint64_t)h << 32;
         for (uint32_t fb = f0; fb < f1; fb += kL2Lanes * kL2Loads) {
             uint32_t idx[kL2Loads], o[kL2Loads];
+            // WALK: wave v takes kL2Loads x 64 consecutive entries, one run search for the
+            // wave's first entry, then each lane walks the run table forward (runs of ~40
+            // entries: a step of 64 crosses one or two), instead of a search per entry
+            const uint32_t fw = fb + (t >> 6) * (64u * kL2Loads);
+            uint32_t i = 0;
+            if constexpr (WALK) i = run_of(s_pre, nt, fw < f1 ? fw : f1 - 1);
 #pragma unroll
             for (int u = 0; u < kL2Loads; ++u) {
-                const uint32_t f = fb + u * kL2Lanes + t;
+                const uint32_t f = WALK ? fw + u * 64u + (t & 63u) : fb + u * kL2Lanes + t;
                 idx[u] = 0xFFFFFFFFu;
                 o[u] = 0;
                 if (f < f1) {
-                    const uint32_t i = run_of(s_pre, nt, f);
+                    if constexpr (WALK) {
+                        while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
+                    } else {
+                        i = run_of(s_pre, nt, f);
+                    }
                     idx[u] = s_gst[i] + (f - s_pre[i]);
                     o[u] = ci.recv[idx[u]];
                 }
@@ -2416,12 +2426,20 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
         hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
                            c.gsum, c.runs, parts, c.istart);
         bf_mark(mk, s, "chunk_group");
+        // entries' runs: one search per wave and a forward walk (1), or a search per entry (0; A/B)
+        static const bool walk = [] {
+            const char* e = std::getenv("BFHIP_L2_WALK");
+            return !(e && *e == '0');
+        }();
         if (side.n)
             hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
                                p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+        else if (walk)
+            hipLaunchKernelGGL((chunk_test_l2_kernel<false, true>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
+                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         else
-            hipLaunchKernelGGL(chunk_test_l2_kernel<false>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
-                               p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+            hipLaunchKernelGGL((chunk_test_l2_kernel<false, false>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
+                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         bf_mark(mk, s, side.n ? "test_l2_hash" : "test_l2");
         return hipGetLastError();
     }
