@@ -1743,14 +1743,17 @@ __global__ __launch_bounds__(kCombineLanes) void combine_chunks_packed_kernel(
     constexpr int U = 8;   // entries per lane in flight
     for (uint32_t fb = 0; fb < E; fb += U * kCombineLanes) {
         uint32_t key[U], byte[U], sh[U];
+        // wave v takes U x 64 consecutive entries: one window search, then a forward walk
+        const uint32_t fw = fb + (t >> 6) * (64u * U);
+        uint32_t w = run_of(s_pre, nwin, fw < E ? fw : E - 1);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t f = fb + u * kCombineLanes + t;
+            const uint32_t f = fw + u * 64u + (t & 63u);
             key[u] = 0xFFFFFFFFu;
             byte[u] = 0xFFu;
             sh[u] = 0;
             if (f < E) {
-                const uint32_t w = run_of(s_pre, nwin, f);
+                while (w + 1 < nwin && s_pre[w + 1] <= f) ++w;
                 const uint64_t e = (uint64_t)s_st[w] + (f - s_pre[w]);
                 key[u] = slot16[(uint64_t)w * wcap + e];
                 byte[u] = packed[(uint64_t)w * wcap8 + (e >> 3)];
