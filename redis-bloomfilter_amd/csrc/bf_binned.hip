@@ -2526,7 +2526,7 @@ constexpr uint32_t kSetsMagic = 0x53524642u;   // "BFRS"
 constexpr uint32_t kSetsHdr = 4;
 constexpr uint32_t kSetsBitmap = 31u;
 constexpr uint32_t kMaxSetSrc = 16;            // sources per sets_apply launch
-constexpr uint32_t kLowsStage = 2304;           // low-bit words sets_apply stages in LDS (9 KB: two 2^19-bit workgroups per CU)
+constexpr uint32_t kLowsStage = 3840;           // low-bit words sets_apply stages in LDS (15 KB: two 2^19-bit workgroups per CU)
 // [4, 4 + R): each region's first word; [4 + R, 4 + 2R): each region's set header (so a
 // reader gets both in one round trip); the sets from sets_first_word(R)
 __host__ __device__ inline uint64_t sets_first_word(uint32_t nbins) {
@@ -2768,7 +2768,7 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
 // A source whose header does not match (magic, region geometry, capacity) is skipped and
 // flagged in *status.
 template <uint32_t RLOG2, uint32_t LANES, uint32_t STAGE>
-__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(8, 8))) void sets_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
+__global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
                                                            const uint32_t* __restrict__ sets, uint64_t stride_words,
                                                            uint32_t nsrc, uint32_t nbins, uint32_t dense,
                                                            uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
@@ -2782,8 +2782,6 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ uint32_t s_st[kMaxSetSrc], s_hdr[kMaxSetSrc], s_uw0[kMaxSetSrc + 1], s_np[kMaxSetSrc + 1];
     __shared__ uint32_t s_lw0[kMaxSetSrc + 1];
     __shared__ uint32_t s_lows[STAGE + 1];   // every Elias-Fano source's low-bit words, back to back
-    __shared__ uint16_t s_wp[LANES + 1];      // a decode pass: each word's first offset, pass-local
-    __shared__ uint32_t s_wd[LANES];          // ... and the word
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
     const uint32_t r = blockIdx.x;
@@ -2874,48 +2872,17 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         uint32_t tot;
         const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);   // (its barriers also order the staging)
-        // The pass's offsets split evenly over the lanes (a word holds 0..32 of them, and the
-        // busiest lane of a wave would set the wave's pace): lane t decodes pass-local offsets
-        // [t tot / LANES, (t + 1) tot / LANES), walking the staged words from the one that holds
-        // its first offset.  The previous pass's readers of s_wp / s_wd are past this pass's
-        // scan barriers.
-        s_wp[t] = (uint16_t)pre;
-        s_wd[t] = word;
-        if (t == LANES - 1) s_wp[LANES] = (uint16_t)tot;   // (tot <= 32 LANES < 2^16)
-        __syncthreads();
-        const uint32_t f0 = (t * tot) / LANES, f1 = ((t + 1) * tot) / LANES;
-        if (f0 < f1) {
-            uint32_t w = 0;   // the last word whose prefix is <= f0: it holds offset f0
-#pragma unroll
-            for (uint32_t step = LANES / 2; step; step >>= 1)
-                if (s_wp[w + step] <= f0) w += step;
-            uint32_t cur = s_wd[w];
-            for (uint32_t k = f0 - s_wp[w]; k; --k) cur &= cur - 1u;   // skip the word's earlier offsets
-            uint32_t sw = 0, l = 0, lmask = 0, lim = 0, p0 = 0, ibase = 0;
-            const uint32_t* lows = sets;
-            const uint32_t* slows = s_lows;
-            auto enter = [&]() {   // word w's source and its decode constants
-                const uint32_t gw = g0 + w;
-                sw = source_of(s_uw0, gw);
-                const uint32_t n = s_hdr[sw] & 0xFFFFFFu;
-                l = s_hdr[sw] >> 24;
-                lows = sets + (uint64_t)sw * stride_words + s_st[sw] + 1;
-                slows = s_lows + s_lw0[sw];
-                lmask = (1u << l) - 1u;
-                lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
-                p0 = (gw - s_uw0[sw]) * 32u;
-                ibase = carry - s_np[sw];   // rank in the set = ibase + pass-local offset index
-            };
-            enter();
-            for (uint32_t f = f0; f < f1; ++f) {
-                while (!cur) {   // (f < f1 <= tot: a later word holds it)
-                    ++w;
-                    cur = s_wd[w];
-                    if (cur) enter();
-                }
-                const uint32_t i = ibase + f;
-                const uint32_t p = p0 + (uint32_t)__builtin_ctz(cur);
-                cur &= cur - 1u;
+        if (word) {   // ~16 offsets: their low bits are consecutive
+            const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
+            const uint32_t* lows = sets + (uint64_t)s * stride_words + s_st[s] + 1;
+            const uint32_t* slows = s_lows + s_lw0[s];
+            const uint32_t lmask = (1u << l) - 1u;
+            uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
+            const uint32_t p0 = (g - s_uw0[s]) * 32u;
+            const uint32_t lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
+            while (word) {
+                const uint32_t p = p0 + (uint32_t)__builtin_ctz(word);
+                word &= word - 1u;
                 uint32_t lo = 0;
                 if (l) {
                     const uint32_t bp = i * l, wi = bp >> 5;
@@ -2931,6 +2898,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 }
                 const uint32_t x = ((p - i) << l) | lo;
                 if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
+                ++i;
             }
         }
         carry += tot;
@@ -3050,9 +3018,9 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
     const uint64_t nwords = bitset_bytes / 4;
     const uint64_t vecs = (uint64_t)nbins << (region_log2 - 7);
     const uint32_t dense = probes_hint >= vecs ? 2u : (probes_hint >= vecs / 8 ? 1u : 0u);
-    // low-bit stage: 1 (default) 9 KB at 2^19-bit regions (two workgroups per CU), 4.5 KB at
-    // 2^18 (four); 0: none (A/B; a 48-KB stage at one workgroup per CU measured 7.07 against
-    // 4.72 ms at 10B, profiles/r04g_ab_sets_stage.jsonl)
+    // low-bit stage: 1 (default) 15 KB at 2^19-bit regions (two workgroups per CU), 7.5 KB at
+    // 2^18; 0: none (A/B; a 48-KB stage at one workgroup per CU measured 7.07 against 4.72 ms
+    // at 10B, profiles/r04g_ab_sets_stage.jsonl)
     static const uint32_t stage = [] {
         const char* e = std::getenv("BFHIP_SETS_STAGE");
         return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
