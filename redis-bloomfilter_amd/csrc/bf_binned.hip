@@ -1463,7 +1463,7 @@ constexpr uint32_t kL2Lanes = 256;
 constexpr int kL2Loads = 8;
 constexpr uint32_t kL2Grid = 1024;   // 256 CUs x 4 workgroups of 4 waves (grid A/B: 256-2048)
 constexpr uint32_t kL2MaxParts = 256;
-template <bool SIDE, bool WALK = true>
+template <bool SIDE, bool WALK = true, int LOADS = kL2Loads>
 __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
                                                                  uint32_t nsup, uint32_t nq, uint32_t parts,
                                                                  const uint32_t* __restrict__ gsum,
@@ -1548,16 +1548,16 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
         __syncthreads();
         const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
         const uint64_t hoff = (uint64_t)h << 32;
-        for (uint32_t fb = f0; fb < f1; fb += kL2Lanes * kL2Loads) {
-            uint32_t idx[kL2Loads], o[kL2Loads];
-            // WALK: wave v takes kL2Loads x 64 consecutive entries, one run search for the
+        for (uint32_t fb = f0; fb < f1; fb += kL2Lanes * LOADS) {
+            uint32_t idx[LOADS], o[LOADS];
+            // WALK: wave v takes LOADS x 64 consecutive entries, one run search for the
             // wave's first entry, then each lane walks the run table forward (runs of ~40
             // entries: a step of 64 crosses one or two), instead of a search per entry
-            const uint32_t fw = fb + (t >> 6) * (64u * kL2Loads);
+            const uint32_t fw = fb + (t >> 6) * (64u * LOADS);
             uint32_t i = 0;
             if constexpr (WALK) i = run_of(s_pre, nt, fw < f1 ? fw : f1 - 1);
 #pragma unroll
-            for (int u = 0; u < kL2Loads; ++u) {
+            for (int u = 0; u < LOADS; ++u) {
                 const uint32_t f = WALK ? fw + u * 64u + (t & 63u) : fb + u * kL2Lanes + t;
                 idx[u] = 0xFFFFFFFFu;
                 o[u] = 0;
@@ -1571,15 +1571,15 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
                     o[u] = ci.recv[idx[u]];
                 }
             }
-            uint32_t v[kL2Loads];
+            uint32_t v[LOADS];
 #pragma unroll
-            for (int u = 0; u < kL2Loads; ++u) {
+            for (int u = 0; u < LOADS; ++u) {
                 v[u] = 0;
                 if (idx[u] != 0xFFFFFFFFu && (o[u] >> ci.sup_log2) == lsb && hoff + o[u] < ci.limit)
                     v[u] = bits[(hoff + o[u]) >> 5];
             }
 #pragma unroll
-            for (int u = 0; u < kL2Loads; ++u)
+            for (int u = 0; u < LOADS; ++u)
                 if (idx[u] != 0xFFFFFFFFu) {
                     const bool ok = (o[u] >> ci.sup_log2) == lsb && hoff + o[u] < ci.limit;
                     out8[idx[u]] = ok ? (uint8_t)((v[u] >> ((o[u] ^ 7u) & 31u)) & 1u) : (uint8_t)0;
@@ -2434,9 +2434,19 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
             const char* e = std::getenv("BFHIP_L2_WALK");
             return !(e && *e == '0');
         }();
+        static const int l2_loads = [] {
+            const char* e = std::getenv("BFHIP_L2_LOADS");
+            return e && *e ? std::atoi(e) : kL2Loads;
+        }();
         if (side.n)
             hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
                                p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+        else if (walk && l2_loads == 16)   // (A/B: BFHIP_L2_LOADS, entries per lane in flight)
+            hipLaunchKernelGGL((chunk_test_l2_kernel<false, true, 16>), dim3(grid), dim3(kL2Lanes), 0, s, ci,
+                               g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+        else if (walk && l2_loads == 4)
+            hipLaunchKernelGGL((chunk_test_l2_kernel<false, true, 4>), dim3(grid), dim3(kL2Lanes), 0, s, ci,
+                               g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         else if (walk)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, true>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
                                p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
