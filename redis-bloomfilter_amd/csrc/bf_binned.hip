@@ -1461,7 +1461,10 @@ __global__ __launch_bounds__(kRunsPerPass) void chunk_group_sum_kernel(BfChunkIn
 // outside its superbin or past the shard answers 0.  Every live entry gets an answer.
 constexpr uint32_t kL2Lanes = 256;
 constexpr int kL2Loads = 8;
-constexpr uint32_t kL2Grid = 1024;   // 256 CUs x 4 workgroups of 4 waves (grid A/B: 256-2048)
+// 256 CUs x 6 workgroups of 4 waves.  With the per-wave run search, grid A/B (P = 8): 1024 /
+// 1280 / 1536 / 1792 / 2048 -> test_l2 0.81 / 1.02 / 0.74 / 0.95 / 0.97 ms; P = 4: 0.78 at 1024,
+// 0.72 at 1536 (profiles/r04o8_ab_l2_grid.jsonl, r04n_ab_l2_grid.jsonl, r04p_ab_l2_grid_P4.jsonl)
+constexpr uint32_t kL2Grid = 1536;
 constexpr uint32_t kL2MaxParts = 256;
 template <bool SIDE, bool WALK = true, int LOADS = kL2Loads>
 __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,

@@ -16,7 +16,7 @@
 #   replprof   kernel trace of the 10B x 8 region-set replica step
 #   replpmc    stall/LDS + VALU counters of the 10B x 8 region-set replica step
 #   ab         an A/B over one environment variable: AB_VAR, AB_VALUES (interleaved, e.g.
-#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, repl10b, replnstar}; lines appended to
+#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, repl10b, replnstar}; lines appended to
 #              gpurun_out/ab_${AB_VAR}_<tag>.jsonl
 # Default: tests smoke bench prof pmc.  Every GPU step runs under its own time limit; a failing
 # step ends the script (no further GPU work after a fault, abort or time limit).
@@ -33,6 +33,7 @@ ab_cmd() {   # one A/B line's command, stdout = its JSON
     case $1 in
         nstar|10b|200b) timeout -k 10 150 python bench.py --config $1 --steps 10 --warmup 3 $NOEXTRA 2>>"$ABERR" ;;
         simP8)   timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 2>>"$ABERR" ;;
+        simP4)   timeout -k 10 120 python tools/sim_rank.py --shards 4 --chunks --steps 5 2>>"$ABERR" ;;
         repl10b) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 2>>"$ABERR" ;;
         replnstar) timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --steps 5 2>>"$ABERR" ;;
         *) echo "unknown AB_CMD $1" >&2; return 2 ;;
