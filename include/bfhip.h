@@ -203,7 +203,9 @@ int  bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
  *                            probes_hint = the probes they hold (sum of n * k: picks the apply's
  *                            density form, never the result); d_any_new as bf_insert_many_dev;
  *                            d_status (nullable) gets 1 ORed in when a buffer's header does not
- *                            match this filter (that buffer is skipped). */
+ *                            match this filter (that buffer is skipped), or a region's entry
+ *                            would reach past its buffer (that region of that buffer is
+ *                            skipped).  A set body is read only inside its own bounds. */
 int  bf_region_sets_capacity(const bf_handle* h, uint64_t n, uint64_t* bytes);
 int  bf_encode_region_sets_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                                uint32_t* d_sets, uint64_t sets_bytes, void* stream);
