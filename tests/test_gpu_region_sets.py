@@ -198,3 +198,33 @@ def test_foreign_set_buffer_is_skipped(pkg):
         small = torch.zeros(64, dtype=torch.int32, device="cuda")
         with pytest.raises(pkg.ArgumentError):
             f.encode_region_sets_dev(kb.data_ptr(), ko.data_ptr(), 10_000, small.data_ptr(), 256, stream=0)
+
+
+def test_damaged_region_entry_is_skipped(pkg, oracle):
+    """A region whose table entry points past its buffer, or whose header is not a set shape,
+    is skipped and flagged; every other region of the buffer is applied as encoded."""
+    torch = pytest.importorskip("torch")
+    m, k = 9585058377, 6
+    rng = np.random.default_rng(SEED + 11)
+    buf, offs = _keys(pkg, rng, 50_000)
+    idx = oracle.indexes_many(buf, offs, m, k)
+    with pkg.Filter(m, k) as f:
+        sets = _encode(torch, f, buf, offs)
+        words = sets.cpu().numpy().view(np.uint32).copy()
+        _, rl, R, _ = sets_codec.header(words)
+        want = sets_codec.expected(idx, rl)
+        bad = sorted(want)[:2]
+        words[4 + bad[0]] = len(words) - 2            # a place whose set runs past the buffer
+        words[4 + R + bad[1]] = (1 << 24) | (25 << 24)   # l = 26 > region_log2: not a set shape
+        damaged = torch.from_numpy(words.view(np.int32)).cuda()
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        f.insert_region_sets_dev(damaged.data_ptr(), damaged.numel() * 4, 1, 50_000 * k,
+                                 d_status=status.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(status.item()) == 1
+        got = np.frombuffer(f.export_redis(), np.uint8)
+        exp_bits = np.concatenate([(np.uint64(r) << np.uint64(rl)) + want[r] for r in want if r not in bad])
+        expect = np.zeros(len(got), np.uint8)
+        np.bitwise_or.at(expect, (exp_bits >> np.uint64(3)).astype(np.int64),
+                         (np.uint8(0x80) >> (exp_bits & np.uint64(7)).astype(np.uint8)))
+        np.testing.assert_array_equal(got, expect[: len(got)])
