@@ -131,6 +131,27 @@ __device__ __forceinline__ void sha1_key_staged(const uint32_t* src, uint32_t s,
     const uint32_t lim = wave_max_u32(pw);   // words above lim are zero in every lane
     const uint32_t base = s >> 2;
     const uint32_t sh = s & 3u;
+#ifndef BFHIP_SHA_SHORT
+#define BFHIP_SHA_SHORT 1
+#endif
+    if (BFHIP_SHA_SHORT && lim <= 4u) {   // wave-uniform: every key <= 19 bytes (the bench's
+        // decimal keys): w5..w14 are zero at compile time, so their adds and the early message
+        // schedule's XORs fold away (a separate unrolled compression)
+        uint32_t w[16];
+        uint32_t lo = src[base];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) {
+            const uint32_t hi = src[base + j + 1];
+            const uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+            w[j] = __builtin_bswap32(j < pw ? d : (j == pw ? ((d & keep) | pad) : 0u));
+        }
+#pragma unroll
+        for (uint32_t j = 5; j < 15; ++j) w[j] = 0u;
+        w[15] = L << 3;
+        sha1_compress(H, w);
+        return;
+    }
     uint32_t w[16];
     uint32_t lo = src[base];
 #pragma unroll
