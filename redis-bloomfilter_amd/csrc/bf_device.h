@@ -132,11 +132,13 @@ __device__ __forceinline__ void sha1_key_staged(const uint32_t* src, uint32_t s,
     const uint32_t base = s >> 2;
     const uint32_t sh = s & 3u;
 #ifndef BFHIP_SHA_SHORT
-#define BFHIP_SHA_SHORT 1
+#define BFHIP_SHA_SHORT 0
 #endif
     if (BFHIP_SHA_SHORT && lim <= 4u) {   // wave-uniform: every key <= 19 bytes (the bench's
         // decimal keys): w5..w14 are zero at compile time, so their adds and the early message
-        // schedule's XORs fold away (a separate unrolled compression)
+        // schedule's XORs fold away (a separate unrolled compression).  Off by default: the
+        // north-star step 2.467 / 2.420 vs 2.481 / 2.433 ms, the P = 8 routes within noise
+        // (profiles/r04r_ab_sha_short.jsonl); build with -DBFHIP_SHA_SHORT=1 to take it
         uint32_t w[16];
         uint32_t lo = src[base];
 #pragma unroll
