@@ -2075,7 +2075,7 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
         static const int forced = [] {
             const char* e = std::getenv("BFHIP_APPLY_LOADS");
             const int v = e && *e ? std::atoi(e) : 0;
-            return v == 2 || v == 4 || v == 8 ? v : 0;
+            return v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
         }();
         const int loads = forced ? forced : (p.probes <= (uint64_t)p.nbins * 4096u ? 2 : 8);
 #define BF_APPLY19(LD)                                                                                          \
@@ -2083,6 +2083,7 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
                        nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense, \
                        any_flag, g.dirty, apply_store_fresh(), apply_xcd_group())
         if (loads == 2) BF_APPLY19(2);
+        else if (loads == 1) BF_APPLY19(1);
         else if (loads == 4) BF_APPLY19(4);
         else BF_APPLY19(8);
 #undef BF_APPLY19
@@ -3002,7 +3003,7 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
     static const int loads = [] {
         const char* e = std::getenv("BFHIP_SETS_ENC_LOADS");
         const int v = e && *e ? std::atoi(e) : 2;
-        return v == 8 || v == 4 ? v : 2;
+        return v == 8 || v == 4 || v == 1 ? v : 2;
     }();
 #define BF_SETS_ENCODE(RL, LN, LD)                                                                              \
     hipLaunchKernelGGL((sets_encode_kernel<RL, LN, LD>), dim3(p.nbins), dim3(LN), 0, s, c.level2, c.cb_base,    \
@@ -3011,6 +3012,7 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
     if (p.region_log2 == 19) {
         if (loads == 8) BF_SETS_ENCODE(19, kApplyLanes, 8);
         else if (loads == 4) BF_SETS_ENCODE(19, kApplyLanes, 4);
+        else if (loads == 1) BF_SETS_ENCODE(19, kApplyLanes, 1);
         else BF_SETS_ENCODE(19, kApplyLanes, 2);
     } else if (p.region_log2 == 18) {
         if (loads == 8) BF_SETS_ENCODE(18, kApplyLanes / 2, 8);
