@@ -989,9 +989,11 @@ def main():
                                                   "batches routed to owner GPUs, grouped RCCL send/recv%s)"
                                                   % (D.world, "; the next step's inserts routed and sent during "
                                                      "this step" if args.comm_prefetch else ""),
-                                   "replicated": "replicated x%d (include? local; insert batches all-gathered "
-                                                 "over RCCL and every replica applies every batch, or own batch + "
-                                                 "OR-all-reduce of the bitset when that moves fewer bytes: %s%s)"
+                                   "replicated": "replicated x%d (include? local; every rank's insert batch "
+                                                 "all-gathered over RCCL as keys, SHA-1 words or region sets "
+                                                 "(sorted once by its own rank) and applied by every replica, or "
+                                                 "own batch + OR-all-reduce of the bitset when that moves fewer "
+                                                 "bytes: %s%s)"
                                                  % (D.world, main_res.get("replicated_insert_mode"),
                                                     "; the next step's batches gathered during this step"
                                                     if args.comm_prefetch else ""),
