@@ -286,6 +286,13 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
     return (uint32_t)strtoul(v, nullptr, 10);
 }
 
+// A/B knobs (bf_internal.h): the environment only in -DBFHIP_AB_KNOBS builds
+#ifdef BFHIP_AB_KNOBS
+#define ab_u32(name, dflt) env_u32(name, dflt)
+#else
+#define ab_u32(name, dflt) (dflt)
+#endif
+
 int free_staging(bf_handle* h) {
     for (Slot& s : h->slot) {
         if (s.done) (void)hipEventSynchronize(s.done);
@@ -898,7 +905,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     if ((e = hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming)) != hipSuccess) return fail(BF_EDEVICE, "hipEventCreate", e);
     // Bitset memory kind (A/B knob): 0 coarse-grained hipMalloc, 1 uncached (MTYPE UC),
     // 2 fine-grained.
-    h->mem_kind = env_u32("BFHIP_BITS_MEM", kDefaultMemKind);
+    h->mem_kind = ab_u32("BFHIP_BITS_MEM", kDefaultMemKind);
     if (h->mem_kind == 1) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocUncached);
     else if (h->mem_kind == 2) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocFinegrained);
     else e = hipMalloc((void**)&h->g.bits, h->dev_bytes);
@@ -915,7 +922,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.mod_f32 = (m_bits >= (1ull << 17)) ? 1u : 0u;
     h->g.inv_m_f = (float)(1.0 / (double)m_bits);
     // BFHIP_MOD_SUB=0: the float-estimate modulo everywhere (A/B)
-    h->g.mod_sub = env_u32("BFHIP_MOD_SUB", 1) ? bf_mod_sub(m_bits, (uint64_t)k * 0xFFFFFFFFull) : 0u;
+    h->g.mod_sub = ab_u32("BFHIP_MOD_SUB", 1) ? bf_mod_sub(m_bits, (uint64_t)k * 0xFFFFFFFFull) : 0u;
     h->g.shards = h->shards;
     h->g.block_log2 = h->block_log2;
     h->g.inv_shards = 1.0 / (double)h->shards;
@@ -923,13 +930,13 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->g.shard_log2 = (uint32_t)__builtin_ctz(h->shards);
     h->g.route32 = h->route32 ? 1u : 0u;
     h->g.limit = h->local_bits;
-    h->g.first_round = env_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k, h->dev_bytes));
-    h->g.next_round = env_u32("BFHIP_INCLUDE_NEXT_ROUND", default_next_round(h->dev_bytes));
+    h->g.first_round = ab_u32("BFHIP_INCLUDE_FIRST_ROUND", default_first_round(k, h->dev_bytes));
+    h->g.next_round = ab_u32("BFHIP_INCLUDE_NEXT_ROUND", default_next_round(h->dev_bytes));
     h->g.route_agg = env_u32("BFHIP_ROUTE_AGG", 1);   // P = 1 only: at P = 8 the per-owner loop costs more than the LDS atomics (sim_rank A/B)
-    h->g.insert_test = env_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
+    h->g.insert_test = ab_u32("BFHIP_INSERT_TEST", kDefaultInsertTest);
     h->binned_mode = env_u32("BFHIP_INSERT_BINNED", kDefaultBinnedMode);
     h->bin_region_log2 = env_u32("BFHIP_BIN_REGION_LOG2", kDefaultBinRegionLog2);
-    h->chunk_buckets = env_u32("BFHIP_CHUNK_BUCKETS", 0);
+    h->chunk_buckets = ab_u32("BFHIP_CHUNK_BUCKETS", 0);
     h->chunk_test_l2 = env_u32("BFHIP_CHUNK_TEST_L2", 2);
     h->include_binned_mode = env_u32("BFHIP_INCLUDE_BINNED", kDefaultIncludeBinnedMode);
     h->shard_test_binned_mode = env_u32("BFHIP_SHARD_TEST_BINNED", 2);

@@ -1858,7 +1858,7 @@ hipError_t launch_partition(const BfGeom& g, const BfBinPlan& p, const Carve& c,
     if (dig) {
         if (p.with_keys) return hipErrorInvalidValue;
         static const bool wide2 = [] {   // A/B: BFHIP_FRONT_WIDE2=0 takes one workgroup per CU
-            const char* e = std::getenv("BFHIP_FRONT_WIDE2");
+            const char* e = BF_AB_GETENV("BFHIP_FRONT_WIDE2");
             return !(e && e[0] == '0');
         }();
         if (g.k > (uint32_t)kSlots && wide2)
@@ -1994,7 +1994,7 @@ namespace {
 // BFHIP_APPLY_FRESH=0 stores every touched vector (A/B only)
 uint32_t apply_store_fresh() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("BFHIP_APPLY_FRESH");
+        const char* e = BF_AB_GETENV("BFHIP_APPLY_FRESH");
         return (uint32_t)!(e && e[0] == '0');
     }();
     return v;
@@ -2004,7 +2004,7 @@ uint32_t apply_store_fresh() {
 // 2.431 (1) and 2.409 / 2.401 (4) at 10B (profiles/r04a_ab_xg.jsonl).  BFHIP_APPLY_XG overrides.
 uint32_t apply_xcd_group() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("BFHIP_APPLY_XG");
+        const char* e = BF_AB_GETENV("BFHIP_APPLY_XG");
         return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
     }();
     return v;
@@ -2014,7 +2014,7 @@ uint32_t apply_xcd_group() {
 // plus two run-table buffers; 4 waves per SIMD for its register pipeline).  BFHIP_APPLY_PIPE_GRID=n overrides it; 0 takes bin_apply_kernel (A/B).
 uint32_t apply_pipe_grid() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("BFHIP_APPLY_PIPE_GRID");
+        const char* e = BF_AB_GETENV("BFHIP_APPLY_PIPE_GRID");
         if (e && e[0]) return (uint32_t)std::strtoul(e, nullptr, 10);
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -2032,7 +2032,7 @@ uint32_t apply_pipe_grid() {
 // prefetched measured 2.44: the 10B apply is not bound by its dependent round trips).
 uint32_t apply_form(uint32_t dense) {
     static const uint32_t v = [] {
-        const char* e = std::getenv("BFHIP_APPLY_FORM");
+        const char* e = BF_AB_GETENV("BFHIP_APPLY_FORM");
         return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 255u;
     }();
     return v != 255u ? v : (dense == 2 ? 1u : 0u);
@@ -2052,16 +2052,19 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
     // the pipeline pays off over many regions per workgroup: a 150 MB shard (2288 regions, 9
     // per workgroup) measured 0.206 pipelined against 0.164 ms (P = 8 owner insert)
     if (dense && pg && p.region_log2 == 19 && form == 1 && p.nbins >= 16 * pg) {   // 2^20-bit regions: not pipelined
-        static const int pl = [] {
-            const char* e = std::getenv("BFHIP_APPLY_PIPE_LOADS");
+        [[maybe_unused]] static const int pl = [] {
+            const char* e = BF_AB_GETENV("BFHIP_APPLY_PIPE_LOADS");
             return e && *e && std::atoi(e) == 4 ? 4 : 8;
         }();
 #define BF_APPLY_PIPE(LD)                                                                                         \
     hipLaunchKernelGGL((bin_apply_pipe_kernel<19, kPipeLanes, LD>), dim3(std::min<uint32_t>(p.nbins, pg)),         \
                        dim3(kPipeLanes), 0, s, g.bits, nwords, p.nbins, c.level2, c.cb_base, c.cb_start, c.tabs,   \
                        p.max_chunks, p.ngroups, p.rel_log2, dense, any_flag, g.dirty, apply_store_fresh())
+#ifdef BFHIP_AB_KNOBS
         if (pl == 4) BF_APPLY_PIPE(4);
-        else BF_APPLY_PIPE(8);
+        else
+#endif
+        BF_APPLY_PIPE(8);
 #undef BF_APPLY_PIPE
     } else if (p.region_log2 == 18)
         hipLaunchKernelGGL((bin_apply_kernel<18, kApplyLanes / 2>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
@@ -2073,7 +2076,7 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
         // (8).  10B@0.01 % (~2k probes per region): 2.37 -> 2.25 ms; a P = 8 owner's insert
         // (~44k per region): 0.16 ms at 8 against 0.23 at 2 (profiles/r04i_ab_apply_loads.jsonl)
         static const int forced = [] {
-            const char* e = std::getenv("BFHIP_APPLY_LOADS");
+            const char* e = BF_AB_GETENV("BFHIP_APPLY_LOADS");
             const int v = e && *e ? std::atoi(e) : 0;
             return v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
         }();
@@ -2083,8 +2086,10 @@ hipError_t launch_apply(const BfGeom& g, const BfBinPlan& p, const Carve& c, uin
                        nwords, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, dense, \
                        any_flag, g.dirty, apply_store_fresh(), apply_xcd_group())
         if (loads == 2) BF_APPLY19(2);
+#ifdef BFHIP_AB_KNOBS
         else if (loads == 1) BF_APPLY19(1);
         else if (loads == 4) BF_APPLY19(4);
+#endif
         else BF_APPLY19(8);
 #undef BF_APPLY19
     }
@@ -2424,7 +2429,7 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
     if (p.l2test) {   // no sort: a superbin-major sweep, probes in receive order, answers stored in place
         // each XCD sweeps its own superbins, >= grid / 8 items each (chunk_test_l2_kernel)
         static const uint32_t grid = [] {
-            const char* e = std::getenv("BFHIP_L2_GRID");   // A/B: resident workgroups of the sweep
+            const char* e = BF_AB_GETENV("BFHIP_L2_GRID");   // A/B: resident workgroups of the sweep
             const int v = e ? std::atoi(e) : (int)kL2Grid;
             return (uint32_t)(v >= 64 && v <= 8192 ? v : (int)kL2Grid) & ~7u;   // whole XCD groups
         }();
@@ -2434,28 +2439,30 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
                            c.gsum, c.runs, parts, c.istart);
         bf_mark(mk, s, "chunk_group");
         // entries' runs: one search per wave and a forward walk (1), or a search per entry (0; A/B)
-        static const bool walk = [] {
-            const char* e = std::getenv("BFHIP_L2_WALK");
+        [[maybe_unused]] static const bool walk = [] {
+            const char* e = BF_AB_GETENV("BFHIP_L2_WALK");
             return !(e && *e == '0');
         }();
-        static const int l2_loads = [] {
-            const char* e = std::getenv("BFHIP_L2_LOADS");
+        [[maybe_unused]] static const int l2_loads = [] {
+            const char* e = BF_AB_GETENV("BFHIP_L2_LOADS");
             return e && *e ? std::atoi(e) : kL2Loads;
         }();
         if (side.n)
             hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
                                p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+#ifdef BFHIP_AB_KNOBS
         else if (walk && l2_loads == 16)   // (A/B: BFHIP_L2_LOADS, entries per lane in flight)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, true, 16>), dim3(grid), dim3(kL2Lanes), 0, s, ci,
                                g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         else if (walk && l2_loads == 4)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, true, 4>), dim3(grid), dim3(kL2Lanes), 0, s, ci,
                                g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
-        else if (walk)
-            hipLaunchKernelGGL((chunk_test_l2_kernel<false, true>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
-                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
-        else
+        else if (!walk)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, false>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
+                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
+#endif
+        else
+            hipLaunchKernelGGL((chunk_test_l2_kernel<false, true>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
                                p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         bf_mark(mk, s, side.n ? "test_l2_hash" : "test_l2");
         return hipGetLastError();
@@ -2656,10 +2663,12 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     for (uint32_t v = t; v < NW / 4; v += LANES) s_m4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     if (!(rv & 0x80000000u)) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
+#ifdef BFHIP_AB_KNOBS
     if (stop == 3) {   // (A/B: where the time goes; BFHIP_SETS_STOP) the region left absent
         if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;   // every lane read rv before the barrier
         return;
     }
+#endif
     const uint32_t st = sbf + (rv & 0x7FFFFFFFu);
     // LOADS level-2 loads per lane and step: a region's ~2k probes over all 16 waves (2), or
     // over 4 of them with more loads in flight each (8)
@@ -2672,10 +2681,12 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
             for (int c = 0; c < LOADS; ++c)
                 if (l[c] != 0xFFFFFFFFu) atomicOr(s_m + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
         });
+#ifdef BFHIP_AB_KNOBS
     if (stop == 2) {   // (A/B)
         if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
         return;
     }
+#endif
     // the run table is dead (for_region_probes ends on a barrier); the scan's barriers below
     // order these stores before the upper bitmap's first atomic
     for (uint32_t v = t; v < UPW; v += LANES) s_up[v] = 0;
@@ -2711,10 +2722,14 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     }
     if (!fits) return;   // workgroup-uniform
     uint32_t* o = out + st;
+#ifdef BFHIP_AB_KNOBS
     if (stop == 1) {   // (A/B) the region left absent, so no reader decodes the unwritten set
         if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
         return;
     }
+#else
+    (void)stop;
+#endif
     if (bitmap) {   // the LDS bitmap is still intact
         if (t == 0) o[0] = n | (kSetsBitmap << 24);
         for (uint32_t v = t; v < NW; v += LANES) o[1 + v] = s_m[v];
@@ -2947,11 +2962,12 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
 }  // namespace
 
 namespace {
-// A/B only (BFHIP_SETS_STOP): the encode stops after its probe pass (2), before writing the set
-// (1), or at once (3); the output is then incomplete.  0: the whole encode.
+// A/B only (BFHIP_SETS_STOP, -DBFHIP_AB_KNOBS builds): the encode stops after its probe pass
+// (2), before writing the set (1), or at once (3); the output is then incomplete.  0: the whole
+// encode (the shipped library has no stop points at all).
 uint32_t sets_stop() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("BFHIP_SETS_STOP");
+        const char* e = BF_AB_GETENV("BFHIP_SETS_STOP");
         return (e && e[0]) ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
     }();
     return v;
@@ -3000,8 +3016,8 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
                        p.rel_log2, p.nbins, 1u << p.region_log2, out, c.stot);
     hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, out, c.stot, p.nsup, p.region_log2, p.nbins);
     // level-2 loads per lane and gather step (BFHIP_SETS_ENC_LOADS A/B: 2, 4, 8)
-    static const int loads = [] {
-        const char* e = std::getenv("BFHIP_SETS_ENC_LOADS");
+    [[maybe_unused]] static const int loads = [] {
+        const char* e = BF_AB_GETENV("BFHIP_SETS_ENC_LOADS");
         const int v = e && *e ? std::atoi(e) : 2;
         return v == 8 || v == 4 || v == 1 ? v : 2;
     }();
@@ -3010,14 +3026,20 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
                        c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot, (uint32_t)cap_words, \
                        sets_stop())
     if (p.region_log2 == 19) {
+#ifdef BFHIP_AB_KNOBS
         if (loads == 8) BF_SETS_ENCODE(19, kApplyLanes, 8);
         else if (loads == 4) BF_SETS_ENCODE(19, kApplyLanes, 4);
         else if (loads == 1) BF_SETS_ENCODE(19, kApplyLanes, 1);
-        else BF_SETS_ENCODE(19, kApplyLanes, 2);
+        else
+#endif
+        BF_SETS_ENCODE(19, kApplyLanes, 2);
     } else if (p.region_log2 == 18) {
+#ifdef BFHIP_AB_KNOBS
         if (loads == 8) BF_SETS_ENCODE(18, kApplyLanes / 2, 8);
         else if (loads == 4) BF_SETS_ENCODE(18, kApplyLanes / 2, 4);
-        else BF_SETS_ENCODE(18, kApplyLanes / 2, 2);
+        else
+#endif
+        BF_SETS_ENCODE(18, kApplyLanes / 2, 2);
     } else {
         return hipErrorInvalidValue;
     }
@@ -3036,8 +3058,8 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
     // low-bit stage: 1 (default) 15 KB at 2^19-bit regions (two workgroups per CU), 7.5 KB at
     // 2^18; 0: none (A/B; a 48-KB stage at one workgroup per CU measured 7.07 against 4.72 ms
     // at 10B, profiles/r04g_ab_sets_stage.jsonl)
-    static const uint32_t stage = [] {
-        const char* e = std::getenv("BFHIP_SETS_STAGE");
+    [[maybe_unused]] static const uint32_t stage = [] {
+        const char* e = BF_AB_GETENV("BFHIP_SETS_STAGE");
         return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
     }();
     for (uint32_t s0 = 0; s0 < nsrc; s0 += kMaxSetSrc) {
@@ -3047,11 +3069,17 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
     hipLaunchKernelGGL((sets_apply_kernel<RL, LN, ST>), dim3(nbins), dim3(LN), 0, s, g.bits, nwords, src,       \
                        stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status)
         if (region_log2 == 19) {
+#ifdef BFHIP_AB_KNOBS
             if (stage == 0) BF_SETS_APPLY(19, kApplyLanes, 0);
-            else BF_SETS_APPLY(19, kApplyLanes, kLowsStage);
+            else
+#endif
+            BF_SETS_APPLY(19, kApplyLanes, kLowsStage);
         } else if (region_log2 == 18) {
+#ifdef BFHIP_AB_KNOBS
             if (stage == 0) BF_SETS_APPLY(18, kApplyLanes / 2, 0);
-            else BF_SETS_APPLY(18, kApplyLanes / 2, kLowsStage / 2);
+            else
+#endif
+            BF_SETS_APPLY(18, kApplyLanes / 2, kLowsStage / 2);
         } else {
             return hipErrorInvalidValue;
         }

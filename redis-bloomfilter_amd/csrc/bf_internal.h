@@ -2,6 +2,18 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
+
+// A/B knobs (kernel variants measured against the defaults) are read from the
+// environment only in the builds tools/build_ab_libs.sh makes with -DBFHIP_AB_KNOBS.  The
+// shipped library takes the measured defaults: the names are not even in its strings, so no
+// inherited variable can change what it computes or how (tests/test_abi.py checks the list).
+// The knobs a test uses to force a path (all of which give identical results) stay readable.
+#ifdef BFHIP_AB_KNOBS
+#define BF_AB_GETENV(name) std::getenv(name)
+#else
+#define BF_AB_GETENV(name) ((const char*)nullptr)
+#endif
 
 // Filter geometry as the kernels see it.
 struct BfGeom {

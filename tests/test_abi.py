@@ -157,6 +157,20 @@ def test_library_is_gfx950_only(pkg):
     assert targets == {b"gfx950"}
 
 
+# The only environment knobs the shipped library reads: path choices the GPU tests force (every
+# one gives identical results) and the host staging thread count.  The A/B knobs of DESIGN §6f,
+# including the encode stop points that write incomplete region sets, exist only in
+# -DBFHIP_AB_KNOBS builds (tools/build_ab_libs.sh) — VERDICT r04 item 2.
+PRODUCT_KNOBS = {"BFHIP_INSERT_BINNED", "BFHIP_INCLUDE_BINNED", "BFHIP_BIN_REGION_LOG2",
+                 "BFHIP_SHARD_TEST_BINNED", "BFHIP_CHUNK_TEST_L2", "BFHIP_ROUTE_AGG", "BFHIP_HOST_THREADS"}
+
+
+def test_library_reads_only_path_knobs(pkg):
+    blob = open(pkg._lib.lib_path(), "rb").read()
+    knobs = {m.decode() for m in re.findall(rb"BFHIP_[A-Z0-9_]+", blob)}
+    assert knobs == PRODUCT_KNOBS, sorted(knobs ^ PRODUCT_KNOBS)
+
+
 def test_version(pkg):
     assert pkg.version().startswith("bfhip ")
 

@@ -17,7 +17,9 @@
 #   replpmc    stall/LDS + VALU counters of the 10B x 8 region-set replica step
 #   ab         an A/B over one environment variable: AB_VAR, AB_VALUES (interleaved, e.g.
 #              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, repl10b, replnstar}; lines appended to
-#              gpurun_out/ab_${AB_VAR}_<tag>.jsonl
+#              gpurun_out/ab_${AB_VAR}_<tag>.jsonl.  The shipped library reads no A/B knob: the step
+#              loads AB_LIB (default ab_libs/ab/libbfhip.so, built on the CPU host by
+#              `bash tools/build_ab_libs.sh ab=-DBFHIP_AB_KNOBS`)
 # Default: tests smoke bench prof pmc.  Every GPU step runs under its own time limit; a failing
 # step ends the script (no further GPU work after a fault, abort or time limit).
 export TMPDIR=/tmp
@@ -88,6 +90,8 @@ for st in $STEPS; do
                     python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 1 \
                     > gpurun_out/pmc_${TAG}_sets_2.log 2>&1 ;;
         ab)     ABERR=gpurun_out/ab_${AB_VAR}_${TAG}.err
+                export BFHIP_LIB=${AB_LIB:-$PWD/ab_libs/ab/libbfhip.so}
+                [ -f "$BFHIP_LIB" ] || { echo "no A/B library $BFHIP_LIB"; exit 2; }
                 for v in ${AB_VALUES:?}; do
                     line=$(export "${AB_VAR:?}=$v"; ab_cmd "${AB_CMD:?}") || exit $?
                     echo "{\"var\": \"$AB_VAR\", \"value\": \"$v\", \"cmd\": \"$AB_CMD\", \"line\": $line}" \
