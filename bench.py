@@ -290,25 +290,16 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         f.hash_many_dev(ikb0.data_ptr(), iko0.data_ptr(), batch, digs[0].data_ptr(), stream=sp)
         step_no = [0]
 
-    # Replicated, comm_prefetch: step i starts the all-gather of batch i+1's keys before its
-    # own work, so the exchange runs beside step i's inserts and include? (the process group's
-    # stream); step i then inserts every rank's batch i — its own with the others, as ONE
-    # insert — before its include?, so every answer still sees all of the step's inserts.  The
-    # last step gathers batch 0 again, so every step does the same work.
+    # Replicated, comm_prefetch (distributed.ReplicatedPipeline, the code the multi-rank oracle
+    # test runs: tests/dist_worker.py rpipe_case): step i starts the all-gather of batch i+1
+    # before its own work, so the exchange runs beside step i's inserts and include? (the
+    # process group's stream); step i then inserts every rank's batch i — its own with the
+    # others, as ONE insert — before its include?, so every answer still sees all of the step's
+    # inserts.  The last step gathers batch 0 again, so every step does the same work.  rpipe:
+    # batches 0 and 1 are hashed here, before the timed region (the pipeline's fill).
     comm_prefetch_flag = comm_prefetch
     comm_prefetch = comm_prefetch and rf is not None
-    gpend, rstep, szp = {}, [0], {}
-    rdig = {}
-
-    def rdigs(b: int) -> torch.Tensor:   # batch b's SHA-1 words (a ring of three buffers)
-        if b % 3 not in rdig:
-            rdig[b % 3] = torch.empty((batch, 4), dtype=torch.int32, device=dev)
-        return rdig[b % 3]
-
-    if rpipe:   # the pipeline's fill: batches 0 and 1 hashed before the timed region
-        for b in (0, 1):
-            kb_, ko_ = batches[b % len(batches)][0]
-            f.hash_many_dev(kb_.data_ptr(), ko_.data_ptr(), batch, rdigs(b).data_ptr(), stream=sp)
+    rpl = pkg.distributed.ReplicatedPipeline(rf, batches, batch, fused_hash=rpipe) if comm_prefetch else None
 
     # Every timed insert asks for any_new, the reference's !found that drives EXPIRE
     # (ruby.rb:61-62): one pre-zeroed flag word per step, so no memset joins the step.
@@ -327,14 +318,7 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
         elif comm_prefetch:
             # the sizes of batch i+2 are all-gathered now, so step i+1's gather_start reads them
             # from pinned memory without waiting for the kernels in flight
-            i, L = rstep[0], len(batches)
-            st = gpend.pop(i % L, None) or rf.gather_start(ikb, iko, batch, digests=rdigs(i) if rpipe else None)
-            nxt = (i + 1) % L
-            gpend[nxt] = rf.gather_start(*batches[nxt][0], batch, sizes=szp.pop(nxt, None),
-                                         digests=rdigs(i + 1) if rpipe else None)
-            szp[(i + 2) % L] = rf.sizes_start(*batches[(i + 2) % L][0], batch)
-            rf.insert_gathered(st)
-            rstep[0] = i + 1
+            rpl.insert()
         elif rf is not None:
             rf.insert_many_dev(ikb, iko, batch)
         elif pf is None:
@@ -350,11 +334,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
             f.include_hash_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), nkb.data_ptr(), nko.data_ptr(),
                                batch, digs[(i + 1) % 2].data_ptr(), stream=sp)
             step_no[0] = i + 1
-        elif rpipe:   # include? of batch i with batch i+2's SHA-1 fused in
-            i = rstep[0] - 1
-            nkb, nko = batches[(i + 2) % len(batches)][0]
-            f.include_hash_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), nkb.data_ptr(), nko.data_ptr(),
-                               batch, rdigs(i + 2).data_ptr(), stream=sp)
+        elif comm_prefetch:   # include? of batch i (rpipe: with batch i+2's SHA-1 fused in)
+            rpl.include(out)
         elif rf is not None:
             out.copy_(rf.include_many_dev(pkb, pko, batch))
         elif pf is None:
@@ -401,9 +382,9 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     torch.cuda.synchronize()
     D.barrier()
     wall = time.perf_counter() - t_start
-    for st in gpend.values():   # the wrap-around gather of batch 0 (comm_prefetch)
-        for w in st.get("works", []):
-            w.wait()
+    if rpl is not None:   # the wrap-around gather of batch 0 (comm_prefetch)
+        rpl.drain()
+        rf.sets_check()   # no region-set apply skipped a buffer or a region
     if pf_prefetch:   # the wrap-around route of batch 0 (already inserted: idempotent)
         pf.drain_prefetch()
     wall = D.max(wall)

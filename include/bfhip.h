@@ -194,7 +194,10 @@ int  bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
  *      after bf_insert_region_sets_dev of every rank's sets equals the one after inserting
  *      every rank's keys (OR is idempotent and commutative).
  *   bf_region_sets_capacity  bytes a set buffer needs for any batch of <= n keys (a bound,
- *                            the same on every handle of this m and k: size the all-gather)
+ *                            the same on every handle of this m and k: size the all-gather).
+ *                            BF_EINVAL when one encode cannot take n keys (more than one
+ *                            binned pass) or the handle is not the ruby derivation: sized from
+ *                            the largest batch of all ranks, every rank learns it together
  *   bf_encode_region_sets_dev / _digests_dev   keys (or their SHA-1 words) -> d_sets
  *                            (sets_bytes >= the capacity; 16-byte aligned; the filter is not
  *                            modified).  n = 0 writes an empty set buffer.
@@ -202,6 +205,8 @@ int  bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
  *                            an encode on a handle of the same m and k) ORed into the filter;
  *                            probes_hint = the probes they hold (sum of n * k: picks the apply's
  *                            density form, never the result); d_any_new as bf_insert_many_dev;
+ *                            BF_EINVAL for an engine handle (BF_FLAG_ENGINE_*), or a stride
+ *                            below a buffer's header and per-region tables;
  *                            d_status (nullable) gets 1 ORed in when a buffer's header does not
  *                            match this filter (that buffer is skipped), or a region's entry
  *                            would reach past its buffer (that region of that buffer is

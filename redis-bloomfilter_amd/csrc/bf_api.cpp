@@ -1889,8 +1889,25 @@ int bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
 }
 
 // ---- replicated inserts from region sets (include/bfhip.h) ----
+namespace {
+// The encode sorts a batch in one binned pass whose regions are the geometry's: the plan of
+// n keys must exist and keep that region size (bf_encode_region_sets_dev refuses others).
+bool sets_one_pass(const bf_handle* h, uint64_t n, uint32_t rl, BfBinPlan* plan) {
+    if (n == 0) return true;
+    return bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, false, plan) && plan->region_log2 == rl;
+}
+}  // namespace
+
 int bf_region_sets_capacity(const bf_handle* h, uint64_t n, uint64_t* bytes) {
     if (!h || h->multi || !bytes) return BF_EINVAL;
+    *bytes = 0;
+    uint32_t rl = 0, nbins = 0;
+    BfBinPlan plan{};
+    // no buffer holds a batch the encode cannot take: every rank sizes the all-gather from the
+    // largest batch of all ranks, so all of them learn it here together (and fall back alike)
+    if (h->engine != BF_ENGINE_RUBY || !bf_sets_geometry(h->dev_bytes, h->bin_region_log2, &rl, &nbins) ||
+        !sets_one_pass(h, n, rl, &plan))
+        return BF_EINVAL;
     *bytes = bf_sets_capacity_bytes(h->dev_bytes, h->bin_region_log2, n, h->k);
     return *bytes ? BF_OK : BF_EINVAL;
 }
@@ -1915,7 +1932,7 @@ int encode_sets(bf_handle* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
     BfBinPlan plan{};
     plan.region_log2 = rl;
     plan.nbins = nbins;
-    if (n && (!bf_binned_plan(h->dev_bytes, n, h->k, h->bin_region_log2, false, &plan) || plan.region_log2 != rl))
+    if (!sets_one_pass(h, n, rl, &plan))
         return set_err(h, BF_EINVAL, "a batch of %llu keys does not sort in one pass (at most %llu keys per set buffer)",
                        (unsigned long long)n,
                        (unsigned long long)bf_binned_max_keys(h->k, h->dev_bytes, h->bin_region_log2));
@@ -1954,10 +1971,14 @@ int bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t str
     if (!d_sets || (reinterpret_cast<uintptr_t>(d_sets) & 15u) || (stride_bytes & 15u))
         return set_err(h, BF_EINVAL, "d_sets and stride_bytes must be 16-byte aligned");
     if (h->shards > 1) return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter");
+    // the sets hold offsets of the ruby driver's derivation: ORing them into an engine filter of
+    // the same m and k would set bits its own derivation never probes
+    if (h->engine != BF_ENGINE_RUBY) return set_err(h, BF_EINVAL, "region sets carry the ruby driver's derivation only");
     uint32_t rl = 0, nbins = 0;
     if (!bf_sets_geometry(h->dev_bytes, h->bin_region_log2, &rl, &nbins))
         return set_err(h, BF_EINVAL, "this filter's regions cannot take region sets");
-    if (stride_bytes < 4 * (nbins + 4ull)) return set_err(h, BF_EINVAL, "stride_bytes below a set buffer's header");
+    if (stride_bytes < 4 * bf_sets_header_words(nbins))   // the apply reads both per-region tables
+        return set_err(h, BF_EINVAL, "stride_bytes below a set buffer's header and tables");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);

@@ -2828,7 +2828,10 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     uint32_t st = 0, hdr = 0;
     if (t < nsrc) {   // source t's set for this region
         const uint32_t* S = sets + (uint64_t)t * stride_words;
-        bool ok = S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] <= stride_words;
+        // (the host checked stride_words >= sets_first_word(nbins): the tables read below are
+        // inside every buffer; [3] must cover them too and stay inside the stride)
+        bool ok = S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] >= sets_first_word(nbins) &&
+                  S[3] <= stride_words;
         if (ok) {
             st = S[kSetsHdr + r];
             hdr = S[kSetsHdr + nbins + r];   // beside the place: one round trip
@@ -2973,6 +2976,8 @@ uint32_t sets_stop() {
     return v;
 }
 }  // namespace
+
+uint64_t bf_sets_header_words(uint32_t nbins) { return sets_first_word(nbins); }
 
 bool bf_sets_geometry(uint64_t bitset_bytes, uint32_t pref_region_log2, uint32_t* region_log2, uint32_t* nbins) {
     BfBinPlan p{};

@@ -206,6 +206,8 @@ hipError_t bf_launch_include_binned(const BfGeom& g, const BfBinPlan& p, uint64_
 // batch of n keys.  The encode's plan (bf_binned_plan) must have the geometry's region size.
 bool bf_sets_geometry(uint64_t bitset_bytes, uint32_t pref_region_log2, uint32_t* region_log2, uint32_t* nbins);
 uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2, uint64_t n, uint32_t k);
+// Words before a set buffer's first set: the header and the two per-region tables.
+uint64_t bf_sets_header_words(uint32_t nbins);
 hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,
                                  const uint64_t* offsets, uint64_t bias, uint64_t n, bool dig, void* scratch,
                                  uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* marks = nullptr);

@@ -40,7 +40,7 @@ import torch
 import torch.distributed as dist
 
 from . import keys as _keys
-from ._lib import BF_FLAG_ROUTE32, ArgumentError, Filter
+from ._lib import BF_EINVAL, BF_FLAG_ROUTE32, ArgumentError, BfHipError, Filter
 
 # -- collectives -------------------------------------------------------------------------
 # RCCL (backend "nccl") moves device tensors directly.  Under gloo the device tensors are
@@ -1053,6 +1053,16 @@ class ReplicatedFilter:
         self.insert_mode = insert_mode
         self.last_insert_mode = None
         self.host_wait_s = 0.0   # time the host spent waiting for batch sizes (gather_start)
+        # "sets": the apply ORs a device status word when it skips a buffer or a region (a header
+        # that does not match, an entry past its buffer, an encode past its capacity).  Its value
+        # after each apply is copied to pinned memory behind an event; _sets_check reads the copy
+        # two inserts later (by then the pipelined caller's host has already waited past that
+        # apply), so no step waits for its own apply.  Every replica applies the same gathered
+        # buffers, so every rank sees the same value at the same call and raises together.
+        self._sets_status = None
+        self._sets_host = None
+        self._sets_pending = []   # (insert number, event, pinned slot)
+        self._sets_done = 0
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -1123,9 +1133,16 @@ class ReplicatedFilter:
             mode = "or" if 2 * self.filter.device_bytes < gather_bytes else "gather"
         if mode == "or":
             return dict(mode="or", kb=kb, ko=ko, n=n)
+        if mode == "sets":
+            # every rank sizes the buffers from the largest batch of all ranks, so a batch one
+            # encode cannot take (more than one binned pass) is found on every rank at once, and
+            # they all take the digests form for it together (an error on one rank alone would
+            # leave the others waiting in the all-gather)
+            try:
+                cap = self.filter.region_sets_capacity(max(max(sz[1] for sz in all_sizes), 1))
+            except ArgumentError:
+                mode = "digests"
         if mode == "sets":   # this rank sorts and encodes its batch once; the region sets travel
-            max_n = max(max(sz[1] for sz in all_sizes), 1)
-            cap = self.filter.region_sets_capacity(max_n)   # the same on every rank: one gather size
             mine = torch.empty(cap // 4, dtype=torch.int32, device=self.device)
             if digests is not None and n:
                 self.filter.encode_region_sets_digests_dev(digests.data_ptr(), n, mine.data_ptr(), cap,
@@ -1139,7 +1156,9 @@ class ReplicatedFilter:
         if mode == "digests":   # this rank hashes its batch once; the words travel
             max_n = max(max(sz[1] for sz in all_sizes), 1)
             mine = torch.zeros((max_n, 4), dtype=torch.int32, device=self.device)
-            if n:
+            if n and digests is not None:   # already hashed (a pipelined caller)
+                mine[:n].copy_(digests[:n])
+            elif n:
                 self.filter.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, mine.data_ptr(), stream=self._stream())
             gd = torch.empty((self.P * max_n, 4), dtype=torch.int32, device=self.device)
             works = [_all_gather_into_tensor(gd.view(-1), mine.view(-1), group=self.group, async_op=True)]
@@ -1174,8 +1193,18 @@ class ReplicatedFilter:
         if st["mode"] == "sets":   # every rank's sets ORed in by one pass over the bitset
             probes = sum(sz[1] for sz in st["sizes"]) * self.k
             if probes:
+                if self._sets_status is None:
+                    self._sets_status = torch.zeros(1, dtype=torch.int32, device=self.device)
+                    self._sets_host = torch.zeros(3, dtype=torch.int32, pin_memory=self._sets_status.is_cuda)
                 self.filter.insert_region_sets_dev(st["gs"].data_ptr(), st["cap"], self.P, probes,
-                                                   stream=self._stream())
+                                                   d_status=self._sets_status.data_ptr(), stream=self._stream())
+                self._sets_done += 1
+                slot = self._sets_done % 3
+                self._sets_host[slot:slot + 1].copy_(self._sets_status, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+                self._sets_pending.append((self._sets_done, ev, slot))
+                self._sets_check(lag=2)
             return
         if st["mode"] == "digests":   # every rank's words as ONE insert (padding rows cut out)
             counts = [sz[1] for sz in st["sizes"]]
@@ -1193,6 +1222,24 @@ class ReplicatedFilter:
         if on:
             self.filter.insert_many_dev(ob.data_ptr(), oo.data_ptr(), on, stream=self._stream())
 
+    def _sets_check(self, lag: int = 0) -> None:
+        """Read the status copies of all but the last ``lag`` region-set inserts; raise if an
+        apply skipped a buffer or a region (those inserts are lost: include? would answer
+        false for keys that were inserted, the one thing a Bloom filter must never do)."""
+        while len(self._sets_pending) > lag:
+            no, ev, slot = self._sets_pending.pop(0)
+            ev.synchronize()
+            if int(self._sets_host[slot]):
+                self._sets_pending.clear()
+                raise BfHipError(BF_EINVAL, "region-set insert %d: the apply skipped a set buffer or region "
+                                            "(foreign, damaged or over-capacity sets); inserts were lost" % no)
+
+    def sets_check(self) -> None:
+        """Raise now if any region-set insert so far skipped a buffer or a region (collective
+        in effect: every replica applied the same buffers; the host-pointer calls and export do
+        this themselves)."""
+        self._sets_check(lag=0)
+
     def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
         out = torch.empty(n, dtype=torch.uint8, device=self.device)
         self.filter.include_many_dev(kb.data_ptr(), ko.data_ptr(), n, out.data_ptr(), stream=self._stream())
@@ -1201,14 +1248,85 @@ class ReplicatedFilter:
     def insert_many(self, keys: Iterable) -> None:
         kb, ko, n = _device_batch(keys, self.device)
         self.insert_many_dev(kb, ko, n)
+        self.sets_check()
 
     def include_many(self, keys: Iterable) -> np.ndarray:
         kb, ko, n = _device_batch(keys, self.device)
-        return self.include_many_dev(kb, ko, n).cpu().numpy().astype(bool)
+        ans = self.include_many_dev(kb, ko, n).cpu().numpy().astype(bool)
+        self.sets_check()
+        return ans
 
     def export_redis(self) -> bytes:
         torch.cuda.current_stream(self.device).synchronize()
+        self.sets_check()
         return self.filter.export_redis()
 
     def close(self):
         self.filter.close()
+
+
+class ReplicatedPipeline:
+    """The pipelined replicated step (``bench.py --gpus N`` on a replicated layout): a ring of
+    batches ``batches[b] = ((insert key bytes, offsets), (include? key bytes, offsets))`` of
+    ``n`` keys each, stepped in order (batch b = step number mod len(batches)).  Step i
+
+    1. starts the all-gather of batch i+1 (its sizes were all-gathered during step i-1, so the
+       host reads them without waiting for the kernels in flight) and the sizes of batch i+2;
+    2. inserts every rank's batch i — this rank's own with the others, as one insert — whose
+       gather started during step i-1 (``insert``);
+    3. answers include? batch i after those inserts (``include``).
+
+    With ``fused_hash`` ("sets" form): batch i+2's SHA-1 words come out of step i's include?
+    kernel (``bf_include_hash_dev``, as the single-GPU step hashes its next batch), so step
+    i+1 encodes batch i+2's region sets from words, with no hash pass; the words live in a ring
+    of three buffers.  Every key is still hashed once per step.  The answers and every
+    replica's bitset equal those of inserting all ranks' batches 0..i before include? i
+    (``tests/dist_worker.py``'s ``rpipe`` check).  The last step's gather of the wrapped-around
+    batch is left pending: ``drain`` completes it (nothing is inserted from it)."""
+
+    def __init__(self, rf: "ReplicatedFilter", batches, n: int, fused_hash: bool = True):
+        self.rf, self.batches, self.n, self.L = rf, batches, n, len(batches)
+        if self.L < 3:
+            raise ArgumentError("ReplicatedPipeline needs at least 3 batches in its ring")
+        self.fused = fused_hash and rf.insert_mode == "sets"
+        self.step = 0
+        self.gpend, self.szp, self.dig = {}, {}, {}
+        if self.fused:   # the pipeline's fill: batches 0 and 1 hashed ahead of step 0
+            for b in (0, 1):
+                kb, ko = batches[b % self.L][0]
+                rf.filter.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, self._digests(b).data_ptr(),
+                                        stream=rf._stream())
+
+    def _digests(self, i: int) -> torch.Tensor:   # step i's batch's SHA-1 words (ring of three)
+        if i % 3 not in self.dig:
+            self.dig[i % 3] = torch.empty((self.n, 4), dtype=torch.int32, device=self.rf.device)
+        return self.dig[i % 3]
+
+    def insert(self) -> None:
+        rf, i, L, n = self.rf, self.step, self.L, self.n
+        st = self.gpend.pop(i % L, None) or rf.gather_start(*self.batches[i % L][0], n,
+                                                              digests=self._digests(i) if self.fused else None)
+        nxt = (i + 1) % L
+        self.gpend[nxt] = rf.gather_start(*self.batches[nxt][0], n, sizes=self.szp.pop(nxt, None),
+                                          digests=self._digests(i + 1) if self.fused else None)
+        self.szp[(i + 2) % L] = rf.sizes_start(*self.batches[(i + 2) % L][0], n)
+        rf.insert_gathered(st)
+        self.step = i + 1
+
+    def include(self, out: torch.Tensor) -> None:
+        """include? batch i (the step ``insert`` just finished) into ``out`` (n bytes, 0/1)."""
+        rf, i, n = self.rf, self.step - 1, self.n
+        pkb, pko = self.batches[i % self.L][1]
+        if self.fused:   # ... with batch i+2's SHA-1 fused in
+            nkb, nko = self.batches[(i + 2) % self.L][0]
+            rf.filter.include_hash_dev(pkb.data_ptr(), pko.data_ptr(), n, out.data_ptr(), nkb.data_ptr(),
+                                       nko.data_ptr(), n, self._digests(i + 2).data_ptr(), stream=rf._stream())
+        else:
+            rf.filter.include_many_dev(pkb.data_ptr(), pko.data_ptr(), n, out.data_ptr(), stream=rf._stream())
+
+    def drain(self) -> None:
+        """Complete the pending gathers (collective: every rank calls it after its last step)."""
+        for st in self.gpend.values():
+            for w in st.get("works", []):
+                w.wait()
+        self.gpend.clear()

@@ -213,7 +213,104 @@ def replicated_big_case(rank, P, cfg, dev):
         rf.close()
     if not ok:
         print("rank %d replicated 10B uneven MISMATCH" % rank, flush=True)
-    return ok
+    # bench.py --gpus 8 --config 10b's own step (ReplicatedPipeline, fused hash, region sets)
+    return rpipe_case(rank, P, dict(cfg, n=n // 2, steps=4), dev) and ok
+
+
+def rpipe_case(rank, P, cfg, dev):
+    """The exact replicated step bench.py --gpus N times on the replicated layouts
+    (distributed.ReplicatedPipeline): step i's include? kernel hashes batch
+    i+2 into a ring of three word buffers, step i+1 encodes those words into region sets
+    (gather_start(..., digests=)) and all-gathers them while batch i+2's sizes travel, step i+2
+    ORs every rank's sets in (insert_gathered, "sets"), and the last step's gather wraps around
+    to batch 0.  After every step the include? answers must equal the oracle's over every
+    rank's batches 0..i (ruby.rb:20-30); after the last, every replica's bitset must equal the
+    oracle's over all of them (ruby.rb:57-63), compared sparsely.  Then: a damaged set buffer
+    makes every rank raise at its sets check, and a batch one encode cannot take
+    on one rank moves every rank to the digests form for that batch."""
+    m, k, n, L = cfg["m"], cfg["k"], cfg["n"], cfg.get("steps", 5)
+    orc = O.COracle()
+
+    def ins_keys(r, b):
+        return ["p%d-%d-%d" % (r, b, int(v)) for v in np.random.default_rng([cfg["seed"], r, b]).integers(0, 10**12, n)]
+
+    def inc_keys(r, b):   # half that step's inserts, half fresh
+        return ins_keys(r, b)[: n // 2] + ["np%d-%d-%d" % (r, b, i) for i in range(n - n // 2)]
+
+    batches = [(D._device_batch(ins_keys(rank, b), dev)[:2], D._device_batch(inc_keys(rank, b), dev)[:2])
+               for b in range(L)]
+    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="sets")
+    rpl = D.ReplicatedPipeline(rf, batches, n, fused_hash=True)
+    outs = []
+    for _ in range(L):
+        out = torch.empty(n, dtype=torch.uint8, device=dev)
+        rpl.insert()
+        rpl.include(out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    rpl.drain()
+    ok = rf.last_insert_mode == "sets"
+    rf.sets_check()
+    set_idx = np.zeros(0, np.uint64)
+    for b in range(L):   # the answers of step b see every rank's batches 0..b
+        keys_b = [x for r in range(P) for x in ins_keys(r, b)]
+        kb_, ko_ = O.pack_keys(keys_b)
+        set_idx = np.union1d(set_idx, orc.indexes_many(kb_, ko_, m, k).reshape(-1))
+        want = sparse_include(orc, set_idx, inc_keys(rank, b), m, k)
+        good = bool((outs[b].cpu().numpy().astype(bool) == want).all())
+        if not good:
+            print("rank %d rpipe step %d: %d answers differ" % (rank, b, int((outs[b].cpu().numpy().astype(bool) != want).sum())),
+                  flush=True)
+        ok = ok and good
+    all_keys = [x for b in range(L) for r in range(P) for x in ins_keys(r, b)]
+    want_pos, want_val, _ = sparse_bits(orc, all_keys, m, k)
+    gp, gv = device_sparse(rf.filter)
+    same = bool(np.array_equal(gp, want_pos) and np.array_equal(gv, want_val))
+    if not same:
+        print("rank %d rpipe: bitset differs from the oracle" % rank, flush=True)
+    ok = ok and same
+    rf.close()
+    # a damaged buffer (the last rank's header) is skipped by every replica, and every rank
+    # raises at its next sets check instead of answering false for inserted keys later
+    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="sets")
+    st = rf.gather_start(*batches[0][0], n)
+    for w in st["works"]:
+        w.wait()
+    st["gs"].view(P, -1)[P - 1, 0] = 0
+    rf.insert_gathered(st)
+    try:
+        rf.sets_check()
+        ok = False
+        print("rank %d: a damaged set buffer went unreported" % rank, flush=True)
+    except pkg.BfHipError:
+        pass
+    rf.close()
+    # rank 0's batch past what one encode takes (here: a capacity bound lowered to below it):
+    # every rank learns it from the gathered sizes and takes the digests form for that batch
+    rf = D.ReplicatedFilter(m, k, device=dev, insert_mode="sets")
+    real = rf.filter.region_sets_capacity
+    lim = n // 2
+
+    def capped(nk):
+        if nk > lim:
+            raise pkg.ArgumentError("test: %d keys past one encode" % nk)
+        return real(nk)
+
+    rf.filter.region_sets_capacity = capped
+    mine = ins_keys(rank, 0)[: (n if rank == 0 else lim)]
+    rf.insert_many(mine)
+    ok = ok and rf.last_insert_mode == "digests"
+    rf.insert_many(ins_keys(rank, 1)[:lim])
+    ok = ok and rf.last_insert_mode == "sets"
+    sub = [x for r in range(P) for x in ins_keys(r, 0)[: (n if r == 0 else lim)]]
+    sub += [x for r in range(P) for x in ins_keys(r, 1)[:lim]]
+    up, uv, _ = sparse_bits(orc, sub, m, k)
+    gp, gv = device_sparse(rf.filter)
+    fb = bool(np.array_equal(gp, up) and np.array_equal(gv, uv))
+    if not fb:
+        print("rank %d: the digests fallback differs from the oracle" % rank, flush=True)
+    rf.close()
+    return ok and fb
 
 
 def uneven_case(rank, P, cfg, dev, make_engine):
@@ -304,8 +401,8 @@ def main():
     cfg = json.loads(os.environ["BF_DIST_CFG"])
     hip = cfg.get("engine") == "hip"
     dev = torch.device("cuda", 0) if hip else None
-    if cfg.get("case") in ("replicated", "replicated_big"):
-        fn = replicated_case if cfg["case"] == "replicated" else replicated_big_case
+    if cfg.get("case") in ("replicated", "replicated_big", "rpipe"):
+        fn = {"replicated": replicated_case, "replicated_big": replicated_big_case, "rpipe": rpipe_case}[cfg["case"]]
         flag = torch.tensor([1 if fn(rank, P, cfg, dev) else 0])
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if rank == 0:

@@ -112,6 +112,21 @@ def test_replicated_hip_10b_x8():
     assert "DIST_RESULT ok" in out.stdout
 
 
+@pytest.mark.timeout(300)
+def test_replicated_bench_step_nstar_x2():
+    """The exact step bench.py --gpus 2 times on the north-star filter (replicated, region
+    sets, fused hash: distributed.ReplicatedPipeline), five steps with the wrap-around, every
+    step's include? answers and both replicas' bitsets against the oracle; plus a damaged set
+    buffer raising on every rank and one rank's oversized batch taking the digests form on
+    every rank (tests/dist_worker.py rpipe_case).  The 10B x 8 run of the same step is in
+    test_replicated_hip_10b_x8."""
+    cfg = {"case": "rpipe", "m": 9585058377, "k": 6, "n": 60000, "steps": 5, "seed": 17, "engine": "hip"}
+    out = torchrun(2, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},
+                   timeout=280)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "DIST_RESULT ok" in out.stdout
+
+
 def test_or_allreduce_device_tensors():
     cfg = {"case": "or_allreduce", "engine": "hip"}
     out = torchrun(3, os.path.join(HERE, "dist_worker.py"), env_extra={"BF_DIST_CFG": json.dumps(cfg)},

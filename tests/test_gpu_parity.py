@@ -315,10 +315,13 @@ def test_binned_insert_matches_oracle(pkg, oracle, monkeypatch, mode, m, k, n):
         assert f.export_redis() == s
 
 
-# Every case at the default 2^19-bit regions; the 2^18 / 2^20 templates (512-lane apply / test,
-# 128 KiB LDS images) on the cheap cases, and the 10B filter at 2^20 (at 2^18 it takes 2^19)
+# Every case at every region size: 2^19 bits (the default), and the 2^18 / 2^20 templates
+# (512-lane apply / test, 128 KiB LDS images) — ADVICE r04: the DPP block scan, the apply's
+# XCD remap and LOADS template and the route fronts' compile-time slots reach all of them
+# (the 10B filter at 2^18 takes 2^19, so k13 runs at 19 and 20 only)
 EDGE_CASES = ([("19", c) for c in ("dup", "tiny", "long", "k12", "k13", "k16", "nstar")] +
-              [("18", c) for c in ("dup", "long", "k12")] + [("20", c) for c in ("dup", "long", "k12", "k13")])
+              [("18", c) for c in ("dup", "tiny", "long", "k12", "k16", "nstar")] +
+              [("20", c) for c in ("dup", "tiny", "long", "k12", "k13", "k16", "nstar")])
 
 
 @pytest.mark.parametrize("rl,case", EDGE_CASES)

@@ -228,3 +228,62 @@ def test_damaged_region_entry_is_skipped(pkg, oracle):
         np.bitwise_or.at(expect, (exp_bits >> np.uint64(3)).astype(np.int64),
                          (np.uint8(0x80) >> (exp_bits & np.uint64(7)).astype(np.uint8)))
         np.testing.assert_array_equal(got, expect[: len(got)])
+
+
+@pytest.mark.parametrize("nsrc", [17, 33])
+def test_many_sources_take_several_launches(pkg, oracle, nsrc):
+    """More sources than one sets_apply launch takes (kMaxSetSrc = 16): the sources go in 16
+    at a time, and the bitset equals the oracle's insert of every batch."""
+    torch = pytest.importorskip("torch")
+    m, k = 9585058, 6
+    rng = np.random.default_rng(SEED + nsrc)
+    batches = [_keys(pkg, rng, 3_000 + 97 * s, "m%d" % s) for s in range(nsrc)]
+    with pkg.Filter(m, k) as f:
+        cap = max(f.region_sets_capacity(len(o) - 1) for _, o in batches)
+        sets = torch.cat([_encode(torch, f, b, o, cap=cap) for b, o in batches])
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        probes = sum(len(o) - 1 for _, o in batches) * k
+        f.insert_region_sets_dev(sets.data_ptr(), cap, nsrc, probes, d_any_new=flag.data_ptr(),
+                                 d_status=status.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(status.item()) == 0 and int(flag.item()) == 1
+        got = f.export_redis()
+    bits = oracle.new_bitset(m, k)
+    for b, o in batches:
+        oracle.insert_many(bits, m, k, b, o)
+    assert got == oracle.redis_string(bits)
+
+
+def test_sets_api_refusals(pkg):
+    """a stride shorter than a buffer's header and tables, an engine filter (the
+    sets carry the ruby driver's offsets), and a batch one encode cannot take (no capacity is
+    given for it, so every rank that sizes its buffers from the largest batch learns it) are
+    refused; a buffer whose reserved-words field does not cover its own tables is skipped."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(SEED + 21)
+    buf, offs = _keys(pkg, rng, 5_000)
+    m, k = 9585058377, 6
+    with pkg.Filter(m, k) as f:
+        sets = _encode(torch, f, buf, offs)
+        words = sets.cpu().numpy().view(np.uint32)
+        R = int(words[2])
+        first = (4 + 2 * R + 63) // 64 * 64
+        with pytest.raises(pkg.ArgumentError):
+            f.insert_region_sets_dev(sets.data_ptr(), 4 * (R + 4), 1, 30_000, stream=0)
+        with pytest.raises(pkg.ArgumentError):
+            f.region_sets_capacity(1 << 34)
+        bad = words.copy()
+        bad[3] = first - 1
+        damaged = torch.from_numpy(bad.view(np.int32)).cuda()
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        f.insert_region_sets_dev(damaged.data_ptr(), damaged.numel() * 4, 1, 30_000, d_status=status.data_ptr(),
+                                 stream=0)
+        torch.cuda.synchronize()
+        assert int(status.item()) == 1 and f.export_redis() == b""
+    with pkg.Filter(m, k, flags=pkg.BF_FLAG_ENGINE_MD5) as e:
+        with pytest.raises(pkg.ArgumentError):
+            e.insert_region_sets_dev(sets.data_ptr(), sets.numel() * 4, 1, 30_000, stream=0)
+        with pytest.raises(pkg.ArgumentError):
+            e.region_sets_capacity(1000)
+
