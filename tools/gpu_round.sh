@@ -4,6 +4,7 @@
 #   tests      every -m gpu test (PYTEST_EXTRA adds flags, e.g. --durations=100)
 #   parity     the parity files alone: parity, distributed primitives, digests, region sets
 #   sets       region-set tests + the replicated / region-set multi-rank gloo cases
+#   edge       the forced-binned edge cases at every region size (test_binned_edge_cases)
 #   smoke      __graft_entry__.smoke()
 #   bench      the driver's bench command (--gpus 1 --steps 20 --warmup 5)
 #   bench10b / bench200b / bench100m   the other single-GPU configs
@@ -29,7 +30,7 @@ STEPS=${*:-tests smoke bench prof pmc}
 NOEXTRA="--no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes"
 STALL="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS"
 VALU="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_SALU"
-PYT="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 
 ab_cmd() {   # one A/B line's command, stdout = its JSON
     case $1 in
@@ -48,8 +49,10 @@ for st in $STEPS; do
                     ${PYTEST_EXTRA:-} > gpurun_out/tests_${TAG}.log 2>&1 ;;
         parity) timeout -k 10 560 $PYT tests/test_gpu_parity.py tests/test_gpu_distributed.py tests/test_gpu_digests.py \
                     tests/test_gpu_region_sets.py > gpurun_out/tests_${TAG}_parity.log 2>&1 ;;
-        sets)   timeout -k 10 300 $PYT tests/test_gpu_region_sets.py tests/test_gpu_dist_gloo.py -k "sets or replicated" \
+        sets)   timeout -k 10 700 $PYT tests/test_gpu_region_sets.py tests/test_gpu_dist_gloo.py -k "sets or replicated" \
                     > gpurun_out/tests_${TAG}_sets.log 2>&1 ;;
+        edge)   timeout -k 10 500 $PYT tests/test_gpu_parity.py -k binned_edge \
+                    > gpurun_out/tests_${TAG}_edge.log 2>&1 ;;
         smoke)  timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
         bench)  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
                     > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
