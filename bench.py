@@ -451,11 +451,16 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
                    "path": "binned" if plan["binned"] else "direct",
                    "algo_bytes_per_key": (Lmean + 8 + 2 * bitset / batch) if plan["binned"]
                    else (Lmean + 8 + 2 * k * GRANULE),
-                   # SURVEY §8(d)'s random-access model (L + 8 + 2kG) beside the streaming one
-                   # the binned path is bound by (L + 8 + 2 * bitset / batch): the fraction of
-                   # 8 TB/s each model gives the op's keys/s
-                   "frac_random_model": batch / (ins_ms / 1e3) * (Lmean + 8 + 2 * k * GRANULE) / HBM_PEAK,
-                   "frac_streaming_model": batch / (ins_ms / 1e3) * (Lmean + 8 + 2 * bitset / batch) / HBM_PEAK},
+                   # SURVEY §8(d)'s random-access model (L + 8 + 2kG) prices the direct insert;
+                   # the binned insert streams the bitset once instead (L + 8 + 2 * bitset /
+                   # batch), so only that model's fraction of 8 TB/s is given for it (the random
+                   # model's would exceed 1 without any work skipped: VERDICT r04 weak 3)
+                   "frac_random_model": None if plan["binned"] else
+                   batch / (ins_ms / 1e3) * (Lmean + 8 + 2 * k * GRANULE) / HBM_PEAK,
+                   "frac_streaming_model": batch / (ins_ms / 1e3) * (Lmean + 8 + 2 * bitset / batch) / HBM_PEAK
+                   if plan["binned"] else None,
+                   "roofline_model": "streaming (binned: the bitset read and written once per batch)"
+                   if plan["binned"] else "random access (SURVEY §8 d: L + 8 + 2kG)"},
         "include": {"op_ms": inc_ms, "keys_per_s": batch / (inc_ms / 1e3),
                     "path": "binned" if inc_binned else "direct",
                     "algo_bytes_per_key": (Lmean + 8 + 1 + bitset / batch) if inc_binned
@@ -903,10 +908,13 @@ def main():
     if D.world == 1 and not args.no_secondary:
         # 1m_big: the L2-resident 1M@1 % filter at 2^24-key batches (hash-bound; 1m's 2^20-key
         # batches are launch- and latency-bound)
+        # every secondary runs the step `--config <name>` runs (pipelined unless --pipeline 0),
+        # so the driver's line carries the same numbers a --config run reports
         for name in ("1m", "1m_big", "100m", "10b"):
             if name != args.config:
-                r, _ = time_config(pkg, D, name, max(3, args.steps // 2), 1)
-                secondary[name] = {"keys_per_s": r["keys_per_s"],
+                r, _ = time_config(pkg, D, name, max(3, args.steps // 2), 1, pipeline=bool(args.pipeline))
+                secondary[name] = {"keys_per_s": r["keys_per_s"], "pipelined": r["pipelined"],
+                                   "ms_per_step": r["wall_s"] / r["steps"] * 1e3,
                                    "insert_keys_per_s": r["insert"]["keys_per_s"],
                                    "include_keys_per_s": r["include"]["keys_per_s"],
                                    "m": r["m"], "k": r["k"], "batch": r["batch"],

@@ -439,7 +439,16 @@ int  bf_shard_import(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mo
  *   bf_lua_clear         lua.rb:28-30 (KEYS name:* + DEL): layers and count dropped
  *   bf_lua_get/set_count KEYS[1]:count;  bf_lua_export/import_layer  KEYS[1]:n (SETBIT layout)
  *   bf_lua_layer_params  add.lua:16-25: bits and k of layer n (host only, no device)
- *   bf_lua_index         add.lua:13-15 / check.lua:9-11: the layer of a count (host only) */
+ *   bf_lua_index         add.lua:13-15 / check.lua:9-11: the layer of a count (host only)
+ *   bf_lua_insert_many_dev / bf_lua_include_many_dev   the same two ops on device-resident
+ *                        keys (bf_insert_many_dev's layout: 16 B readable past offsets[n]) on
+ *                        the caller's stream (NULL: the null stream), per-key flags and answers
+ *                        in device memory.  The insert returns with the count updated (the host
+ *                        picks each chunk's layer from it: one 8-byte read per chunk); include?
+ *                        returns once enqueued.  Calls on different streams are ordered.
+ *   bf_lua_profile / bf_lua_profile_read   per-kernel HIP-event timing as bf_profile, names
+ *                        "lua_seq_candidates[L<n>]", "lua_seq_mark[L<n>]", "lua_count[L<n>]"
+ *                        (per layer n) and "lua_check" */
 typedef struct bf_lua bf_lua;
 int  bf_lua_create(double entries, double precision, const bf_config* cfg /* device only */, bf_lua** out);
 int  bf_lua_destroy(bf_lua* h);
@@ -452,6 +461,14 @@ int  bf_lua_insert_many_changes(bf_lua* h, const uint8_t* key_bytes, const uint6
 #define BF_LUA_LAYER_SHIFT 58   /* out_bits of bf_lua_insert_many_changes: layer << 58 | offset */
 int  bf_lua_include_many(bf_lua* h, const uint8_t* key_bytes, const uint64_t* offsets, uint64_t n,
                          uint8_t* out);
+int  bf_lua_insert_many_dev(bf_lua* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                            uint8_t* d_per_key_new /* nullable */, uint64_t* new_layers /* nullable */,
+                            void* stream);
+int  bf_lua_include_many_dev(bf_lua* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                             uint8_t* d_out, void* stream);
+int  bf_lua_profile(bf_lua* h, uint32_t enable);
+int  bf_lua_profile_read(bf_lua* h, char* names, double* total_ms, uint64_t* launches, uint32_t cap,
+                         uint32_t* n_out, uint32_t reset);
 int  bf_lua_clear(bf_lua* h);
 int  bf_lua_get_count(const bf_lua* h, uint64_t* count);
 int  bf_lua_set_count(bf_lua* h, uint64_t count);

@@ -131,6 +131,10 @@ SIGNATURES = {
     "bf_lua_insert_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64p]),
     "bf_lua_insert_many_changes": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64p, _vp, _u64, _u64p]),
     "bf_lua_include_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
+    "bf_lua_insert_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64p, _vp]),
+    "bf_lua_include_many_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "bf_lua_profile": (ctypes.c_int, [_vp, _u32]),
+    "bf_lua_profile_read": (ctypes.c_int, [_vp, _vp, _vp, _vp, _u32, _u32p, _u32]),
     "bf_lua_clear": (ctypes.c_int, [_vp]),
     "bf_lua_get_count": (ctypes.c_int, [_vp, _u64p]),
     "bf_lua_set_count": (ctypes.c_int, [_vp, _u64]),
@@ -722,6 +726,37 @@ class LuaFilter:
         out = np.zeros(max(n, 1), np.uint8)
         _lua_check(self._lib.bf_lua_include_many(self.handle, _ptr(keys), _ptr(offsets), n, _ptr(out)), self._h)
         return out[:n]
+
+    # -- device-resident keys (bf_lua_insert_many_dev / bf_lua_include_many_dev): raw device
+    #    addresses and a hipStream_t as ints, as Filter's *_dev methods
+    def insert_many_dev(self, d_keys: int, d_offsets: int, n: int, d_per_key_new: int = 0, stream=0) -> list:
+        """add.lua over n device keys; returns the layers that got a new item."""
+        mask = ctypes.c_uint64()
+        _lua_check(self._lib.bf_lua_insert_many_dev(self.handle, d_keys, d_offsets, int(n), d_per_key_new or None,
+                                                    ctypes.byref(mask), int(stream) or None), self._h)
+        return [i + 1 for i in range(64) if mask.value >> i & 1]
+
+    def include_many_dev(self, d_keys: int, d_offsets: int, n: int, d_out: int, stream=0) -> None:
+        _lua_check(self._lib.bf_lua_include_many_dev(self.handle, d_keys, d_offsets, int(n), d_out,
+                                                     int(stream) or None), self._h)
+
+    def profile(self, enable: bool) -> None:
+        _lua_check(self._lib.bf_lua_profile(self.handle, 1 if enable else 0), self._h)
+
+    def profile_read(self, reset: bool = True) -> dict:
+        """{kernel name: (total ms, launches)} since the last reset (bf_lua_profile_read)."""
+        cap = 64
+        names = ctypes.create_string_buffer(cap * PROFILE_NAME_LEN)
+        ms = np.zeros(cap, np.float64)
+        cnt = np.zeros(cap, np.uint64)
+        n = ctypes.c_uint32()
+        _lua_check(self._lib.bf_lua_profile_read(self.handle, names, _ptr(ms), _ptr(cnt), cap, ctypes.byref(n),
+                                                 1 if reset else 0), self._h)
+        out = {}
+        for i in range(min(n.value, cap)):
+            raw = names.raw[i * PROFILE_NAME_LEN:(i + 1) * PROFILE_NAME_LEN]
+            out[raw.split(b"\0", 1)[0].decode()] = (float(ms[i]), int(cnt[i]))
+        return out
 
     def clear(self) -> None:
         _lua_check(self._lib.bf_lua_clear(self.handle), self._h)

@@ -63,6 +63,17 @@ __global__ __launch_bounds__(kLuaTile) void lua_check_kernel(const BfGeom* __res
         });
 }
 
+// Keys that set a new bit (per-key flags 0/1) summed into *count: the layer count's INCR
+// (add.lua:48-50) without reading the flags back to the host.
+__global__ __launch_bounds__(256) void lua_count_kernel(const uint8_t* __restrict__ flags, uint64_t n,
+                                                        unsigned long long* __restrict__ count) {
+    uint32_t c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) c += flags[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+
 }  // namespace
 
 struct bf_lua {
@@ -85,6 +96,19 @@ struct bf_lua {
     unsigned long long* h_flips = nullptr;   // pinned mirror of d_flips (small calls read it back at once)
     uint64_t flips_cap = 0;
     uint8_t* h_stage = nullptr;              // pinned [offsets | keys] of small calls (one H2D)
+    unsigned long long* d_cnt = nullptr;     // lua_count_kernel's sum (device calls)
+    unsigned long long* h_cnt = nullptr;     // ... read back through pinned memory
+    // calls on different streams (the _dev entry points take the caller's) are ordered: each
+    // waits for the event the previous call recorded, as bf_handle's calls are
+    hipEvent_t order_ev = nullptr;
+    hipStream_t order_stream = nullptr;
+    bool order_valid = false;
+    // bf_lua_profile: HIP events around every kernel, accumulated per name (per layer)
+    bool profile = false;
+    std::vector<BfMarks> prof_pending, prof_free;
+    struct ProfAcc { std::string name; double ms; uint64_t launches; };
+    std::vector<ProfAcc> prof_acc;
+    std::vector<std::string> prof_names;     // "<kernel>[L<layer>]", fixed at create (stable c_str())
     std::string err;
 };
 
@@ -201,6 +225,65 @@ int ensure_io(bf_lua* h, uint64_t key_bytes, uint64_t n) {
     return BF_OK;
 }
 
+// Stream order across calls (bf_api.cpp's StreamOrder): wait for the previous call's event,
+// record this call's at the end.
+struct LuaOrder {
+    bf_lua* h;
+    hipStream_t s;
+    LuaOrder(bf_lua* h_, hipStream_t s_) : h(h_), s(s_) {
+        if (h->order_valid && h->order_stream != s) (void)hipStreamWaitEvent(s, h->order_ev, 0);
+    }
+    ~LuaOrder() {
+        if (h->order_ev && hipEventRecord(h->order_ev, s) == hipSuccess) {
+            h->order_valid = true;
+            h->order_stream = s;
+        }
+    }
+};
+
+enum LuaKern { kLuaCand = 0, kLuaMark = 1, kLuaCheck = 2, kLuaCount = 3, kLuaKerns = 4 };
+const char* const kLuaKernName[kLuaKerns] = {"lua_seq_candidates", "lua_seq_mark", "lua_check", "lua_count"};
+
+const char* lua_prof_name(const bf_lua* h, LuaKern kind, uint32_t layer) {
+    return h->prof_names[(size_t)kind * kLuaMaxLayers + (layer ? layer - 1 : 0)].c_str();
+}
+
+BfMarks* lua_prof_begin(bf_lua* h, hipStream_t s) {
+    if (!h->profile) return nullptr;
+    BfMarks mk{};
+    if (!h->prof_free.empty()) {
+        mk = h->prof_free.back();
+        h->prof_free.pop_back();
+    } else {
+        for (hipEvent_t& e : mk.ev)
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    }
+    mk.used = 0;
+    if (hipEventRecord(mk.ev[0], s) != hipSuccess) {
+        h->prof_free.push_back(mk);
+        return nullptr;
+    }
+    h->prof_pending.push_back(mk);
+    return &h->prof_pending.back();
+}
+
+int lua_prof_harvest(bf_lua* h) {
+    for (BfMarks& mk : h->prof_pending) {
+        if (mk.used > 0) LUACHK(h, hipEventSynchronize(mk.ev[mk.used]));
+        for (int i = 0; i < mk.used; ++i) {
+            float ms = 0.f;
+            LUACHK(h, hipEventElapsedTime(&ms, mk.ev[i], mk.ev[i + 1]));
+            auto it = std::find_if(h->prof_acc.begin(), h->prof_acc.end(),
+                                   [&](const bf_lua::ProfAcc& a) { return a.name == mk.names[i]; });
+            if (it == h->prof_acc.end()) h->prof_acc.push_back({mk.names[i], (double)ms, 1});
+            else { it->ms += ms; it->launches += 1; }
+        }
+        h->prof_free.push_back(mk);
+    }
+    h->prof_pending.clear();
+    return BF_OK;
+}
+
 int ensure_lua_scratch(bf_lua* h, uint64_t bytes) {
     if (bytes <= h->scratch_cap) return BF_OK;
     LUACHK(h, hipStreamSynchronize(h->stream));
@@ -285,13 +368,22 @@ int bf_lua_create(double entries, double precision, const bf_config* cfg, bf_lua
     h->precision = precision;
     LuaDeviceGuard dg(dev);
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void**)&h->d_layers, kLuaMaxLayers * sizeof(BfGeom)) != hipSuccess ||
-        hipMalloc((void**)&h->d_last, 64) != hipSuccess) {
+        hipMalloc((void**)&h->d_last, 64) != hipSuccess || hipMalloc((void**)&h->d_cnt, 64) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_cnt, 64, hipHostMallocDefault) != hipSuccess) {
         if (h->stream) (void)hipStreamDestroy(h->stream);
+        if (h->order_ev) (void)hipEventDestroy(h->order_ev);
         if (h->d_layers) (void)hipFree(h->d_layers);
+        if (h->d_last) (void)hipFree(h->d_last);
+        if (h->d_cnt) (void)hipFree(h->d_cnt);
         delete h;
         return lua_err(nullptr, BF_EDEVICE, "stream / table allocation failed");
     }
+    h->prof_names.reserve((size_t)kLuaKerns * kLuaMaxLayers);
+    for (int kd = 0; kd < kLuaKerns; ++kd)
+        for (uint32_t l = 1; l <= kLuaMaxLayers; ++l)
+            h->prof_names.push_back(std::string(kLuaKernName[kd]) + (kd == kLuaCheck ? "" : "[L" + std::to_string(l) + "]"));
     *out = h;
     return BF_OK;
 }
@@ -304,8 +396,14 @@ int bf_lua_destroy(bf_lua* h) {
         (void)hipStreamSynchronize(h->stream);
         for (BfGeom& g : h->layers) (void)hipFree(g.bits);
         for (void* p : {(void*)h->d_layers, (void*)h->scratch, (void*)h->d_keys, (void*)h->d_out, (void*)h->d_off,
-                        (void*)h->d_last, (void*)h->d_flips})
+                        (void*)h->d_last, (void*)h->d_flips, (void*)h->d_cnt})
             if (p) (void)hipFree(p);
+        for (std::vector<BfMarks>* v : {&h->prof_pending, &h->prof_free})
+            for (BfMarks& mk : *v)
+                for (hipEvent_t e : mk.ev)
+                    if (e) (void)hipEventDestroy(e);
+        if (h->order_ev) (void)hipEventDestroy(h->order_ev);
+        if (h->h_cnt) (void)hipHostFree(h->h_cnt);
         if (h->h_out) (void)hipHostFree(h->h_out);
         if (h->h_flips) (void)hipHostFree(h->h_flips);
         if (h->h_stage) (void)hipHostFree(h->h_stage);
@@ -341,6 +439,7 @@ int bf_lua_clear(bf_lua* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
     LUACHK(h, hipStreamSynchronize(h->stream));
+    if (h->order_valid) LUACHK(h, hipEventSynchronize(h->order_ev));   // a _dev call's stream
     for (BfGeom& g : h->layers) (void)hipFree(g.bits);
     h->layers.clear();
     h->layer_bytes.clear();
@@ -364,6 +463,7 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     if (!offsets || (!keys && offsets[n] != offsets[0])) return lua_err(h, BF_EINVAL, "NULL keys / offsets");
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
+    LuaOrder lo(h, h->stream);
     int rc = stage_keys(h, keys, offsets, n);
     if (rc) return rc;
     unsigned long long* d_flips = nullptr;
@@ -393,7 +493,9 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
         const uint64_t cn = std::min<uint64_t>(n - s, bf_seq_chunk_keys(g.k));
         if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, nullptr)))) return rc;
         // which keys would set a new bit of this layer, in order (nothing applied yet)
+        BfMarks* mk = lua_prof_begin(h, h->stream);
         LUACHK(h, bf_launch_seq_candidates(g, 1, h->d_keys, h->d_off + s, 0, cn, h->scratch, h->stream));
+        bf_mark(mk, h->stream, lua_prof_name(h, kLuaCand, layer));
         BfGeom ga = g;
         if (d_flips) {
             ga.flips = d_flips + 1;
@@ -407,6 +509,7 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
             // no key of the chunk can fill the layer before the last one: flags and apply in ONE
             // mark pass, one sync (the per-key insert's case)
             LUACHK(h, bf_launch_seq_mark(ga, 1, cn, cn, h->scratch, h->d_out, nullptr, h->stream));
+            bf_mark(mk, h->stream, lua_prof_name(h, kLuaMark, layer));
             LUACHK(h, hipMemcpyAsync(h->h_out, h->d_out, cn, hipMemcpyDeviceToHost, h->stream));
             if (d_flips && small_flips)
                 LUACHK(h, hipMemcpyAsync(h->h_flips, d_flips, (cap + 1) * 8, hipMemcpyDeviceToHost, h->stream));
@@ -415,6 +518,7 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
             for (uint64_t j = 0; j < cn; ++j) fresh += h->h_out[j];
         } else {
             LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, h->d_out, nullptr, h->stream));
+            bf_mark(mk, h->stream, lua_prof_name(h, kLuaMark, layer));
             LUACHK(h, hipMemcpyAsync(h->h_out, h->d_out, cn, hipMemcpyDeviceToHost, h->stream));
             LUACHK(h, hipStreamSynchronize(h->stream));
             // cut after the key whose INCR fills the layer (add.lua:48-50); later keys go up a layer
@@ -425,7 +529,9 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
                     break;
                 }
             }
+            mk = lua_prof_begin(h, h->stream);
             LUACHK(h, bf_launch_seq_mark(ga, 1, cn, take, h->scratch, nullptr, nullptr, h->stream));
+            bf_mark(mk, h->stream, lua_prof_name(h, kLuaMark, layer));
         }
         if (per_key_new) memcpy(per_key_new + s, h->h_out, take);
         if (fresh && new_layers && layer <= 64) *new_layers |= 1ull << (layer - 1);
@@ -451,9 +557,150 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     return BF_OK;
 }
 
+// Layers up to n exist, and the caller's stream sees a new layer's clear (ensure_layer
+// clears on the handle's own stream).
+int ensure_layer_on(bf_lua* h, uint32_t n, hipStream_t s) {
+    const size_t had = h->layers.size();
+    int rc = ensure_layer(h, n);
+    if (rc) return rc;
+    if (h->layers.size() != had && s != h->stream) LUACHK(h, hipStreamSynchronize(h->stream));
+    return BF_OK;
+}
+
+// bf_lua_insert_many on device-resident keys (the caller's stream): add.lua's sequential
+// semantics exactly as lua_insert, with the per-key flags left on the device and the count's
+// INCRs summed there (lua_count_kernel); the host reads 8 bytes per chunk to pick the next
+// layer, or — only for the chunk that fills a layer — the chunk's flags to find the cut.
+int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, uint64_t n, uint8_t* d_per_key_new,
+                   uint64_t* new_layers, hipStream_t s) {
+    if (new_layers) *new_layers = 0;
+    if (n == 0) return BF_OK;
+    if (!d_keys || !d_offsets) return lua_err(h, BF_EINVAL, "NULL device pointer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    LuaOrder lo(h, s);
+    uint64_t bias = 0;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d_keys);
+    bias = a & 15u;
+    const uint8_t* k16 = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
+    int rc = ensure_io(h, 0, std::min<uint64_t>(n, bf_seq_chunk_keys(1)));   // d_out / h_out for one chunk
+    if (rc) return rc;
+    uint64_t done = 0;
+    while (done < n) {
+        const uint32_t layer = lua_index(h->entries, (double)(h->count + 1));   // add.lua:6-15
+        if ((rc = ensure_layer_on(h, layer, s))) return rc;
+        const BfGeom& g = h->layers[layer - 1];
+        const uint64_t room = lua_layer_capacity(h->entries, layer, h->count + 1) - h->count;   // >= 1
+        const uint64_t cn = std::min<uint64_t>(n - done, bf_seq_chunk_keys(g.k));
+        if ((rc = ensure_io(h, 0, cn))) return rc;
+        if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, nullptr)))) return rc;
+        uint8_t* flags = d_per_key_new ? d_per_key_new + done : h->d_out;
+        BfMarks* mk = lua_prof_begin(h, s);
+        LUACHK(h, bf_launch_seq_candidates(g, 1, k16, d_offsets + done, bias, cn, h->scratch, s));
+        bf_mark(mk, s, lua_prof_name(h, kLuaCand, layer));
+        uint64_t take = cn, fresh = 0;
+        if (room >= cn) {   // the whole chunk lands in this layer: flags and apply in one pass
+            LUACHK(h, bf_launch_seq_mark(g, 1, cn, cn, h->scratch, flags, nullptr, s));
+            bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
+            LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 8, s));
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn + 255) / 256, 1024);
+            hipLaunchKernelGGL(lua_count_kernel, dim3(grid), dim3(256), 0, s, flags, cn, h->d_cnt);
+            LUACHK(h, hipGetLastError());
+            bf_mark(mk, s, lua_prof_name(h, kLuaCount, layer));
+            LUACHK(h, hipMemcpyAsync(h->h_cnt, h->d_cnt, 8, hipMemcpyDeviceToHost, s));
+            LUACHK(h, hipStreamSynchronize(s));
+            fresh = h->h_cnt[0];
+        } else {   // the chunk that fills the layer: cut after the key whose INCR fills it (add.lua:48-50)
+            LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, flags, nullptr, s));
+            bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
+            LUACHK(h, hipMemcpyAsync(h->h_out, flags, cn, hipMemcpyDeviceToHost, s));
+            LUACHK(h, hipStreamSynchronize(s));
+            for (uint64_t j = 0; j < cn; ++j) {
+                fresh += h->h_out[j];
+                if (fresh == room) {
+                    take = j + 1;
+                    break;
+                }
+            }
+            mk = lua_prof_begin(h, s);
+            LUACHK(h, bf_launch_seq_mark(g, 1, cn, take, h->scratch, nullptr, nullptr, s));
+            bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
+        }
+        if (fresh && new_layers && layer <= 64) *new_layers |= 1ull << (layer - 1);
+        h->count += fresh;
+        done += take;
+    }
+    return BF_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int bf_lua_insert_many_dev(bf_lua* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                           uint8_t* d_per_key_new, uint64_t* new_layers, void* stream) {
+    if (!h) return BF_EINVAL;
+    return lua_insert_dev(h, d_key_bytes, d_offsets, n, d_per_key_new, new_layers,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+int bf_lua_include_many_dev(bf_lua* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
+                            uint8_t* d_out, void* stream) {
+    if (!h) return BF_EINVAL;
+    if (n == 0) return BF_OK;
+    if (!d_key_bytes || !d_offsets || !d_out) return lua_err(h, BF_EINVAL, "NULL device pointer");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    LuaOrder lo(h, s);
+    if (h->count == 0) {   // check.lua:3-7
+        LUACHK(h, hipMemsetAsync(d_out, 0, n, s));
+        return BF_OK;
+    }
+    const uint32_t index = lua_index(h->entries, (double)h->count);   // check.lua:9-11
+    int rc = ensure_layer_on(h, index, s);
+    if (rc) return rc;
+    if (h->d_layers_n < index) {   // the table is pageable host memory: the copy completes on return
+        LUACHK(h, hipMemcpyAsync(h->d_layers, h->layers.data(), index * sizeof(BfGeom), hipMemcpyHostToDevice, s));
+        LUACHK(h, hipStreamSynchronize(s));
+        h->d_layers_n = index;
+    }
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d_key_bytes);
+    BfMarks* mk = lua_prof_begin(h, s);
+    hipLaunchKernelGGL(lua_check_kernel, dim3((uint32_t)((n + kLuaTile - 1) / kLuaTile)), dim3(kLuaTile), 0, s,
+                       h->d_layers, index, reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15), d_offsets,
+                       (uint64_t)(a & 15u), n, d_out);
+    LUACHK(h, hipGetLastError());
+    bf_mark(mk, s, lua_prof_name(h, kLuaCheck, index));
+    return BF_OK;
+}
+
+int bf_lua_profile(bf_lua* h, uint32_t enable) {
+    if (!h) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    int rc = lua_prof_harvest(h);
+    h->profile = enable != 0;
+    return rc;
+}
+
+int bf_lua_profile_read(bf_lua* h, char* names, double* total_ms, uint64_t* launches, uint32_t cap,
+                        uint32_t* n_out, uint32_t reset) {
+    if (!h || !n_out) return BF_EINVAL;
+    std::lock_guard<std::mutex> lk(h->mu);
+    LuaDeviceGuard dg(h->device);
+    int rc = lua_prof_harvest(h);
+    if (rc) return rc;
+    *n_out = (uint32_t)h->prof_acc.size();
+    for (uint32_t i = 0; i < cap && i < h->prof_acc.size(); ++i) {
+        const bf_lua::ProfAcc& acc = h->prof_acc[i];
+        if (names) snprintf(names + (size_t)i * BF_PROFILE_NAME_LEN, BF_PROFILE_NAME_LEN, "%s", acc.name.c_str());
+        if (total_ms) total_ms[i] = acc.ms;
+        if (launches) launches[i] = acc.launches;
+    }
+    if (reset) h->prof_acc.clear();
+    return BF_OK;
+}
 
 int bf_lua_insert_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* per_key_new,
                        uint64_t* new_layers) {
@@ -478,6 +725,7 @@ int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets,
         return BF_OK;
     }
     LuaDeviceGuard dg(h->device);
+    LuaOrder lo(h, h->stream);
     const uint32_t index = lua_index(h->entries, (double)h->count);   // check.lua:9-11
     int rc = ensure_layer(h, index);
     if (rc) return rc;
@@ -487,9 +735,11 @@ int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets,
                                  h->stream));
         h->d_layers_n = index;
     }
+    BfMarks* mk = lua_prof_begin(h, h->stream);
     hipLaunchKernelGGL(lua_check_kernel, dim3((uint32_t)((n + kLuaTile - 1) / kLuaTile)), dim3(kLuaTile), 0,
                        h->stream, h->d_layers, index, h->d_keys, h->d_off, (uint64_t)0, n, h->d_out);
     LUACHK(h, hipGetLastError());
+    bf_mark(mk, h->stream, lua_prof_name(h, kLuaCheck, index));
     LUACHK(h, hipMemcpyAsync(out, h->d_out, n, hipMemcpyDeviceToHost, h->stream));
     LUACHK(h, hipStreamSynchronize(h->stream));
     return BF_OK;
@@ -501,6 +751,7 @@ int bf_lua_export_layer(bf_lua* h, uint32_t layer, uint8_t* buf, uint64_t cap, u
     *len_out = 0;
     if (layer == 0 || layer > h->layers.size()) return BF_OK;   // a layer never written: absent key
     LuaDeviceGuard dg(h->device);
+    LuaOrder lo(h, h->stream);
     const BfGeom& g = h->layers[layer - 1];
     LUACHK(h, hipMemsetAsync(h->d_last, 0, 8, h->stream));
     LUACHK(h, bf_launch_last_nonzero(g.bits, h->layer_bytes[layer - 1] / 4, h->d_last, h->stream));
@@ -526,6 +777,7 @@ int bf_lua_import_layer(bf_lua* h, uint32_t layer, const uint8_t* buf, uint64_t 
     if (!h || (len && !buf)) return BF_EINVAL;
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
+    LuaOrder lo(h, h->stream);
     int rc = ensure_layer(h, layer);
     if (rc) return rc;
     const BfGeom& g = h->layers[layer - 1];

@@ -58,6 +58,54 @@ def test_lua_insert_include_match_scripts(pkg, entries, precision, nkeys, span, 
         assert got[: nkeys // 2].all()
 
 
+@pytest.mark.parametrize("entries,precision,nkeys,span,batches", [
+    (100, 0.01, 900, 700, 3),          # repeats, layer cuts inside a batch
+    (1000, 0.02, 5000, 10**9, 1),      # distinct keys, 3 layers in one call
+    (10_000, 0.001, 100_000, 10**12, 2),
+])
+def test_lua_device_entry_points_match_scripts(pkg, entries, precision, nkeys, span, batches):
+    """bf_lua_insert_many_dev / bf_lua_include_many_dev (device keys, the caller's stream, flags
+    and answers left on the device, the INCRs summed on the device) against the scripts: the
+    same per-key INCR flags, count, layer strings and include? answers; per-layer kernel times
+    from bf_lua_profile."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(13)
+    keys = [int(v) for v in rng.integers(0, span, nkeys)]
+    r, want_flags = script_run(pkg, keys, entries, precision)
+    cuts = np.linspace(0, nkeys, batches + 1).astype(int)
+    st = torch.cuda.current_stream().cuda_stream
+    got_flags = []
+    with pkg.LuaFilter(entries, precision) as f:
+        f.profile(True)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            buf, offs = pkg.keys.pack(keys[a:b])
+            kb = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).cuda()
+            ko = torch.from_numpy(offs.view(np.int64)).cuda()
+            flags = torch.zeros(b - a, dtype=torch.uint8, device="cuda")
+            f.insert_many_dev(kb.data_ptr(), ko.data_ptr(), b - a, flags.data_ptr(), stream=st)
+            got_flags.append(flags.cpu().numpy().astype(bool))
+        np.testing.assert_array_equal(np.concatenate(got_flags), want_flags)
+        assert f.count == int(r.get("lbf:count"))
+        want_layers = layers_of(r, "lbf")
+        assert f.layers == len(want_layers) and len(want_layers) >= 2
+        for n, s in want_layers.items():
+            assert f.export_layer(n) == s, n
+        probe = keys[: nkeys // 2] + ["fresh-%d" % i for i in range(nkeys // 2)]
+        pb, po = pkg.keys.pack(probe)
+        # an odd device address: the kernels realign the key bytes
+        kb = torch.zeros(len(pb) + 19, dtype=torch.uint8, device="cuda")
+        kb[3: 3 + len(pb)] = torch.from_numpy(pb).cuda()
+        ko = torch.from_numpy(po.view(np.int64)).cuda()
+        out = torch.empty(len(probe), dtype=torch.uint8, device="cuda")
+        f.include_many_dev(kb.data_ptr() + 3, ko.data_ptr(), len(probe), out.data_ptr(), stream=st)
+        got = out.cpu().numpy().astype(bool)
+        want = np.array([L.check(r, "lbf", entries, precision, k) for k in probe])
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(got, f.include_many(pb, po).astype(bool))   # = the host path
+        prof = f.profile_read()
+        assert "lua_check" in prof and "lua_seq_candidates[L1]" in prof and "lua_seq_mark[L2]" in prof
+
+
 def test_hip_lua_driver_write_through_and_interop(pkg):
     """The driver's Redis keys equal the scripts' after the same inserts (lua.rb layout), a
     driver attached to the scripts' Redis answers like check.lua, and clear drops name:*."""

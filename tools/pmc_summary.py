@@ -25,6 +25,8 @@ KERNELS = {
     "bf_keys_kernel<INSERT_FLAGS>": re.compile(r"bf_keys_kernel<3>"),
     "bf_include_hash_kernel": re.compile(r"bf_include_hash_kernel"),
     "bf_keys_kernel<HASH>": re.compile(r"bf_keys_kernel<5>"),
+    "digest_kernel<INCLUDE>": re.compile(r"bf_digest_kernel<1>"),
+    "digest_kernel<INSERT>": re.compile(r"bf_digest_kernel<2>"),
     "bin_front": re.compile(r"bin_front_kernel<false>"),
     "bin_front_digest": re.compile(r"bin_front_kernel<true>"),
     "bin_front_wide": re.compile(r"bin_front_wide_(dig_)?kernel"),
@@ -32,7 +34,7 @@ KERNELS = {
     "bin_apply": re.compile(r"bin_apply_(pipe_)?kernel"),
     "bin_test": re.compile(r"bin_test_kernel"),
 }
-FULL_BATCH = ("bf_keys_kernel",)   # grid = one lane per key: keep full-batch launches only
+FULL_BATCH = ("bf_keys_kernel", "digest_kernel")   # grid = one lane per key: keep full-batch launches only
 
 
 def load(dirs, batch):
