@@ -51,6 +51,11 @@ FILL_CEILING = 55.1e9      # fills/s, plain loads, 1143 MiB working set
 FILL_CEILING_7GB = 50.2e9
 
 
+# ... and 258 G/s over a 2 MiB working set (L2-resident: the Lua layout's 1.38 MB first layer at
+# 1M@1 %, profiles/r02z_probe_sweep.log line 1)
+FILL_CEILING_L2 = 258.4e9
+
+
 def fill_ceiling(bitset_bytes: int):
     """The measured random-fill ceiling for a bitset of this size, and its source."""
     if bitset_bytes > (2 << 30):
@@ -166,6 +171,70 @@ def make_batches(n_filter: int, batch: int, rank: int, count: int, dev):
         inc = torch.cat([ins[: batch // 2], fresh])
         out.append((pack_decimal_dev(ins), pack_decimal_dev(inc)))
     return out
+
+
+def lua_config(pkg, D: Dist, reps: int = 5, entries: int = 10**6, precision: float = 0.01, batch: int = 1 << 20):
+    """SURVEY §8 f1 on the device at the README's 1M scale (README.md:84-87 quotes the lua driver
+    at 1M items): the scalable layout of lua.rb / add.lua / check.lua for entries = 1M,
+    precision = 1 % (layer 1: 11,028,238 bits = 1.38 MB, k = 7), device-resident keys.  One rep
+    = a fresh filter, bf_lua_insert_many_dev of 2^20 keys (decimal strings of uniform ints in
+    [0, 1M): the bf_100_000_flat.rb shape at 1M) with add.lua's sequential semantics, then
+    bf_lua_include_many_dev of 2^20 keys (half that batch, half fresh).  The insert returns once
+    the count is known (the layer choice needs it); the timing brackets both calls with a device
+    sync.  Median of `reps` reps after one warm-up rep; kernel times per layer by bf_lua_profile."""
+    dev = torch.device("cuda", D.local)
+    batches = make_batches(entries, batch, D.rank, reps + 1, dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    out = torch.empty(batch, dtype=torch.uint8, device=dev)
+    flags = torch.empty(batch, dtype=torch.uint8, device=dev)
+    f = pkg.LuaFilter(entries, precision, device=D.local)
+    t_ins, t_inc, counts, layers = [], [], [], []
+    for i, ((ikb, iko), (pkb, pko)) in enumerate(batches):
+        f.clear()
+        if i == 1:
+            f.profile(True)
+            f.profile_read(reset=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        f.insert_many_dev(ikb.data_ptr(), iko.data_ptr(), batch, flags.data_ptr(), stream=st)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        f.include_many_dev(pkb.data_ptr(), pko.data_ptr(), batch, out.data_ptr(), stream=st)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        assert bool(out[: batch // 2].all().item()), "lua_1m: an inserted key answered false"
+        if i:
+            t_ins.append(t1 - t0)
+            t_inc.append(t2 - t1)
+            counts.append(f.count)
+            layers.append(f.layers)
+    prof = f.profile_read(reset=True)
+    f.profile(False)
+    fp = float(out[batch // 2:].float().mean().item())
+    f.close()
+    ti, tc = sorted(t_ins)[len(t_ins) // 2], sorted(t_inc)[len(t_inc) // 2]
+    bits1, k1 = pkg._lib.lua_layer_params(entries, precision, 1)
+    # check.lua's probes (layer 1 only while count <= entries): members all k, non-members up to
+    # their first 0 bit (density d = fp^(1/k) from the batch's observed false-positive rate)
+    d = fp ** (1.0 / k1) if fp > 0 else 0.0
+    per_key = 0.5 * k1 + 0.5 * ((1 - fp) / (1 - d) if d < 1 else k1)
+    kern = {nm: {"ms": tot / cnt, "launches": cnt} for nm, (tot, cnt) in prof.items()}
+    chk = kern.get("lua_check")
+    return {"keys_per_s": 2 * batch / (ti + tc), "insert_keys_per_s": batch / ti, "include_keys_per_s": batch / tc,
+            "insert_ms": ti * 1e3, "include_ms": tc * 1e3, "batch": batch, "entries": entries,
+            "precision": precision, "count_after_insert": int(np.median(counts)), "layers": int(max(layers)),
+            "layer1_bits": bits1, "layer1_k": k1, "layer1_bytes": (bits1 + 7) // 8,
+            "kernels": {nm: round(v["ms"], 4) for nm, v in kern.items()},
+            "include_fills": {"fills_per_key": per_key, "observed_fp_rate": fp,
+                              "fills_per_s": batch * per_key / (chk["ms"] / 1e3) if chk else None,
+                              "ceiling_fills_per_s": FILL_CEILING_L2,
+                              "frac": batch * per_key / (chk["ms"] / 1e3) / FILL_CEILING_L2 if chk else None,
+                              "ceiling_source": "tools/probe_granularity.hip sweep, 2 MiB working set "
+                                                "(profiles/r02z_probe_sweep.log): the 1.38 MB layer is "
+                                                "L2-resident, so SHA-1 (VALU), not fills, bounds it"},
+            "timing": "median of %d reps, each on a fresh filter, wall time of each device call incl. its "
+                      "syncs (the insert reads the count back per chunk)" % len(t_ins),
+            "pmc": load_pmc("lua_1m")}
 
 
 def to_host(kb: torch.Tensor, ko: torch.Tensor):
@@ -860,6 +929,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="nstar", choices=sorted(CONFIGS))
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--secondary", default="1m,1m_big,100m,10b,lua_1m",
+                    help="comma list of the secondary workloads (1-GPU runs): configs and lua_1m")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
     ap.add_argument("--no-reference-shapes", action="store_true",
@@ -910,8 +981,10 @@ def main():
         # batches are launch- and latency-bound)
         # every secondary runs the step `--config <name>` runs (pipelined unless --pipeline 0),
         # so the driver's line carries the same numbers a --config run reports
-        for name in ("1m", "1m_big", "100m", "10b"):
-            if name != args.config:
+        for name in [x for x in args.secondary.split(",") if x]:
+            if name == "lua_1m":   # SURVEY §8 f1, the Lua layout on the device
+                secondary[name] = lua_config(pkg, D)
+            elif name != args.config:
                 r, _ = time_config(pkg, D, name, max(3, args.steps // 2), 1, pipeline=bool(args.pipeline))
                 secondary[name] = {"keys_per_s": r["keys_per_s"], "pipelined": r["pipelined"],
                                    "ms_per_step": r["wall_s"] / r["steps"] * 1e3,

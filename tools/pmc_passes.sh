@@ -8,10 +8,16 @@ export TMPDIR=/tmp
 CONFIG=${1:-nstar}
 TAG=${2:-$CONFIG}
 if [ $# -gt 2 ]; then shift 2; PASSES="$*"; else PASSES="rd wr dram valu"; fi
+# lua_1m: the Lua layout's secondary alone (bench.py lua_config), behind the tiny 10k config
+if [ "$CONFIG" = lua_1m ]; then
+    BENCH_ARGS="--config 10k --secondary lua_1m --steps 3 --warmup 1"
+else
+    BENCH_ARGS="--config $CONFIG --steps 3 --warmup 1 --no-secondary"
+fi
 run() {   # pass, counters...
     local pass=$1; shift
     timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_${TAG}_${pass} -o run -- \
-        python bench.py --config $CONFIG --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes \
+        python bench.py $BENCH_ARGS --no-cpu-baseline --no-host-api --no-reference-shapes \
         > gpurun_out/pmc_${TAG}_${pass}.log 2>&1
 }
 for p in $PASSES; do

@@ -33,6 +33,10 @@ KERNELS = {
     "bin_mid": re.compile(r"bin_mid_kernel"),
     "bin_apply": re.compile(r"bin_apply_(pipe_)?kernel"),
     "bin_test": re.compile(r"bin_test_kernel"),
+    # the Lua layout (bf_lua.hip, bench.py lua_config)
+    "lua_check": re.compile(r"lua_check_kernel"),
+    "lua_seq_candidates": re.compile(r"seq_candidates_kernel"),
+    "lua_seq_mark": re.compile(r"seq_mark_kernel"),
 }
 FULL_BATCH = ("bf_keys_kernel", "digest_kernel")   # grid = one lane per key: keep full-batch launches only
 
