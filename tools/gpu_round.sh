@@ -5,6 +5,7 @@
 #   parity     the parity files alone: parity, distributed primitives, digests, region sets
 #   sets       region-set tests + the replicated / region-set multi-rank gloo cases
 #   edge       the forced-binned edge cases at every region size (test_binned_edge_cases)
+#   lua        the Lua layout's GPU tests (host and device entry points)
 #   smoke      __graft_entry__.smoke()
 #   bench      the driver's bench command (--gpus 1 --steps 20 --warmup 5)
 #   bench10b / bench200b / bench100m   the other single-GPU configs
@@ -53,6 +54,7 @@ for st in $STEPS; do
                     > gpurun_out/tests_${TAG}_sets.log 2>&1 ;;
         edge)   timeout -k 10 500 $PYT tests/test_gpu_parity.py -k binned_edge \
                     > gpurun_out/tests_${TAG}_edge.log 2>&1 ;;
+        lua)    timeout -k 10 300 $PYT tests/test_gpu_lua.py > gpurun_out/tests_${TAG}_lua.log 2>&1 ;;
         smoke)  timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
         bench)  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
                     > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
