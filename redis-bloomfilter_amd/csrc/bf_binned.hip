@@ -2962,6 +2962,258 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     }
     if (any_flag) report_any_new(any_flag, fresh != 0);
 }
+
+// sets_apply_kernel, persistent and software-pipelined (one 1024-lane workgroup per CU walking
+// regions r, r + G, ...), for batches dense enough to rewrite every region (VERDICT r04 item
+// 4).  The one-shot kernel pays, per region, two dependent round trips (the per-source headers,
+// then the sets' words) before it can decode, and at the 10B filter decodes every offset's low
+// bits with a dependent global load (16 KB of them do not fit its 15 KB stage at two workgroups
+// per CU).  Here, while region r is decoded from LDS, region r + G's set words (the first UPL
+// upper-bitmap words and up to LPL low-bit words per lane) and its 64 KB of bitset vectors are
+// already in flight in registers, and r + 2G's headers too; r's low bits were staged into LDS
+// (LPL x LANES words, 24 KB) at the top of its iteration.  Region r + G's source tables (place,
+// header, the three per-source prefixes) are built into the second of two LDS table buffers.
+// The prefetch loads are unconditional (a clamped stand-in address past the data), so the
+// compiler's in-order vmcnt waits leave them outstanding while r decodes.  Words beyond the
+// prefetch (more than UPL x LANES upper words, or low bits past the stage) and bitmap sets are
+// read on the spot, as the one-shot kernel does.  Results are the one-shot kernel's, bit for
+// bit (tests/test_gpu_region_sets.py runs both).
+template <uint32_t RLOG2, uint32_t LANES, uint32_t UPL, uint32_t LPL>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) void sets_apply_pipe_kernel(
+    uint32_t* __restrict__ bits, uint64_t nwords, const uint32_t* __restrict__ sets, uint64_t stride_words,
+    uint32_t nsrc, uint32_t nbins, uint32_t dense, uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
+    uint32_t store_fresh, uint32_t* __restrict__ status) {
+    constexpr uint32_t kVec = 1u << (RLOG2 - 7);
+    constexpr uint32_t kPer = kVec / LANES;
+    constexpr uint32_t U = 1u << RLOG2, NW = U / 32;
+    constexpr uint32_t kStage = LPL * LANES;
+    static_assert(kPer * LANES == kVec, "region must tile the workgroup");
+    __shared__ uint4 s_mask4[kVec];
+    __shared__ uint32_t s_lows[kStage + 1];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_st[2][kMaxSetSrc], s_hdr[2][kMaxSetSrc];
+    __shared__ uint32_t s_uw0[2][kMaxSetSrc + 1], s_np[2][kMaxSetSrc + 1], s_lw0[2][kMaxSetSrc + 1];
+    __shared__ uint32_t s_ok;
+    uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
+    const uint32_t t = threadIdx.x;
+    const uint32_t G = gridDim.x;
+    const uint64_t nvec = nwords / 4;
+    uint4* gv = reinterpret_cast<uint4*>(bits);
+    if (blockIdx.x >= nbins) return;   // workgroup-uniform
+    const uint32_t last = blockIdx.x + (nbins - 1 - blockIdx.x) / G * G;
+    auto clampr = [&](uint32_t q) { return q < last ? q : last; };
+
+    // which sources' buffers match this filter (one header check per workgroup)
+    if (t == 0) s_ok = 0;
+    for (uint32_t v = t; v < kVec; v += LANES) s_mask4[v] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (t < nsrc) {
+        const uint32_t* S = sets + (uint64_t)t * stride_words;
+        const bool ok = S[0] == kSetsMagic && S[1] == RLOG2 && S[2] == nbins && S[3] >= sets_first_word(nbins) &&
+                        S[3] <= stride_words;
+        if (ok) atomicOr(&s_ok, 1u << t);
+        else if (status) atomicOr(status, 1u);
+    }
+    __syncthreads();
+    const uint32_t okmask = s_ok;
+    const bool my_ok = t < nsrc && ((okmask >> t) & 1u);
+    const uint32_t* mine = sets + (uint64_t)(t < nsrc ? t : 0) * stride_words;
+
+    // region q's place and header of source t (lanes t < nsrc)
+    auto load_hdr = [&](uint32_t q, uint32_t& st, uint32_t& hdr) {
+        st = hdr = 0;
+        if (my_ok) {
+            st = mine[kSetsHdr + q];
+            hdr = mine[kSetsHdr + nbins + q];
+        }
+    };
+    // the tables of a region into buffer bi: damaged entries dropped (and flagged), the
+    // per-source prefixes of upper words, offsets and low-bit words.  Contains a barrier.
+    auto tables = [&](uint32_t bi, uint32_t st, uint32_t hdr) {
+        if (t < 64) {
+            if (t < nsrc && st) {
+                const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
+                const bool shape = n && n <= U && (l == kSetsBitmap || l <= RLOG2);
+                const uint64_t need = !shape ? 0 : 1ull + (l == kSetsBitmap ? NW : (n * l + 31u) / 32u +
+                                                                                 (n + (U >> l) + 31u) / 32u);
+                if (!shape || (uint64_t)st + need > stride_words) {
+                    st = hdr = 0;
+                    if (status) atomicOr(status, 1u);
+                }
+            }
+            if (t >= nsrc) st = hdr = 0;
+            const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
+            const bool ef = st && l != kSetsBitmap;
+            const uint32_t ua = ef ? (n + (U >> l) + 31u) / 32u : 0u, nn = ef ? n : 0u,
+                           ll = ef ? (n * l + 31u) / 32u : 0u;
+            const uint32_t ia = wave_incl_scan(ua), in = wave_incl_scan(nn), il = wave_incl_scan(ll);
+            if (t < nsrc) {
+                s_st[bi][t] = st;
+                s_hdr[bi][t] = hdr;
+            }
+            if (t <= nsrc) {
+                s_uw0[bi][t] = ia - ua;
+                s_np[bi][t] = in - nn;
+                s_lw0[bi][t] = il - ll;
+            }
+        }
+        __syncthreads();
+    };
+    // the last source whose start in table `starts` is <= q (four dependent LDS reads)
+    auto source_of = [&](const uint32_t* starts, uint32_t q) {
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t stp = kMaxSetSrc / 2; stp; stp >>= 1)
+            if (s + stp < nsrc && starts[s + stp] <= q) s += stp;
+        return s;
+    };
+    // address of upper-bitmap word g / low-bit word q of the region in table bi (a stand-in,
+    // the buffer's first word, past the region's words: every prefetch issues)
+    auto upper_addr = [&](uint32_t bi, uint32_t g) -> const uint32_t* {
+        if (g >= s_uw0[bi][nsrc]) return sets;
+        const uint32_t s = source_of(s_uw0[bi], g);
+        const uint32_t n = s_hdr[bi][s] & 0xFFFFFFu, l = s_hdr[bi][s] >> 24;
+        return sets + (uint64_t)s * stride_words + s_st[bi][s] + 1 + (n * l + 31u) / 32u + (g - s_uw0[bi][s]);
+    };
+    auto lows_addr = [&](uint32_t bi, uint32_t q) -> const uint32_t* {
+        if (q >= s_lw0[bi][nsrc]) return sets;
+        const uint32_t s = source_of(s_lw0[bi], q);
+        return sets + (uint64_t)s * stride_words + s_st[bi][s] + 1 + (q - s_lw0[bi][s]);
+    };
+    auto load_words = [&](uint32_t bi, uint32_t* uw, uint32_t* lo) {
+#pragma unroll
+        for (uint32_t p = 0; p < UPL; ++p) uw[p] = *upper_addr(bi, p * LANES + t);
+#pragma unroll
+        for (uint32_t j = 0; j < LPL; ++j) lo[j] = *lows_addr(bi, j * LANES + t);
+    };
+    auto load_vecs = [&](uint32_t q, uint4* vo) {
+        const uint64_t v0 = (uint64_t)q * kVec;
+#pragma unroll
+        for (uint32_t c = 0; c < kPer; ++c) {
+            const uint64_t v = v0 + c * LANES + t;
+            vo[c] = apply_load(gv + (v < nvec ? v : nvec - 1));
+        }
+    };
+
+    uint32_t fresh = 0;
+    // Region r (tables in buffer bi, its vectors cur, words uw / lo in registers), r + G's
+    // headers (hst, hhd) loaded.  Issues r + G's words / vectors into (nuw, nlo, nxt) and r + 2G's
+    // headers into (nst, nhd).
+    auto region = [&](uint32_t r, uint32_t bi, const uint4* cur, const uint32_t* uw, const uint32_t* lo,
+                      uint32_t hst, uint32_t hhd, uint4* nxt, uint32_t* nuw, uint32_t* nlo, uint32_t& nst,
+                      uint32_t& nhd) {
+        // r's low bits into the stage (the previous region's decode ended on a barrier)
+        const uint32_t TL = s_lw0[bi][nsrc];
+        const bool staged = TL <= kStage;   // workgroup-uniform
+        if (staged) {
+#pragma unroll
+            for (uint32_t j = 0; j < LPL; ++j) s_lows[j * LANES + t] = lo[j];
+            if (t == 0) s_lows[TL] = 0;   // read past the last source's lows, masked off
+        }
+        // r + G's tables (their barrier also publishes the stage), then its prefetches
+        const uint32_t rn = clampr(r + G);
+        tables(bi ^ 1u, hst, hhd);
+        load_hdr(clampr(r + 2 * G), nst, nhd);
+        load_words(bi ^ 1u, nuw, nlo);
+        load_vecs(rn, nxt);
+        // decode r: bitmap sets word by word (rare: read on the spot)
+        for (uint32_t s = 0; s < nsrc; ++s) {
+            if (!s_st[bi][s] || (s_hdr[bi][s] >> 24) != kSetsBitmap) continue;   // workgroup-uniform
+            const uint32_t* B = sets + (uint64_t)s * stride_words + s_st[bi][s] + 1;
+            for (uint32_t v = t; v < NW; v += LANES) {
+                const uint32_t x = B[v];
+                if (x) atomicOr(s_mask + v, x);
+            }
+        }
+        // Elias-Fano sets: one pass of LANES upper words at a time over all sources (the first
+        // UPL passes' words prefetched, any further ones read on the spot)
+        const uint32_t TW = s_uw0[bi][nsrc];
+        uint32_t carry = 0;
+        for (uint32_t p = 0; p * LANES < TW; ++p) {   // workgroup-uniform trip count
+            const uint32_t g = p * LANES + t;
+            uint32_t word = 0;
+            if (g < TW) {
+                if (p < UPL) {
+#pragma unroll
+                    for (uint32_t q = 0; q < UPL; ++q)
+                        if (p == q) word = uw[q];
+                } else {
+                    word = *upper_addr(bi, g);
+                }
+            }
+            uint32_t tot;
+            const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);
+            if (word) {
+                const uint32_t s = source_of(s_uw0[bi], g);
+                const uint32_t n = s_hdr[bi][s] & 0xFFFFFFu, l = s_hdr[bi][s] >> 24;
+                const uint32_t* lows = sets + (uint64_t)s * stride_words + s_st[bi][s] + 1;
+                const uint32_t* slows = s_lows + s_lw0[bi][s];
+                const uint32_t lmask = (1u << l) - 1u;
+                uint32_t i = carry + pre - s_np[bi][s];   // rank of this word's first offset in its set
+                const uint32_t p0 = (g - s_uw0[bi][s]) * 32u;
+                const uint32_t lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
+                while (word) {
+                    const uint32_t pp = p0 + (uint32_t)__builtin_ctz(word);
+                    word &= word - 1u;
+                    uint32_t lo_ = 0;
+                    if (l) {
+                        const uint32_t bp = i * l, wi = bp >> 5;
+                        uint32_t a, b;
+                        if (staged) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
+                            a = slows[min(wi, lim)];
+                            b = slows[min(wi, lim) + 1u];
+                        } else {
+                            a = lows[min(wi, lim)];
+                            b = lows[min(wi + 1u, lim)];
+                        }
+                        lo_ = (uint32_t)(((uint64_t)b << 32 | a) >> (bp & 31u)) & lmask;
+                    }
+                    const uint32_t x = ((pp - i) << l) | lo_;
+                    if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
+                    ++i;
+                }
+            }
+            carry += tot;
+        }
+        __syncthreads();   // the image is complete
+        const uint64_t v0 = (uint64_t)r * kVec;
+#pragma unroll
+        for (uint32_t c = 0; c < kPer; ++c) {
+            const uint32_t v = c * LANES + t;
+            const uint4 m = s_mask4[v];
+            s_mask4[v] = make_uint4(0, 0, 0, 0);
+            if (v0 + v < nvec && (dense == 2 || (m.x | m.y | m.z | m.w))) {
+                const uint32_t fr = (m.x & ~cur[c].x) | (m.y & ~cur[c].y) | (m.z & ~cur[c].z) | (m.w & ~cur[c].w);
+                fresh |= fr;
+                if (store_fresh && dense != 2 && !fr) continue;
+                apply_store(gv + v0 + v, make_uint4(cur[c].x | m.x, cur[c].y | m.y, cur[c].z | m.z, cur[c].w | m.w));
+                if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
+            }
+        }
+        __syncthreads();   // every lane is past its reads of the stage and of table bi
+    };
+
+    // prologue: region blockIdx.x's tables, words and vectors; the next region's headers
+    uint32_t r = blockIdx.x;
+    uint4 bufA[kPer], bufB[kPer];
+    uint32_t uwA[UPL], uwB[UPL], loA[LPL], loB[LPL];
+    uint32_t stA, hdA, stB, hdB;
+    {
+        uint32_t st0, hd0;
+        load_hdr(r, st0, hd0);
+        tables(0u, st0, hd0);
+        load_hdr(clampr(r + G), stA, hdA);
+        load_words(0u, uwA, loA);
+        load_vecs(r, bufA);
+    }
+    for (;; r += 2 * G) {
+        region(r, 0u, bufA, uwA, loA, stA, hdA, bufB, uwB, loB, stB, hdB);
+        if (r + G >= nbins) break;
+        region(r + G, 1u, bufB, uwB, loB, stB, hdB, bufA, uwA, loA, stA, hdA);
+        if (r + 2 * G >= nbins) break;
+    }
+    if (any_flag) report_any_new(any_flag, fresh != 0);
+}
 }  // namespace
 
 namespace {
@@ -3067,9 +3319,23 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
         const char* e = BF_AB_GETENV("BFHIP_SETS_STAGE");
         return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
     }();
+    // the persistent pipelined form (sets_apply_pipe_kernel) for dense batches at 2^19-bit regions
+    // with many regions per workgroup (BFHIP_SETS_PIPE=0: the one-shot kernel, A/B)
+    static const uint32_t pg = apply_pipe_grid();
+    static const bool pipe_on = [] {
+        const char* e = BF_AB_GETENV("BFHIP_SETS_PIPE");
+        return !(e && e[0] == '0');
+    }();
+    const bool pipe = pipe_on && dense && region_log2 == 19 && pg && nbins >= 16 * pg;
     for (uint32_t s0 = 0; s0 < nsrc; s0 += kMaxSetSrc) {
         const uint32_t ns = std::min<uint32_t>(kMaxSetSrc, nsrc - s0);
         const uint32_t* src = sets + (uint64_t)s0 * stride_words;
+        if (pipe) {
+            hipLaunchKernelGGL((sets_apply_pipe_kernel<19, kPipeLanes, 2, 5>), dim3(std::min<uint32_t>(nbins, pg)),
+                               dim3(kPipeLanes), 0, s, g.bits, nwords, src, stride_words, ns, nbins, dense, any_flag,
+                               g.dirty, apply_store_fresh(), status);
+            continue;
+        }
 #define BF_SETS_APPLY(RL, LN, ST)                                                                              \
     hipLaunchKernelGGL((sets_apply_kernel<RL, LN, ST>), dim3(nbins), dim3(LN), 0, s, g.bits, nwords, src,       \
                        stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status)

@@ -84,6 +84,9 @@ struct bf_lua {
     uint64_t count = 0;
     std::vector<BfGeom> layers;   // layers[n - 1]: bitset of layer n (allocated on first use)
     std::vector<uint64_t> layer_bytes;
+    // layer bitsets a clear dropped, kept for the next filter's layers of the same size (layer n
+    // always has the same bits for one handle): a cleared filter refills without hipMalloc
+    std::vector<std::pair<uint64_t, uint32_t*>> pool;
     BfGeom* d_layers = nullptr;   // device copy of the layer table for lua_check_kernel
     uint32_t d_layers_n = 0;      // layers of that copy (layers never change once made; clear resets)
     void* scratch = nullptr;
@@ -185,7 +188,15 @@ int ensure_layer(bf_lua* h, uint32_t n) {
                            (unsigned long long)m, k, h->entries, h->precision);
         BfGeom g{};
         const uint64_t bytes = ((m + 7) / 8 + 255) / 256 * 256;
-        LUACHK(h, hipMalloc((void**)&g.bits, bytes));
+        auto it = std::find_if(h->pool.begin(), h->pool.end(), [&](const std::pair<uint64_t, uint32_t*>& x) {
+            return x.first == bytes;
+        });
+        if (it != h->pool.end()) {
+            g.bits = it->second;
+            h->pool.erase(it);
+        } else {
+            LUACHK(h, hipMalloc((void**)&g.bits, bytes));
+        }
         LUACHK(h, hipMemsetAsync(g.bits, 0, bytes, h->stream));
         g.m = m;
         g.inv_m = 1.0 / (double)m;
@@ -395,6 +406,7 @@ int bf_lua_destroy(bf_lua* h) {
         LuaDeviceGuard dg(h->device);
         (void)hipStreamSynchronize(h->stream);
         for (BfGeom& g : h->layers) (void)hipFree(g.bits);
+        for (auto& x : h->pool) (void)hipFree(x.second);
         for (void* p : {(void*)h->d_layers, (void*)h->scratch, (void*)h->d_keys, (void*)h->d_out, (void*)h->d_off,
                         (void*)h->d_last, (void*)h->d_flips, (void*)h->d_cnt})
             if (p) (void)hipFree(p);
@@ -440,7 +452,7 @@ int bf_lua_clear(bf_lua* h) {
     LuaDeviceGuard dg(h->device);
     LUACHK(h, hipStreamSynchronize(h->stream));
     if (h->order_valid) LUACHK(h, hipEventSynchronize(h->order_ev));   // a _dev call's stream
-    for (BfGeom& g : h->layers) (void)hipFree(g.bits);
+    for (size_t i = 0; i < h->layers.size(); ++i) h->pool.push_back({h->layer_bytes[i], h->layers[i].bits});
     h->layers.clear();
     h->layer_bytes.clear();
     h->d_layers_n = 0;
