@@ -3102,8 +3102,11 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     auto region = [&](uint32_t r, uint32_t bi, const uint4* cur, const uint32_t* uw, const uint32_t* lo,
                       uint32_t hst, uint32_t hhd, uint4* nxt, uint32_t* nuw, uint32_t* nlo, uint32_t& nst,
                       uint32_t& nhd) {
-        // r's low bits into the stage (the previous region's decode ended on a barrier)
-        const uint32_t TL = s_lw0[bi][nsrc];
+        // r's low bits into the stage (the previous region's decode ended on a barrier).  The
+        // workgroup-uniform values read from LDS go through readfirstlane, so that their branches
+        // are scalar: a wait inside a branch the compiler must treat as divergent runs on every
+        // path, and a vmcnt(0) there would wait for r + G's prefetch
+        const uint32_t TL = __builtin_amdgcn_readfirstlane(s_lw0[bi][nsrc]);
         const bool staged = TL <= kStage;   // workgroup-uniform
         if (staged) {
 #pragma unroll
@@ -3118,29 +3121,25 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
         load_vecs(rn, nxt);
         // decode r: bitmap sets word by word (rare: read on the spot)
         for (uint32_t s = 0; s < nsrc; ++s) {
-            if (!s_st[bi][s] || (s_hdr[bi][s] >> 24) != kSetsBitmap) continue;   // workgroup-uniform
-            const uint32_t* B = sets + (uint64_t)s * stride_words + s_st[bi][s] + 1;
+            const uint32_t sst = __builtin_amdgcn_readfirstlane(s_st[bi][s]);
+            const uint32_t shd = __builtin_amdgcn_readfirstlane(s_hdr[bi][s]);
+            if (!sst || (shd >> 24) != kSetsBitmap) continue;   // workgroup-uniform
+            const uint32_t* B = sets + (uint64_t)s * stride_words + sst + 1;
             for (uint32_t v = t; v < NW; v += LANES) {
                 const uint32_t x = B[v];
                 if (x) atomicOr(s_mask + v, x);
             }
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
         }
-        // Elias-Fano sets: one pass of LANES upper words at a time over all sources (the first
-        // UPL passes' words prefetched, any further ones read on the spot)
-        const uint32_t TW = s_uw0[bi][nsrc];
+        // Elias-Fano sets: one pass of LANES upper words at a time over all sources.  The first
+        // UPL passes use the prefetched words, as straight-line code: in a loop the compiler's
+        // wait for those registers becomes vmcnt(0), which would also wait for r + G's prefetch.
+        const uint32_t TW = __builtin_amdgcn_readfirstlane(s_uw0[bi][nsrc]);
         uint32_t carry = 0;
-        for (uint32_t p = 0; p * LANES < TW; ++p) {   // workgroup-uniform trip count
-            const uint32_t g = p * LANES + t;
-            uint32_t word = 0;
-            if (g < TW) {
-                if (p < UPL) {
-#pragma unroll
-                    for (uint32_t q = 0; q < UPL; ++q)
-                        if (p == q) word = uw[q];
-                } else {
-                    word = *upper_addr(bi, g);
-                }
-            }
+        // (staged is a compile-time branch: a run-time select between the LDS stage and global
+        // memory would be a flat load, whose wait is vmcnt(0) as well)
+        auto pass = [&](auto stg, uint32_t g, uint32_t word) {   // contains barriers (the scan)
+            constexpr bool kStaged = decltype(stg)::value;
             uint32_t tot;
             const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);
             if (word) {
@@ -3159,7 +3158,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
                     if (l) {
                         const uint32_t bp = i * l, wi = bp >> 5;
                         uint32_t a, b;
-                        if (staged) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
+                        if constexpr (kStaged) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
                             a = slows[min(wi, lim)];
                             b = slows[min(wi, lim) + 1u];
                         } else {
@@ -3174,6 +3173,22 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
                 }
             }
             carry += tot;
+        };
+        if (staged) {
+#pragma unroll
+            for (uint32_t p = 0; p < UPL; ++p)   // workgroup-uniform tests
+                if (p * LANES < TW) pass(std::true_type{}, p * LANES + t, p * LANES + t < TW ? uw[p] : 0u);
+        } else {   // (low bits past the stage: read on the spot, each read waited out)
+#pragma unroll
+            for (uint32_t p = 0; p < UPL; ++p)
+                if (p * LANES < TW) pass(std::false_type{}, p * LANES + t, p * LANES + t < TW ? uw[p] : 0u);
+        }
+        for (uint32_t g0 = UPL * LANES; g0 < TW; g0 += LANES) {   // more upper words: read on the spot
+            const uint32_t g = g0 + t;
+            const uint32_t word = g < TW ? *upper_addr(bi, g) : 0u;
+            if (staged) pass(std::true_type{}, g, word);
+            else pass(std::false_type{}, g, word);
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);   // (the rare path ends on a full wait, as the main path may assume)
         }
         __syncthreads();   // the image is complete
         const uint64_t v0 = (uint64_t)r * kVec;
