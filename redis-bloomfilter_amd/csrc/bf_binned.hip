@@ -2963,6 +2963,10 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     if (any_flag) report_any_new(any_flag, fresh != 0);
 }
 
+#ifdef BFHIP_AB_KNOBS
+// (A/B only, BFHIP_SETS_PIPE=1; measured slower, DESIGN §6f: 5.06 vs 4.58 ms at 10B x 8, 0.61
+// vs 0.53 ms at the north star x 2 — one region per CU at a time loses to two one-shot
+// workgroups per CU, whose decodes overlap each other's barrier and scan latency.)
 // sets_apply_kernel, persistent and software-pipelined (one 1024-lane workgroup per CU walking
 // regions r, r + G, ...), for batches dense enough to rewrite every region (VERDICT r04 item
 // 4).  The one-shot kernel pays, per region, two dependent round trips (the per-source headers,
@@ -3229,6 +3233,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
     if (any_flag) report_any_new(any_flag, fresh != 0);
 }
+#endif  // BFHIP_AB_KNOBS
 }  // namespace
 
 namespace {
@@ -3334,23 +3339,27 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
         const char* e = BF_AB_GETENV("BFHIP_SETS_STAGE");
         return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
     }();
-    // the persistent pipelined form (sets_apply_pipe_kernel) for dense batches at 2^19-bit regions
-    // with many regions per workgroup (BFHIP_SETS_PIPE=0: the one-shot kernel, A/B)
+#ifdef BFHIP_AB_KNOBS
+    // (A/B: BFHIP_SETS_PIPE=1 takes the persistent pipelined form for dense batches at 2^19-bit
+    // regions with many regions per workgroup; measured slower, kept for the record)
     static const uint32_t pg = apply_pipe_grid();
     static const bool pipe_on = [] {
         const char* e = BF_AB_GETENV("BFHIP_SETS_PIPE");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     const bool pipe = pipe_on && dense && region_log2 == 19 && pg && nbins >= 16 * pg;
+#endif
     for (uint32_t s0 = 0; s0 < nsrc; s0 += kMaxSetSrc) {
         const uint32_t ns = std::min<uint32_t>(kMaxSetSrc, nsrc - s0);
         const uint32_t* src = sets + (uint64_t)s0 * stride_words;
+#ifdef BFHIP_AB_KNOBS
         if (pipe) {
             hipLaunchKernelGGL((sets_apply_pipe_kernel<19, kPipeLanes, 2, 5>), dim3(std::min<uint32_t>(nbins, pg)),
                                dim3(kPipeLanes), 0, s, g.bits, nwords, src, stride_words, ns, nbins, dense, any_flag,
                                g.dirty, apply_store_fresh(), status);
             continue;
         }
+#endif
 #define BF_SETS_APPLY(RL, LN, ST)                                                                              \
     hipLaunchKernelGGL((sets_apply_kernel<RL, LN, ST>), dim3(nbins), dim3(LN), 0, s, g.bits, nwords, src,       \
                        stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status)
