@@ -463,7 +463,7 @@ int launch_op(bf_handle* h, BfOp op, const uint8_t* k16, const uint64_t* offs, u
     if (op == BF_OP_INSERT_FLAGS && out8) {
         // Per-key flags: exact sequential semantics (bf_seq.hip), chunk after chunk in stream order.
         const uint64_t chunk = bf_seq_chunk_keys(h->k);
-        int rc = ensure_scratch(h, bf_seq_scratch_bytes(std::min(n, chunk), h->k, nullptr));
+        int rc = ensure_scratch(h, bf_seq_scratch_bytes(std::min(n, chunk), h->k, h->g.m));
         if (rc) return rc;
         for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
             const uint64_t cn = std::min(chunk, n - c0);

@@ -216,10 +216,10 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
                                  uint32_t* any_flag, uint32_t* status, hipStream_t s, BfMarks* marks = nullptr);
 
 // Exact sequential per-key results (bf_seq.hip): batches of at most
-// bf_seq_chunk_keys(k) keys, scratch of bf_seq_scratch_bytes(n, k).  Probe
+// bf_seq_chunk_keys(k) keys, scratch of bf_seq_scratch_bytes(n, k, m) (m: the filter's bits).  Probe
 // indices i0 .. i0+k-1 (0 for the ruby driver, 1 for the Lua scripts).
 uint64_t bf_seq_chunk_keys(uint32_t k);
-uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t* slots);
+uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t m);
 hipError_t bf_launch_seq_candidates(const BfGeom& g, uint32_t i0, const uint8_t* keys16, const uint64_t* offsets,
                                     uint64_t bias, uint64_t n, void* scratch, hipStream_t s);
 // new(j) -> out8 / any_flag (nullable) for j < n; ORs the 0-probes of keys j < limit into g.bits.

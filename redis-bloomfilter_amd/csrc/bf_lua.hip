@@ -503,7 +503,7 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
         const BfGeom& g = h->layers[layer - 1];
         const uint64_t room = lua_layer_capacity(h->entries, layer, h->count + 1) - h->count;   // >= 1
         const uint64_t cn = std::min<uint64_t>(n - s, bf_seq_chunk_keys(g.k));
-        if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, nullptr)))) return rc;
+        if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, g.m)))) return rc;
         // which keys would set a new bit of this layer, in order (nothing applied yet)
         BfMarks* mk = lua_prof_begin(h, h->stream);
         LUACHK(h, bf_launch_seq_candidates(g, 1, h->d_keys, h->d_off + s, 0, cn, h->scratch, h->stream));
@@ -605,7 +605,7 @@ int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
         const uint64_t room = lua_layer_capacity(h->entries, layer, h->count + 1) - h->count;   // >= 1
         const uint64_t cn = std::min<uint64_t>(n - done, bf_seq_chunk_keys(g.k));
         if ((rc = ensure_io(h, 0, cn))) return rc;
-        if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, nullptr)))) return rc;
+        if ((rc = ensure_lua_scratch(h, bf_seq_scratch_bytes(cn, g.k, g.m)))) return rc;
         uint8_t* flags = d_per_key_new ? d_per_key_new + done : h->d_out;
         BfMarks* mk = lua_prof_begin(h, s);
         LUACHK(h, bf_launch_seq_candidates(g, 1, k16, d_offsets + done, bias, cn, h->scratch, s));

@@ -9,9 +9,12 @@
 //
 // (first(b) <= j always holds for j's own probes).  Two kernels per chunk:
 //   1. seq_candidates: hash (shared SHA-1 / ruby.rb:41-55 derivation), test every
-//      probe against the pre-batch bitset; for each 0 bit record the min index in
-//      a global open-addressing table keyed by bit offset (atomicCAS claim +
-//      atomicMin); keep the digest and the key's mask of 0-probes;
+//      probe against the pre-batch bitset; for each 0 bit record the min index j —
+//      DIRECT: in a table of one uint32 per bit of the filter (one atomicMin at the
+//      offset), for filters whose table is not much larger than the hash table below
+//      (seq_direct: the Lua layout's 1M-scale layers, 44 MB at 11M bits); else in a
+//      global open-addressing table keyed by bit offset (atomicCAS claim + atomicMin);
+//      keep the digest and the key's mask of 0-probes;
 //   2. seq_mark: new(j) from the table, then OR the 0-probes of keys j < limit in.
 // Chunks run in stream order, so chunk c+1 tests against chunk c's bits: the
 // result is that of inserting every key one by one.  "Found before its own
@@ -36,6 +39,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {   // SplitMix64 finalize
     return x;
 }
 
+template <bool DIRECT>
 __global__ __launch_bounds__(kSeqTile) void seq_candidates_kernel(BfGeom g, uint32_t i0,
                                                                   const uint8_t* __restrict__ keys16,
                                                                   const uint64_t* __restrict__ offsets, uint64_t bias,
@@ -58,6 +62,10 @@ __global__ __launch_bounds__(kSeqTile) void seq_candidates_kernel(BfGeom g, uint
                 const uint64_t o = probe_offset(g, H[0], H[1], H[2], H[3], i0 + i);
                 if ((g.bits[o >> 5] >> ((uint32_t)(o ^ 7u) & 31u)) & 1u) continue;
                 cm |= 1ull << i;
+                if constexpr (DIRECT) {   // one word per bit (o < m): no claim, no probing
+                    atomicMin(tvals + o, j);
+                    continue;
+                }
                 const unsigned long long key = o + 1;   // 0 marks an empty slot
                 uint64_t slot = mix64(o) & tmask;
                 for (;;) {   // the table holds <= half its slots: a free or matching slot exists
@@ -74,6 +82,7 @@ __global__ __launch_bounds__(kSeqTile) void seq_candidates_kernel(BfGeom g, uint
 }
 
 // out8 / any_flag (nullable) get new(j) for j < n; the 0-probes of keys j < limit are ORed in.
+template <bool DIRECT>
 __global__ __launch_bounds__(256) void seq_mark_kernel(BfGeom g, uint32_t i0, uint64_t n, uint64_t limit,
                                                        const unsigned long long* __restrict__ tkeys,
                                                        const uint32_t* __restrict__ tvals, uint64_t tmask,
@@ -90,9 +99,12 @@ __global__ __launch_bounds__(256) void seq_mark_kernel(BfGeom g, uint32_t i0, ui
                 const uint32_t i = (uint32_t)__builtin_ctzll(cm);
                 cm &= cm - 1;
                 const uint64_t o = probe_offset(g, H.x, H.y, H.z, H.w, i0 + i);
-                const unsigned long long key = o + 1;
-                uint64_t slot = mix64(o) & tmask;
-                while (tkeys[slot] != key) slot = (slot + 1) & tmask;   // inserted by seq_candidates
+                uint64_t slot = o;
+                if constexpr (!DIRECT) {
+                    const unsigned long long key = o + 1;
+                    slot = mix64(o) & tmask;
+                    while (tkeys[slot] != key) slot = (slot + 1) & tmask;   // inserted by seq_candidates
+                }
                 isnew |= tvals[slot] == (uint32_t)j ? 1u : 0u;
                 if (j < limit) {
                     __hip_atomic_fetch_or(g.bits + (o >> 5), 1u << ((uint32_t)(o ^ 7u) & 31u), __ATOMIC_RELAXED,
@@ -121,14 +133,36 @@ struct SeqCarve {
     uint64_t slots;
 };
 
-SeqCarve seq_carve(void* scratch, uint64_t n, uint32_t k) {
+// The hash table's slots for n keys of k probes (at most half full).
+uint64_t seq_slots(uint64_t n, uint32_t k) {
+    uint64_t s = 1024;
+    while (s < 2 * n * (uint64_t)k) s <<= 1;
+    return s;
+}
+
+// One uint32 per filter bit when that table is at most twice the hash table's bytes (so its
+// clear costs no more) and at most 1 GiB: the Lua layout's 1M-scale layers (11M bits against
+// a 16M-slot table for a 2^20-key chunk), small filters under big batches.  Probe updates are
+// then one atomicMin each, with no claim loop.
+bool seq_direct(uint64_t n, uint32_t k, uint64_t m) {
+    return m <= (1ull << 28) && 4 * m <= 2 * 12 * seq_slots(n, k);
+}
+
+SeqCarve seq_carve(void* scratch, uint64_t n, uint32_t k, uint64_t m) {
     SeqCarve c{};
-    (void)bf_seq_scratch_bytes(n, k, &c.slots);
     uint8_t* at = static_cast<uint8_t*>(scratch);
-    c.tkeys = reinterpret_cast<unsigned long long*>(at);
-    at += align256(c.slots * 8);
-    c.tvals = reinterpret_cast<uint32_t*>(at);
-    at += align256(c.slots * 4);
+    if (seq_direct(n, k, m)) {
+        c.slots = m;
+        c.tkeys = nullptr;
+        c.tvals = reinterpret_cast<uint32_t*>(at);
+        at += align256(m * 4);
+    } else {
+        c.slots = seq_slots(n, k);
+        c.tkeys = reinterpret_cast<unsigned long long*>(at);
+        at += align256(c.slots * 8);
+        c.tvals = reinterpret_cast<uint32_t*>(at);
+        at += align256(c.slots * 4);
+    }
     c.digests = reinterpret_cast<uint4*>(at);
     at += align256(n * 16);
     c.cand = reinterpret_cast<unsigned long long*>(at);
@@ -142,32 +176,38 @@ uint64_t bf_seq_chunk_keys(uint32_t k) {
     return c < (1ull << 22) ? (c ? c : 1) : (1ull << 22);
 }
 
-uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t* slots) {
-    uint64_t s = 1024;
-    while (s < 2 * n * (uint64_t)k) s <<= 1;
-    if (slots) *slots = s;
-    return align256(s * 8) + align256(s * 4) + align256(n * 16) + align256(n * 8);
+uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t m) {
+    const uint64_t tab = seq_direct(n, k, m) ? align256(m * 4) : align256(seq_slots(n, k) * 8) + align256(seq_slots(n, k) * 4);
+    return tab + align256(n * 16) + align256(n * 8);
 }
 
 hipError_t bf_launch_seq_candidates(const BfGeom& g, uint32_t i0, const uint8_t* keys16, const uint64_t* offsets,
                                     uint64_t bias, uint64_t n, void* scratch, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const SeqCarve c = seq_carve(scratch, n, g.k);
+    const SeqCarve c = seq_carve(scratch, n, g.k, g.m);
     hipError_t e;
-    if ((e = hipMemsetAsync(c.tkeys, 0, c.slots * 8, s)) != hipSuccess) return e;
+    if (c.tkeys && (e = hipMemsetAsync(c.tkeys, 0, c.slots * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(c.tvals, 0xFF, c.slots * 4, s)) != hipSuccess) return e;
     const uint32_t blocks = (uint32_t)((n + kSeqTile - 1) / kSeqTile);
-    hipLaunchKernelGGL(seq_candidates_kernel, dim3(blocks), dim3(kSeqTile), 0, s, g, i0, keys16, offsets, bias, n,
-                       c.tkeys, c.tvals, c.slots - 1, c.digests, c.cand);
+    if (c.tkeys)
+        hipLaunchKernelGGL(seq_candidates_kernel<false>, dim3(blocks), dim3(kSeqTile), 0, s, g, i0, keys16, offsets,
+                           bias, n, c.tkeys, c.tvals, c.slots - 1, c.digests, c.cand);
+    else
+        hipLaunchKernelGGL(seq_candidates_kernel<true>, dim3(blocks), dim3(kSeqTile), 0, s, g, i0, keys16, offsets,
+                           bias, n, c.tkeys, c.tvals, 0, c.digests, c.cand);
     return hipGetLastError();
 }
 
 hipError_t bf_launch_seq_mark(const BfGeom& g, uint32_t i0, uint64_t n, uint64_t limit, void* scratch, uint8_t* out8,
                               uint32_t* any_flag, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const SeqCarve c = seq_carve(scratch, n, g.k);
-    hipLaunchKernelGGL(seq_mark_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, g, i0, n, limit,
-                       c.tkeys, c.tvals, c.slots - 1, c.digests, c.cand, out8, any_flag);
+    const SeqCarve c = seq_carve(scratch, n, g.k, g.m);
+    if (c.tkeys)
+        hipLaunchKernelGGL(seq_mark_kernel<false>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, g, i0, n, limit,
+                           c.tkeys, c.tvals, c.slots - 1, c.digests, c.cand, out8, any_flag);
+    else
+        hipLaunchKernelGGL(seq_mark_kernel<true>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, g, i0, n, limit,
+                           c.tkeys, c.tvals, 0, c.digests, c.cand, out8, any_flag);
     return hipGetLastError();
 }
 

@@ -6,6 +6,8 @@
 #   sets       region-set tests + the replicated / region-set multi-rank gloo cases
 #   edge       the forced-binned edge cases at every region size (test_binned_edge_cases)
 #   lua        the Lua layout's GPU tests (host and device entry points)
+#   seq        every test file that reaches the sequential per-key flags (bf_seq.hip)
+#   benchlua   the lua_1m secondary alone (bench.py --config 10k --secondary lua_1m)
 #   smoke      __graft_entry__.smoke()
 #   bench      the driver's bench command (--gpus 1 --steps 20 --warmup 5)
 #   bench10b / bench200b / bench100m   the other single-GPU configs
@@ -55,6 +57,12 @@ for st in $STEPS; do
         edge)   timeout -k 10 500 $PYT tests/test_gpu_parity.py -k binned_edge \
                     > gpurun_out/tests_${TAG}_edge.log 2>&1 ;;
         lua)    timeout -k 10 300 $PYT tests/test_gpu_lua.py > gpurun_out/tests_${TAG}_lua.log 2>&1 ;;
+        seq)    timeout -k 10 500 $PYT tests/test_gpu_lua.py tests/test_gpu_parity.py tests/test_gpu_per_key.py \
+                    tests/test_gpu_dirty_sync.py tests/test_gpu_engines.py tests/test_gpu_multi.py \
+                    tests/test_gpu_reference_shapes.py > gpurun_out/tests_${TAG}_seq.log 2>&1 ;;
+        benchlua) timeout -k 10 200 python bench.py --config 10k --secondary lua_1m --steps 5 --warmup 2 \
+                    --no-cpu-baseline --no-host-api --no-reference-shapes \
+                    > gpurun_out/bench_lua_${TAG}.json 2> gpurun_out/bench_lua_${TAG}.err ;;
         smoke)  timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
         bench)  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
                     > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
