@@ -622,16 +622,29 @@ int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
             LUACHK(h, hipMemcpyAsync(h->h_cnt, h->d_cnt, 8, hipMemcpyDeviceToHost, s));
             LUACHK(h, hipStreamSynchronize(s));
             fresh = h->h_cnt[0];
-        } else {   // the chunk that fills the layer: cut after the key whose INCR fills it (add.lua:48-50)
+        } else {   // the chunk may fill the layer: cut after the key whose INCR fills it (add.lua:48-50)
             LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, flags, nullptr, s));
             bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
-            LUACHK(h, hipMemcpyAsync(h->h_out, flags, cn, hipMemcpyDeviceToHost, s));
+            // the chunk's INCRs summed first: below the room (a chunk longer than the room whose
+            // keys are not all new) nothing is cut and the flags stay on the device
+            LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 8, s));
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn + 255) / 256, 1024);
+            hipLaunchKernelGGL(lua_count_kernel, dim3(grid), dim3(256), 0, s, flags, cn, h->d_cnt);
+            LUACHK(h, hipGetLastError());
+            bf_mark(mk, s, lua_prof_name(h, kLuaCount, layer));
+            LUACHK(h, hipMemcpyAsync(h->h_cnt, h->d_cnt, 8, hipMemcpyDeviceToHost, s));
             LUACHK(h, hipStreamSynchronize(s));
-            for (uint64_t j = 0; j < cn; ++j) {
-                fresh += h->h_out[j];
-                if (fresh == room) {
-                    take = j + 1;
-                    break;
+            fresh = h->h_cnt[0];
+            if (fresh >= room) {   // the cut: the flags to the host to find it
+                LUACHK(h, hipMemcpyAsync(h->h_out, flags, cn, hipMemcpyDeviceToHost, s));
+                LUACHK(h, hipStreamSynchronize(s));
+                fresh = 0;
+                for (uint64_t j = 0; j < cn; ++j) {
+                    fresh += h->h_out[j];
+                    if (fresh == room) {
+                        take = j + 1;
+                        break;
+                    }
                 }
             }
             mk = lua_prof_begin(h, s);
