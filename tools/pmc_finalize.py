@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Turn one final tree's GPU passes into the files bench.py reads (run on the CPU host after
+the passes' gpurun_out/ came back):
+
+    python tools/pmc_finalize.py <tag>
+
+* profiles/pmc_<tag>_<workload>.json for every workload whose PMC passes exist
+  (gpurun_out/pmc_<tag>_<workload>_{rd,wr,dram,valu}/, tools/pmc_passes.sh), summarised by
+  tools/pmc_summary.py with the workload's batch;
+* profiles/pmc_traffic.json: the north-star include? kernel's HBM bytes per launch (the
+  line's roofline.traffic), with its source;
+* profiles/rocprof_means.json from profiles/<tag>_kernel_stats.csv (tools/rocprof_means.py).
+
+bench.PMC_FILES must then name the same tag (tests/test_profiles_tagged.py checks it)."""
+import glob
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+BATCH = {"nstar": 1 << 24, "1m": 1 << 20, "1m_big": 1 << 24, "100m": 1 << 24, "10b": 1 << 24, "lua_1m": 1 << 20}
+
+
+def main():
+    tag = sys.argv[1]
+    for wl, batch in BATCH.items():
+        dirs = sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "pmc_%s_%s_*" % (tag, wl))))
+        dirs = [d for d in dirs if os.path.isdir(d)]
+        if not dirs:
+            continue
+        out = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, wl))
+        subprocess.check_call([sys.executable, os.path.join(HERE, "pmc_summary.py"), *dirs, "--workload", wl,
+                               "--batch", str(batch), "--json", out], stdout=subprocess.DEVNULL)
+        print("wrote", os.path.relpath(out, ROOT))
+        if wl == "nstar":
+            rec = json.load(open(out))["nstar"]
+            k = rec.get("bf_include_hash_kernel") or {}
+            traffic = {"nstar": dict(rec, include_hash_kernel=k),   # (bench.py's kernel name for it)
+                       "source": "profiles/pmc_%s_nstar.json" % tag}
+            with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
+                json.dump(traffic, fh, indent=1, sort_keys=True)
+                fh.write("\n")
+            print("wrote profiles/pmc_traffic.json")
+    stats = os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % tag)
+    if os.path.exists(stats):
+        txt = subprocess.check_output([sys.executable, os.path.join(HERE, "rocprof_means.py"),
+                                       os.path.relpath(stats, ROOT), "--workload", "nstar"], cwd=ROOT, text=True)
+        with open(os.path.join(ROOT, "profiles", "rocprof_means.json"), "w") as fh:
+            fh.write(txt)
+        print("wrote profiles/rocprof_means.json")
+
+
+if __name__ == "__main__":
+    main()
