@@ -65,13 +65,32 @@ __global__ __launch_bounds__(kLuaTile) void lua_check_kernel(const BfGeom* __res
 
 // Keys that set a new bit (per-key flags 0/1) summed into *count: the layer count's INCR
 // (add.lua:48-50) without reading the flags back to the host.
+// 16 bytes per lane and step, one atomic per workgroup (atomics on one word serialise).
 __global__ __launch_bounds__(256) void lua_count_kernel(const uint8_t* __restrict__ flags, uint64_t n,
                                                         unsigned long long* __restrict__ count) {
+    __shared__ uint32_t s_part[4];
     uint32_t c = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) c += flags[i];
+    // an unaligned head and the tail byte by byte (workgroup 0), the rest as 16-B vectors
+    const uint64_t head = min<uint64_t>(n, (16u - (reinterpret_cast<uintptr_t>(flags) & 15u)) & 15u);
+    const uint64_t nv = (n - head) / 16;
+    const uint4* fv = reinterpret_cast<const uint4*>(flags + head);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256) {
+        const uint4 v = fv[i];   // bytes are 0 / 1: a byte-wise sum of each word fits 8 bits
+        const uint32_t w = v.x + v.y + v.z + v.w;
+        c += (w & 0xFFu) + ((w >> 8) & 0xFFu) + ((w >> 16) & 0xFFu) + (w >> 24);
+    }
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < head) c += flags[threadIdx.x];
+        for (uint64_t i = head + nv * 16 + threadIdx.x; i < n; i += 256) c += flags[i];
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t tot = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+        if (tot) atomicAdd(count, (unsigned long long)tot);
+    }
 }
 
 }  // namespace
@@ -615,7 +634,7 @@ int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
             LUACHK(h, bf_launch_seq_mark(g, 1, cn, cn, h->scratch, flags, nullptr, s));
             bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
             LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 8, s));
-            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn + 255) / 256, 1024);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn / 16 + 255) / 256 + 1, 256);
             hipLaunchKernelGGL(lua_count_kernel, dim3(grid), dim3(256), 0, s, flags, cn, h->d_cnt);
             LUACHK(h, hipGetLastError());
             bf_mark(mk, s, lua_prof_name(h, kLuaCount, layer));
@@ -628,7 +647,7 @@ int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
             // the chunk's INCRs summed first: below the room (a chunk longer than the room whose
             // keys are not all new) nothing is cut and the flags stay on the device
             LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 8, s));
-            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn + 255) / 256, 1024);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn / 16 + 255) / 256 + 1, 256);
             hipLaunchKernelGGL(lua_count_kernel, dim3(grid), dim3(256), 0, s, flags, cn, h->d_cnt);
             LUACHK(h, hipGetLastError());
             bf_mark(mk, s, lua_prof_name(h, kLuaCount, layer));
