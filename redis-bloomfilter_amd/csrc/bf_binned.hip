@@ -1467,7 +1467,7 @@ constexpr int kL2Loads = 8;
 constexpr uint32_t kL2Grid = 1536;
 constexpr uint32_t kL2MaxParts = 256;
 template <bool SIDE, bool WALK = true, int LOADS = kL2Loads>
-__global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
+__global__ __launch_bounds__(kL2Lanes) __attribute__((amdgpu_waves_per_eu(8, 8))) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
                                                                  uint32_t nsup, uint32_t nq, uint32_t parts,
                                                                  const uint32_t* __restrict__ gsum,
                                                                  const uint2* __restrict__ runs,
@@ -1477,25 +1477,65 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
     const uint32_t t = threadIdx.x;
     // Side job (SIDE, sh.n > 0): SHA-1 words of another batch, by workgroups of their own
-    // (blockIdx.x >= pgrid, about one per CU) that run beside the sweep's: the sweep waits on
-    // its probes' memory (VALU busy ~0.22 at P = 8), so the hashing waves take the idle VALU
-    // instead of lengthening the sweep's own chains (r03 hashed tiles at the sweep workgroups'
-    // item tops, behind barriers: the sweep grew by the whole hash, profiles/r05f_sim_P8_dig.json).
-    // Each wave hashes tiles of 64 keys, one key per lane, reading the key bytes from global
-    // memory: no LDS, no barriers.
+    // (blockIdx.x >= pgrid, two per CU) that run beside the sweep's: the sweep waits on its
+    // probes' memory (VALU busy ~0.22 at P = 8), so the hashing waves take the idle VALU instead
+    // of lengthening the sweep's own chains (r03 hashed tiles at the sweep workgroups' item
+    // tops, behind barriers: the sweep grew by the whole hash, profiles/r05f_sim_P8_dig.json).
+    // Each wave hashes tiles of 64 keys, one key per lane, with no barrier: a tile's key bytes
+    // (<= 1 KiB: one 16-B vector per lane) go into the wave's own LDS stage, and while it hashes
+    // tile i, tile i+1's offsets are in flight (then its bytes, while the loop comes round; a
+    // longer tile hashes from global memory).
+    constexpr uint32_t kHashVec = 64;   // one vector per lane
+    __shared__ uint4 s_hstage[SIDE ? (kL2Lanes / 64) * (kHashVec + kStageSlackVec) : 1];
     if constexpr (SIDE) {
         if (blockIdx.x >= pgrid) {   // workgroup-uniform: a hashing workgroup
             constexpr uint32_t kWaves = kL2Lanes / 64;
-            const uint64_t hw = (uint64_t)(blockIdx.x - pgrid) * kWaves + (t >> 6);
+            const uint32_t lane = t & 63u, wv = t >> 6;
+            uint4* stage = s_hstage + wv * (kHashVec + kStageSlackVec);
+            const uint64_t hw = (uint64_t)(blockIdx.x - pgrid) * kWaves + wv;
             const uint64_t nhw = (uint64_t)(gridDim.x - pgrid) * kWaves;
-            for (uint64_t j0 = hw * 64; j0 < sh.n; j0 += nhw * 64) {
-                const uint64_t j = j0 + (t & 63u);
-                if (j < sh.n) {
-                    const uint64_t ks = sh.offsets[j] + sh.bias, L = sh.offsets[j + 1] + sh.bias - ks;
-                    const uint64_t kbase = ks & ~(uint64_t)3;
+            const uint64_t step = nhw * 64;
+            // key j's start (lane) and the tile's end (lane 63: offsets[j0 + 64]); j past n: n
+            auto load_offs = [&](uint64_t j0, uint64_t& ks, uint64_t& ke) {
+                const uint64_t j = j0 + lane < sh.n ? j0 + lane : sh.n;
+                ks = sh.offsets[j] + sh.bias;
+                ke = sh.offsets[j0 + 64 < sh.n ? j0 + 64 : sh.n] + sh.bias;
+            };
+            auto load_vec = [&](uint64_t ks, uint64_t ke, uint4& v) {   // the tile's bytes, if <= 1 KiB
+                const uint64_t a0 = __shfl(ks, 0) & ~(uint64_t)15, a1 = __shfl(ke, 63);
+                v = make_uint4(0, 0, 0, 0);
+                if (a1 - a0 <= kHashVec * 16 && a0 + lane * 16 < a1)
+                    v = reinterpret_cast<const uint4*>(sh.keys16 + a0)[lane];
+            };
+            uint64_t j0 = hw * 64;
+            if (j0 < sh.n) {
+                uint64_t ks0, ke0;
+                load_offs(j0, ks0, ke0);
+                uint4 v0;
+                load_vec(ks0, ke0, v0);
+                for (; j0 < sh.n; j0 += step) {
+                    // tile j0: offsets (ks0, ke0) and bytes v0 in registers
+                    const uint64_t a0 = __shfl(ks0, 0) & ~(uint64_t)15, a1 = __shfl(ke0, 63);
+                    const bool staged = a1 - a0 <= kHashVec * 16;   // wave-uniform
+                    if (staged) stage[lane] = v0;
+                    // the next tile's offsets arrive while this one hashes; its bytes are issued
+                    // right after, and arrive while the loop comes round
+                    uint64_t ks1 = 0, ke1 = 0;
+                    if (j0 + step < sh.n) load_offs(j0 + step, ks1, ke1);
+                    const uint64_t j = j0 + lane;
+                    const uint64_t L = (lane < 63 ? __shfl_down(ks0, 1) : ke0) - ks0;
                     uint32_t H[5];
-                    sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks - kbase), (uint32_t)L, H);
-                    sh.dig[j] = make_uint4(H[0], H[1], H[2], H[3]);
+                    if (staged)   // (the wave's own LDS: its stores above are ordered before these reads)
+                        sha1_key_staged(reinterpret_cast<const uint32_t*>(stage), (uint32_t)(ks0 - a0), (uint32_t)L, H);
+                    else {
+                        const uint64_t kbase = ks0 & ~(uint64_t)3;
+                        sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks0 - kbase),
+                                 (uint32_t)L, H);
+                    }
+                    if (j < sh.n) sh.dig[j] = make_uint4(H[0], H[1], H[2], H[3]);
+                    if (j0 + step < sh.n) load_vec(ks1, ke1, v0);
+                    ks0 = ks1;
+                    ke0 = ke1;
                 }
             }
             return;
@@ -2429,12 +2469,12 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
             const char* e = BF_AB_GETENV("BFHIP_L2_LOADS");
             return e && *e ? std::atoi(e) : kL2Loads;
         }();
-        // side hash: hashing workgroups beside the sweep's, one per CU by default (A/B:
+        // side hash: hashing workgroups beside the sweep's, two per CU by default (A/B:
         // BFHIP_L2_HASH_GRID); they are the grid's last, so the sweep's XCD map is unchanged
         [[maybe_unused]] static const uint32_t hgrid = [] {
             const char* e = BF_AB_GETENV("BFHIP_L2_HASH_GRID");
             const int v = e && *e ? std::atoi(e) : 0;
-            return v > 0 ? (uint32_t)v : apply_pipe_grid();
+            return v > 0 ? (uint32_t)v : 2 * apply_pipe_grid();
         }();
         if (side.n)
             hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid + hgrid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
