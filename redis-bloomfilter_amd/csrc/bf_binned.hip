@@ -1495,11 +1495,12 @@ __global__ __launch_bounds__(kL2Lanes) __attribute__((amdgpu_waves_per_eu(8, 8))
             const uint64_t hw = (uint64_t)(blockIdx.x - pgrid) * kWaves + wv;
             const uint64_t nhw = (uint64_t)(gridDim.x - pgrid) * kWaves;
             const uint64_t step = nhw * 64;
-            // key j's start (lane) and the tile's end (lane 63: offsets[j0 + 64]); j past n: n
+            // key j's start (lane) and the tile's end (lane 63: offsets[j0 + 64]); j past n: n.  Raw
+            // offsets: the bias is added where they are used, so no wait follows the loads
             auto load_offs = [&](uint64_t j0, uint64_t& ks, uint64_t& ke) {
                 const uint64_t j = j0 + lane < sh.n ? j0 + lane : sh.n;
-                ks = sh.offsets[j] + sh.bias;
-                ke = sh.offsets[j0 + 64 < sh.n ? j0 + 64 : sh.n] + sh.bias;
+                ks = sh.offsets[j];
+                ke = sh.offsets[j0 + 64 < sh.n ? j0 + 64 : sh.n];
             };
             auto load_vec = [&](uint64_t ks, uint64_t ke, uint4& v) {   // the tile's bytes, if <= 1 KiB
                 const uint64_t a0 = __shfl(ks, 0) & ~(uint64_t)15, a1 = __shfl(ke, 63);
@@ -1511,19 +1512,24 @@ __global__ __launch_bounds__(kL2Lanes) __attribute__((amdgpu_waves_per_eu(8, 8))
             if (j0 < sh.n) {
                 uint64_t ks0, ke0;
                 load_offs(j0, ks0, ke0);
+                ks0 += sh.bias;
+                ke0 += sh.bias;
                 uint4 v0;
                 load_vec(ks0, ke0, v0);
                 for (; j0 < sh.n; j0 += step) {
                     // tile j0: offsets (ks0, ke0) and bytes v0 in registers
                     const uint64_t a0 = __shfl(ks0, 0) & ~(uint64_t)15, a1 = __shfl(ke0, 63);
-                    const bool staged = a1 - a0 <= kHashVec * 16;   // wave-uniform
+                    const bool staged = __builtin_amdgcn_readfirstlane(a1 - a0 <= kHashVec * 16 ? 1u : 0u);   // (uniform)
                     if (staged) stage[lane] = v0;
+                    const uint64_t j = j0 + lane;
+                    // (the shuffle outside the select: inside it lane 63 would be inactive, and a
+                    // ds_bpermute from an inactive lane reads 0 — lane 62's length would wrap)
+                    const uint64_t nks = __shfl_down(ks0, 1);
+                    const uint64_t L = (lane < 63 ? nks : ke0) - ks0;
                     // the next tile's offsets arrive while this one hashes; its bytes are issued
                     // right after, and arrive while the loop comes round
                     uint64_t ks1 = 0, ke1 = 0;
                     if (j0 + step < sh.n) load_offs(j0 + step, ks1, ke1);
-                    const uint64_t j = j0 + lane;
-                    const uint64_t L = (lane < 63 ? __shfl_down(ks0, 1) : ke0) - ks0;
                     uint32_t H[5];
                     if (staged)   // (the wave's own LDS: its stores above are ordered before these reads)
                         sha1_key_staged(reinterpret_cast<const uint32_t*>(stage), (uint32_t)(ks0 - a0), (uint32_t)L, H);
@@ -1533,9 +1539,9 @@ __global__ __launch_bounds__(kL2Lanes) __attribute__((amdgpu_waves_per_eu(8, 8))
                                  (uint32_t)L, H);
                     }
                     if (j < sh.n) sh.dig[j] = make_uint4(H[0], H[1], H[2], H[3]);
-                    if (j0 + step < sh.n) load_vec(ks1, ke1, v0);
-                    ks0 = ks1;
-                    ke0 = ke1;
+                    ks0 = ks1 + sh.bias;
+                    ke0 = ke1 + sh.bias;
+                    if (j0 + step < sh.n) load_vec(ks0, ke0, v0);
                 }
             }
             return;
