@@ -1467,97 +1467,68 @@ constexpr int kL2Loads = 8;
 constexpr uint32_t kL2Grid = 1536;
 constexpr uint32_t kL2MaxParts = 256;
 template <bool SIDE, bool WALK = true, int LOADS = kL2Loads>
-__global__ __launch_bounds__(kL2Lanes) __attribute__((amdgpu_waves_per_eu(8, 8))) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
+__global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, const uint32_t* __restrict__ bits,
                                                                  uint32_t nsup, uint32_t nq, uint32_t parts,
                                                                  const uint32_t* __restrict__ gsum,
                                                                  const uint2* __restrict__ runs,
                                                                  const uint16_t* __restrict__ istart,
-                                                                 uint8_t* __restrict__ out8, BfSideHash sh,
-                                                                 uint32_t pgrid) {
+                                                                 uint8_t* __restrict__ out8, BfSideHash sh) {
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
+    constexpr uint32_t kSideVec = 256;   // 4 KiB key stage: a tile of 256 keys of <= ~16 B each
+    __shared__ uint64_t s_soff[kL2Lanes + 1];
+    __shared__ uint4 s_sstage[kSideVec + kStageSlackVec];
     const uint32_t t = threadIdx.x;
-    // Side job (SIDE, sh.n > 0): SHA-1 words of another batch, by workgroups of their own
-    // (blockIdx.x >= pgrid, two per CU) that run beside the sweep's: the sweep waits on its
-    // probes' memory (VALU busy ~0.22 at P = 8), so the hashing waves take the idle VALU instead
-    // of lengthening the sweep's own chains (r03 hashed tiles at the sweep workgroups' item
-    // tops, behind barriers: the sweep grew by the whole hash, profiles/r05f_sim_P8_dig.json).
-    // Each wave hashes tiles of 64 keys, one key per lane, with no barrier: a tile's key bytes
-    // (<= 1 KiB: one 16-B vector per lane) go into the wave's own LDS stage, and while it hashes
-    // tile i, tile i+1's offsets are in flight (then its bytes, while the loop comes round; a
-    // longer tile hashes from global memory).
-    constexpr uint32_t kHashVec = 64;   // one vector per lane
-    __shared__ uint4 s_hstage[SIDE ? (kL2Lanes / 64) * (kHashVec + kStageSlackVec) : 1];
-    if constexpr (SIDE) {
-        if (blockIdx.x >= pgrid) {   // workgroup-uniform: a hashing workgroup
-            constexpr uint32_t kWaves = kL2Lanes / 64;
-            const uint32_t lane = t & 63u, wv = t >> 6;
-            uint4* stage = s_hstage + wv * (kHashVec + kStageSlackVec);
-            const uint64_t hw = (uint64_t)(blockIdx.x - pgrid) * kWaves + wv;
-            const uint64_t nhw = (uint64_t)(gridDim.x - pgrid) * kWaves;
-            const uint64_t step = nhw * 64;
-            // key j's start (lane) and the tile's end (lane 63: offsets[j0 + 64]); j past n: n.  Raw
-            // offsets: the bias is added where they are used, so no wait follows the loads
-            auto load_offs = [&](uint64_t j0, uint64_t& ks, uint64_t& ke) {
-                const uint64_t j = j0 + lane < sh.n ? j0 + lane : sh.n;
-                ks = sh.offsets[j];
-                ke = sh.offsets[j0 + 64 < sh.n ? j0 + 64 : sh.n];
-            };
-            auto load_vec = [&](uint64_t ks, uint64_t ke, uint4& v) {   // the tile's bytes, if <= 1 KiB
-                const uint64_t a0 = __shfl(ks, 0) & ~(uint64_t)15, a1 = __shfl(ke, 63);
-                v = make_uint4(0, 0, 0, 0);
-                if (a1 - a0 <= kHashVec * 16 && a0 + lane * 16 < a1)
-                    v = reinterpret_cast<const uint4*>(sh.keys16 + a0)[lane];
-            };
-            uint64_t j0 = hw * 64;
-            if (j0 < sh.n) {
-                uint64_t ks0, ke0;
-                load_offs(j0, ks0, ke0);
-                ks0 += sh.bias;
-                ke0 += sh.bias;
-                uint4 v0;
-                load_vec(ks0, ke0, v0);
-                for (; j0 < sh.n; j0 += step) {
-                    // tile j0: offsets (ks0, ke0) and bytes v0 in registers
-                    const uint64_t a0 = __shfl(ks0, 0) & ~(uint64_t)15, a1 = __shfl(ke0, 63);
-                    const bool staged = __builtin_amdgcn_readfirstlane(a1 - a0 <= kHashVec * 16 ? 1u : 0u);   // (uniform)
-                    if (staged) stage[lane] = v0;
-                    const uint64_t j = j0 + lane;
-                    // (the shuffle outside the select: inside it lane 63 would be inactive, and a
-                    // ds_bpermute from an inactive lane reads 0 — lane 62's length would wrap)
-                    const uint64_t nks = __shfl_down(ks0, 1);
-                    const uint64_t L = (lane < 63 ? nks : ke0) - ks0;
-                    // the next tile's offsets arrive while this one hashes; its bytes are issued
-                    // right after, and arrive while the loop comes round
-                    uint64_t ks1 = 0, ke1 = 0;
-                    if (j0 + step < sh.n) load_offs(j0 + step, ks1, ke1);
-                    uint32_t H[5];
-                    if (staged)   // (the wave's own LDS: its stores above are ordered before these reads)
-                        sha1_key_staged(reinterpret_cast<const uint32_t*>(stage), (uint32_t)(ks0 - a0), (uint32_t)L, H);
-                    else {
-                        const uint64_t kbase = ks0 & ~(uint64_t)3;
-                        sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks0 - kbase),
-                                 (uint32_t)L, H);
-                    }
-                    if (j < sh.n) sh.dig[j] = make_uint4(H[0], H[1], H[2], H[3]);
-                    ks0 = ks1 + sh.bias;
-                    ke0 = ke1 + sh.bias;
-                    if (j0 + step < sh.n) load_vec(ks0, ke0, v0);
-                }
+    // Side job (sh.n > 0): SHA-1 words of another batch, one key per lane in tiles of kL2Lanes
+    // keys; tile T belongs to workgroup T % gridDim and is hashed at the top of one of its items
+    // (spread evenly), so hashing waves overlap other waves' probe latency, as the single-GPU
+    // include? kernel hashes the next insert batch (bf_include_hash_kernel).  A tile's key bytes
+    // are staged into LDS with one coalesced pass (a tile past the stage reads from global).
+    const uint64_t sh_tiles = (sh.n + kL2Lanes - 1) / kL2Lanes;
+    const uint64_t sh_mine = sh_tiles > blockIdx.x ? (sh_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+    uint64_t sh_done = 0;
+    auto side_hash = [&](uint64_t upto) {   // this workgroup's tiles [sh_done, upto); has barriers
+        for (; sh_done < upto; ++sh_done) {
+            const uint64_t j0 = (blockIdx.x + sh_done * gridDim.x) * kL2Lanes;
+            const uint32_t cnt = (uint32_t)(sh.n - j0 < kL2Lanes ? sh.n - j0 : kL2Lanes);
+            __syncthreads();   // the previous tile's readers of the stage are done
+            if (t < cnt) s_soff[t] = sh.offsets[j0 + t] + sh.bias;
+            if (t == 0) s_soff[cnt] = sh.offsets[j0 + cnt] + sh.bias;
+            __syncthreads();
+            const uint64_t abase = s_soff[0] & ~(uint64_t)15;
+            const uint64_t nvec = (s_soff[cnt] - abase + 15) >> 4;
+            const bool staged = nvec <= kSideVec;   // workgroup-uniform
+            if (staged) {
+                const uint4* gv = reinterpret_cast<const uint4*>(sh.keys16 + abase);
+                for (uint32_t v = t; v < (uint32_t)nvec; v += kL2Lanes) s_sstage[v] = gv[v];
             }
-            return;
+            __syncthreads();
+            if (t < cnt) {
+                const uint64_t ks = s_soff[t], L = s_soff[t + 1] - ks;
+                uint32_t H[5];
+                if (staged) {
+                    sha1_key_staged(reinterpret_cast<const uint32_t*>(s_sstage), (uint32_t)(ks - abase), (uint32_t)L, H);
+                } else {
+                    const uint64_t kbase = ks & ~(uint64_t)3;
+                    sha1_key(reinterpret_cast<const uint32_t*>(sh.keys16 + kbase), (uint32_t)(ks - kbase), (uint32_t)L, H);
+                }
+                sh.dig[j0 + t] = make_uint4(H[0], H[1], H[2], H[3]);
+            }
         }
-    }
+    };
     const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles;
     // XCD-local sweep: workgroup b runs on XCD b % 8 (round-robin dispatch; the grid is a
     // multiple of 8), and XCD x sweeps superbins x, x + 8, ..., its gridDim / 8 workgroups
     // sharing each superbin's items.  So each XCD's L2 holds one superbin, where a sweep of the
     // whole grid over one superbin made every XCD fetch the same lines (tools/probe_xcd.hip is
     // this layout: 178 G probes/s at 4 MiB per XCD).
-    const uint32_t xcd = blockIdx.x & 7u, g8 = pgrid >> 3;
+    const uint32_t xcd = blockIdx.x & 7u, g8 = gridDim.x >> 3;
     const uint64_t per_sb = (uint64_t)nq * parts;
     const uint64_t items = (uint64_t)((nsup + 7u - xcd) >> 3) * per_sb;   // this XCD's superbins
     const uint64_t k0 = blockIdx.x >> 3;
-    for (uint64_t k = k0; k < items; k += g8) {
+    const uint64_t my_items = items > k0 ? (items - 1 - k0) / g8 + 1 : 0;
+    uint64_t ii = 0;
+    for (uint64_t k = k0; k < items; k += g8, ++ii) {
+        if constexpr (SIDE) side_hash((ii + 1) * sh_mine / my_items);
         const uint32_t sb = xcd + 8u * (uint32_t)(k / per_sb);
         const uint64_t kk = k - (uint64_t)(k / per_sb) * per_sb;
         const uint32_t q = (uint32_t)(kk / parts), part = (uint32_t)(kk - (uint64_t)q * parts);
@@ -1618,6 +1589,7 @@ __global__ __launch_bounds__(kL2Lanes) __attribute__((amdgpu_waves_per_eu(8, 8))
                 }
         }
     }
+    if constexpr (SIDE) side_hash(sh_mine);
 }
 
 // bin_mid over chunked windows: window w = (superbin sb, chunk group q) concatenates sb's runs
@@ -2475,30 +2447,23 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
             const char* e = BF_AB_GETENV("BFHIP_L2_LOADS");
             return e && *e ? std::atoi(e) : kL2Loads;
         }();
-        // side hash: hashing workgroups beside the sweep's, two per CU by default (A/B:
-        // BFHIP_L2_HASH_GRID); they are the grid's last, so the sweep's XCD map is unchanged
-        [[maybe_unused]] static const uint32_t hgrid = [] {
-            const char* e = BF_AB_GETENV("BFHIP_L2_HASH_GRID");
-            const int v = e && *e ? std::atoi(e) : 0;
-            return v > 0 ? (uint32_t)v : 2 * apply_pipe_grid();
-        }();
         if (side.n)
-            hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid + hgrid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
-                               p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side, grid);
+            hipLaunchKernelGGL(chunk_test_l2_kernel<true>, dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits, p.nsup,
+                               p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
 #ifdef BFHIP_AB_KNOBS
         else if (walk && l2_loads == 16)   // (A/B: BFHIP_L2_LOADS, entries per lane in flight)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, true, 16>), dim3(grid), dim3(kL2Lanes), 0, s, ci,
-                               g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side, grid);
+                               g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         else if (walk && l2_loads == 4)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, true, 4>), dim3(grid), dim3(kL2Lanes), 0, s, ci,
-                               g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side, grid);
+                               g.bits, p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         else if (!walk)
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, false>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
-                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side, grid);
+                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
 #endif
         else
             hipLaunchKernelGGL((chunk_test_l2_kernel<false, true>), dim3(grid), dim3(kL2Lanes), 0, s, ci, g.bits,
-                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side, grid);
+                               p.nsup, p.ngroups, parts, c.gsum, c.runs, c.istart, out8, side);
         bf_mark(mk, s, side.n ? "test_l2_hash" : "test_l2");
         return hipGetLastError();
     }

@@ -437,6 +437,9 @@ class PartitionedFilter:
         self.replays = 0
         self._pk_seg = {}
         self._pending = None
+        # next_include (insert_include_dev): the SHA-1 words of the next call's include? batch,
+        # hashed by this call's owner test (kb, n, words); that call routes from them
+        self._next_inc = None
         # chunked windows (sync-free exchange on an engine that has them): the route sorts each
         # window's runs by the owner's superbin and sends a directory beside them, so the owner
         # skips its sort pass; BFHIP_CHUNKS=0 keeps the plain windows
@@ -650,7 +653,9 @@ class PartitionedFilter:
             self._chunk_geo[self._sf_n] = self.engine.chunk_info(max(self._sf_n, 1))
         return self._chunk_geo[self._sf_n]
 
-    def _sf_start(self, kb, ko, n: int, want_slot: bool) -> dict:
+    def _sf_start(self, kb, ko, n: int, want_slot: bool, dig=None) -> dict:
+        """dig: the batch's SHA-1 words (n x 4 int32), hashed earlier: a chunked route starts
+        from them (bf_route_chunks_digests_dev) instead of hashing the keys."""
         e, P, nh = self.engine, self.P, self.engine.nh
         if self._sf_n is None:
             self._agree_batch(n)
@@ -660,7 +665,9 @@ class PartitionedFilter:
         if geo is not None and n > self._sf_n:   # past the directory's tiles: overflow the windows instead
             geo = None
         dirb = None
-        if geo is not None:
+        if geo is not None and dig is not None:
+            send, slot, counts, dirb = e.route_chunks(dig, None, n, cap, geo[0], geo[1], want_slot=want_slot)
+        elif geo is not None:
             send, slot, counts, dirb = e.route_chunks(kb, ko, n, cap, geo[0], geo[1], want_slot=want_slot)
         elif self.chunks:
             # a batch the directories cannot hold: its windows are declared overflowed, so every
@@ -721,14 +728,22 @@ class PartitionedFilter:
         for h in range(nh):
             e.shard_insert_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h)
 
-    def _sf_answer(self, st: dict) -> torch.Tensor:
+    def _sf_answer(self, st: dict, next_include=None) -> torch.Tensor:
+        """next_include = (kb, ko, n): the owner test also hashes that batch (chunked windows
+        only); its words are kept for the call that brings it as its include? batch."""
         e, P, nh, cap, n = self.engine, self.P, self.engine.nh, st["cap"], st["n"]
         for w in st["works"]:
             w.wait()
         bits = self._buf(nh * P * cap, torch.uint8, st["recv"].device, answers=True)
         if st["geo"] is not None:
             tiles, dbytes = st["geo"]
-            e.shard_test_chunks(st["recv"], cap, P, st["rdir"], dbytes, tiles, st["rmsg"], nh + 1, bits)
+            nxt = None
+            if next_include is not None and next_include[2] and hasattr(e, "hash_keys"):
+                nkb, nko, nn = next_include
+                dig = torch.empty((nn, 4), dtype=torch.int32, device=st["recv"].device)
+                nxt = (nkb, nko, nn, dig)
+                self._next_inc = dict(kb=nkb, n=nn, dig=dig)
+            e.shard_test_chunks(st["recv"], cap, P, st["rdir"], dbytes, tiles, st["rmsg"], nh + 1, bits, nxt=nxt)
         else:
             for h in range(nh):
                 e.shard_test_windows(st["recv"][h * P * cap:(h + 1) * P * cap], cap, P, st["rmsg"], h, nh + 1, h,
@@ -807,12 +822,19 @@ class PartitionedFilter:
         return out
 
     def insert_include_dev(self, ikb: torch.Tensor, iko: torch.Tensor, ni: int,
-                           qkb: torch.Tensor, qko: torch.Tensor, nq: int, next_insert=None) -> torch.Tensor:
+                           qkb: torch.Tensor, qko: torch.Tensor, nq: int, next_insert=None,
+                           next_include=None) -> torch.Tensor:
         """insert_many_dev(ikb, iko, ni) then include_many_dev(qkb, qko, nq), exchanges overlapped.
 
         ``next_insert`` = (kb, ko, n), sync-free exchange only: the NEXT call's insert batch is
         routed and sent now, so its exchange runs beside this call's owner kernels; the next
-        call must then pass that same batch as (ikb, iko, ni)."""
+        call must then pass that same batch as (ikb, iko, ni).
+
+        ``next_include`` = (kb, ko, n), chunked windows only: this call's owner test also hashes
+        the NEXT call's include? batch (dedicated hashing workgroups beside the L2 sweep), and
+        that call routes it from the words instead of hashing it in its route.  The next call
+        must pass the same batch, unchanged, as (qkb, qko, nq) to use them (any other batch is
+        routed from its keys).  Answers are the same either way."""
         pend = self._pending
         if pend is not None and not (pend["kb"] is ikb and pend["n"] == ni):
             # Refused without touching the prefetch: completing it here would run collectives
@@ -830,13 +852,16 @@ class PartitionedFilter:
             # route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test |
             # send(back) | combine, all enqueued before the host waits for anything
             st_i = pend if pend is not None else self._sf_start(ikb, iko, ni, want_slot=False)
-            st_q = self._sf_start(qkb, qko, nq, want_slot=True)
+            ni_ = self._next_inc
+            self._next_inc = None
+            dig = ni_["dig"] if ni_ is not None and ni_["kb"] is qkb and ni_["n"] == nq else None
+            st_q = self._sf_start(qkb, qko, nq, want_slot=True, dig=dig)
             if next_insert is not None:
                 self._pending = self._sf_start(*next_insert, want_slot=False)
             self._sf_flag(st_i)
             self._sf_flag(st_q)
             self._sf_insert(st_i)
-            out = self._sf_answer(st_q)
+            out = self._sf_answer(st_q, next_include=next_include)
             if self._sf_overflowed(st_i) or self._sf_overflowed(st_q):
                 self.replays += 1
                 self._synced_insert(ikb, iko, ni)

@@ -509,8 +509,12 @@ def main():
     kb2, ko2, n2 = D._device_batch(mine[half:], dev or "cpu")
     qkb, qko, nq = D._device_batch(probe, dev or "cpu")
     pf6 = D.PartitionedFilter(m, k, block_log2=b, engine=engine(m, k, P, rank, b, orc, dev))
-    pf6.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2))
+    # (next_include: the first call's owner test hashes the second call's include? batch, which
+    # the second call then routes from the words — the chunked HIP engine's P = 8 form)
+    pf6.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2), next_include=(qkb, qko, nq))
+    routed_from_words = pf6._next_inc is not None or not pf6.chunks
     got6 = pf6.insert_include_dev(kb2, ko2, n2, qkb, qko, nq, next_insert=(kb1, ko1, n1))
+    same_shard = same_shard and routed_from_words
     pf6.drain_prefetch()
     got6 = got6.cpu().numpy().astype(bool)
     same_shard = same_shard and hashlib.sha1(pf6.engine.shard_export().tobytes()).hexdigest() == shard_sha
