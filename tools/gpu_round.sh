@@ -13,7 +13,8 @@
 #   bench10b / bench200b / bench100m   the other single-GPU configs
 #   prof       kernel trace (rocprofv3 --kernel-trace --stats) of a short bench run
 #   pmc        the PMC passes of tools/pmc_passes.sh on the north-star bench
-#   pmcsec     the same passes for every secondary workload (1m 1m_big 100m 10b lua_1m); then
+#   pmcsec     the same passes for every secondary workload (PMC_WORKLOADS, default 1m 1m_big 100m
+#              10b lua_1m); then
 #              python tools/pmc_finalize.py <tag> on the CPU host writes profiles/pmc_<tag>_*.json
 #   simP8      the P = 8 per-rank step (tools/sim_rank.py): time + stall/LDS + VALU counters
 #   simP8t     the P = 8 per-rank step, time only
@@ -75,7 +76,7 @@ for st in $STEPS; do
                     python bench.py --steps 5 --warmup 2 $NOEXTRA \
                     > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/bench_prof_${TAG}.err ;;
         pmc)    bash tools/pmc_passes.sh nstar ${TAG}_nstar ;;
-        pmcsec) for w in 1m 1m_big 100m 10b lua_1m; do
+        pmcsec) for w in ${PMC_WORKLOADS:-1m 1m_big 100m 10b lua_1m}; do
                     bash tools/pmc_passes.sh $w ${TAG}_$w || exit 1
                 done ;;
         simP8t) timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 \
