@@ -1,6 +1,7 @@
-"""The bench line's counters come from one final tree: the PMC summary
-(`pmc`), the HBM traffic (`roofline.traffic`) and the rocprof kernel means
-(`roofline.rocprof_source`) that bench.py reads for the north-star workload carry one round tag."""
+"""The bench line's counters come from one final tree: the PMC
+summaries of every workload the line reports (`pmc` of the main line and of every `secondary`),
+the HBM traffic (`roofline.traffic`) and the rocprof kernel means (`roofline.rocprof_source`)
+carry one round tag, and every one of them exists."""
 import json
 import os
 import re
@@ -28,3 +29,18 @@ def test_nstar_counters_share_one_tag():
     assert len(tags) == 1, (pmc, traffic_src, rocprof_src)
     for rel in ("profiles/" + pmc, traffic_src, rocprof_src):
         assert os.path.exists(os.path.join(ROOT, rel)), rel
+
+
+def test_every_workload_has_final_tree_counters():
+    import bench
+    want = {"nstar", "1m", "1m_big", "100m", "10b", "lua_1m"}
+    assert want <= set(bench.PMC_FILES)
+    tags = {_tag(f) for f in bench.PMC_FILES.values()}
+    assert tags == {bench.PMC_TAG}, tags
+    for w, f in bench.PMC_FILES.items():
+        path = os.path.join(ROOT, "profiles", f)
+        assert os.path.exists(path), path
+        with open(path) as fh:
+            doc = json.load(fh)
+        assert doc.get(w), (f, "no kernels for workload %s" % w)
+
