@@ -1311,8 +1311,10 @@ class ReplicatedPipeline:
 
     def __init__(self, rf: "ReplicatedFilter", batches, n: int, fused_hash: bool = True):
         self.rf, self.batches, self.n, self.L = rf, batches, n, len(batches)
-        if self.L < 3:
-            raise ArgumentError("ReplicatedPipeline needs at least 3 batches in its ring")
+        if self.L < 1:
+            raise ArgumentError("ReplicatedPipeline needs at least one batch")
+        # (pending gathers and sizes are keyed by batch index, each taken before it is set again,
+        # so any ring length works; the word buffers are keyed by step number)
         self.fused = fused_hash and rf.insert_mode == "sets"
         self.step = 0
         self.gpend, self.szp, self.dig = {}, {}, {}

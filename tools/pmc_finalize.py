@@ -20,13 +20,15 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
+PASSES = ("rd", "wr", "dram", "valu", "stall", "fs", "ws")   # tools/pmc_passes.sh
 BATCH = {"nstar": 1 << 24, "1m": 1 << 20, "1m_big": 1 << 24, "100m": 1 << 24, "10b": 1 << 24, "lua_1m": 1 << 20}
 
 
 def main():
     tag = sys.argv[1]
     for wl, batch in BATCH.items():
-        dirs = sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "pmc_%s_%s_*" % (tag, wl))))
+        # exactly this workload's passes ("1m_*" would also take "1m_big_*")
+        dirs = [os.path.join(ROOT, "gpurun_out", "pmc_%s_%s_%s" % (tag, wl, p)) for p in PASSES]
         dirs = [d for d in dirs if os.path.isdir(d)]
         if not dirs:
             continue

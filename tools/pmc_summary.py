@@ -26,7 +26,7 @@ KERNELS = {
     "bf_include_hash_kernel": re.compile(r"bf_include_hash_kernel"),
     "bf_keys_kernel<HASH>": re.compile(r"bf_keys_kernel<5>"),
     "digest_kernel<INCLUDE>": re.compile(r"bf_digest_kernel<1>"),
-    "digest_kernel<INSERT>": re.compile(r"bf_digest_kernel<2>"),
+    "digest_kernel<INSERT>": re.compile(r"bf_digest_kernel<[23]>"),   # (3: INSERT_FLAGS, any_new asked)
     "bin_front": re.compile(r"bin_front_kernel<false>"),
     "bin_front_digest": re.compile(r"bin_front_kernel<true>"),
     "bin_front_wide": re.compile(r"bin_front_wide_(dig_)?kernel"),
