@@ -2634,10 +2634,19 @@ __global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__
 
 // One workgroup per region: the region's probes (level 2, as bin_apply gathers them) into an
 // LDS bitmap, then each lane's WPL consecutive words -> its offsets in ascending order (their
-// ranks from one workgroup scan), the set built in the same LDS (the bitmap words are in
-// registers by then) and copied out.  72 KiB of LDS at 2^19-bit regions: two workgroups per CU.
+// ranks from one workgroup scan of the lanes' counts), and the set written from them.
+//   l >= 5 (at most U / 32 offsets, the sparse sets of every bench layout): each lane walks its
+//   offsets once, in one loop over all its words — the next non-zero word re-read from the
+//   bitmap, which stays intact — ORing every offset's low bits and upper-bitmap bit into a small
+//   LDS image of the set (at most 14 KB, in the dead run table), copied out whole.  The loop's
+//   trip count is the wave's largest per-lane offset count (~6 at the 10B layout), not the sum
+//   over the lane's words of the wave's largest per-word count (~22: the r04 form, where every
+//   word of every lane took at least one trip; VALU-bound).
+//   l < 5 (dense) and bitmap sets: assembled in the bitmap's own LDS after every lane has taken
+//   its words into registers.
+// 78 KiB of LDS at 2^19-bit regions: two workgroups per CU.
 template <uint32_t RLOG2, uint32_t LANES, int LOADS>
-__global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __restrict__ level2,
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES / 256))) void sets_encode_kernel(const uint32_t* __restrict__ level2,
                                                             const uint32_t* __restrict__ cb_base,
                                                             const uint32_t* __restrict__ cb_start,
                                                             const uint16_t* __restrict__ tabs, uint64_t max_chunks,
@@ -2645,17 +2654,17 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
                                                             const uint32_t* __restrict__ sb_first, uint32_t cap_words,
                                                             uint32_t stop) {
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
-    static_assert(WPL * LANES == NW && WPL % 4 == 0, "region words must tile the lanes in vectors");
-    // the gather's run table, then the upper bitmap of a compacted set (n <= NW, l >= 5: at
-    // most (NW + U / 32) / 32 + 1 words)
-    constexpr uint32_t UPW = (NW + U / 32) / 32 + 2;
-    constexpr uint32_t kRunLds = 2 * kRunsPerPass > UPW ? 2 * kRunsPerPass : UPW;
+    static_assert(WPL * LANES == NW && WPL % 4 == 0 && WPL <= 32, "region words must tile the lanes in vectors");
+    // the gather's run table, then a sparse set's image: at l >= 5 (n <= U / 2^l) the low bits
+    // take at most 5 NW / 32 words (l = 5) and the upper bitmap 2 NW / 32
+    constexpr uint32_t kSetLds = 5u * NW / 32u + 2u * NW / 32u + 2u;
+    constexpr uint32_t kRunLds = 2 * kRunsPerPass > kSetLds ? 2 * kRunsPerPass : kSetLds;
     __shared__ uint4 s_m4[NW / 4];
     __shared__ uint32_t s_runs[kRunLds], s_w[16];
     uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
     uint32_t* s_pre = s_runs;
     uint32_t* s_gst = s_runs + kRunsPerPass;
-    uint32_t* s_up = s_runs;
+    uint32_t* s_set = s_runs;
     const uint32_t t = threadIdx.x, r = blockIdx.x;
     // the region's reserved place: its superbin's first word + its prefix in the superbin
     // (sets_size_kernel / sets_place_kernel); loaded while the LDS image is cleared
@@ -2687,23 +2696,21 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
         return;
     }
 #endif
-    // the run table is dead (for_region_probes ends on a barrier); the scan's barriers below
-    // order these stores before the upper bitmap's first atomic
-    for (uint32_t v = t; v < UPW; v += LANES) s_up[v] = 0;
-    uint32_t wv[WPL];
-    uint32_t cnt = 0;
+    // the run table is dead (for_region_probes ends on a barrier): a sparse set's image is
+    // cleared; the scan's barriers below order these stores before its first atomic
+    for (uint32_t v = t; v < kSetLds; v += LANES) s_set[v] = 0;
+    // the lane's offset count and which of its words hold any (popcounts do not depend on the
+    // bit order inside a word)
+    uint32_t cnt = 0, nz = 0;
 #pragma unroll
     for (uint32_t q = 0; q < WPL / 4; ++q) {
         const uint4 v = s_m4[t * (WPL / 4) + q];
-        wv[4 * q + 0] = offset_order(v.x);
-        wv[4 * q + 1] = offset_order(v.y);
-        wv[4 * q + 2] = offset_order(v.z);
-        wv[4 * q + 3] = offset_order(v.w);
+        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        nz |= (v.x ? 1u : 0u) << (4 * q) | (v.y ? 2u : 0u) << (4 * q) | (v.z ? 4u : 0u) << (4 * q) |
+              (v.w ? 8u : 0u) << (4 * q);
     }
-#pragma unroll
-    for (uint32_t j = 0; j < WPL; ++j) cnt += __popc(wv[j]);
     uint32_t n;
-    const uint32_t base = block_excl_scan(cnt, s_w, &n);   // its barriers: every lane has read s_m
+    const uint32_t base = block_excl_scan(cnt, s_w, &n);
     uint32_t l = 0, lw = 0, uw = 0, words = 0;
     bool bitmap = false;
     if (n) {
@@ -2737,57 +2744,42 @@ __global__ __launch_bounds__(LANES) void sets_encode_kernel(const uint32_t* __re
     }
     const uint32_t lmask = (1u << l) - 1u;   // l <= RLOG2 < 32
     if (t == 0) o[0] = n | (l << 24);
-    // n <= NW: the offsets are compacted in rank order into the LDS the bitmap held (its words
-    // are in registers by now), then every output word is built by one lane from the offsets it
-    // covers: plain coalesced stores, no staging image, no atomics.  More offsets than that:
-    // the set is assembled in that LDS by atomics and copied out.
-    const bool compact = n <= NW;   // workgroup-uniform
-    if (!compact) {
-        for (uint32_t v = t; v < lw + uw; v += LANES) s_m[v] = 0;
-        __syncthreads();
-    }
-    uint32_t i = base;
-#pragma unroll
-    for (uint32_t j = 0; j < WPL; ++j) {
-        uint32_t w = wv[j];
-        const uint32_t x0 = (t * WPL + j) * 32u;
-        while (w) {
-            const uint32_t x = x0 + (uint32_t)__builtin_ctz(w);
-            w &= w - 1u;
-            if (compact) {   // the offset in rank order, and its upper-bitmap bit
-                s_m[i] = x;
-                const uint32_t u = (x >> l) + i;
-                atomicOr(s_up + (u >> 5), 1u << (u & 31u));
-            } else {
-                if (l) {
-                    const uint32_t bp = i * l, wi = bp >> 5, sh = bp & 31u, lo = x & lmask;
-                    atomicOr(s_m + wi, lo << sh);
-                    if (sh + l > 32u) atomicOr(s_m + wi + 1, lo >> (32u - sh));
-                }
-                const uint32_t u = lw * 32u + (x >> l) + i;
-                atomicOr(s_m + (u >> 5), 1u << (u & 31u));
+    // each lane's offsets in ascending order, low bits and upper-bitmap bit ORed into the set's
+    // words at lo / up (one loop over all the lane's words, see above)
+    auto walk = [&](uint32_t* lo_w, uint32_t* up_w) {
+        uint32_t i = base, bp = base * l, w = 0, xb = 0;
+        for (;;) {
+            if (!w) {   // the lane's next non-zero word, from the bitmap
+                if (!nz) break;
+                const uint32_t j = (uint32_t)__builtin_ctz(nz);
+                nz &= nz - 1u;
+                w = offset_order(s_m[t * WPL + j]);
+                xb = (t * WPL + j) * 32u;
             }
+            const uint32_t x = xb | (uint32_t)__builtin_ctz(w);
+            w &= w - 1u;
+            if (l) {
+                const uint32_t lo = x & lmask, sh = bp & 31u, wi = bp >> 5;
+                atomicOr(lo_w + wi, lo << sh);
+                if (sh + l > 32u) atomicOr(lo_w + wi + 1, lo >> (32u - sh));
+            }
+            const uint32_t u = (x >> l) + i;
+            atomicOr(up_w + (u >> 5), 1u << (u & 31u));
             ++i;
+            bp += l;
         }
-    }
-    __syncthreads();
-    if (!compact) {
-        for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_m[v];
+    };
+    if (l >= 5u) {   // workgroup-uniform: a sparse set (lw + uw <= kSetLds), built in LDS
+        walk(s_set, s_set + lw);
+        __syncthreads();
+        for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = s_set[v];
         return;
     }
-    // floor(b / l) as a multiply-high: b < 2^24, so ceil(2^32 / l) is exact for l <= 31
-    const uint32_t mg = l ? 0xFFFFFFFFu / l + 1u : 0u;
-    for (uint32_t wi = t; wi < lw; wi += LANES) {   // low bits: offsets floor(32 wi / l) ..
-        const uint32_t b0 = wi * 32u;
-        uint32_t word = 0;
-        for (uint32_t e = __umulhi(b0, mg); e < n && e * l < b0 + 32u; ++e) {
-            const uint32_t lo = s_m[e] & lmask;
-            const int32_t sh = (int32_t)(e * l) - (int32_t)b0;   // the field's start in this word
-            word |= sh >= 0 ? (lo << sh) : (lo >> (uint32_t)(-sh));
-        }
-        o[1 + wi] = word;
-    }
-    for (uint32_t ui = t; ui < uw; ui += LANES) o[1 + lw + ui] = s_up[ui];   // built during the compaction
+    // dense (more than U / 32 offsets, no bench layout): built in place in global memory, so
+    // that the bitmap stays readable
+    for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = 0;
+    __syncthreads();   // (a workgroup fence: the zeros are in memory before any lane's atomics)
+    walk(o + 1, o + 1 + lw);
 }
 
 // One workgroup per region: every source's set for the region ORed into an LDS image (bitmap
@@ -2906,32 +2898,29 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         const uint32_t pre = block_excl_scan(__popc(word), s_w, &tot);   // (its barriers also order the staging)
         if (word) {   // ~16 offsets: their low bits are consecutive
             const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
-            const uint32_t* lows = sets + (uint64_t)s * stride_words + s_st[s] + 1;
-            const uint32_t* slows = s_lows + s_lw0[s];
             const uint32_t lmask = (1u << l) - 1u;
-            uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
-            const uint32_t p0 = (g - s_uw0[s]) * 32u;
+            const uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
             const uint32_t lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
-            while (word) {
-                const uint32_t p = p0 + (uint32_t)__builtin_ctz(word);
-                word &= word - 1u;
-                uint32_t lo = 0;
-                if (l) {
-                    const uint32_t bp = i * l, wi = bp >> 5;
-                    uint32_t a, b;
-                    if (staged) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
-                        a = slows[min(wi, lim)];
-                        b = slows[min(wi, lim) + 1u];
-                    } else {
-                        a = lows[min(wi, lim)];
-                        b = lows[min(wi + 1u, lim)];
+            // offset i + e: high part p0 + (its bit in the word) - (i + e), low bits at (i + e) l.
+            // The two loops differ only in where the low bits are read (LDS stage or the set in
+            // global memory): one copy each, so neither reads through a flat (either-space) load.
+            auto decode = [&](const uint32_t* lw) {
+                uint32_t d = (g - s_uw0[s]) * 32u - i, bp = i * l;
+                while (word) {
+                    uint32_t lo = 0;
+                    if (l) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
+                        const uint32_t wi = min(bp >> 5, lim);
+                        lo = __builtin_amdgcn_alignbit(lw[wi + 1u], lw[wi], bp & 31u) & lmask;
                     }
-                    lo = (uint32_t)(((uint64_t)b << 32 | a) >> (bp & 31u)) & lmask;
+                    const uint32_t x = ((d + (uint32_t)__builtin_ctz(word)) << l) | lo;
+                    word &= word - 1u;
+                    if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
+                    --d;
+                    bp += l;
                 }
-                const uint32_t x = ((p - i) << l) | lo;
-                if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
-                ++i;
-            }
+            };
+            if (staged) decode(s_lows + s_lw0[s]);   // workgroup-uniform; s_lows[TL] is a readable 0
+            else decode(sets + (uint64_t)s * stride_words + s_st[s] + 1);
         }
         carry += tot;
     }

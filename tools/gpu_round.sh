@@ -20,10 +20,14 @@
 #   simP8t     the P = 8 per-rank step, time only
 #   repl       one replica's step of the replicated 10B x 8 and north-star x 2 layouts, per
 #              insert form
+#   replovl    the region-set replica steps, plain vs the next encode on a second stream (interleaved)
 #   replprof   kernel trace of the 10B x 8 region-set replica step
 #   replpmc    stall/LDS + VALU counters of the 10B x 8 region-set replica step
+#   ablib      one command (AB_CMD) over A/B libraries built side by side: AB_LIBS names ab_libs/<name>
+#              (interleaved, e.g. "old ab old ab"); lines appended to gpurun_out/ablib_<tag>.jsonl
 #   ab         an A/B over one environment variable: AB_VAR, AB_VALUES (interleaved, e.g.
-#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, repl10b, replnstar}; lines appended to
+#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, repl10b, replnstar,
+#              repl10bf, replnstarf (the fused-hash region-set steps)}; lines appended to
 #              gpurun_out/ab_${AB_VAR}_<tag>.jsonl.  The shipped library reads no A/B knob: the step
 #              loads AB_LIB (default ab_libs/ab/libbfhip.so, built on the CPU host by
 #              `bash tools/build_ab_libs.sh ab=-DBFHIP_AB_KNOBS`)
@@ -45,6 +49,10 @@ ab_cmd() {   # one A/B line's command, stdout = its JSON
         simP4)   timeout -k 10 120 python tools/sim_rank.py --shards 4 --chunks --steps 5 2>>"$ABERR" ;;
         repl10b) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 2>>"$ABERR" ;;
         replnstar) timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --steps 5 2>>"$ABERR" ;;
+        repl10bf) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash \
+                      --steps 3 2>>"$ABERR" ;;
+        replnstarf) timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --fused-hash \
+                      --steps 5 2>>"$ABERR" ;;
         *) echo "unknown AB_CMD $1" >&2; return 2 ;;
     esac
 }
@@ -97,6 +105,13 @@ for st in $STEPS; do
                     timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered $g --steps 5 \
                         >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
                 done ;;
+        replovl)   # the region-set replica step with the next encode beside the apply + include? (sim_rank --overlap-encode)
+                for o in "" "--overlap-encode apply" "--overlap-encode include" "" "--overlap-encode apply" "--overlap-encode include"; do
+                    timeout -k 10 240 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash $o \
+                        --steps 3 >> gpurun_out/sim_replovl_${TAG}.jsonl 2>> gpurun_out/sim_replovl_${TAG}.err &&
+                    timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --fused-hash $o \
+                        --steps 5 >> gpurun_out/sim_replovl_${TAG}.jsonl 2>> gpurun_out/sim_replovl_${TAG}.err || exit 1
+                done ;;
         replprof)
                 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sets_${TAG} -o run -- \
                     python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash --steps 3 \
@@ -115,6 +130,12 @@ for st in $STEPS; do
                     line=$(export "${AB_VAR:?}=$v"; ab_cmd "${AB_CMD:?}") || exit $?
                     echo "{\"var\": \"$AB_VAR\", \"value\": \"$v\", \"cmd\": \"$AB_CMD\", \"line\": $line}" \
                         >> gpurun_out/ab_${AB_VAR}_${TAG}.jsonl
+                done ;;
+        ablib)  ABERR=gpurun_out/ablib_${TAG}.err   # the same command over A/B libraries (ab_libs/<name>)
+                for lib in ${AB_LIBS:?}; do
+                    [ -f ab_libs/$lib/libbfhip.so ] || { echo "no A/B library ab_libs/$lib"; exit 2; }
+                    line=$(export BFHIP_LIB=$PWD/ab_libs/$lib/libbfhip.so; ab_cmd "${AB_CMD:?}") || exit $?
+                    echo "{\"lib\": \"$lib\", \"cmd\": \"$AB_CMD\", \"line\": $line}" >> gpurun_out/ablib_${TAG}.jsonl
                 done ;;
         *)      echo "unknown step $st"; exit 2 ;;
     esac || { echo "step $st failed: $?"; exit 1; }

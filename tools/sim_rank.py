@@ -56,6 +56,10 @@ def main():
                     help="--replicated --gathered sets: the own batch's SHA-1 words come out of the previous "
                          "step's include? kernel (bf_include_hash_dev) and the encode starts from them "
                          "(bench.py's pipelined replicated step)")
+    ap.add_argument("--overlap-encode", default="", choices=["", "apply", "include"],
+                    help="--replicated --gathered sets --fused-hash: the NEXT step's own encode runs on a second "
+                         "stream (a second handle) from the start of this step's apply, or of its include?; "
+                         "read the wall time")
     ap.add_argument("--dig", action="store_true",
                     help="--chunks: route the include? batch from SHA-1 words that the previous step's owner "
                          "test hashed between its probe rounds (bf_shard_test_chunks_hash_dev + "
@@ -310,23 +314,77 @@ def replicated(args, pkg):
             f.insert_many_dev(mkb.data_ptr(), mko.data_ptr(), nm, d_any_new=flag.data_ptr(), stream=sp)
         f.include_many_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), stream=sp)
 
-    if args.fused_hash:   # the pipeline's fill: the first step's own words
-        f.hash_many_dev(steps[0][0].data_ptr(), steps[0][1].data_ptr(), batch, own.data_ptr(), stream=sp)
-    step(steps[0], steps[1 % len(steps)])
-    torch.cuda.synchronize()
-    f.profile(True)
-    f.profile_read(reset=True)
-    t0 = time.perf_counter()
-    for j, s_ in enumerate(steps[1:], start=1):
-        step(s_, steps[(j + 1) % len(steps)])
-    torch.cuda.synchronize()
+    ovl = args.overlap_encode
+    if ovl:
+        assert args.gathered == "sets" and args.fused_hash
+        enc = pkg.Filter(m, k, device=0)   # the encoder: its own scratch, so its calls are not ordered
+        side = torch.cuda.Stream(dev)      # behind the main handle's
+        owns = [own, torch.empty_like(own)]
+        main_s = torch.cuda.current_stream(dev)
+
+        def step_ovl(j):
+            s_, n1, n2 = steps[j % len(steps)], steps[(j + 1) % len(steps)], steps[(j + 2) % len(steps)]
+            # side: the next step's own sets, from the words the previous include? hashed
+            side.wait_stream(main_s)
+            if ovl == "include":   # ... once this step's sets are in
+                main_s.wait_event(pend[0])
+                _, _, (qkb, qko), dg = s_
+                f.insert_region_sets_dev(dg.data_ptr(), cap_sets, R, R * batch * k, d_any_new=flag.data_ptr(),
+                                         stream=sp)
+                side.wait_stream(main_s)
+            enc.encode_region_sets_digests_dev(owns[(j + 1) % 2].data_ptr(), batch, n1[3].data_ptr(), cap_sets,
+                                               stream=side.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            # main: this step's sets (encoded during the previous step) in, then the include?
+            if ovl == "apply":
+                main_s.wait_event(pend[0])
+                _, _, (qkb, qko), dg = s_
+                f.insert_region_sets_dev(dg.data_ptr(), cap_sets, R, R * batch * k, d_any_new=flag.data_ptr(),
+                                         stream=sp)
+            f.include_hash_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), n2[0].data_ptr(),
+                               n2[1].data_ptr(), batch, owns[j % 2].data_ptr(), stream=sp)
+            pend[0] = ev
+
+        pend = [None]
+        # the pipeline's fill: batch 0's words and sets, batch 1's words
+        f.hash_many_dev(steps[0][0].data_ptr(), steps[0][1].data_ptr(), batch, owns[0].data_ptr(), stream=sp)
+        f.encode_region_sets_digests_dev(owns[0].data_ptr(), batch, steps[0][3].data_ptr(), cap_sets, stream=sp)
+        f.hash_many_dev(steps[1][0].data_ptr(), steps[1][1].data_ptr(), batch, owns[1].data_ptr(), stream=sp)
+        pend[0] = torch.cuda.Event()
+        pend[0].record(main_s)
+        step_ovl(0)
+        torch.cuda.synchronize()
+        f.profile(True)
+        f.profile_read(reset=True)
+        enc.profile(True)
+        enc.profile_read(reset=True)
+        t0 = time.perf_counter()
+        for j in range(1, args.steps + 1):
+            step_ovl(j)
+        torch.cuda.synchronize()
+    else:
+        if args.fused_hash:   # the pipeline's fill: the first step's own words
+            f.hash_many_dev(steps[0][0].data_ptr(), steps[0][1].data_ptr(), batch, own.data_ptr(), stream=sp)
+        step(steps[0], steps[1 % len(steps)])
+        torch.cuda.synchronize()
+        f.profile(True)
+        f.profile_read(reset=True)
+        t0 = time.perf_counter()
+        for j, s_ in enumerate(steps[1:], start=1):
+            step(s_, steps[(j + 1) % len(steps)])
+        torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.steps
     prof = f.profile_read(reset=True)
+    if ovl:
+        for name, (ms, n) in enc.profile_read(reset=True).items():
+            prof["side:" + name] = (ms, n)
+        enc.close()
     if os.environ.get("BFHIP_SETS_STOP", "0") == "0":   # (the encode stop-point A/B writes no sets)
         assert out.cpu().numpy()[: batch // 2].all(), "false negative"
     one = None
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
-           "fused_hash": bool(args.fused_hash), "m": m, "k": k,
+           "fused_hash": bool(args.fused_hash), "overlap_encode": ovl or None, "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
            "gathered_bytes_per_rank": (cap_sets if args.gathered == "sets" else
                                        batch * 16 if args.gathered == "digests" else None),
