@@ -2793,7 +2793,8 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
                                                            const uint32_t* __restrict__ sets, uint64_t stride_words,
                                                            uint32_t nsrc, uint32_t nbins, uint32_t dense,
                                                            uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
-                                                           uint32_t store_fresh, uint32_t* __restrict__ status) {
+                                                           uint32_t store_fresh, uint32_t* __restrict__ status,
+                                                           uint32_t xg) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);
     constexpr uint32_t kPer = kVec / LANES;
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32;
@@ -2805,7 +2806,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
     __shared__ uint32_t s_lows[STAGE + 1];   // every Elias-Fano source's low-bit words, back to back
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
-    const uint32_t r = blockIdx.x;
+    const uint32_t r = apply_region(blockIdx.x, gridDim.x, xg);
     const uint64_t v0 = (uint64_t)r * kVec;
     const uint64_t nvec = nwords / 4;
     uint4* gv = reinterpret_cast<uint4*>(bits);
@@ -3281,31 +3282,34 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
     hipLaunchKernelGGL(sets_size_kernel, dim3(p.nsup), dim3(1024), 0, s, c.tabs, c.cb_base, p.max_chunks, p.ngroups,
                        p.rel_log2, p.nbins, 1u << p.region_log2, out, c.stot);
     hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, out, c.stot, p.nsup, p.region_log2, p.nbins);
-    // level-2 loads per lane and gather step (BFHIP_SETS_ENC_LOADS A/B: 2, 4, 8)
-    [[maybe_unused]] static const int loads = [] {
+    // level-2 loads per lane and gather step, as bin_apply chooses them: 2 (a region's probes
+    // over all 16 waves) up to 4096 probes per region on average, else 8.  10B (~2k per region):
+    // 2.85 (2) / 2.94 (4) / 3.26 (8) ms, r04 encode; north star x 2 (~5.5k): 0.552 / 0.546 (2),
+    // 0.532 / 0.517 (4), 0.520 / 0.520 (8) ms (profiles/r04h_ab_sets_enc_loads.jsonl,
+    // r05w_ab_sets_enc_loads_nstar.jsonl).  BFHIP_SETS_ENC_LOADS (A/B) forces 1, 2, 4 or 8.
+    static const int forced = [] {
         const char* e = BF_AB_GETENV("BFHIP_SETS_ENC_LOADS");
-        const int v = e && *e ? std::atoi(e) : 2;
-        return v == 8 || v == 4 || v == 1 ? v : 2;
+        const int v = e && *e ? std::atoi(e) : 0;
+        return v == 8 || v == 4 || v == 2 || v == 1 ? v : 0;
     }();
+    const int loads = forced ? forced : (n * g.k <= (uint64_t)p.nbins * 4096u ? 2 : 8);
 #define BF_SETS_ENCODE(RL, LN, LD)                                                                              \
     hipLaunchKernelGGL((sets_encode_kernel<RL, LN, LD>), dim3(p.nbins), dim3(LN), 0, s, c.level2, c.cb_base,    \
                        c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot, (uint32_t)cap_words, \
                        sets_stop())
     if (p.region_log2 == 19) {
-#ifdef BFHIP_AB_KNOBS
         if (loads == 8) BF_SETS_ENCODE(19, kApplyLanes, 8);
+#ifdef BFHIP_AB_KNOBS
         else if (loads == 4) BF_SETS_ENCODE(19, kApplyLanes, 4);
         else if (loads == 1) BF_SETS_ENCODE(19, kApplyLanes, 1);
-        else
 #endif
-        BF_SETS_ENCODE(19, kApplyLanes, 2);
+        else BF_SETS_ENCODE(19, kApplyLanes, 2);
     } else if (p.region_log2 == 18) {
-#ifdef BFHIP_AB_KNOBS
         if (loads == 8) BF_SETS_ENCODE(18, kApplyLanes / 2, 8);
+#ifdef BFHIP_AB_KNOBS
         else if (loads == 4) BF_SETS_ENCODE(18, kApplyLanes / 2, 4);
-        else
 #endif
-        BF_SETS_ENCODE(18, kApplyLanes / 2, 2);
+        else BF_SETS_ENCODE(18, kApplyLanes / 2, 2);
     } else {
         return hipErrorInvalidValue;
     }
@@ -3327,6 +3331,12 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
     [[maybe_unused]] static const uint32_t stage = [] {
         const char* e = BF_AB_GETENV("BFHIP_SETS_STAGE");
         return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
+    // regions per XCD group (apply_region, as bin_apply): 2 measured 4.061 / 4.021 ms against
+    // 4.115 / 4.128 (1) at 10B x 8 (profiles/r05w_ab_sets_xg.jsonl).  BFHIP_SETS_XG (A/B) overrides.
+    static const uint32_t sets_xg = [] {
+        const char* e = BF_AB_GETENV("BFHIP_SETS_XG");
+        return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
     }();
 #ifdef BFHIP_AB_KNOBS
     // (A/B: BFHIP_SETS_PIPE=1 takes the persistent pipelined form for dense batches at 2^19-bit
@@ -3351,7 +3361,7 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
 #endif
 #define BF_SETS_APPLY(RL, LN, ST)                                                                              \
     hipLaunchKernelGGL((sets_apply_kernel<RL, LN, ST>), dim3(nbins), dim3(LN), 0, s, g.bits, nwords, src,       \
-                       stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status)
+                       stride_words, ns, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status, sets_xg)
         if (region_log2 == 19) {
 #ifdef BFHIP_AB_KNOBS
             if (stage == 0) BF_SETS_APPLY(19, kApplyLanes, 0);
