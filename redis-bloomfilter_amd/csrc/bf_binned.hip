@@ -1047,20 +1047,39 @@ __device__ __forceinline__ void for_region_probes(const uint32_t* __restrict__ c
             s_gst[t] = st;
         }
         __syncthreads();
-        // wave v takes kLoads * 64 consecutive entries per step: one binary search per
-        // wave and step, then each lane walks the run table forward
-        const uint32_t span = kLoads * 64u;
+        // wave v takes kLoads * 64 consecutive entries per step.  Its first entry's run: the
+        // count of run starts <= fw, one ballot per 64 table entries (the starts ascend, so
+        // they are a prefix); then every run start inside the wave's span moves the lanes
+        // past it one run on (a wave-uniform loop over the few starts there, ~2 at 10B).
+        // (Was a binary search per wave and a per-lane walk: ~100 VALU per wave and step.)
+        const uint32_t span = kLoads * 64u, lane = t & 63u;
         for (uint32_t fb = 0; fb < E; fb += span * (lanes >> 6)) {
             const uint32_t fw = fb + (t >> 6) * span;
-            uint32_t i = run_of(s_pre, nt, fw < E ? fw : E - 1);
             uint32_t idx[kLoads];
 #pragma unroll
-            for (int c = 0; c < kLoads; ++c) {
-                const uint32_t f = fw + c * 64 + (t & 63u);
-                idx[c] = 0xFFFFFFFFu;
-                if (f < E) {
-                    while (i + 1 < nt && s_pre[i + 1] <= f) ++i;
-                    idx[c] = s_gst[i] + (f - s_pre[i]);
+            for (int c = 0; c < kLoads; ++c) idx[c] = 0xFFFFFFFFu;
+            if (fw < E) {   // wave-uniform
+                uint32_t i0 = 0;
+                for (uint32_t b = 0; b < nt; b += 64u) {
+                    const uint32_t j = b + lane;
+                    const uint32_t c = (uint32_t)__popcll(__ballot(j < nt && s_pre[j] <= fw));
+                    if (c) i0 = b + c - 1u;
+                    if (c < 64u) break;
+                }
+                const uint32_t fend = E - fw < span ? E : fw + span;
+                uint32_t ic[kLoads];
+#pragma unroll
+                for (int c = 0; c < kLoads; ++c) ic[c] = i0;
+                for (uint32_t i = i0 + 1u; i < nt; ++i) {
+                    const uint32_t B = __builtin_amdgcn_readfirstlane(s_pre[i]);
+                    if (B >= fend) break;
+#pragma unroll
+                    for (int c = 0; c < kLoads; ++c) ic[c] += (fw + c * 64u + lane >= B) ? 1u : 0u;
+                }
+#pragma unroll
+                for (int c = 0; c < kLoads; ++c) {
+                    const uint32_t f = fw + c * 64u + lane;
+                    if (f < E) idx[c] = s_gst[ic[c]] + (f - s_pre[ic[c]]);
                 }
             }
             visit(idx);
