@@ -2849,7 +2849,7 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
             hdr = S[kSetsHdr + nbins + r];   // beside the place: one round trip
             if (st) {   // the set must lie inside the buffer: a damaged entry is skipped, not read
                 const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
-                const bool shape = n && n <= U && (l == kSetsBitmap || l <= RLOG2);
+                const bool shape = n && n <= U && (l == kSetsBitmap || (l >= 1u && l <= RLOG2));   // (EF: l >= 1)
                 const uint64_t need = !shape ? 0 : 1ull + (l == kSetsBitmap ? NW : (n * l + 31u) / 32u + (n + (U >> l) + 31u) / 32u);
                 if (!shape || (uint64_t)st + need > stride_words) {
                     ok = false;
@@ -2920,18 +2920,17 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
             const uint32_t n = s_hdr[s] & 0xFFFFFFu, l = s_hdr[s] >> 24;
             const uint32_t lmask = (1u << l) - 1u;
             const uint32_t i = carry + pre - s_np[s];   // rank of this word's first offset in its set
-            const uint32_t lim = l ? (n * l + 31u) / 32u - 1u : 0u;   // last low-bits word
+            const uint32_t lim = (n * l + 31u) / 32u - 1u;   // last low-bits word (l >= 1)
             // offset i + e: high part p0 + (its bit in the word) - (i + e), low bits at (i + e) l.
             // The two loops differ only in where the low bits are read (LDS stage or the set in
             // global memory): one copy each, so neither reads through a flat (either-space) load.
             auto decode = [&](const uint32_t* lw) {
                 uint32_t d = (g - s_uw0[s]) * 32u - i, bp = i * l;
                 while (word) {
-                    uint32_t lo = 0;
-                    if (l) {   // (a damaged set's ranks can pass n: reads stay inside its lows)
-                        const uint32_t wi = min(bp >> 5, lim);
-                        lo = __builtin_amdgcn_alignbit(lw[wi + 1u], lw[wi], bp & 31u) & lmask;
-                    }
+                    // (l >= 1 by the header check; a damaged set's ranks can pass n: reads stay
+                    // inside its lows)
+                    const uint32_t wi = min(bp >> 5, lim);
+                    const uint32_t lo = __builtin_amdgcn_alignbit(lw[wi + 1u], lw[wi], bp & 31u) & lmask;
                     const uint32_t x = ((d + (uint32_t)__builtin_ctz(word)) << l) | lo;
                     word &= word - 1u;
                     if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
@@ -3046,7 +3045,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
         if (t < 64) {
             if (t < nsrc && st) {
                 const uint32_t n = hdr & 0xFFFFFFu, l = hdr >> 24;
-                const bool shape = n && n <= U && (l == kSetsBitmap || l <= RLOG2);
+                const bool shape = n && n <= U && (l == kSetsBitmap || (l >= 1u && l <= RLOG2));   // (EF: l >= 1)
                 const uint64_t need = !shape ? 0 : 1ull + (l == kSetsBitmap ? NW : (n * l + 31u) / 32u +
                                                                                  (n + (U >> l) + 31u) / 32u);
                 if (!shape || (uint64_t)st + need > stride_words) {
