@@ -1113,9 +1113,13 @@ class ReplicatedFilter:
         draining the device.  A caller that starts the sizes one batch ahead of the gather (the
         bench's pipelined step) never makes the host wait for in-flight kernels."""
         z = torch.zeros(1, dtype=torch.int64, device=self.device)
-        lens = (ko[1: n + 1] - ko[:n]) if n else z[:0]
-        # (bytes, keys, longest key, first offset)
-        sizes = torch.cat([ko[n: n + 1] - ko[0:1], z + n, lens.max().view(1) if n else z, ko[0:1]])
+        # the key lengths (and the longest) only for the forms that gather key bytes: the region
+        # sets and SHA-1 word forms never read them, and at 2^24 keys they are a 134 MB pass
+        # plus a reduction on every step
+        need_lens = n and self.insert_mode not in ("sets", "digests")
+        lens = (ko[1: n + 1] - ko[:n]) if need_lens else z[:0]
+        # (bytes, keys, longest key (0 when not needed), first offset)
+        sizes = torch.cat([ko[n: n + 1] - ko[0:1], z + n, lens.max().view(1) if need_lens else z, ko[0:1]])
         all_sizes = torch.empty(self.P * 4, dtype=torch.int64, device=self.device)
         _all_gather_into_tensor(all_sizes, sizes, group=self.group)
         dev = all_sizes.is_cuda
