@@ -2797,7 +2797,8 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES
     // dense (more than U / 32 offsets, no bench layout): built in place in global memory, so
     // that the bitmap stays readable
     for (uint32_t v = t; v < lw + uw; v += LANES) o[1 + v] = 0;
-    __syncthreads();   // (a workgroup fence: the zeros are in memory before any lane's atomics)
+    __threadfence();   // every lane's zeros are complete in memory (the barrier alone does not
+    __syncthreads();   // wait for global stores) before any lane's atomics reach those words
     walk(o + 1, o + 1 + lw);
 }
 
