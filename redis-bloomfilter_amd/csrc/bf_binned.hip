@@ -2925,18 +2925,27 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
             // offset i + e: high part p0 + (its bit in the word) - (i + e), low bits at (i + e) l.
             // The two loops differ only in where the low bits are read (LDS stage or the set in
             // global memory): one copy each, so neither reads through a flat (either-space) load.
+            // Two offsets per trip: both low-bit reads are in flight together.
             auto decode = [&](const uint32_t* lw) {
                 uint32_t d = (g - s_uw0[s]) * 32u - i, bp = i * l;
                 while (word) {
                     // (l >= 1 by the header check; a damaged set's ranks can pass n: reads stay
                     // inside its lows)
-                    const uint32_t wi = min(bp >> 5, lim);
-                    const uint32_t lo = __builtin_amdgcn_alignbit(lw[wi + 1u], lw[wi], bp & 31u) & lmask;
-                    const uint32_t x = ((d + (uint32_t)__builtin_ctz(word)) << l) | lo;
+                    const uint32_t b0 = (uint32_t)__builtin_ctz(word);
                     word &= word - 1u;
-                    if (x < U) atomicOr(s_mask + (x >> 5), 1u << ((x ^ 7u) & 31u));
-                    --d;
-                    bp += l;
+                    const bool two = word != 0u;
+                    const uint32_t b1 = two ? (uint32_t)__builtin_ctz(word) : 0u;
+                    word &= two ? word - 1u : word;
+                    const uint32_t bq = bp + l;
+                    const uint32_t w0 = min(bp >> 5, lim), w1 = min(bq >> 5, lim);
+                    const uint32_t lo0 = __builtin_amdgcn_alignbit(lw[w0 + 1u], lw[w0], bp & 31u) & lmask;
+                    const uint32_t lo1 = __builtin_amdgcn_alignbit(lw[w1 + 1u], lw[w1], bq & 31u) & lmask;
+                    const uint32_t x0 = ((d + b0) << l) | lo0;
+                    const uint32_t x1 = ((d - 1u + b1) << l) | lo1;
+                    if (x0 < U) atomicOr(s_mask + (x0 >> 5), 1u << ((x0 ^ 7u) & 31u));
+                    if (two && x1 < U) atomicOr(s_mask + (x1 >> 5), 1u << ((x1 ^ 7u) & 31u));
+                    d -= two ? 2u : 1u;
+                    bp += two ? 2u * l : l;
                 }
             };
             if (staged) decode(s_lows + s_lw0[s]);   // workgroup-uniform; s_lows[TL] is a readable 0
