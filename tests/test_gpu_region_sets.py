@@ -201,7 +201,8 @@ def test_foreign_set_buffer_is_skipped(pkg):
 
 
 def test_damaged_region_entry_is_skipped(pkg, oracle):
-    """A region whose table entry points past its buffer, or whose header is not a set shape,
+    """A region whose table entry points past its buffer, or whose header is not a set shape
+    (l past the region size; an Elias-Fano set with l = 0, which the encoder never writes),
     is skipped and flagged; every other region of the buffer is applied as encoded."""
     torch = pytest.importorskip("torch")
     m, k = 9585058377, 6
@@ -213,9 +214,10 @@ def test_damaged_region_entry_is_skipped(pkg, oracle):
         words = sets.cpu().numpy().view(np.uint32).copy()
         _, rl, R, _ = sets_codec.header(words)
         want = sets_codec.expected(idx, rl)
-        bad = sorted(want)[:2]
+        bad = sorted(want)[:3]
         words[4 + bad[0]] = len(words) - 2            # a place whose set runs past the buffer
         words[4 + R + bad[1]] = (1 << 24) | (25 << 24)   # l = 26 > region_log2: not a set shape
+        words[4 + R + bad[2]] &= 0xFFFFFF                # l = 0: not an Elias-Fano set shape
         damaged = torch.from_numpy(words.view(np.int32)).cuda()
         status = torch.zeros(1, dtype=torch.int32, device="cuda")
         f.insert_region_sets_dev(damaged.data_ptr(), damaged.numel() * 4, 1, 50_000 * k,
