@@ -25,7 +25,8 @@
  *                      (the SETBITs that changed something: what write-through replays)
  *   bf_include_many    Ruby#include?                                  ruby.rb:20-30
  *   bf_indexes_many    Ruby#indexes_for (protected)                   ruby.rb:41-55
- *   bf_clear           Ruby#clear (DEL key_name)                      ruby.rb:33-35
+ *   bf_check_offsets   `data.to_s` of every key (a packed batch's offsets are consistent) ruby.rb:42
+ *   bf_clear          Ruby#clear (DEL key_name)                      ruby.rb:33-35
  *   bf_export_redis    GET key_name — the Redis string SETBIT builds  ruby.rb:59 (SETBIT layout)
  *   bf_import_redis    SET key_name — load a string written by the ruby driver
  *   bf_optimal_m/_k    Redis::Bloomfilter.optimal_m / optimal_k       lib/redis/bloomfilter.rb:50-58
@@ -152,7 +153,17 @@ int  bf_import_redis(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mo
 /* ---- device-resident API (device pointers; async on `stream`).
  *      Key bytes: the kernels read d_key_bytes in aligned 16-byte vectors, so the buffer
  *      must stay readable up to 16 bytes past d_key_bytes + d_offsets[n] (pad the
- *      allocation by 16 bytes; the host-pointer API does this in its staging copy). */
+ *      allocation by 16 bytes; the host-pointer API does this in its staging copy).
+ *      Key offsets: d_offsets[0..n] must be non-decreasing and every key shorter than 2 GiB
+ *      (ruby.rb:42 hashes `data.to_s`: every key has a finite length).  The host-pointer API
+ *      checks this before any copy; the device entry points cannot read the offsets without a
+ *      sync, so every hashing kernel checks each key against its tile's first and last
+ *      offsets (the rule bf_check_offsets applies) and hashes a key that fails as the empty
+ *      string — it never loops over a wrapped length or reads outside [d_offsets[0],
+ *      d_offsets[n]) — and the NEXT call on the handle (bf_sync at the latest) returns
+ *      BF_EINVAL once; the results of the call that met it are not meaningful. */
+int  bf_check_offsets(const uint64_t* offsets /* n+1 */, uint64_t n,
+                      uint64_t* bad_key /* nullable: the first key j the rule refuses */);
 int  bf_insert_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets,
                         uint64_t n, uint32_t* d_any_new /* nullable: OR-ed with 1 when a bit flips */,
                         uint8_t* d_per_key_new /* nullable */, void* stream);
@@ -261,7 +272,9 @@ int  bf_profile(bf_handle* h, uint32_t enable);
 int  bf_profile_read(bf_handle* h, char* names, double* total_ms, uint64_t* launches, uint32_t cap,
                      uint32_t* n_out, uint32_t reset);
 int  bf_stream(bf_handle* h, void** stream);   /* the handle's own (non-blocking) hipStream_t */
-int  bf_sync(bf_handle* h);                    /* synchronise the handle's own stream */
+int  bf_sync(bf_handle* h);                    /* synchronise the handle's own stream and the stream of its
+                                                  last call; BF_EINVAL if a kernel met inconsistent key
+                                                  offsets since the last call (see the *_dev API) */
 
 /* ---- partitioned filters (multi-GPU; the collective between the steps is the
  *      caller's, e.g. RCCL all-to-all through torch.distributed).

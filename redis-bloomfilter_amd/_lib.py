@@ -76,6 +76,7 @@ SIGNATURES = {
     "bf_include_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
     "bf_indexes_many": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp]),
     "bf_indexes": (ctypes.c_int, [_vp, _u64, _u64, _u32, _vp]),
+    "bf_check_offsets": (ctypes.c_int, [_vp, _u64, _u64p]),
     "bf_clear": (ctypes.c_int, [_vp]),
     "bf_export_redis": (ctypes.c_int, [_vp, _vp, _u64, _u64p]),
     "bf_import_redis": (ctypes.c_int, [_vp, _vp, _u64, _u32]),
@@ -222,6 +223,17 @@ def indexes(key: bytes, m: int, k: int) -> List[int]:
     out = np.zeros(max(int(k), 1), np.uint64)
     _check(load().bf_indexes(_ptr(buf), len(key), int(m), int(k), _ptr(out)))
     return [int(x) for x in out[: int(k)]]
+
+
+def check_offsets(offsets: np.ndarray) -> None:
+    """The key-offset rule every hashing kernel applies (bf_check_offsets): offsets[0..n]
+    non-decreasing, every key below 2 GiB.  Raises ArgumentError naming the first bad key.
+    Host-only: callers of the *_dev entry points can check their offsets before the upload."""
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if offs.size == 0:
+        raise ArgumentError("offsets needs n + 1 entries")
+    bad = ctypes.c_uint64()
+    _check(load().bf_check_offsets(_ptr(offs), offs.size - 1, ctypes.byref(bad)))
 
 
 def _ptr(a: Optional[np.ndarray]):

@@ -6,6 +6,7 @@
 #include "bfhip.h"
 #include "bf_internal.h"
 #include "bf_multi.h"
+#include "bf_device.h"   // bfdev::key_ok: bf_check_offsets applies the kernels' rule
 
 #include <sched.h>
 
@@ -180,6 +181,7 @@ struct bf_handle {
     uint32_t* d_flag = nullptr;
     unsigned long long* d_scan = nullptr;
     uint32_t* h_flag = nullptr;   // pinned
+    uint32_t* h_key_status = nullptr;   // pinned, written by the hashing kernels (take_key_status)
     // latency path of small host-pointer calls (run_small): one pinned and one device arena
     uint8_t* h_small = nullptr;
     uint8_t* d_small = nullptr;
@@ -208,6 +210,14 @@ namespace {
 // than the previous call's first waits for that call's last launch (hipStreamWaitEvent,
 // no host sync), so *_dev calls on two streams never race on the shared scratch or on
 // bin_apply's plain region stores.  Calls on one stream pay only an event record.
+// The key-status word (BfGeom::key_status, pinned host memory the kernels write): a hashing
+// kernel of an earlier call met a key whose offsets were inconsistent (offsets not
+// non-decreasing, or a key of 2 GiB or more) and hashed it as the empty key instead of running
+// off the key buffer or looping over a wrapped length (bfdev::key_ok).  The kernels run
+// asynchronously, so the error is reported once, as BF_EINVAL, by the next call on the handle
+// (bf_sync after the call at the latest), as the region-set status is checked lazily.
+int take_key_status(bf_handle* h);
+
 struct StreamOrder {
     bf_handle* h;
     hipStream_t s;
@@ -232,6 +242,13 @@ int set_err(bf_handle* h, int code, const char* fmt, ...) {
     va_end(ap);
     if (h) h->err = buf; else g_create_error = buf;
     return code;
+}
+
+int take_key_status(bf_handle* h) {
+    if (!h->h_key_status || __atomic_load_n(h->h_key_status, __ATOMIC_ACQUIRE) == 0u) return BF_OK;
+    __atomic_store_n(h->h_key_status, 0u, __ATOMIC_RELEASE);
+    return set_err(h, BF_EINVAL, "an earlier call's key offsets were inconsistent (offsets must be non-decreasing "
+                                 "and every key below 2 GiB): those keys were hashed as empty strings");
 }
 
 #define HIPCHK(h, expr)                                                                      \
@@ -740,6 +757,7 @@ int run_dev(bf_handle* h, BfOp op, const uint8_t* d_keys, const uint64_t* d_offs
     uint64_t bias = 0;
     const uint8_t* k16 = align_keys(d_keys, &bias);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     return launch_op(h, op, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, so.s);
 }
 
@@ -784,6 +802,23 @@ int bf_indexes(const uint8_t* key, uint64_t len, uint64_t m_bits, uint32_t k, ui
     if (e == hipSuccess) e = hipMemcpy(out, d_out, 8ull * k, hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return set_err(nullptr, BF_EDEVICE, "bf_indexes: %s", hipGetErrorString(e));
+    return BF_OK;
+}
+
+int bf_check_offsets(const uint64_t* offsets, uint64_t n, uint64_t* bad_key) {
+    // the rule every hashing kernel applies per key (bfdev::key_ok over the whole batch: the
+    // first and last offsets bound every key, each key's end is not before its start, and every
+    // key is below 2 GiB, the host path's cap)
+    if (bad_key) *bad_key = 0;
+    if (!offsets) return set_err(nullptr, BF_EINVAL, "offsets is NULL");
+    const uint64_t lo = offsets[0], hi = offsets[n];
+    for (uint64_t j = 0; j < n; ++j) {
+        if (!bfdev::key_ok(lo, offsets[j], offsets[j + 1], hi, nullptr)) {
+            if (bad_key) *bad_key = j;
+            return set_err(nullptr, BF_EINVAL, "key %llu: offsets must be non-decreasing and every key below 2 GiB",
+                           (unsigned long long)j);
+        }
+    }
     return BF_OK;
 }
 
@@ -894,6 +929,7 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
         if (h->d_flag) (void)hipFree(h->d_flag);
         if (h->d_scan) (void)hipFree(h->d_scan);
         if (h->h_flag) (void)hipHostFree(h->h_flag);
+        if (h->h_key_status) (void)hipHostFree(h->h_key_status);
         if (h->order_ev) (void)hipEventDestroy(h->order_ev);
         if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
@@ -913,6 +949,11 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     if ((e = hipMalloc((void**)&h->d_flag, 256)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(flag)", e);
     if ((e = hipMalloc((void**)&h->d_scan, 256)) != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(scan)", e);
     if ((e = hipHostMalloc((void**)&h->h_flag, 64, hipHostMallocDefault)) != hipSuccess) return fail(BF_ENOMEM, "hipHostMalloc", e);
+    if ((e = hipHostMalloc((void**)&h->h_key_status, 64, hipHostMallocDefault)) != hipSuccess)
+        return fail(BF_ENOMEM, "hipHostMalloc(key status)", e);
+    *h->h_key_status = 0u;
+    if ((e = hipHostGetDevicePointer((void**)&h->g.key_status, h->h_key_status, 0)) != hipSuccess)
+        return fail(BF_EDEVICE, "hipHostGetDevicePointer(key status)", e);
     if ((e = hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream)) != hipSuccess) return fail(BF_EDEVICE, "hipMemset", e);
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(BF_EDEVICE, "hipStreamSynchronize", e);
     h->g.m = m_bits;
@@ -963,6 +1004,7 @@ int bf_destroy(bf_handle* h) {
         if (h->d_flag) (void)hipFree(h->d_flag);
         if (h->d_scan) (void)hipFree(h->d_scan);
         if (h->h_flag) (void)hipHostFree(h->h_flag);
+        if (h->h_key_status) (void)hipHostFree(h->h_key_status);
         if (h->d_tmp_local) (void)hipFree(h->d_tmp_local);
         if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
         if (h->d_cursor) (void)hipFree(h->d_cursor);
@@ -999,6 +1041,7 @@ int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offse
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     const BfOp op = (any_new || per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
     StreamOrder so(h, h->stream);
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     int rc = run_host(h, op, key_bytes, offsets, n, per_key_new, nullptr, any_new);
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1025,6 +1068,7 @@ int bf_insert_many_changes(bf_handle* h, const uint8_t* key_bytes, const uint64_
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     return run_small(h, BF_OP_INSERT_FLAGS, key_bytes, offsets, n, nullptr, nullptr, out_bits, count);
 }
 
@@ -1036,6 +1080,7 @@ int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     return run_host(h, BF_OP_INCLUDE, key_bytes, offsets, n, out, nullptr, nullptr);
 }
 
@@ -1047,6 +1092,7 @@ int bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     return run_host(h, BF_OP_INDEXES, key_bytes, offsets, n, nullptr, out, nullptr);
 }
 
@@ -1069,7 +1115,8 @@ int bf_sync(bf_handle* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    return BF_OK;
+    if (h->order_valid) HIPCHK(h, hipEventSynchronize(h->order_ev));   // the last call, on whatever stream
+    return take_key_status(h);
 }
 
 }  // extern "C"
@@ -1079,6 +1126,7 @@ namespace {
 // Trimmed length of the first `max_bytes` bytes of the device bitset (Redis STRLEN after SETBITs).
 int device_trimmed_len(bf_handle* h, uint64_t* len_out) {
     StreamOrder so(h, h->stream);
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     HIPCHK(h, hipMemsetAsync(h->d_scan, 0, sizeof(unsigned long long), h->stream));
     HIPCHK(h, bf_launch_last_nonzero(h->g.bits, h->dev_bytes / 4, h->d_scan, h->stream));
     unsigned long long last = 0;
@@ -1112,6 +1160,7 @@ int import_bytes(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode, 
             return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)max_bits);
     }
     StreamOrder so(h, h->stream);
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 1, h->dirty_blocks, h->stream));
     if (mode == BF_IMPORT_REPLACE) {
         HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
@@ -1229,6 +1278,7 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
     BfBinPlan plan;
@@ -1289,6 +1339,7 @@ int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfBinPlan plan;
     if (n && !bf_route_plan(n, h->k, nwin, false, d_slot != nullptr, &plan))
@@ -1382,6 +1433,7 @@ int route_chunks_impl(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfBinPlan plan;
     if (n && !bf_route_plan(n, h->k, nwin, false, d_slot16 != nullptr, &plan))
@@ -1474,6 +1526,7 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     if ((rc = ensure_scratch(h, plan.scratch_bytes))) return rc;
     BfMarks* mk = prof_begin(h, s);
@@ -1483,6 +1536,7 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
         side.offsets = side_offsets;
         side.n = side_n;
         side.dig = reinterpret_cast<uint4*>(side_dig);
+        side.key_status = h->g.key_status;
     }
     if (test)
         HIPCHK(h, bf_launch_shard_test_chunks(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_bits, s, mk, side));
@@ -1536,6 +1590,7 @@ int bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const ui
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_chunks_packed(d_packed, d_slot16, window_cap, cg, h->shards * nh,
@@ -1555,6 +1610,7 @@ static int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     // Binned when the routed probes' random line fills clearly exceed a streaming pass
     // over the shard (same policy and knob as the whole-filter insert).
@@ -1618,6 +1674,7 @@ static int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     // Binned like the shard insert: routed probes carry no early exit (all k arrive), so
     // one streaming pass over the shard beats a random line fill per probe once the
@@ -1711,6 +1768,7 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, s));
@@ -1727,6 +1785,7 @@ int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows(d_bits, d_slot, window_cap, reinterpret_cast<const unsigned long long*>(d_counts),
@@ -1745,6 +1804,7 @@ int bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_pack_segments(d_bits, reinterpret_cast<const unsigned long long*>(d_seg), nseg, max_count,
@@ -1762,6 +1822,7 @@ int bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const u
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows_packed(d_packed, d_slot, window_cap,
@@ -1806,6 +1867,7 @@ static int run_digests(bf_handle* h, BfOp op, const uint32_t* d_dig, uint64_t n,
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     const uint4* dig = reinterpret_cast<const uint4*>(d_dig);
     const bool is_insert = op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS;
     BfBinPlan plan;
@@ -1842,6 +1904,7 @@ int bf_hash_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     uint64_t bias = 0;
     const uint8_t* k16 = align_keys(d_key_bytes, &bias);
     BfMarks* mk = prof_begin(h, so.s);
@@ -1878,6 +1941,7 @@ int bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     uint64_t bias = 0, nbias = 0;
     const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
     const uint8_t* nk16 = n_next ? align_keys(d_next_key_bytes, &nbias) : nullptr;
@@ -1940,6 +2004,7 @@ int encode_sets(bf_handle* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     if (n) {
         int rc = ensure_scratch(h, plan.scratch_bytes);
         if (rc) return rc;
@@ -1983,6 +2048,7 @@ int bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t str
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
     BfMarks* mk = prof_begin(h, so.s);
     HIPCHK(h, bf_launch_insert_sets(h->g, h->dev_bytes, rl, nbins, d_sets, stride_bytes / 4, nsrc, probes_hint,
                                     d_any_new, d_status, so.s, mk));

@@ -137,14 +137,14 @@ __device__ __forceinline__ void bin_front_body(BfGeom g, const uint8_t* __restri
             if (kTile + t < tk) H1 = dig[key0 + kTile + t];
         } else {
             for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off,
-                                           s_stage, [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                                           s_stage, g.key_status, [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
                 uint32_t H[5];
                 sha1_any<decltype(staged)::value>(src, s, L, H);
                 H0 = make_uint4(H[0], H[1], H[2], H[3]);
             });
             if (tk > (uint32_t)kTile) {   // workgroup-uniform: the second key of each lane
                 for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0 + kTile, tk - kTile, s_off, s_stage,
-                    [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                    g.key_status, [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
                         uint32_t H[5];
                         sha1_any<decltype(staged)::value>(src, s, L, H);
                         H1 = make_uint4(H[0], H[1], H[2], H[3]);
@@ -648,14 +648,14 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
             if (kTile + t < tk) H1 = dg[key0 + kTile + t];
         } else {
         for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk < (uint32_t)kTile ? tk : kTile, s_off, s_stage,
-            [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+            g.key_status, [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
                 uint32_t H[5];
                 sha1_any<decltype(staged)::value>(src, s, L, H);
                 H0 = make_uint4(H[0], H[1], H[2], H[3]);
             });
         if (tk > (uint32_t)kTile) {
             for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0 + kTile, tk - kTile, s_off, s_stage,
-                [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
+                g.key_status, [&](auto staged, uint32_t, const uint32_t* src, uint32_t s, uint32_t L) {
                     uint32_t H[5];
                     sha1_any<decltype(staged)::value>(src, s, L, H);
                     H1 = make_uint4(H[0], H[1], H[2], H[3]);
@@ -1514,7 +1514,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
             if (t == 0) s_soff[cnt] = sh.offsets[j0 + cnt] + sh.bias;
             __syncthreads();
             const uint64_t abase = s_soff[0] & ~(uint64_t)15;
-            const uint64_t nvec = (s_soff[cnt] - abase + 15) >> 4;
+            const uint64_t nvec = s_soff[cnt] >= s_soff[0] ? (s_soff[cnt] - abase + 15) >> 4 : ~0ull;
             const bool staged = nvec <= kSideVec;   // workgroup-uniform
             if (staged) {
                 const uint4* gv = reinterpret_cast<const uint4*>(sh.keys16 + abase);
@@ -1522,7 +1522,8 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
             }
             __syncthreads();
             if (t < cnt) {
-                const uint64_t ks = s_soff[t], L = s_soff[t + 1] - ks;
+                const bool ok = key_ok(s_soff[0], s_soff[t], s_soff[t + 1], s_soff[cnt], sh.key_status);
+                const uint64_t ks = ok ? s_soff[t] : (staged ? abase : 0), L = ok ? s_soff[t + 1] - ks : 0;
                 uint32_t H[5];
                 if (staged) {
                     sha1_key_staged(reinterpret_cast<const uint32_t*>(s_sstage), (uint32_t)(ks - abase), (uint32_t)L, H);

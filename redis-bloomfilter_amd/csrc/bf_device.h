@@ -232,15 +232,32 @@ __device__ __forceinline__ void owner_local(const BfGeom& g, uint64_t o, uint32_
 }
 
 
+// Longest key a kernel hashes: the host path's cap (bf_api.cpp run_host refuses keys of 2 GiB).
+constexpr uint64_t kMaxKeyBytes = 1ull << 31;
+
+// Whether key [a, b) of a tile whose offsets run from lo to hi may be hashed: lo <= a <= b <=
+// hi and b - a < kMaxKeyBytes.  Tiles chain (one tile's last offset is the next one's first),
+// so every key of a batch passing means offsets[0..n] is non-decreasing and every key lies
+// inside [offsets[0], offsets[n]).  A key that fails is hashed as the empty string (no byte
+// read) and *status (the handle's key-status word, nullable) gets 1: a wrapped length would
+// run ~2^26 SHA-1 blocks in one lane (round 5's hang came from a wrapped length) or read past
+// the key buffer.  Only failing lanes store; the comparisons cost a few VALU per key.
+__host__ __device__ __forceinline__ bool key_ok(uint64_t lo, uint64_t a, uint64_t b, uint64_t hi, uint32_t* status) {
+    const bool ok = lo <= a && a <= b && b <= hi && b - a < kMaxKeyBytes;
+    if (!ok && status) *status = 1u;
+    return ok;
+}
+
 // Stages one tile of up to TILE consecutive keys (offsets + packed bytes) into
 // LDS and hands each lane its key: f(lane, src_words, start_byte, len).  When the
-// tile's bytes exceed the stage, lanes read their key straight from global.
+// tile's bytes exceed the stage (or its offsets run backwards), lanes read their key straight
+// from global.  A key key_ok refuses is handed over as the empty key at byte 0.
 // Ends with a barrier, so the caller may restage the same LDS right after.
 template <int TILE, int STAGE_VEC, typename F>
 __device__ __forceinline__ void for_key_tile(const uint8_t* __restrict__ keys16,
                                              const uint64_t* __restrict__ offsets, uint64_t bias,
                                              uint64_t tile0, uint32_t cnt, uint64_t* s_off,
-                                             uint4* s_stage, F&& f) {
+                                             uint4* s_stage, uint32_t* key_status, F&& f) {
     const uint32_t t = threadIdx.x;
     if (t < cnt) s_off[t] = offsets[tile0 + t] + bias;
     if (t == 0) s_off[cnt] = offsets[tile0 + cnt] + bias;
@@ -248,19 +265,22 @@ __device__ __forceinline__ void for_key_tile(const uint8_t* __restrict__ keys16,
     const uint64_t start = s_off[0];
     const uint64_t end = s_off[cnt];
     const uint64_t abase = start & ~(uint64_t)15;
-    const uint64_t nvec = (end - abase + 15) >> 4;
+    const uint64_t nvec = end >= start ? (end - abase + 15) >> 4 : ~0ull;
     if (nvec <= (uint64_t)STAGE_VEC) {   // workgroup-uniform
         const uint4* gv = reinterpret_cast<const uint4*>(keys16 + abase);
         for (uint32_t v = t; v < (uint32_t)nvec; v += TILE) s_stage[v] = gv[v];
         __syncthreads();
-        if (t < cnt)
-            f(std::true_type{}, t, reinterpret_cast<const uint32_t*>(s_stage), (uint32_t)(s_off[t] - abase),
-              (uint32_t)(s_off[t + 1] - s_off[t]));
+        if (t < cnt) {
+            const bool ok = key_ok(start, s_off[t], s_off[t + 1], end, key_status);
+            f(std::true_type{}, t, reinterpret_cast<const uint32_t*>(s_stage), ok ? (uint32_t)(s_off[t] - abase) : 0u,
+              ok ? (uint32_t)(s_off[t + 1] - s_off[t]) : 0u);
+        }
     } else if (t < cnt) {
-        const uint64_t ks = s_off[t];
+        const bool ok = key_ok(start, s_off[t], s_off[t + 1], end, key_status);
+        const uint64_t ks = ok ? s_off[t] : 0;
         const uint64_t kbase = ks & ~(uint64_t)3;
         f(std::false_type{}, t, reinterpret_cast<const uint32_t*>(keys16 + kbase), (uint32_t)(ks - kbase),
-          (uint32_t)(s_off[t + 1] - ks));
+          ok ? (uint32_t)(s_off[t + 1] - ks) : 0u);
     }
     __syncthreads();
 }

@@ -141,8 +141,11 @@ __global__ __launch_bounds__(kLanes) void engine_kernel(BfGeom g, const uint8_t*
     if (t < total) {
         const uint64_t key = t / g.k;
         const uint32_t i = (uint32_t)(t - key * g.k);
-        const uint64_t s = offsets[key] + bias;
-        const uint32_t L = (uint32_t)(offsets[key + 1] - offsets[key]);
+        // a key whose offsets are inconsistent is hashed as the empty key (bfdev::key_ok)
+        const bool ok = bfdev::key_ok(offsets[0], offsets[key], offsets[key + 1], offsets[n],
+                                      i == 0 ? g.key_status : nullptr);
+        const uint64_t s = ok ? offsets[key] + bias : bias + offsets[0];
+        const uint32_t L = ok ? (uint32_t)(offsets[key + 1] - offsets[key]) : 0u;
         const uint64_t o = engine_offset<ENGINE>(keys16 + s, L, i, g.m);
         const uint64_t w = o >> 5;
         const uint32_t mask = 1u << ((uint32_t)(o ^ 7u) & 31u);

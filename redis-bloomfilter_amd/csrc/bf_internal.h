@@ -48,6 +48,10 @@ struct BfGeom {
     unsigned long long* flip_count;
     uint64_t  flip_cap;
     uint64_t  flip_tag;     // ORed into every reported offset (the Lua layout: layer << 58)
+    // nullable: the handle's key-status word (pinned host memory the device writes): a hashing
+    // kernel stores 1 when a key's offsets are inconsistent (bfdev::key_ok) and hashes that key
+    // as the empty string; the next call on the handle returns BF_EINVAL (bf_api.cpp)
+    uint32_t* key_status;
 };
 
 // BfGeom::mod_sub for a modulus m and the largest value the derivation reaches (ruby.rb:51:
@@ -245,6 +249,7 @@ struct BfSideHash {
     const uint64_t* offsets = nullptr;
     uint64_t bias = 0, n = 0;
     uint4* dig = nullptr;
+    uint32_t* key_status = nullptr;   // BfGeom::key_status of the handle
 };
 hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,

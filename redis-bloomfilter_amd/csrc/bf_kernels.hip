@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
     const uint64_t start = s_off[0];
     const uint64_t end = s_off[cnt];
     const uint64_t abase = start & ~(uint64_t)15;
-    const uint64_t nvec = (end - abase + 15) >> 4;
+    const uint64_t nvec = end >= start ? (end - abase + 15) >> 4 : ~0ull;
     const bool staged = nvec <= (uint64_t)kStageVec;   // workgroup-uniform
 
     uint32_t newflag = 0;
@@ -166,17 +166,19 @@ __global__ __launch_bounds__(kBlock) void bf_keys_kernel(BfGeom g, const uint8_t
         for (uint32_t v = t; v < (uint32_t)nvec; v += kBlock) s_stage[v] = gv[v];
         __syncthreads();
         if (t < cnt) {
-            const uint32_t s = (uint32_t)(s_off[t] - abase);
-            const uint32_t L = (uint32_t)(s_off[t + 1] - s_off[t]);
+            const bool ok = key_ok(start, s_off[t], s_off[t + 1], end, g.key_status);   // else the empty key
+            const uint32_t s = ok ? (uint32_t)(s_off[t] - abase) : 0u;
+            const uint32_t L = ok ? (uint32_t)(s_off[t + 1] - s_off[t]) : 0u;
             const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_stage);
             key_op<OP, true>(g, sw, s, L, blk0 + t, out8, out64, newflag, s_hist);
         }
     } else if (t < cnt) {
         // Span too large for the stage (long keys): read each key straight from global.
-        const uint64_t ks = s_off[t];
+        const bool ok = key_ok(start, s_off[t], s_off[t + 1], end, g.key_status);
+        const uint64_t ks = ok ? s_off[t] : 0;
         const uint64_t kbase = ks & ~(uint64_t)3;
         const uint32_t* gw = reinterpret_cast<const uint32_t*>(keys16 + kbase);
-        const uint64_t L64 = s_off[t + 1] - ks;
+        const uint64_t L64 = ok ? s_off[t + 1] - ks : 0;
         key_op<OP, false>(g, gw, (uint32_t)(ks - kbase), (uint32_t)L64, blk0 + t, out8, out64, newflag, s_hist);
     }
 
@@ -228,7 +230,7 @@ __device__ __forceinline__ bool stage_tile(const uint8_t* __restrict__ keys16, c
     const uint64_t start = s_off[0];
     const uint64_t end = s_off[cnt];
     const uint64_t abase = start & ~(uint64_t)15;
-    const uint64_t nvec = (end - abase + 15) >> 4;
+    const uint64_t nvec = end >= start ? (end - abase + 15) >> 4 : ~0ull;
     *abase_out = abase;
     if (nvec > (uint64_t)kHalfStageVec) return false;
     const uint4* gv = reinterpret_cast<const uint4*>(keys16 + abase);
@@ -237,17 +239,19 @@ __device__ __forceinline__ bool stage_tile(const uint8_t* __restrict__ keys16, c
     return true;
 }
 
+// Key t of a staged tile of cnt keys (a key bfdev::key_ok refuses: the empty key).
 __device__ __forceinline__ void hash_tile_key(const uint8_t* __restrict__ keys16, const uint64_t* s_off,
                                               const uint4* s_stage, bool staged, uint64_t abase, uint32_t t,
-                                              uint32_t H[5]) {
+                                              uint32_t cnt, uint32_t* key_status, uint32_t H[5]) {
+    const bool ok = key_ok(s_off[0], s_off[t], s_off[t + 1], s_off[cnt], key_status);
     if (staged) {
-        sha1_key_staged(reinterpret_cast<const uint32_t*>(s_stage), (uint32_t)(s_off[t] - abase),
-                        (uint32_t)(s_off[t + 1] - s_off[t]), H);
+        sha1_key_staged(reinterpret_cast<const uint32_t*>(s_stage), ok ? (uint32_t)(s_off[t] - abase) : 0u,
+                        ok ? (uint32_t)(s_off[t + 1] - s_off[t]) : 0u, H);
     } else {
-        const uint64_t ks = s_off[t];
+        const uint64_t ks = ok ? s_off[t] : 0;
         const uint64_t kbase = ks & ~(uint64_t)3;
         sha1_key(reinterpret_cast<const uint32_t*>(keys16 + kbase), (uint32_t)(ks - kbase),
-                 (uint32_t)(s_off[t + 1] - ks), H);
+                 ok ? (uint32_t)(s_off[t + 1] - ks) : 0u, H);
     }
 }
 
@@ -275,13 +279,13 @@ __global__ __launch_bounds__(kBlock) void bf_include_hash_kernel(BfGeom g, const
     auto side = [&]() {
         if (t < scnt) {
             uint32_t H[5];
-            hash_tile_key(skeys16, s_soff, s_sstage, sstaged, sabase, t, H);
+            hash_tile_key(skeys16, s_soff, s_sstage, sstaged, sabase, t, scnt, g.key_status, H);
             sdig[blk0 + t] = make_uint4(H[0], H[1], H[2], H[3]);
         }
     };
     if (t < cnt) {
         uint32_t H[5];
-        hash_tile_key(keys16, s_off, s_stage, qstaged, abase, t, H);
+        hash_tile_key(keys16, s_off, s_stage, qstaged, abase, t, cnt, g.key_status, H);
         uint32_t newflag = 0;
         digest_op<BF_OP_INCLUDE>(g, H, blk0 + t, out8, nullptr, newflag, nullptr, side);
     } else {
@@ -491,14 +495,35 @@ __global__ __launch_bounds__(256) void combine_windows_kernel(const uint8_t* __r
 
 // Answer bytes -> bits for the return trip of a partitioned include?: segment q =
 // (src offset, count, dst byte offset) packs bits[src .. src + count) LSB-first into
-// ceil(count / 8) bytes at packed[dst].  One grid row per segment.
+// ceil(count / 8) bytes at packed[dst].  One grid row per segment.  A segment whose source is
+// 16-B aligned and whose destination is 4-B aligned (every window of the sync-free exchange:
+// caps are multiples of 12288) takes 32 answer bytes per lane in two 16-B loads and stores one
+// u32: each 8 bytes fold to a byte by one multiply (the bytes are 0 or 1; bit 8i -> bit 56 + i).
+// (The byte-per-load form ran at 0.74 TB/s: 0.33 ms per 218M answers at 200B x 8.)
+__device__ __forceinline__ uint32_t pack8(uint64_t x) {
+    return (uint32_t)(((x & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+}
+
 __global__ __launch_bounds__(256) void pack_segments_kernel(const uint8_t* __restrict__ bits,
                                                             const unsigned long long* __restrict__ seg,
                                                             uint8_t* __restrict__ packed) {
     const unsigned long long src = seg[3 * blockIdx.y], cnt = seg[3 * blockIdx.y + 1], dst = seg[3 * blockIdx.y + 2];
     const uint64_t nbytes = (cnt + 7) / 8;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nbytes; b += stride) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t b0 = 0;   // packed bytes done by the vector loop
+    if (((src & 15u) | (dst & 3u)) == 0) {   // segment-uniform
+        const uint64_t nw = cnt / 32;   // whole u32 words of output
+        const uint4* in = reinterpret_cast<const uint4*>(bits + src);
+        uint32_t* out = reinterpret_cast<uint32_t*>(packed + dst);
+        for (uint64_t w = t0; w < nw; w += stride) {
+            const uint4 a = in[2 * w], b = in[2 * w + 1];
+            out[w] = pack8(((uint64_t)a.y << 32) | a.x) | (pack8(((uint64_t)a.w << 32) | a.z) << 8) |
+                     (pack8(((uint64_t)b.y << 32) | b.x) << 16) | (pack8(((uint64_t)b.w << 32) | b.z) << 24);
+        }
+        b0 = nw * 4;
+    }
+    for (uint64_t b = b0 + t0; b < nbytes; b += stride) {   // the tail (or an unaligned segment)
         uint32_t v = 0;
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i)
@@ -652,7 +677,7 @@ hipError_t bf_launch_combine_windows(const uint8_t* bits, const uint32_t* slot, 
 hipError_t bf_launch_pack_segments(const uint8_t* bits, const unsigned long long* seg, uint32_t nseg,
                                    uint64_t max_count, uint8_t* packed, hipStream_t s) {
     if (nseg == 0 || max_count == 0) return hipSuccess;
-    uint32_t gx = stream_grid((max_count + 7) / 8) / nseg;
+    uint32_t gx = stream_grid((max_count + 31) / 32) / nseg;   // a lane per 32 answers
     hipLaunchKernelGGL(pack_segments_kernel, dim3(gx ? gx : 1u, nseg), dim3(256), 0, s, bits, seg, packed);
     return hipGetLastError();
 }

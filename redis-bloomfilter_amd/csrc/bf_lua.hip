@@ -40,12 +40,13 @@ thread_local std::string g_lua_create_error;
 __global__ __launch_bounds__(kLuaTile) void lua_check_kernel(const BfGeom* __restrict__ layers, uint32_t nlayers,
                                                              const uint8_t* __restrict__ keys16,
                                                              const uint64_t* __restrict__ offsets, uint64_t bias,
-                                                             uint64_t n, uint8_t* __restrict__ out) {
+                                                             uint64_t n, uint8_t* __restrict__ out,
+                                                             uint32_t* __restrict__ key_status) {
     __shared__ uint64_t s_off[kLuaTile + 1];
     __shared__ uint4 s_stage[kLuaStageVec + kStageSlackVec];
     const uint64_t tile0 = (uint64_t)blockIdx.x * kLuaTile;
     const uint32_t cnt = (uint32_t)((n - tile0) < (uint64_t)kLuaTile ? (n - tile0) : kLuaTile);
-    for_key_tile<kLuaTile, kLuaStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage,
+    for_key_tile<kLuaTile, kLuaStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage, key_status,
         [&](auto staged, uint32_t lane, const uint32_t* src, uint32_t s, uint32_t L) {
             uint32_t H[5];
             sha1_any<decltype(staged)::value>(src, s, L, H);
@@ -120,6 +121,8 @@ struct bf_lua {
     uint8_t* h_stage = nullptr;              // pinned [offsets | keys] of small calls (one H2D)
     unsigned long long* d_cnt = nullptr;     // lua_count_kernel's sum (device calls)
     unsigned long long* h_cnt = nullptr;     // ... read back through pinned memory
+    uint32_t* h_key_status = nullptr;        // pinned, written by the hashing kernels (bf_api.cpp take_key_status)
+    uint32_t* d_key_status = nullptr;        // ... its device address (every layer's BfGeom::key_status)
     // calls on different streams (the _dev entry points take the caller's) are ordered: each
     // waits for the event the previous call recorded, as bf_handle's calls are
     hipEvent_t order_ev = nullptr;
@@ -227,6 +230,7 @@ int ensure_layer(bf_lua* h, uint32_t n) {
         g.shards = 1;
         g.inv_shards = 1.0;
         g.block_log2 = 20;
+        g.key_status = h->d_key_status;
         h->layers.push_back(g);
         h->layer_bytes.push_back(bytes);
     }
@@ -253,6 +257,15 @@ int ensure_io(bf_lua* h, uint64_t key_bytes, uint64_t n) {
         LUACHK(h, hipHostMalloc((void**)&h->h_out, h->n_cap, hipHostMallocDefault));
     }
     return BF_OK;
+}
+
+// The key-status word the hashing kernels write (bfdev::key_ok): reported once, as BF_EINVAL,
+// by the next call on the handle (bf_api.cpp take_key_status).
+int lua_take_key_status(bf_lua* h) {
+    if (!h->h_key_status || __atomic_load_n(h->h_key_status, __ATOMIC_ACQUIRE) == 0u) return BF_OK;
+    __atomic_store_n(h->h_key_status, 0u, __ATOMIC_RELEASE);
+    return lua_err(h, BF_EINVAL, "an earlier call's key offsets were inconsistent (offsets must be non-decreasing "
+                                 "and every key below 2 GiB): those keys were hashed as empty strings");
 }
 
 // Stream order across calls (bf_api.cpp's StreamOrder): wait for the previous call's event,
@@ -401,8 +414,12 @@ int bf_lua_create(double entries, double precision, const bf_config* cfg, bf_lua
         hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming) != hipSuccess ||
         hipMalloc((void**)&h->d_layers, kLuaMaxLayers * sizeof(BfGeom)) != hipSuccess ||
         hipMalloc((void**)&h->d_last, 64) != hipSuccess || hipMalloc((void**)&h->d_cnt, 64) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_cnt, 64, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&h->h_cnt, 64, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_key_status, 64, hipHostMallocDefault) != hipSuccess ||
+        (*h->h_key_status = 0u, hipHostGetDevicePointer((void**)&h->d_key_status, h->h_key_status, 0)) != hipSuccess) {
         if (h->stream) (void)hipStreamDestroy(h->stream);
+        if (h->h_cnt) (void)hipHostFree(h->h_cnt);
+        if (h->h_key_status) (void)hipHostFree(h->h_key_status);
         if (h->order_ev) (void)hipEventDestroy(h->order_ev);
         if (h->d_layers) (void)hipFree(h->d_layers);
         if (h->d_last) (void)hipFree(h->d_last);
@@ -438,6 +455,7 @@ int bf_lua_destroy(bf_lua* h) {
         if (h->h_out) (void)hipHostFree(h->h_out);
         if (h->h_flips) (void)hipHostFree(h->h_flips);
         if (h->h_stage) (void)hipHostFree(h->h_stage);
+        if (h->h_key_status) (void)hipHostFree(h->h_key_status);
         (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -495,6 +513,7 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, h->stream);
+    if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     int rc = stage_keys(h, keys, offsets, n);
     if (rc) return rc;
     unsigned long long* d_flips = nullptr;
@@ -610,6 +629,7 @@ int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, s);
+    if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     uint64_t bias = 0;
     const uintptr_t a = reinterpret_cast<uintptr_t>(d_keys);
     bias = a & 15u;
@@ -697,6 +717,7 @@ int bf_lua_include_many_dev(bf_lua* h, const uint8_t* d_key_bytes, const uint64_
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, s);
+    if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     if (h->count == 0) {   // check.lua:3-7
         LUACHK(h, hipMemsetAsync(d_out, 0, n, s));
         return BF_OK;
@@ -713,7 +734,7 @@ int bf_lua_include_many_dev(bf_lua* h, const uint8_t* d_key_bytes, const uint64_
     BfMarks* mk = lua_prof_begin(h, s);
     hipLaunchKernelGGL(lua_check_kernel, dim3((uint32_t)((n + kLuaTile - 1) / kLuaTile)), dim3(kLuaTile), 0, s,
                        h->d_layers, index, reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15), d_offsets,
-                       (uint64_t)(a & 15u), n, d_out);
+                       (uint64_t)(a & 15u), n, d_out, h->d_key_status);
     LUACHK(h, hipGetLastError());
     bf_mark(mk, s, lua_prof_name(h, kLuaCheck, index));
     return BF_OK;
@@ -770,6 +791,7 @@ int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets,
     }
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, h->stream);
+    if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     const uint32_t index = lua_index(h->entries, (double)h->count);   // check.lua:9-11
     int rc = ensure_layer(h, index);
     if (rc) return rc;
@@ -781,7 +803,8 @@ int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets,
     }
     BfMarks* mk = lua_prof_begin(h, h->stream);
     hipLaunchKernelGGL(lua_check_kernel, dim3((uint32_t)((n + kLuaTile - 1) / kLuaTile)), dim3(kLuaTile), 0,
-                       h->stream, h->d_layers, index, h->d_keys, h->d_off, (uint64_t)0, n, h->d_out);
+                       h->stream, h->d_layers, index, h->d_keys, h->d_off, (uint64_t)0, n, h->d_out,
+                       h->d_key_status);
     LUACHK(h, hipGetLastError());
     bf_mark(mk, h->stream, lua_prof_name(h, kLuaCheck, index));
     LUACHK(h, hipMemcpyAsync(out, h->d_out, n, hipMemcpyDeviceToHost, h->stream));
@@ -796,6 +819,7 @@ int bf_lua_export_layer(bf_lua* h, uint32_t layer, uint8_t* buf, uint64_t cap, u
     if (layer == 0 || layer > h->layers.size()) return BF_OK;   // a layer never written: absent key
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, h->stream);
+    if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     const BfGeom& g = h->layers[layer - 1];
     LUACHK(h, hipMemsetAsync(h->d_last, 0, 8, h->stream));
     LUACHK(h, bf_launch_last_nonzero(g.bits, h->layer_bytes[layer - 1] / 4, h->d_last, h->stream));
@@ -822,6 +846,7 @@ int bf_lua_import_layer(bf_lua* h, uint32_t layer, const uint8_t* buf, uint64_t 
     std::lock_guard<std::mutex> lk(h->mu);
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, h->stream);
+    if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     int rc = ensure_layer(h, layer);
     if (rc) return rc;
     const BfGeom& g = h->layers[layer - 1];

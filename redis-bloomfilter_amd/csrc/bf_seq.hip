@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kSeqTile) void seq_candidates_kernel(BfGeom g, uint
     __shared__ uint4 s_stage[kSeqStageVec + kStageSlackVec];
     const uint64_t tile0 = (uint64_t)blockIdx.x * kSeqTile;
     const uint32_t cnt = (uint32_t)((n - tile0) < (uint64_t)kSeqTile ? (n - tile0) : kSeqTile);
-    for_key_tile<kSeqTile, kSeqStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage,
+    for_key_tile<kSeqTile, kSeqStageVec>(keys16, offsets, bias, tile0, cnt, s_off, s_stage, g.key_status,
         [&](auto staged, uint32_t lane, const uint32_t* src, uint32_t s, uint32_t L) {
             uint32_t H[5];
             sha1_any<decltype(staged)::value>(src, s, L, H);
@@ -140,12 +140,13 @@ uint64_t seq_slots(uint64_t n, uint32_t k) {
     return s;
 }
 
-// One uint32 per filter bit when that table is at most twice the hash table's bytes (so its
-// clear costs no more) and at most 1 GiB: the Lua layout's 1M-scale layers (11M bits against
-// a 16M-slot table for a 2^20-key chunk), small filters under big batches.  Probe updates are
-// then one atomicMin each, with no claim loop.
+// One uint32 per filter bit when that table is no bigger than the hash table (12 B per slot),
+// so neither its clear nor the scratch grows, and at most 1 GiB: the Lua layout's 1M-scale
+// layers (11M bits = 44 MB against a 16M-slot, 192 MB table for a 2^20-key chunk), small
+// filters under big batches.  Probe updates are then one atomicMin each, with no claim loop.
+// (the old bound let the direct table reach twice the hash table's bytes.)
 bool seq_direct(uint64_t n, uint32_t k, uint64_t m) {
-    return m <= (1ull << 28) && 4 * m <= 2 * 12 * seq_slots(n, k);
+    return m <= (1ull << 28) && 4 * m <= 12 * seq_slots(n, k);
 }
 
 SeqCarve seq_carve(void* scratch, uint64_t n, uint32_t k, uint64_t m) {

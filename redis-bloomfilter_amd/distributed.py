@@ -440,6 +440,7 @@ class PartitionedFilter:
         # next_include (insert_include_dev): the SHA-1 words of the next call's include? batch,
         # hashed by this call's owner test (kb, n, words); that call routes from them
         self._next_inc = None
+        self.routed_from_digests = 0   # include? routes that started from next_include's words
         # chunked windows (sync-free exchange on an engine that has them): the route sorts each
         # window's runs by the owner's superbin and sends a directory beside them, so the owner
         # skips its sort pass; BFHIP_CHUNKS=0 keeps the plain windows
@@ -666,6 +667,7 @@ class PartitionedFilter:
             geo = None
         dirb = None
         if geo is not None and dig is not None:
+            self.routed_from_digests += 1
             send, slot, counts, dirb = e.route_chunks(dig, None, n, cap, geo[0], geo[1], want_slot=want_slot)
         elif geo is not None:
             send, slot, counts, dirb = e.route_chunks(kb, ko, n, cap, geo[0], geo[1], want_slot=want_slot)
@@ -742,7 +744,7 @@ class PartitionedFilter:
                 nkb, nko, nn = next_include
                 dig = torch.empty((nn, 4), dtype=torch.int32, device=st["recv"].device)
                 nxt = (nkb, nko, nn, dig)
-                self._next_inc = dict(kb=nkb, n=nn, dig=dig)
+                self._next_inc = dict(kb=nkb, ko=nko, n=nn, dig=dig)
             e.shard_test_chunks(st["recv"], cap, P, st["rdir"], dbytes, tiles, st["rmsg"], nh + 1, bits, nxt=nxt)
         else:
             for h in range(nh):
@@ -799,6 +801,7 @@ class PartitionedFilter:
 
     # -- device-resident batch API (keys already in device memory)
     def insert_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> None:
+        self._next_inc = None
         if not self.sync_free:
             return self._synced_insert(kb, ko, n)
         st = self._sf_start(kb, ko, n, want_slot=False)
@@ -810,6 +813,7 @@ class PartitionedFilter:
             self._agree_batch(n)
 
     def include_many_dev(self, kb: torch.Tensor, ko: torch.Tensor, n: int) -> torch.Tensor:
+        self._next_inc = None   # next_include words belong to the next insert_include_dev only
         if not self.sync_free:
             return self._synced_include(kb, ko, n)
         st = self._sf_start(kb, ko, n, want_slot=True)
@@ -833,8 +837,14 @@ class PartitionedFilter:
         ``next_include`` = (kb, ko, n), chunked windows only: this call's owner test also hashes
         the NEXT call's include? batch (dedicated hashing workgroups beside the L2 sweep), and
         that call routes it from the words instead of hashing it in its route.  The next call
-        must pass the same batch, unchanged, as (qkb, qko, nq) to use them (any other batch is
-        routed from its keys).  Answers are the same either way."""
+        must pass the same batch as (qkb, qko, nq) to use them (any other batch is routed from
+        its keys).  Answers are the same either way.  Contract: the batch's key and offset
+        tensors must not be refilled in place between the two calls — only their identity is
+        checked (the same ``kb`` and ``ko`` objects, the same n), so a ring buffer rewritten
+        in place would be routed from stale words.  Any call other than the next
+        ``insert_include_dev`` drops the words."""
+        # words hashed by the previous call; taken (and dropped) by this call whatever happens
+        ni_, self._next_inc = self._next_inc, None
         pend = self._pending
         if pend is not None and not (pend["kb"] is ikb and pend["n"] == ni):
             # Refused without touching the prefetch: completing it here would run collectives
@@ -852,9 +862,8 @@ class PartitionedFilter:
             # route(ins) | send(ins) || route(inc) | send(inc) || shard_insert | shard_test |
             # send(back) | combine, all enqueued before the host waits for anything
             st_i = pend if pend is not None else self._sf_start(ikb, iko, ni, want_slot=False)
-            ni_ = self._next_inc
-            self._next_inc = None
-            dig = ni_["dig"] if ni_ is not None and ni_["kb"] is qkb and ni_["n"] == nq else None
+            dig = (ni_["dig"] if ni_ is not None and ni_["kb"] is qkb and ni_["ko"] is qko and ni_["n"] == nq
+                   else None)
             st_q = self._sf_start(qkb, qko, nq, want_slot=True, dig=dig)
             if next_insert is not None:
                 self._pending = self._sf_start(*next_insert, want_slot=False)
@@ -1088,6 +1097,15 @@ class ReplicatedFilter:
         self._sets_host = None
         self._sets_pending = []   # (insert number, event, pinned slot)
         self._sets_done = 0
+        if insert_mode == "sets":
+            # a filter that cannot take region sets at all (a non-ruby engine, regions with no
+            # set geometry) is refused here; the per-batch fallback to the digests form in
+            # gather_start is only for a batch too large for one encode pass
+            try:
+                self.filter.region_sets_capacity(1)
+            except (ArgumentError, BfHipError) as e:
+                self.filter.close()
+                raise ArgumentError("insert_mode='sets': this filter cannot take region sets (%s)" % e)
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -1225,6 +1243,8 @@ class ReplicatedFilter:
                 if self._sets_status is None:
                     self._sets_status = torch.zeros(1, dtype=torch.int32, device=self.device)
                     self._sets_host = torch.zeros(3, dtype=torch.int32, pin_memory=self._sets_status.is_cuda)
+                # each apply ORs into a fresh word, so each pinned slot holds that insert's own status
+                self._sets_status.zero_()
                 self.filter.insert_region_sets_dev(st["gs"].data_ptr(), st["cap"], self.P, probes,
                                                    d_status=self._sets_status.data_ptr(), stream=self._stream())
                 self._sets_done += 1
@@ -1311,7 +1331,13 @@ class ReplicatedPipeline:
     of three buffers.  Every key is still hashed once per step.  The answers and every
     replica's bitset equal those of inserting all ranks' batches 0..i before include? i
     (``tests/dist_worker.py``'s ``rpipe`` check).  The last step's gather of the wrapped-around
-    batch is left pending: ``drain`` completes it (nothing is inserted from it)."""
+    batch is left pending: ``drain`` completes it (nothing is inserted from it).
+
+    Errors lag: a region-set apply that skipped a buffer or a region (lost inserts) is raised
+    two inserts later (``ReplicatedFilter._sets_check(lag=2)``) so no step waits on its own
+    apply; the include? answers of up to two steps can therefore come back before the
+    ``BfHipError`` that says they may hold false negatives.  ``drain`` (or
+    ``rf.sets_check()``) checks every apply so far."""
 
     def __init__(self, rf: "ReplicatedFilter", batches, n: int, fused_hash: bool = True):
         self.rf, self.batches, self.n, self.L = rf, batches, n, len(batches)
@@ -1356,8 +1382,11 @@ class ReplicatedPipeline:
             rf.filter.include_many_dev(pkb.data_ptr(), pko.data_ptr(), n, out.data_ptr(), stream=rf._stream())
 
     def drain(self) -> None:
-        """Complete the pending gathers (collective: every rank calls it after its last step)."""
+        """Complete the pending gathers (collective: every rank calls it after its last step),
+        then check every region-set apply so far (raises on every rank alike)."""
         for st in self.gpend.values():
             for w in st.get("works", []):
                 w.wait()
         self.gpend.clear()
+        if self.rf.insert_mode == "sets":
+            self.rf.sets_check()

@@ -512,8 +512,10 @@ def main():
     # (next_include: the first call's owner test hashes the second call's include? batch, which
     # the second call then routes from the words — the chunked HIP engine's P = 8 form)
     pf6.insert_include_dev(kb1, ko1, n1, qkb, qko, nq, next_insert=(kb2, ko2, n2), next_include=(qkb, qko, nq))
-    routed_from_words = pf6._next_inc is not None or not pf6.chunks
+    words_ready = pf6._next_inc is not None or not pf6.chunks
     got6 = pf6.insert_include_dev(kb2, ko2, n2, qkb, qko, nq, next_insert=(kb1, ko1, n1))
+    # ... and the second call's include? route really started from those words
+    routed_from_words = words_ready and (not pf6.chunks or pf6.routed_from_digests == 1)
     same_shard = same_shard and routed_from_words
     pf6.drain_prefetch()
     got6 = got6.cpu().numpy().astype(bool)

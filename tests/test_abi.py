@@ -243,3 +243,23 @@ def test_bfbench_binary_is_built_and_reports_its_version():
     exe = os.path.join(ROOT, "redis-bloomfilter_amd", "lib", "bfbench")
     out = subprocess.run([exe, "--version"], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0 and out.stdout.startswith("bfhip ")
+
+
+def test_check_offsets_is_the_kernels_rule(pkg):
+    """bf_check_offsets applies bfdev::key_ok, the rule every hashing kernel checks per key
+    before it hashes: non-decreasing offsets, every key below 2 GiB.
+    A wrapped length (round 5's hang: a key end read back as 0) is refused, not looped over."""
+    import numpy as np
+    pkg._lib.check_offsets(np.array([0, 3, 3, 10, 4096], np.uint64))
+    pkg._lib.check_offsets(np.array([7], np.uint64))                     # n = 0
+    with pytest.raises(pkg.ArgumentError, match="key 1:"):
+        pkg._lib.check_offsets(np.array([0, 5, 2, 9], np.uint64))       # 5 -> 2 runs backwards
+    with pytest.raises(pkg.ArgumentError, match="key 0:"):
+        pkg._lib.check_offsets(np.array([0, 5, 9, 0], np.uint64))       # the r05 wrap: the end read as 0
+        #                                                                 (every key then passes the last offset)
+    with pytest.raises(pkg.ArgumentError, match="key 0:"):
+        pkg._lib.check_offsets(np.array([0, 1 << 31], np.uint64))       # a 2 GiB key
+    pkg._lib.check_offsets(np.array([0, (1 << 31) - 1], np.uint64))
+    # the kernels carry the same guard and report through the handle's key-status word
+    blob = open(pkg._lib.lib_path(), "rb").read()
+    assert b"key offsets were inconsistent" in blob

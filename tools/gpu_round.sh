@@ -17,20 +17,21 @@
 #              10b lua_1m); then
 #              python tools/pmc_finalize.py <tag> on the CPU host writes profiles/pmc_<tag>_*.json
 #   simP8      the P = 8 per-rank step (tools/sim_rank.py): time + stall/LDS + VALU counters
-#   simP8t     the P = 8 per-rank step, time only
+#   simP8t     the P = 8 per-rank step, time only (SIMCFG=200b: BASELINE configs[4]'s filter)
 #   repl       one replica's step of the replicated 10B x 8 and north-star x 2 layouts, per
 #              insert form
 #   replovl    the region-set replica steps, plain vs the next encode on a second stream (interleaved)
 #   replprof   kernel trace of the 10B x 8 region-set replica step
 #   replpmc    stall/LDS + VALU counters of the 10B x 8 region-set replica step
-#   ablib      one command (AB_CMD) over A/B libraries built side by side: AB_LIBS names ab_libs/<name>
+#   ablib      one command (AB_CMD) over A/B libraries built side by side on the box from AB_BUILD
+#              ("name=-DFLAGS ...", tools/build_ab_libs.sh; ab_libs/ is gpurun-ignored): AB_LIBS names ab_libs/<name>
 #              (interleaved, e.g. "old ab old ab"); lines appended to gpurun_out/ablib_<tag>.jsonl
 #   ab         an A/B over one environment variable: AB_VAR, AB_VALUES (interleaved, e.g.
-#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, repl10b, replnstar,
+#              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, simP8_200b, repl10b, replnstar,
 #              repl10bf, replnstarf (the fused-hash region-set steps)}; lines appended to
 #              gpurun_out/ab_${AB_VAR}_<tag>.jsonl.  The shipped library reads no A/B knob: the step
-#              loads AB_LIB (default ab_libs/ab/libbfhip.so, built on the CPU host by
-#              `bash tools/build_ab_libs.sh ab=-DBFHIP_AB_KNOBS`)
+#              loads AB_LIB (default ab_libs/ab/libbfhip.so, built on the box by
+#              `bash tools/build_ab_libs.sh ${AB_BUILD:-ab=-DBFHIP_AB_KNOBS}` when absent)
 # Default: tests smoke bench prof pmc.  Every GPU step runs under its own time limit; a failing
 # step ends the script (no further GPU work after a fault, abort or time limit).
 export TMPDIR=/tmp
@@ -40,6 +41,8 @@ STEPS=${*:-tests smoke bench prof pmc}
 NOEXTRA="--no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes"
 STALL="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS"
 VALU="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_SALU"
+SIMCFG=${SIMCFG:-nstar}                       # simP8 / simP8t: the filter (nstar, 200b)
+SIMSFX=$([ "$SIMCFG" = nstar ] || echo "_$SIMCFG")
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 
 ab_cmd() {   # one A/B line's command, stdout = its JSON
@@ -47,6 +50,7 @@ ab_cmd() {   # one A/B line's command, stdout = its JSON
         nstar|10b|200b) timeout -k 10 150 python bench.py --config $1 --steps 10 --warmup 3 $NOEXTRA 2>>"$ABERR" ;;
         simP8)   timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 2>>"$ABERR" ;;
         simP4)   timeout -k 10 120 python tools/sim_rank.py --shards 4 --chunks --steps 5 2>>"$ABERR" ;;
+        simP8_200b) timeout -k 10 180 python tools/sim_rank.py --config 200b --shards 8 --chunks --steps 5 2>>"$ABERR" ;;
         repl10b) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --steps 3 2>>"$ABERR" ;;
         replnstar) timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --steps 5 2>>"$ABERR" ;;
         repl10bf) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash \
@@ -87,16 +91,16 @@ for st in $STEPS; do
         pmcsec) for w in ${PMC_WORKLOADS:-1m 1m_big 100m 10b lua_1m}; do
                     bash tools/pmc_passes.sh $w ${TAG}_$w || exit 1
                 done ;;
-        simP8t) timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 \
-                    > gpurun_out/sim_P8_${TAG}.json 2> gpurun_out/sim_P8_${TAG}.err ;;
-        simP8)  timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 \
-                    > gpurun_out/sim_P8_${TAG}.json 2> gpurun_out/sim_P8_${TAG}.err &&
-                timeout -s KILL 120 rocprofv3 --pmc $STALL --output-format csv \
-                    -d gpurun_out/pmc_${TAG}_P8_stall -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
-                    > gpurun_out/pmc_${TAG}_P8_stall.log 2>&1 &&
-                timeout -s KILL 120 rocprofv3 --pmc $VALU --output-format csv \
-                    -d gpurun_out/pmc_${TAG}_P8_valu -o run -- python tools/sim_rank.py --shards 8 --chunks --steps 2 \
-                    > gpurun_out/pmc_${TAG}_P8_valu.log 2>&1 ;;
+        simP8t) timeout -k 10 180 python tools/sim_rank.py --config $SIMCFG --shards 8 --chunks --steps 5 \
+                    > gpurun_out/sim_P8${SIMSFX}_${TAG}.json 2> gpurun_out/sim_P8${SIMSFX}_${TAG}.err ;;
+        simP8)  timeout -k 10 180 python tools/sim_rank.py --config $SIMCFG --shards 8 --chunks --steps 5 \
+                    > gpurun_out/sim_P8${SIMSFX}_${TAG}.json 2> gpurun_out/sim_P8${SIMSFX}_${TAG}.err &&
+                timeout -s KILL 150 rocprofv3 --pmc $STALL --output-format csv \
+                    -d gpurun_out/pmc_${TAG}_P8${SIMSFX}_stall -o run -- python tools/sim_rank.py --config $SIMCFG \
+                    --shards 8 --chunks --steps 2 > gpurun_out/pmc_${TAG}_P8${SIMSFX}_stall.log 2>&1 &&
+                timeout -s KILL 150 rocprofv3 --pmc $VALU --output-format csv \
+                    -d gpurun_out/pmc_${TAG}_P8${SIMSFX}_valu -o run -- python tools/sim_rank.py --config $SIMCFG \
+                    --shards 8 --chunks --steps 2 > gpurun_out/pmc_${TAG}_P8${SIMSFX}_valu.log 2>&1 ;;
         repl)   for g in digests sets "sets --fused-hash"; do
                     timeout -k 10 240 python tools/sim_rank.py --replicated 8 --config 10b --gathered $g --steps 3 \
                         >> gpurun_out/sim_repl_${TAG}.jsonl 2>> gpurun_out/sim_repl_${TAG}.err || exit 1
@@ -125,6 +129,9 @@ for st in $STEPS; do
                     > gpurun_out/pmc_${TAG}_sets_2.log 2>&1 ;;
         ab)     ABERR=gpurun_out/ab_${AB_VAR}_${TAG}.err
                 export BFHIP_LIB=${AB_LIB:-$PWD/ab_libs/ab/libbfhip.so}
+                # ab_libs/ is gpurun-ignored (A/B builds never ship beside the product): build on the box
+                [ -f "$BFHIP_LIB" ] || timeout -k 10 600 bash tools/build_ab_libs.sh ${AB_BUILD:-ab=-DBFHIP_AB_KNOBS} \
+                    > gpurun_out/ab_build_${TAG}.log 2>&1 || exit 2
                 [ -f "$BFHIP_LIB" ] || { echo "no A/B library $BFHIP_LIB"; exit 2; }
                 for v in ${AB_VALUES:?}; do
                     line=$(export "${AB_VAR:?}=$v"; ab_cmd "${AB_CMD:?}") || exit $?
@@ -132,6 +139,9 @@ for st in $STEPS; do
                         >> gpurun_out/ab_${AB_VAR}_${TAG}.jsonl
                 done ;;
         ablib)  ABERR=gpurun_out/ablib_${TAG}.err   # the same command over A/B libraries (ab_libs/<name>)
+                # built on the box from AB_BUILD ("name=-DFLAGS ..."; ab_libs/ does not travel)
+                [ -z "${AB_BUILD:-}" ] || timeout -k 10 900 bash tools/build_ab_libs.sh $AB_BUILD \
+                    > gpurun_out/ablib_build_${TAG}.log 2>&1 || exit 2
                 for lib in ${AB_LIBS:?}; do
                     [ -f ab_libs/$lib/libbfhip.so ] || { echo "no A/B library ab_libs/$lib"; exit 2; }
                     line=$(export BFHIP_LIB=$PWD/ab_libs/$lib/libbfhip.so; ab_cmd "${AB_CMD:?}") || exit $?

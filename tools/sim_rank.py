@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--dig-side", action="store_true",
                     help="--chunks --dig, but the next include? batch is hashed by bf_hash_many_dev on a second "
                          "stream (a second handle) beside the owner test, not inside it; read the wall time")
+    ap.add_argument("--no-prefill", action="store_true",
+                    help="partitioned: start from an empty shard (default: 50 %% random bit density, as "
+                         "bench.py prefills every rank's shard; the owner test stores an answer per 0-probe)")
     ap.add_argument("--overlap", action="store_true",
                     help="--chunks: route the NEXT step's insert batch on a second stream while this step's "
                          "owner kernels run (what PartitionedFilter's next_insert prefetch would do on a side "
@@ -81,6 +84,11 @@ def main():
     dev = torch.device("cuda", 0)
     eng = pkg.distributed.HipEngine(m, k, args.shards, 0, 20, dev)
     f = eng.filter
+    if not args.no_prefill:   # bench.py's partitioned prefill: 50 % random bits in every shard
+        sh = pkg.distributed.device_bytes_view(f, (f.local_bits + 7) // 8)
+        g = torch.Generator(device=dev)
+        g.manual_seed(bench.SEED * 7919)
+        sh.random_(0, 256, generator=g)
     batches = bench.make_batches(n_items, batch, 0, args.steps + 1, dev)
     torch.cuda.synchronize()
 
@@ -241,14 +249,16 @@ def main():
     wall = (time.perf_counter() - t0) / args.steps
     prof = f.profile_read(reset=True)
     out = {"config": args.config, "shards": args.shards, "m": m, "k": k, "batch": batch,
+           "prefill": None if args.no_prefill else "50% random bits",
            "shard_bytes": f.device_bytes, "route32": bool(eng.offset_dtype == torch.int32),
            "route": "chunked windows" if args.chunks else
                     ("sync-free windows" if args.sync_free else ("windows" if args.windows else "contiguous")),
            "ms_per_step_compute": wall * 1e3,
            "kernels_ms_per_step": {name: ms / args.steps for name, (ms, _) in prof.items()},
            "kernels_ms_sum": sum(ms for ms, _ in prof.values()) / args.steps,
-           "note": "ms_per_step_compute includes the stand-in receive copies of --windows "
-                   "(the exchange's job in a real run); kernels_ms_sum does not"}
+           "note": "per-rank compute = kernels_ms_sum; ms_per_step_compute also holds the stand-in receive "
+                   "copies (--windows; --chunks with nh > 1: the windows permuted into the receive layout), "
+                   "which are the exchange's job in a real run"}
     print(json.dumps(out))
 
 
