@@ -583,6 +583,48 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
     return res, (ib, io, pb, po, host_bits, m, k)
 
 
+# Per-rank models of the multi-GPU layouts, timed on this one GPU by tools/sim_rank.py (the kernels
+# one rank runs per step; the exchange itself is not in them): the partitioned north-star filter
+# at P = 8 (the driver's N = 8 layout), BASELINE configs[4] (200B@0.01 %, partitioned x 8) and
+# configs[3] (10B@0.01 %, replicated x 8: one replica's step).  With no 8-GPU node the driver's
+# own run is the only independent check of them.
+MODEL_LEGS = {
+    "model_P8_nstar": (["--shards", "8", "--chunks", "--config", "nstar", "--steps", "5"], "nstar", "partitioned"),
+    "model_P8_200b": (["--shards", "8", "--chunks", "--config", "200b", "--steps", "5"], "200b", "partitioned"),
+    "model_repl8_10b": (["--replicated", "8", "--config", "10b", "--gathered", "sets", "--fused-hash", "--steps", "3"],
+                        "10b", "replicated"),
+}
+
+
+def model_legs(names, single_ms: dict) -> dict:
+    """Each model's per-rank step (partitioned: the kernels' sum — the stand-in receive copies
+    are the exchange's job; replicated: the replica's wall time, every kernel of the step), its
+    kernel breakdown, its PMC source and the predicted weak-scaling efficiency = the single-GPU
+    step of the same filter (this run's line) / the per-rank step, before any exchange time."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("sim_rank", os.path.join(ROOT, "tools", "sim_rank.py"))
+    sim = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sim)
+    out = {}
+    for name in names:
+        argv, config, layout = MODEL_LEGS[name]
+        t0 = time.time()
+        r = sim.run(argv)
+        torch.cuda.synchronize()
+        per_rank = r["kernels_ms_sum"] if layout == "partitioned" else r["ms_per_step_compute"]
+        one = single_ms.get(config)
+        out[name] = {"layout": layout, "config": config, "world": 8, "argv": " ".join(argv),
+                     "per_rank_ms": per_rank, "wall_ms_per_step": r["ms_per_step_compute"],
+                     "single_gpu_ms_per_step": one,
+                     "predicted_efficiency": one / per_rank if one else None,
+                     "kernels": {kn: round(v, 4) for kn, v in r["kernels_ms_per_step"].items()},
+                     "pmc": load_pmc(name), "model_s": round(time.time() - t0, 1),
+                     "note": "one rank's compute per step on this GPU (tools/sim_rank.py); the all-to-all / "
+                             "all-gather is not in it"}
+        log("[%s] per-rank %.3f ms, single GPU %s ms" % (name, per_rank, one))
+    return out
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as fh:
@@ -932,8 +974,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="nstar", choices=sorted(CONFIGS))
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--secondary", default="1m,1m_big,100m,10b,lua_1m",
+    ap.add_argument("--secondary", default="1m,1m_big,100m,10b,200b,lua_1m",
                     help="comma list of the secondary workloads (1-GPU runs): configs and lua_1m")
+    ap.add_argument("--models", default=",".join(MODEL_LEGS),
+                    help="comma list of the per-rank multi-GPU models timed on this GPU (tools/sim_rank.py), "
+                         "'' for none: %s" % ", ".join(MODEL_LEGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true", help="skip the PCIe-inclusive host-API timing")
     ap.add_argument("--no-reference-shapes", action="store_true",
@@ -996,6 +1041,11 @@ def main():
                                    "m": r["m"], "k": r["k"], "batch": r["batch"],
                                    "kernels": {kn: round(v["ms"], 4) for kn, v in r["kernels"].items()},
                                    "pmc": load_pmc(name)}
+    models = None
+    if D.world == 1 and args.models and not args.no_secondary:
+        single = {name: r["ms_per_step"] for name, r in secondary.items() if "ms_per_step" in r}
+        single[args.config] = main_res["wall_s"] / args.steps * 1e3
+        models = model_legs([x for x in args.models.split(",") if x], single)
     shapes = None
     if D.world == 1 and not args.no_reference_shapes:
         shapes = reference_shapes(pkg)
@@ -1092,6 +1142,7 @@ def main():
         "host_api": main_res.get("host_api"),
         "replicated_host_wait_ms_per_step": main_res.get("replicated_host_wait_ms_per_step"),
         "secondary": secondary or None,
+        "multi_gpu_models": models,
         "reference_shapes": shapes,
         "reference_published_keys_per_s": {"ruby_insert": 5103, "ruby_include": 4322,
                                            "lua_insert": 6235, "lua_include": 5712,

@@ -118,6 +118,12 @@ typedef struct bf_config {
  * reference's engine_crc32 raises at its first call (Integer#to_i takes no radix, :52). */
 #define BF_FLAG_ENGINE_MD5  2u
 #define BF_FLAG_ENGINE_SHA1 4u
+/* An encoder handle: the filter's geometry (m, k, its regions) and binned scratch but NO bitset
+ * in device memory.  Only bf_encode_region_sets_dev / _digests_dev run on it (every other op
+ * returns BF_EINVAL): a replicated filter encodes its next batch on a second stream through it,
+ * beside its own handle's apply, since one handle orders all of its calls (the set buffers are
+ * the same as its filter handle's). */
+#define BF_FLAG_ENCODER     8u
 
 /* ---- lifecycle */
 int  bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out);
@@ -383,6 +389,21 @@ int  bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t
  *                           + hi] (a window past window_cap is skipped whole); one call for
  *                           every sub-range.  The test writes d_bits[(hi*nsrc + src)*window_cap
  *                           + i] for the live entries i.
+ * bf_shard_test_chunks_packed_dev  the test with its answers as packed bits in the return
+ *                           trip's layout: window (hi, src) at d_packed + (src*nh + hi) *
+ *                           ceil(window_cap/8), bit i (LSB first) = live entry i (1 = its bit
+ *                           is set; an offset past the shard answers 0) — what
+ *                           bf_combine_chunks_packed_dev reads, with no pack pass between.  The
+ *                           sorted owner test ranks each window's route tiles by their run's
+ *                           start so that a group of chunks is one contiguous range of its
+ *                           window, stores the answers in sorted order and moves each group's
+ *                           back to receive order in LDS (no scattered answer stores).
+ * bf_shard_insert_test_chunks_packed_dev  one step's owner work: the insert windows (as
+ *                           bf_shard_insert_chunks_dev) then the include? windows (as
+ *                           bf_shard_test_chunks_packed_dev), in ONE pass over the shard where
+ *                           both take their sorted forms (each region read once, its inserts
+ *                           ORed in and written back, its include? probes tested against the
+ *                           result); every answer sees every insert, as the two calls in order.
  * bf_combine_chunks_packed_dev  requester: the include? answers from window w's answer bits
  *                           at d_packed + w*ceil(window_cap/8), through this rank's own
  *                           route directory and slots.  A window whose count exceeds
@@ -411,6 +432,16 @@ int  bf_shard_insert_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t w
 int  bf_shard_test_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
                               const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
                               uint32_t count_stride, uint8_t* d_bits, void* stream);
+int  bf_shard_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                                     const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
+                                     const uint64_t* d_counts, uint32_t count_stride,
+                                     uint8_t* d_packed /* nsrc*nh*ceil(window_cap/8) */, void* stream);
+int  bf_shard_insert_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_ins_recv, const uint8_t* d_ins_dir,
+                                            const uint64_t* d_ins_counts, const uint32_t* d_tst_recv,
+                                            const uint8_t* d_tst_dir, const uint64_t* d_tst_counts,
+                                            uint64_t window_cap, uint32_t nsrc, uint64_t dir_bytes, uint64_t tiles,
+                                            uint32_t count_stride, uint32_t* d_any_new /* nullable */,
+                                            uint8_t* d_packed, void* stream);
 int  bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint16_t* d_slot16,
                                   uint64_t window_cap, const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
                                   const uint64_t* d_counts /* nwin */, uint64_t n, uint8_t* d_out, void* stream);

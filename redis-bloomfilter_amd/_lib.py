@@ -119,6 +119,9 @@ SIGNATURES = {
     "bf_route_chunks_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp]),
     "bf_shard_insert_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
     "bf_shard_test_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
+    "bf_shard_test_chunks_packed_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
+    "bf_shard_insert_test_chunks_packed_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _u64,
+                                                              _u64, _u32, _vp, _vp, _vp]),
     "bf_route_chunks_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp]),
     "bf_shard_test_chunks_hash_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp,
                                                      _vp, _vp, _u64, _vp, _vp]),
@@ -572,6 +575,25 @@ class Filter:
         _check(self._lib.bf_shard_test_chunks_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
                                                   int(dir_bytes), int(tiles), d_counts, int(count_stride), d_bits,
                                                   self._s(stream)), self._h)
+
+    def shard_test_chunks_packed_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int,
+                                     tiles: int, d_counts: int, count_stride: int, d_packed: int, stream=None) -> None:
+        """The owner test with its answers as packed bits in the return trip's layout (window
+        (hi, src) at d_packed + (src * nh + hi) * ceil(window_cap / 8))."""
+        _check(self._lib.bf_shard_test_chunks_packed_dev(self.handle, d_recv, int(window_cap), int(nsrc), d_dir,
+                                                         int(dir_bytes), int(tiles), d_counts, int(count_stride),
+                                                         d_packed, self._s(stream)), self._h)
+
+    def shard_insert_test_chunks_packed_dev(self, d_ins_recv: int, d_ins_dir: int, d_ins_counts: int,
+                                            d_tst_recv: int, d_tst_dir: int, d_tst_counts: int, window_cap: int,
+                                            nsrc: int, dir_bytes: int, tiles: int, count_stride: int,
+                                            d_packed: int, d_any_new: int = 0, stream=None) -> None:
+        """One step's owner work: the insert windows ORed in, then the include? windows tested
+        (packed answers as shard_test_chunks_packed_dev), in one pass over the shard."""
+        _check(self._lib.bf_shard_insert_test_chunks_packed_dev(
+            self.handle, d_ins_recv, d_ins_dir, d_ins_counts, d_tst_recv, d_tst_dir, d_tst_counts, int(window_cap),
+            int(nsrc), int(dir_bytes), int(tiles), int(count_stride), d_any_new or None, d_packed,
+            self._s(stream)), self._h)
 
     def shard_test_chunks_hash_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int,
                                    tiles: int, d_counts: int, count_stride: int, d_bits: int, d_next_keys: int,

@@ -182,6 +182,13 @@ struct bf_handle {
     unsigned long long* d_scan = nullptr;
     uint32_t* h_flag = nullptr;   // pinned
     uint32_t* h_key_status = nullptr;   // pinned, written by the hashing kernels (take_key_status)
+    // bf_shard_test_chunks_packed_dev's answer bytes and segment table (forms that pack afterwards)
+    uint8_t* d_ans8 = nullptr;
+    uint64_t ans8_cap = 0;
+    uint64_t* d_seg = nullptr;
+    uint64_t seg_cap = 0;
+    uint32_t seg_nsrc = 0, seg_nh = 0;   // the geometry d_seg holds
+    uint64_t seg_wcap = 0;
     // latency path of small host-pointer calls (run_small): one pinned and one device arena
     uint8_t* h_small = nullptr;
     uint8_t* d_small = nullptr;
@@ -217,6 +224,9 @@ namespace {
 // asynchronously, so the error is reported once, as BF_EINVAL, by the next call on the handle
 // (bf_sync after the call at the latest), as the region-set status is checked lazily.
 int take_key_status(bf_handle* h);
+// Every op's entry check (after its StreamOrder): take_key_status, and a handle created with
+// BF_FLAG_ENCODER (no bitset) refused unless the op needs no bitset (the region-set encodes).
+int op_check(bf_handle* h, bool needs_bits = true);
 
 struct StreamOrder {
     bf_handle* h;
@@ -242,6 +252,12 @@ int set_err(bf_handle* h, int code, const char* fmt, ...) {
     va_end(ap);
     if (h) h->err = buf; else g_create_error = buf;
     return code;
+}
+
+int op_check(bf_handle* h, bool needs_bits) {
+    if (needs_bits && !h->g.bits)
+        return set_err(h, BF_EINVAL, "an encoder handle (BF_FLAG_ENCODER) holds no bitset: region-set encodes only");
+    return take_key_status(h);
 }
 
 int take_key_status(bf_handle* h) {
@@ -757,7 +773,7 @@ int run_dev(bf_handle* h, BfOp op, const uint8_t* d_keys, const uint64_t* d_offs
     uint64_t bias = 0;
     const uint8_t* k16 = align_keys(d_keys, &bias);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     return launch_op(h, op, k16, d_offsets, bias, n, d_out8, d_out64, d_flag, so.s);
 }
 
@@ -883,6 +899,10 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     h->k = k;
     const uint64_t maxval = (uint64_t)k * 0xFFFFFFFFull;      // largest offset ruby.rb:51 can produce
     const uint32_t eng = c.flags & (BF_FLAG_ENGINE_MD5 | BF_FLAG_ENGINE_SHA1);
+    if ((c.flags & BF_FLAG_ENCODER) && (eng || c.shard_count > 1)) {
+        delete h;
+        return set_err(nullptr, BF_EINVAL, "BF_FLAG_ENCODER: a whole-filter ruby-derivation handle only");
+    }
     if (eng == (BF_FLAG_ENGINE_MD5 | BF_FLAG_ENGINE_SHA1) || (eng && c.shard_count > 1)) {
         delete h;
         return set_err(nullptr, BF_EINVAL, "one hash engine per filter, whole-filter handles only");
@@ -942,7 +962,11 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     // Bitset memory kind (A/B knob): 0 coarse-grained hipMalloc, 1 uncached (MTYPE UC),
     // 2 fine-grained.
     h->mem_kind = ab_u32("BFHIP_BITS_MEM", kDefaultMemKind);
-    if (h->mem_kind == 1) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocUncached);
+    // BF_FLAG_ENCODER: the filter's geometry without its bitset (a second handle that encodes a
+    // replicated filter's next batch beside its apply: bf_encode_region_sets*_dev only)
+    const bool encoder = (c.flags & BF_FLAG_ENCODER) != 0;
+    if (encoder) e = hipSuccess;
+    else if (h->mem_kind == 1) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocUncached);
     else if (h->mem_kind == 2) e = hipExtMallocWithFlags((void**)&h->g.bits, h->dev_bytes, hipDeviceMallocFinegrained);
     else e = hipMalloc((void**)&h->g.bits, h->dev_bytes);
     if (e != hipSuccess) return fail(BF_ENOMEM, "hipMalloc(bitset)", e);
@@ -954,7 +978,8 @@ int bf_create(uint64_t m_bits, uint32_t k, const bf_config* cfg, bf_handle** out
     *h->h_key_status = 0u;
     if ((e = hipHostGetDevicePointer((void**)&h->g.key_status, h->h_key_status, 0)) != hipSuccess)
         return fail(BF_EDEVICE, "hipHostGetDevicePointer(key status)", e);
-    if ((e = hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream)) != hipSuccess) return fail(BF_EDEVICE, "hipMemset", e);
+    if (!encoder && (e = hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream)) != hipSuccess)
+        return fail(BF_EDEVICE, "hipMemset", e);
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(BF_EDEVICE, "hipStreamSynchronize", e);
     h->g.m = m_bits;
     h->g.inv_m = 1.0 / (double)m_bits;
@@ -1009,6 +1034,8 @@ int bf_destroy(bf_handle* h) {
         if (h->d_tmp_owner) (void)hipFree(h->d_tmp_owner);
         if (h->d_cursor) (void)hipFree(h->d_cursor);
         if (h->d_bin_scratch) (void)hipFree(h->d_bin_scratch);
+        if (h->d_ans8) (void)hipFree(h->d_ans8);
+        if (h->d_seg) (void)hipFree(h->d_seg);
         if (h->d_dirty) (void)hipFree(h->d_dirty);
         (void)prof_harvest(h);   // waits for marks recorded on caller streams
         for (BfMarks& mk : h->prof_free)
@@ -1041,7 +1068,7 @@ int bf_insert_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offse
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     const BfOp op = (any_new || per_key_new) ? BF_OP_INSERT_FLAGS : BF_OP_INSERT;
     StreamOrder so(h, h->stream);
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     int rc = run_host(h, op, key_bytes, offsets, n, per_key_new, nullptr, any_new);
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1068,7 +1095,7 @@ int bf_insert_many_changes(bf_handle* h, const uint8_t* key_bytes, const uint64_
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     return run_small(h, BF_OP_INSERT_FLAGS, key_bytes, offsets, n, nullptr, nullptr, out_bits, count);
 }
 
@@ -1080,7 +1107,7 @@ int bf_include_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     return run_host(h, BF_OP_INCLUDE, key_bytes, offsets, n, out, nullptr, nullptr);
 }
 
@@ -1092,7 +1119,7 @@ int bf_indexes_many(bf_handle* h, const uint8_t* key_bytes, const uint64_t* offs
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     return run_host(h, BF_OP_INDEXES, key_bytes, offsets, n, nullptr, out, nullptr);
 }
 
@@ -1103,6 +1130,7 @@ int bf_clear(bf_handle* h) {
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, h->stream);
+    if (!h->g.bits) return set_err(h, BF_EINVAL, "an encoder handle (BF_FLAG_ENCODER) holds no bitset");
     HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
     if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 0, h->dirty_blocks, h->stream));   // the driver DELs the key
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1126,7 +1154,7 @@ namespace {
 // Trimmed length of the first `max_bytes` bytes of the device bitset (Redis STRLEN after SETBITs).
 int device_trimmed_len(bf_handle* h, uint64_t* len_out) {
     StreamOrder so(h, h->stream);
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     HIPCHK(h, hipMemsetAsync(h->d_scan, 0, sizeof(unsigned long long), h->stream));
     HIPCHK(h, bf_launch_last_nonzero(h->g.bits, h->dev_bytes / 4, h->d_scan, h->stream));
     unsigned long long last = 0;
@@ -1160,7 +1188,7 @@ int import_bytes(bf_handle* h, const uint8_t* buf, uint64_t len, uint32_t mode, 
             return set_err(h, BF_ERANGE, "string sets bits at offsets >= %llu", (unsigned long long)max_bits);
     }
     StreamOrder so(h, h->stream);
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     if (h->d_dirty) HIPCHK(h, hipMemsetAsync(h->d_dirty, 1, h->dirty_blocks, h->stream));
     if (mode == BF_IMPORT_REPLACE) {
         HIPCHK(h, hipMemsetAsync(h->g.bits, 0, h->dev_bytes, h->stream));
@@ -1278,7 +1306,7 @@ int bf_route_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_off
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     auto* counts = reinterpret_cast<unsigned long long*>(d_counts);
     BfBinPlan plan;
@@ -1339,7 +1367,7 @@ int bf_route_windows_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfBinPlan plan;
     if (n && !bf_route_plan(n, h->k, nwin, false, d_slot != nullptr, &plan))
@@ -1433,7 +1461,7 @@ int route_chunks_impl(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfBinPlan plan;
     if (n && !bf_route_plan(n, h->k, nwin, false, d_slot16 != nullptr, &plan))
@@ -1469,17 +1497,22 @@ int bf_route_chunks_digests_dev(bf_handle* h, const uint32_t* d_digests, uint64_
 
 namespace {
 // side (test only): a key batch [keys, offsets, n) whose SHA-1 words go to side_dig (nullable).
+// d_packed (test only, instead of d_bits): the answers as packed bits in the return trip's layout
+// (window (h, src) at d_packed + (src * nh + h) * ceil(window_cap / 8)).  The sorted test takes
+// ordered chunks and stores them so directly; every other form (the L2 sweep, the direct owner
+// ops, a geometry the ordered form does not take) writes answer bytes into the handle's own
+// buffer and packs them.
 static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc, const uint8_t* d_dir,
                       uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts, uint32_t count_stride,
                       uint32_t* d_any_new, uint8_t* d_bits, bool test, void* stream,
                       const uint8_t* side_keys = nullptr, const uint64_t* side_offsets = nullptr, uint64_t side_n = 0,
-                      uint32_t* side_dig = nullptr) {
+                      uint32_t* side_dig = nullptr, uint8_t* d_packed = nullptr) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (side_n && (!side_keys || !side_offsets || !side_dig)) return set_err(h, BF_EINVAL, "NULL side-hash pointer");
     if (!nsrc || !window_cap)
         return side_n ? bf_hash_many_dev(h, side_keys, side_offsets, side_n, side_dig, stream) : BF_OK;
-    if (!d_recv || !d_dir || !d_counts || (test && !d_bits)) return set_err(h, BF_EINVAL, "NULL device pointer");
+    if (!d_recv || !d_dir || !d_counts || (test && !d_bits && !d_packed)) return set_err(h, BF_EINVAL, "NULL device pointer");
     BfChunks cg;
     uint32_t nh = 1;
     bool sweep = false;
@@ -1511,6 +1544,68 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
                         ((test ? h->shard_test_binned_mode : h->binned_mode) == 1 ||
                          (h->dev_bytes >= (64ull << 20) &&
                           (double)total * 128.0 > kBinnedCostRatio * (double)h->dev_bytes));
+    if (d_packed && binned && !plan.l2test && !side_n &&
+        bf_chunk_plan(h->dev_bytes, cg, nh, nsrc, window_cap, true, &plan, false, true)) {
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceGuard dg(h->device);
+        if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+        StreamOrder so(h, pick_stream(h, stream));
+        if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
+        if ((rc = ensure_scratch(h, plan.scratch_bytes))) return rc;
+        BfMarks* mk = prof_begin(h, so.s);
+        HIPCHK(h, bf_launch_shard_test_chunks_packed(h->g, plan, h->dev_bytes, ci, h->d_bin_scratch, d_packed, so.s, mk));
+        return BF_OK;
+    }
+    if (d_packed) {   // answer bytes into the handle's buffer, then packed per window
+        const uint64_t nbytes = (uint64_t)nh * nsrc * window_cap;
+        if (nbytes > h->ans8_cap) {
+            std::lock_guard<std::mutex> lk(h->mu);
+            DeviceGuard dg(h->device);
+            if (h->order_valid) HIPCHK(h, hipEventSynchronize(h->order_ev));   // a previous call may still read it
+            if (h->d_ans8) (void)hipFree(h->d_ans8);
+            h->d_ans8 = nullptr;
+            h->ans8_cap = 0;
+            HIPCHK(h, hipMalloc((void**)&h->d_ans8, nbytes));
+            h->ans8_cap = nbytes;
+        }
+        rc = shard_chunks_impl(h, d_recv, window_cap, nsrc, d_dir, dir_bytes, tiles, d_counts, count_stride, nullptr,
+                               h->d_ans8, true, stream, side_keys, side_offsets, side_n, side_dig);
+        if (rc) return rc;
+        std::vector<uint64_t> seg;   // (src, count, dst): sub-range h of source src -> its packed window
+        const uint64_t cap8 = (window_cap + 7) / 8;
+        for (uint32_t src = 0; src < nsrc; ++src)
+            for (uint32_t hh = 0; hh < nh; ++hh) {
+                seg.push_back(((uint64_t)hh * nsrc + src) * window_cap);
+                seg.push_back(window_cap);
+                seg.push_back(((uint64_t)src * nh + hh) * cap8);
+            }
+        std::lock_guard<std::mutex> lk(h->mu);
+        DeviceGuard dg(h->device);
+        if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+        StreamOrder so(h, pick_stream(h, stream));
+        const uint64_t sb = seg.size() * 8;
+        // the table depends on (nsrc, nh, window_cap) only: uploaded (with one sync) when they change
+        if (h->seg_nsrc != nsrc || h->seg_nh != nh || h->seg_wcap != window_cap) {
+            if (h->order_valid) HIPCHK(h, hipEventSynchronize(h->order_ev));   // a previous call may still read it
+            HIPCHK(h, hipStreamSynchronize(so.s));
+            if (sb > h->seg_cap) {
+                if (h->d_seg) (void)hipFree(h->d_seg);
+                h->d_seg = nullptr;
+                h->seg_cap = 0;
+                HIPCHK(h, hipMalloc((void**)&h->d_seg, sb));
+                h->seg_cap = sb;
+            }
+            HIPCHK(h, hipMemcpy(h->d_seg, seg.data(), sb, hipMemcpyHostToDevice));
+            h->seg_nsrc = nsrc;
+            h->seg_nh = nh;
+            h->seg_wcap = window_cap;
+        }
+        BfMarks* mk = prof_begin(h, so.s);
+        HIPCHK(h, bf_launch_pack_segments(h->d_ans8, reinterpret_cast<const unsigned long long*>(h->d_seg),
+                                          nh * nsrc, window_cap, d_packed, so.s));
+        bf_mark(mk, so.s, "pack_answers");
+        return BF_OK;
+    }
     if (!binned) {   // the direct owner ops read the same windows (the directories unused)
         for (uint32_t hi = 0; hi < nh; ++hi) {
             const uint32_t* rw = d_recv + (uint64_t)hi * nsrc * window_cap;
@@ -1526,7 +1621,7 @@ static int shard_chunks_impl(bf_handle* h, const uint32_t* d_recv, uint64_t wind
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     if ((rc = ensure_scratch(h, plan.scratch_bytes))) return rc;
     BfMarks* mk = prof_begin(h, s);
@@ -1560,6 +1655,82 @@ int bf_shard_test_chunks_dev(bf_handle* h, const uint32_t* d_recv, uint64_t wind
                              d_bits, true, stream);
 }
 
+int bf_shard_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
+                                    const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
+                                    uint32_t count_stride, uint8_t* d_packed, void* stream) {
+    if (h && !h->multi && !d_packed) return set_err(h, BF_EINVAL, "d_packed is NULL");
+    return shard_chunks_impl(h, d_recv, window_cap, nsrc, d_dir, dir_bytes, tiles, d_counts, count_stride, nullptr,
+                             nullptr, true, stream, nullptr, nullptr, 0, nullptr, d_packed);
+}
+
+int bf_shard_insert_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_ins_recv, const uint8_t* d_ins_dir,
+                                           const uint64_t* d_ins_counts, const uint32_t* d_tst_recv,
+                                           const uint8_t* d_tst_dir, const uint64_t* d_tst_counts,
+                                           uint64_t window_cap, uint32_t nsrc, uint64_t dir_bytes, uint64_t tiles,
+                                           uint32_t count_stride, uint32_t* d_any_new, uint8_t* d_packed,
+                                           void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (!d_packed) return set_err(h, BF_EINVAL, "d_packed is NULL");
+    if (!nsrc || !window_cap) return BF_OK;
+    if (!d_ins_recv || !d_ins_dir || !d_ins_counts || !d_tst_recv || !d_tst_dir || !d_tst_counts)
+        return set_err(h, BF_EINVAL, "NULL device pointer");
+    BfChunks cg;
+    uint32_t nh = 1;
+    bool sweep = false;
+    if (!handle_chunks(h, &cg, &nh, &sweep)) return set_err(h, BF_EINVAL, "this shard count cannot take chunked windows");
+    int rc = check_chunk_args(h, cg, dir_bytes, tiles);
+    if (rc) return rc;
+    if (count_stride < nh) return set_err(h, BF_EINVAL, "count_stride %u < %u sub-ranges", count_stride, nh);
+    const uint64_t total = (uint64_t)nh * nsrc * window_cap;
+    if (total / window_cap != (uint64_t)nh * nsrc || total >= (1ull << 32))
+        return set_err(h, BF_EINVAL, "%u sub-ranges x %u windows x %llu entries must stay below 2^32", nh, nsrc,
+                       (unsigned long long)window_cap);
+    cg.tiles = tiles;
+    BfBinPlan pi, pt;
+    // one pass only where both owner ops would take their sorted binned forms on this shard (the
+    // same rule as shard_chunks_impl) and the include? its ordered form; else the two calls
+    const bool dense_enough = h->dev_bytes >= (64ull << 20) && (double)total * 128.0 > kBinnedCostRatio * (double)h->dev_bytes;
+    const bool fused = h->binned_mode != 0 && h->shard_test_binned_mode != 0 && !sweep &&
+                       (h->binned_mode == 1 || dense_enough) && (h->shard_test_binned_mode == 1 || dense_enough) &&
+                       bf_chunk_plan(h->dev_bytes, cg, nh, nsrc, window_cap, false, &pi) &&
+                       bf_chunk_plan(h->dev_bytes, cg, nh, nsrc, window_cap, true, &pt, false, true);
+    if (!fused) {
+        rc = bf_shard_insert_chunks_dev(h, d_ins_recv, window_cap, nsrc, d_ins_dir, dir_bytes, tiles, d_ins_counts,
+                                        count_stride, d_any_new, stream);
+        if (rc) return rc;
+        return bf_shard_test_chunks_packed_dev(h, d_tst_recv, window_cap, nsrc, d_tst_dir, dir_bytes, tiles, d_tst_counts,
+                                               count_stride, d_packed, stream);
+    }
+    BfChunkIn cii;
+    cii.recv = d_ins_recv;
+    cii.dir = d_ins_dir;
+    cii.dir_bytes = dir_bytes;
+    cii.tiles = tiles;
+    cii.cap = window_cap;
+    cii.limit = h->local_bits;
+    cii.counts = reinterpret_cast<const unsigned long long*>(d_ins_counts);
+    cii.cstride = count_stride;
+    cii.nsrc = nsrc;
+    cii.nh = nh;
+    cii.S = cg.S;
+    cii.sup_log2 = cg.sup_log2;
+    BfChunkIn cit = cii;
+    cit.recv = d_tst_recv;
+    cit.dir = d_tst_dir;
+    cit.counts = reinterpret_cast<const unsigned long long*>(d_tst_counts);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
+    if ((rc = ensure_scratch(h, bf_chunk_scratch_bytes(pi) + bf_chunk_scratch_bytes(pt)))) return rc;
+    BfMarks* mk = prof_begin(h, so.s);
+    HIPCHK(h, bf_launch_shard_insert_test_chunks_packed(h->g, pi, pt, h->dev_bytes, cii, cit, h->d_bin_scratch,
+                                                        d_any_new, d_packed, so.s, mk));
+    return BF_OK;
+}
+
 int bf_shard_test_chunks_hash_dev(bf_handle* h, const uint32_t* d_recv, uint64_t window_cap, uint32_t nsrc,
                                   const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles, const uint64_t* d_counts,
                                   uint32_t count_stride, uint8_t* d_bits, const uint8_t* d_next_keys,
@@ -1590,7 +1761,7 @@ int bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const ui
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_chunks_packed(d_packed, d_slot16, window_cap, cg, h->shards * nh,
@@ -1610,7 +1781,7 @@ static int shard_insert_impl(bf_handle* h, const void* d_local, bool u32, uint64
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     // Binned when the routed probes' random line fills clearly exceed a streaming pass
     // over the shard (same policy and knob as the whole-filter insert).
@@ -1674,7 +1845,7 @@ static int shard_test_impl(bf_handle* h, const void* d_local, bool u32, uint64_t
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     // Binned like the shard insert: routed probes carry no early exit (all k arrive), so
     // one streaming pass over the shard beats a random line fill per probe once the
@@ -1768,7 +1939,7 @@ int bf_combine_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* d_slot, 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine(d_bits, d_slot, n, h->k, d_out, s));
@@ -1785,7 +1956,7 @@ int bf_combine_windows_dev(bf_handle* h, const uint8_t* d_bits, const uint32_t* 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows(d_bits, d_slot, window_cap, reinterpret_cast<const unsigned long long*>(d_counts),
@@ -1804,7 +1975,7 @@ int bf_pack_segments_dev(bf_handle* h, const uint8_t* d_bits, const uint64_t* d_
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_pack_segments(d_bits, reinterpret_cast<const unsigned long long*>(d_seg), nseg, max_count,
@@ -1822,7 +1993,7 @@ int bf_combine_windows_packed_dev(bf_handle* h, const uint8_t* d_packed, const u
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     hipStream_t s = so.s;
     BfMarks* mk = prof_begin(h, s);
     HIPCHK(h, bf_launch_combine_windows_packed(d_packed, d_slot, window_cap,
@@ -1867,7 +2038,7 @@ static int run_digests(bf_handle* h, BfOp op, const uint32_t* d_dig, uint64_t n,
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     const uint4* dig = reinterpret_cast<const uint4*>(d_dig);
     const bool is_insert = op == BF_OP_INSERT || op == BF_OP_INSERT_FLAGS;
     BfBinPlan plan;
@@ -1904,7 +2075,7 @@ int bf_hash_many_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     uint64_t bias = 0;
     const uint8_t* k16 = align_keys(d_key_bytes, &bias);
     BfMarks* mk = prof_begin(h, so.s);
@@ -1941,7 +2112,7 @@ int bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     uint64_t bias = 0, nbias = 0;
     const uint8_t* k16 = n ? align_keys(d_key_bytes, &bias) : nullptr;
     const uint8_t* nk16 = n_next ? align_keys(d_next_key_bytes, &nbias) : nullptr;
@@ -2004,7 +2175,7 @@ int encode_sets(bf_handle* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h, false)) return krc;   // (an encoder handle encodes: no bitset read)
     if (n) {
         int rc = ensure_scratch(h, plan.scratch_bytes);
         if (rc) return rc;
@@ -2048,7 +2219,7 @@ int bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t str
     DeviceGuard dg(h->device);
     if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
     StreamOrder so(h, pick_stream(h, stream));
-    if (int krc = take_key_status(h)) return krc;   // an earlier call's bad key offsets
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     BfMarks* mk = prof_begin(h, so.s);
     HIPCHK(h, bf_launch_insert_sets(h->g, h->dev_bytes, rl, nbins, d_sets, stride_bytes / 4, nsrc, probes_hint,
                                     d_any_new, d_status, so.s, mk));
@@ -2065,6 +2236,7 @@ int bf_stream(bf_handle* h, void** stream) {
 int bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
+    if (!h->g.bits) return set_err(h, BF_EINVAL, "an encoder handle (BF_FLAG_ENCODER) holds no bitset");
     if (d_bits) *d_bits = h->g.bits;
     if (device_bytes) *device_bytes = h->dev_bytes;
     return BF_OK;
@@ -2109,6 +2281,7 @@ int bf_track_dirty(bf_handle* h, uint32_t enable) {
 }  // extern "C"
 
 int bfi_track_dirty(bf_handle* h, uint32_t enable) {
+    if (!h->g.bits) return set_err(h, BF_EINVAL, "an encoder handle (BF_FLAG_ENCODER) holds no bitset");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     HIPCHK(h, hipDeviceSynchronize());   // no launch may still use the map
@@ -2213,6 +2386,7 @@ int bf_export_range(bf_handle* h, uint64_t offset, uint64_t len, uint8_t* buf) {
     if (h && h->multi) return (len && !buf) ? BF_EINVAL : bfm_export_range(h->multi, offset, len, buf);
     if (!h || (len && !buf)) return BF_EINVAL;
     if (h->shards > 1) return set_err(h, BF_EINVAL, "partitioned shard: use bf_shard_export");
+    if (!h->g.bits) return set_err(h, BF_EINVAL, "an encoder handle (BF_FLAG_ENCODER) holds no bitset");
     if (offset > h->dev_bytes || len > h->dev_bytes - offset)
         return set_err(h, BF_ERANGE, "range [%llu, +%llu) outside the %llu-byte bitset", (unsigned long long)offset,
                        (unsigned long long)len, (unsigned long long)h->dev_bytes);

@@ -723,7 +723,23 @@ __device__ __forceinline__ void route_front_body(BfGeom g, const uint8_t* __rest
                 const uint32_t lo_b = (t * wS) << sub_log2, hi_b = ((t + 1) * wS) << sub_log2;
                 const uint32_t ob = s_lbase[lo_b], oc = (hi_b < NB ? s_lbase[hi_b] : tk * k) - ob;
                 unsigned long long gb = 0;
-                if (oc) gb = atomicAdd(wcounts + t, (unsigned long long)oc);
+                if constexpr (CHUNK) {
+                    // one 64-bit atomic gives the run's place AND its rank among the window's runs
+                    // (claims counted in the high bits): the owner then walks the runs in window
+                    // order through the directory's rank table, with no sort (BfChunkIn::ranked)
+                    if (oc) {
+                        uint8_t* dw = cg.dir + (uint64_t)t * cg.dir_bytes;
+                        const unsigned long long x = atomicAdd(
+                            reinterpret_cast<unsigned long long*>(dw + bf_chunk_dir_claim_offset(cg, cg.tiles)),
+                            (1ull << kClaimRankShift) | (unsigned long long)oc);
+                        gb = x & ((1ull << kClaimRankShift) - 1ull);
+                        reinterpret_cast<uint16_t*>(dw + bf_chunk_dir_rank_offset(cg, cg.tiles))
+                            [x >> kClaimRankShift] = (uint16_t)(tile + 1u);   // 0: no run at that rank
+                        atomicAdd(wcounts + t, (unsigned long long)oc);   // the window's live count
+                    }
+                } else if (oc) {
+                    gb = atomicAdd(wcounts + t, (unsigned long long)oc);
+                }
                 s_gbase[t] = (gb + oc <= wcap) ? (unsigned long long)t * wcap + gb : ~0ull;   // ~0: overflow
                 s_obase[t] = ob;
                 if constexpr (CHUNK)   // the chunk's place in window t (0xFFFFFFFF: dropped, the window overflows)
@@ -1374,7 +1390,10 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 // include?: the region in LDS; a probe on a 0 bit clears its key's answer.  The probe
 // streams and the region are read non-temporally, so that the scattered answer bytes keep
 // their lines in the caches (0.745 -> 0.691 ms at P = 8).
-template <uint32_t RLOG2, uint32_t LANES>
+// L2ORDER (the chunked owner's packed answers): each probe's answer byte (0/1) is stored at its
+// level-2 index instead — runs of consecutive bytes, no scatter, no key array read — and
+// chunk_unsort_kernel moves them to receive order (200B x 8: 1.74 -> ~0.5 ms).
+template <uint32_t RLOG2, uint32_t LANES, bool L2ORDER = false>
 __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restrict__ bits, uint64_t nwords,
                                                          const uint32_t* __restrict__ level2,
                                                          const uint32_t* __restrict__ level2_key,
@@ -1408,27 +1427,124 @@ __global__ __launch_bounds__(LANES) void bin_test_kernel(const uint32_t* __restr
                 key[c] = 0;
                 if (idx[c] != 0xFFFFFFFFu) {
                     l[c] = __builtin_nontemporal_load(level2 + idx[c]);
-                    key[c] = __builtin_nontemporal_load(level2_key + idx[c]);
+                    if constexpr (!L2ORDER) key[c] = __builtin_nontemporal_load(level2_key + idx[c]);
                 }
             }
 #pragma unroll
-            for (int c = 0; c < kLoads; ++c)
-                if (l[c] != 0xFFFFFFFFu && !((s_bits[l[c] >> 5] >> ((l[c] ^ 7u) & 31u)) & 1u)) out8[key[c]] = 0;
+            for (int c = 0; c < kLoads; ++c) {
+                if constexpr (L2ORDER) {
+                    if (l[c] != 0xFFFFFFFFu) out8[idx[c]] = (uint8_t)((s_bits[l[c] >> 5] >> ((l[c] ^ 7u) & 31u)) & 1u);
+                } else if (l[c] != 0xFFFFFFFFu && !((s_bits[l[c] >> 5] >> ((l[c] ^ 7u) & 31u)) & 1u)) {
+                    out8[key[c]] = 0;
+                }
+            }
         });
+}
+
+// The owner's insert and include? of one partitioned step in ONE pass over the shard: region r
+// is read once, its insert probes (level-2 arrays of the insert plan) ORed into the LDS image and
+// the region written back as bin_apply does, then its include? probes (the test plan's level
+// 2) tested against the updated image, each answer stored at its level-2 index (bin_test
+// <L2ORDER>).  The answers see every insert of the step, as insert-then-test does: a test probe
+// in region r reads only region r.  One read of the shard and one run-table walk set-up fewer
+// than bin_apply + bin_test.
+struct BfL2 {   // one plan's level-2 arrays and run tables
+    const uint32_t* level2;
+    const uint32_t* cb_base;
+    const uint32_t* cb_start;
+    const uint16_t* tabs;
+    uint64_t max_chunks;
+    uint32_t nq;
+};
+template <uint32_t RLOG2, uint32_t LANES, int ILOADS>
+__global__ __launch_bounds__(LANES) void bin_apply_test_kernel(uint32_t* __restrict__ bits, uint64_t nwords, BfL2 ins,
+                                                               BfL2 tst, uint32_t rel_log2, uint32_t dense,
+                                                               uint32_t* __restrict__ any_flag,
+                                                               uint8_t* __restrict__ dirty, uint32_t store_fresh,
+                                                               uint8_t* __restrict__ ans2) {
+    constexpr uint32_t kVec = 1u << (RLOG2 - 7);
+    constexpr uint32_t kPer = kVec / LANES;
+    constexpr int kTLoads = 8;
+    static_assert(kPer * LANES == kVec, "region must tile the workgroup");
+    __shared__ uint4 s_img4[kVec];
+    __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass], s_w[16];
+    uint32_t* s_img = reinterpret_cast<uint32_t*>(s_img4);
+    const uint32_t t = threadIdx.x;
+    const uint32_t r = apply_region(blockIdx.x, gridDim.x, 2u);
+    const uint64_t v0 = (uint64_t)r * kVec;
+    const uint64_t nvec = nwords / 4;
+    uint4* gv = reinterpret_cast<uint4*>(bits);
+    // every region is read: the test needs all of it (dense or not)
+    uint4 old[kPer];
+#pragma unroll
+    for (uint32_t c = 0; c < kPer; ++c) {
+        const uint32_t v = c * LANES + t;
+        old[c] = v0 + v < nvec ? apply_load(gv + v0 + v) : make_uint4(0, 0, 0, 0);
+    }
+    for (uint32_t v = t; v < kVec; v += LANES) s_img4[v] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for_region_probes<ILOADS>(ins.cb_base, ins.cb_start, ins.tabs, ins.max_chunks, r, ins.nq, rel_log2, s_pre, s_gst,
+                              s_w, [&](const uint32_t* idx) {
+        uint32_t l[ILOADS];
+#pragma unroll
+        for (int c = 0; c < ILOADS; ++c) l[c] = idx[c] != 0xFFFFFFFFu ? ins.level2[idx[c]] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int c = 0; c < ILOADS; ++c)
+            if (l[c] != 0xFFFFFFFFu) atomicOr(s_img + (l[c] >> 5), 1u << ((l[c] ^ 7u) & 31u));
+    });
+    // (for_region_probes ends with a barrier: the insert image is complete)
+    uint32_t fresh = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kPer; ++c) {
+        const uint32_t v = c * LANES + t;
+        const uint4 m = s_img4[v];
+        const uint4 nw = make_uint4(old[c].x | m.x, old[c].y | m.y, old[c].z | m.z, old[c].w | m.w);
+        s_img4[v] = nw;   // the image becomes the region after the step's inserts
+        const uint32_t fr = (m.x & ~old[c].x) | (m.y & ~old[c].y) | (m.z & ~old[c].z) | (m.w & ~old[c].w);
+        fresh |= fr;
+        if (v0 + v >= nvec) continue;
+        bool st;
+        if (dense == 2) st = true;
+        else if (store_fresh) st = fr != 0u;
+        else st = (m.x | m.y | m.z | m.w) != 0u;
+        if (st) apply_store(gv + v0 + v, nw);
+        if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
+    }
+    if (any_flag) report_any_new(any_flag, fresh != 0);
+    __syncthreads();
+    for_region_probes<kTLoads>(tst.cb_base, tst.cb_start, tst.tabs, tst.max_chunks, r, tst.nq, rel_log2, s_pre, s_gst,
+                               s_w, [&](const uint32_t* idx) {
+        uint32_t l[kTLoads];
+#pragma unroll
+        for (int c = 0; c < kTLoads; ++c)
+            l[c] = idx[c] != 0xFFFFFFFFu ? __builtin_nontemporal_load(tst.level2 + idx[c]) : 0xFFFFFFFFu;
+#pragma unroll
+        for (int c = 0; c < kTLoads; ++c)
+            if (l[c] != 0xFFFFFFFFu) ans2[idx[c]] = (uint8_t)((s_img[l[c] >> 5] >> ((l[c] ^ 7u) & 31u)) & 1u);
+    });
 }
 
 // ---- chunked windows, owner side (bf_route_chunks_dev's windows as level 1) ----------------
 
 // The run of superbin lsb (window-local) in chunk c of sub-range h: c = src * tiles + tile.
 // An overflowed window (live count past cap) or a dropped chunk has none.
+__device__ __forceinline__ uint64_t chunks_per_src(const BfChunkIn& ci) { return ci.ranked ? ci.cps : ci.tiles; }
+// The tile holding rank r's run in window j (ranked chunks), or ~0 when no run has that rank.
+__device__ __forceinline__ uint64_t ranked_tile(const BfChunkIn& ci, uint32_t j, uint64_t r) {
+    const uint8_t* d = ci.dir + (uint64_t)j * ci.dir_bytes;
+    const uint32_t v = reinterpret_cast<const uint16_t*>(d + 4 * ci.tiles + 2 * (uint64_t)(ci.S + 1) * ci.tiles)[r];
+    return v && v <= ci.tiles ? (uint64_t)v - 1u : ~0ull;
+}
 __device__ __forceinline__ void chunk_run(const BfChunkIn& ci, uint32_t h, uint32_t lsb, uint64_t c, uint32_t* len,
                                           uint32_t* st) {
-    const uint32_t src = (uint32_t)(c / ci.tiles);
-    const uint64_t tile = c - (uint64_t)src * ci.tiles;
+    const uint64_t cps = chunks_per_src(ci);
+    const uint32_t src = (uint32_t)(c / cps);
+    uint64_t tile = c - (uint64_t)src * cps;
     const uint32_t j = h * ci.nsrc + src;
     *len = 0;
     *st = 0;
-    if (ci.counts[(uint64_t)src * ci.cstride + h] > ci.cap) return;
+    if (tile >= ci.tiles || ci.counts[(uint64_t)src * ci.cstride + h] > ci.cap) return;
+    if (ci.ranked && (tile = ranked_tile(ci, j, tile)) == ~0ull) return;   // rank -> tile
     const uint8_t* d = ci.dir + (uint64_t)j * ci.dir_bytes;
     const uint32_t start = reinterpret_cast<const uint32_t*>(d)[tile];
     if (start == 0xFFFFFFFFu) return;
@@ -1455,7 +1571,7 @@ __global__ __launch_bounds__(kRunsPerPass) void chunk_group_sum_kernel(BfChunkIn
     const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
     const uint64_t c = (uint64_t)q * kRunsPerPass + t;
     uint32_t len = 0, st = 0;
-    if (c < (uint64_t)ci.nsrc * ci.tiles) chunk_run(ci, h, lsb, c, &len, &st);
+    if (c < (uint64_t)ci.nsrc * chunks_per_src(ci)) chunk_run(ci, h, lsb, c, &len, &st);
     uint32_t total;
     const uint32_t ex = block_excl_scan(len, s_w, &total);
     if (t == 0) gsum[sb * nq + q] = total;
@@ -1535,7 +1651,7 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
             }
         }
     };
-    const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles;
+    const uint64_t nch = (uint64_t)ci.nsrc * chunks_per_src(ci);
     // XCD-local sweep: workgroup b runs on XCD b % 8 (round-robin dispatch; the grid is a
     // multiple of 8), and XCD x sweeps superbins x, x + 8, ..., its gridDim / 8 workgroups
     // sharing each superbin's items.  So each XCD's L2 holds one superbin, where a sweep of the
@@ -1651,7 +1767,7 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
     const uint64_t hoff = (uint64_t)h << 32;
     const uint32_t smask = (1u << ci.sup_log2) - 1u;
     // run table of the group's chunks
-    const uint64_t nch = (uint64_t)ci.nsrc * ci.tiles, c0 = (uint64_t)q * kRunsPerPass;
+    const uint64_t nch = (uint64_t)ci.nsrc * chunks_per_src(ci), c0 = (uint64_t)q * kRunsPerPass;
     const uint32_t nt = (uint32_t)(nch - c0 < kRunsPerPass ? nch - c0 : kRunsPerPass);
     uint32_t len = 0, st = 0;
     if (t < nt) chunk_run(ci, h, lsb, c0 + t, &len, &st);
@@ -1677,7 +1793,7 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
                     lv[u] = o & smask;
                     kv[u] = idx;
                 } else if constexpr (KEYS) {
-                    out8[idx] = 0;   // an offset past the shard answers 0
+                    if (out8) out8[idx] = 0;   // an offset past the shard answers 0 (packed answers: never set)
                 }
             }
         }
@@ -1791,11 +1907,126 @@ __global__ __launch_bounds__(kCombineLanes) void combine_chunks_packed_kernel(
     for (uint32_t j = t; j < tk; j += kCombineLanes) out[key0 + j] = s_ans[j];
 }
 
+// ---- the sorted owner test's answers as packed bits, without a scatter -------------------
+//
+// bin_test writes each probe's answer at its receive position: at 200B x 8 that is ~10^8
+// scattered byte stores per step (1.74 ms of bin_test's time, against ~0.5 ms for the same
+// kernel storing the answers at their level-2 index: profiles/r06d_ab_test_order.jsonl).  The
+// route claims window space tile by tile in arbitrary order, so a group of chunks spans its
+// whole window.  Ranked chunks fix that: the route records the order it claimed each window's
+// runs in (the directory's rank table), the owner's mid groups chunks by rank, and then group q's runs in
+// sub-range h are ONE contiguous range of one window.  The test stores answers in level-2
+// order (bin_test<L2ORDER>); chunk_unsort_kernel, one workgroup per (h, q), reads the group's
+// level-2 entries (receive index + answer), sets the answer bits of that range in an LDS
+// bitmap and stores them as the window's packed bits — the return trip's layout, so no
+// separate pack pass either.
+constexpr uint32_t kUnsortWords = 38912;       // LDS bitmap of one group's range per pass: 1,245,184 entries
+
+// One workgroup per (group q, sub-range h): the answers of group q's level-2 entries in the
+// superbins of h (ans2[l] at level-2 index l, its receive index level2_key[l]) as bits of the
+// window's packed answers (window (h, src) at packed + (src * nh + h) * cap8, bit e = entry e,
+// LSB first: combine_chunks_packed_kernel's layout).  packed must be zeroed: a live entry with no
+// level-2 entry (its offset was past the shard) answers 0, and the range's two edge words, which
+// it may share with the neighbouring groups, are ORed in.  A range wider than the LDS bitmap
+// takes several passes over the group's entries (the 200B x 8 shard's first 2^32-bit sub-range:
+// ~1.04M entries per group, one pass).
+__global__ __launch_bounds__(1024) void chunk_unsort_kernel(BfChunkIn ci, uint32_t nq, uint32_t nsup,
+                                                            const uint32_t* __restrict__ base,
+                                                            const uint32_t* __restrict__ level2_key,
+                                                            const uint8_t* __restrict__ ans2,
+                                                            uint8_t* __restrict__ packed, uint64_t cap8) {
+    __shared__ uint32_t s_bits[kUnsortWords];
+    __shared__ uint32_t s_lo[16], s_hi[16];
+    const uint32_t t = threadIdx.x, q = blockIdx.x, h = blockIdx.y;
+    const uint64_t c0 = (uint64_t)q * kRunsPerPass;
+    const uint32_t src = (uint32_t)(c0 / ci.cps);
+    const uint64_t r0 = c0 - (uint64_t)src * ci.cps;
+    if (src >= ci.nsrc || ci.counts[(uint64_t)src * ci.cstride + h] > ci.cap) return;   // overflowed: replayed
+    const uint32_t j = h * ci.nsrc + src;
+    // the group's range [lo, hi) of window j: its chunks' runs, consecutive by rank
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    const uint64_t tile = r0 + t < ci.tiles ? ranked_tile(ci, j, r0 + t) : ~0ull;
+    if (tile != ~0ull) {
+        const uint8_t* d = ci.dir + (uint64_t)j * ci.dir_bytes;
+        const uint32_t st = reinterpret_cast<const uint32_t*>(d)[tile];
+        const uint32_t ln = reinterpret_cast<const uint16_t*>(d + 4 * ci.tiles)[(uint64_t)ci.S * ci.tiles + tile];
+        if (st != 0xFFFFFFFFu && ln && st < ci.cap) {   // chunk_run reads runs inside [st, min(st + ln, cap))
+            lo = st;
+            hi = (uint64_t)st + ln < ci.cap ? st + ln : (uint32_t)ci.cap;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {   // every lane of the workgroup is active here
+        const uint32_t a = (uint32_t)__shfl_xor((int)lo, off), b = (uint32_t)__shfl_xor((int)hi, off);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((t & 63u) == 0) {
+        s_lo[t >> 6] = lo;
+        s_hi[t >> 6] = hi;
+    }
+    __syncthreads();
+    uint32_t LO = 0xFFFFFFFFu, HI = 0;
+    for (uint32_t i = 0; i < 16; ++i) {
+        LO = s_lo[i] < LO ? s_lo[i] : LO;
+        HI = s_hi[i] > HI ? s_hi[i] : HI;
+    }
+    if (LO >= HI) return;   // workgroup-uniform: no probe of this group reached sub-range h
+    const uint32_t a0 = LO & ~31u, nw = (HI - a0 + 31u) >> 5;
+    uint32_t* out = reinterpret_cast<uint32_t*>(packed + ((uint64_t)src * ci.nh + h) * cap8) + (a0 >> 5);
+    const uint64_t jbase = (uint64_t)j * ci.cap;
+    const uint32_t sb1 = (h + 1) * ci.S < nsup ? (h + 1) * ci.S : nsup;
+    constexpr uint32_t kU = 4;   // loads in flight per lane: 4 entries each (16 B of receive indices, 4 answers)
+    for (uint32_t w0 = 0; w0 < nw; w0 += kUnsortWords) {   // passes of kUnsortWords words
+        const uint32_t pw = nw - w0 < kUnsortWords ? nw - w0 : kUnsortWords;
+        for (uint32_t i = t; i < pw; i += 1024) s_bits[i] = 0;
+        __syncthreads();
+        const uint32_t b0 = w0 << 5, b1 = (w0 + pw) << 5;   // this pass's entries, relative to a0
+        for (uint32_t sb = h * ci.S; sb < sb1; ++sb) {
+            const uint32_t w = sb * nq + q, l0 = base[w], l1 = base[w + 1];
+            for (uint32_t q0 = (l0 & ~3u) + 4u * t; q0 < l1; q0 += 4u * 1024u * kU) {
+                uint4 kv[kU];
+                uint32_t av[kU];
+#pragma unroll
+                for (uint32_t u = 0; u < kU; ++u) {
+                    const uint32_t qa = q0 + u * 4u * 1024u;
+                    kv[u] = make_uint4(0, 0, 0, 0);
+                    av[u] = 0;
+                    if (qa < l1) {
+                        kv[u] = *reinterpret_cast<const uint4*>(level2_key + qa);
+                        av[u] = *reinterpret_cast<const uint32_t*>(ans2 + qa);
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kU; ++u) {
+                    const uint32_t qa = q0 + u * 4u * 1024u;
+                    const uint32_t k4[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        // e < cap (chunk_run's runs end inside the window); ri in [b0, b1): this pass
+                        const uint32_t ri = (uint32_t)(k4[i] - jbase) - a0;
+                        if (((av[u] >> (8 * i)) & 0xFFu) && qa + i >= l0 && qa + i < l1 && ri >= b0 && ri < b1)
+                            atomicOr(s_bits + ((ri - b0) >> 5), 1u << (ri & 31u));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < pw; i += 1024) {
+            const bool edge = (w0 + i == 0) || (w0 + i == nw - 1);   // shared with the neighbouring groups
+            if (edge) atomicOr(out + w0 + i, s_bits[i]);
+            else out[w0 + i] = s_bits[i];
+        }
+        __syncthreads();   // the next pass clears the bitmap
+    }
+}
+
 uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Carve {
     uint32_t *level1, *level1_key, *level2, *level2_key, *gcnt, *gsum, *base, *cb_base, *cb_window, *cb_start;
     uint16_t *stab, *tabs;
+    uint8_t* ans2;   // ranked chunked test: the answers in level-2 order
     uint2* runs;   // the chunked L2-local test's window run tables
     uint16_t* istart;   // ... and the first run of each of its items
     uint32_t* stot;   // hierarchical scan: per-superbin totals
@@ -1828,6 +2059,7 @@ Carve carve(const BfBinPlan& p, void* at0) {
         return c;
     }
     c.tabs = reinterpret_cast<uint16_t*>(take(p.max_chunks * ((1ull << p.rel_log2) + 1) * 2));   // [region][block]
+    if (p.ordered) c.ans2 = take(p.probes + 16);   // the unsort reads whole 4-byte quads
     c.bytes = off;
     return c;
 }
@@ -2383,11 +2615,15 @@ bool bf_chunk_geometry(uint64_t shard0_bits, uint32_t nwin, uint32_t pref_region
 }
 
 uint64_t bf_chunk_dir_bytes(const BfChunks& cg, uint64_t tiles) {
-    return (4 * tiles + 2 * (uint64_t)(cg.S + 1) * tiles + 15) & ~(uint64_t)15;
+    return (bf_chunk_dir_claim_offset(cg, tiles) + 8 + 15) & ~(uint64_t)15;
+}
+
+bool bf_chunk_ordered_ok(uint64_t tiles, uint64_t cap) {
+    return tiles >= 1 && tiles < 0xFFFFu && ((cap + 7) / 8) % 4 == 0;
 }
 
 bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint32_t nsrc, uint64_t cap,
-                   bool with_keys, BfBinPlan* plan, bool l2test) {
+                   bool with_keys, BfBinPlan* plan, bool l2test, bool ordered) {
     if (nh == 0 || nsrc == 0 || cap == 0 || cg.tiles == 0) return false;
     const uint64_t probes = (uint64_t)nh * nsrc * cap;
     if (probes >= (1ull << 32)) return false;
@@ -2395,6 +2631,11 @@ bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint3
     p.chunked = true;
     p.with_keys = with_keys;
     p.l2test = l2test && with_keys;
+    p.ordered = ordered && with_keys && !p.l2test;
+    if (p.ordered && !bf_chunk_ordered_ok(cg.tiles, cap)) return false;
+    p.tiles = cg.tiles;
+    p.nwin = nh * nsrc;
+    p.cps = p.ordered ? (cg.tiles + kRunsPerPass - 1) / kRunsPerPass * kRunsPerPass : cg.tiles;
     p.region_log2 = cg.region_log2;
     p.rel_log2 = cg.rel_log2;
     const uint64_t bits = bitset_bytes * 8;
@@ -2402,7 +2643,7 @@ bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint3
     p.nbins = (uint32_t)nbins;
     p.nsup = (uint32_t)((nbins + (1ull << p.rel_log2) - 1) >> p.rel_log2);
     if (p.nsup == 0 || p.nsup > (uint64_t)nh * cg.S) return false;
-    p.ngroups = (uint32_t)(((uint64_t)nsrc * cg.tiles + kRunsPerPass - 1) / kRunsPerPass);
+    p.ngroups = (uint32_t)(((uint64_t)nsrc * p.cps + kRunsPerPass - 1) / kRunsPerPass);
     if ((uint64_t)p.nsup * p.ngroups > kMaxWindows || p.ngroups > kMaxGroups) return false;
     p.probes = probes;
     p.max_chunks = (probes + kBlockProbes - 1) / kBlockProbes + (uint64_t)p.nsup * p.ngroups;
@@ -2440,6 +2681,52 @@ hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, ui
     if (e != hipSuccess) return e;
     return launch_apply(g, p, c, bitset_bytes, any_flag, s, mk);
 }
+
+hipError_t bf_launch_shard_insert_test_chunks_packed(const BfGeom& g, const BfBinPlan& pi, const BfBinPlan& pt,
+                                                     uint64_t bitset_bytes, const BfChunkIn& cii, BfChunkIn cit,
+                                                     void* scratch, uint32_t* any_flag, uint8_t* packed, hipStream_t s,
+                                                     BfMarks* mk) {
+    if (!pi.chunked || pi.with_keys || !pt.chunked || !pt.with_keys || !pt.ordered || !packed ||
+        pi.region_log2 != pt.region_log2 || pi.rel_log2 != pt.rel_log2 || pi.nbins != pt.nbins ||
+        pt.tiles != cit.tiles || pt.nwin != cit.nh * cit.nsrc)
+        return hipErrorInvalidValue;
+    const Carve ci_ = carve(pi, scratch);
+    const Carve ct = carve(pt, static_cast<uint8_t*>(scratch) + carve(pi, nullptr).bytes);
+    hipError_t e = launch_chunk_mid(pi, ci_, cii, nullptr, s, mk);   // the inserts' level 2
+    if (e != hipSuccess) return e;
+    cit.ranked = true;
+    cit.cps = pt.cps;
+    const uint64_t cap8 = (cit.cap + 7) / 8;
+    if ((e = hipMemsetAsync(packed, 0, (uint64_t)pt.nwin * cap8, s)) != hipSuccess) return e;
+    if ((e = launch_chunk_mid(pt, ct, cit, nullptr, s, mk)) != hipSuccess) return e;   // the tests' level 2 + keys
+    const uint64_t nwords = bitset_bytes / 4;
+    const BfL2 li{ci_.level2, ci_.cb_base, ci_.cb_start, ci_.tabs, pi.max_chunks, pi.ngroups};
+    const BfL2 lt{ct.level2, ct.cb_base, ct.cb_start, ct.tabs, pt.max_chunks, pt.ngroups};
+    const uint64_t vecs = (uint64_t)pi.nbins << (pi.region_log2 - 7);
+    const uint32_t dense = pi.probes >= vecs ? 2u : (pi.probes >= vecs / 8 ? 1u : 0u);
+    const int iloads = pi.probes <= (uint64_t)pi.nbins * 4096u ? 2 : 8;   // as launch_apply
+#define BF_APPLY_TEST(RL, LANES, LD)                                                                              \
+    hipLaunchKernelGGL((bin_apply_test_kernel<RL, LANES, LD>), dim3(pi.nbins), dim3(LANES), 0, s, g.bits, nwords, li, \
+                       lt, pi.rel_log2, dense, any_flag, g.dirty, apply_store_fresh(), ct.ans2)
+    if (pi.region_log2 == 18) {
+        if (iloads == 2) BF_APPLY_TEST(18, kApplyLanes / 2, 2);
+        else BF_APPLY_TEST(18, kApplyLanes / 2, 8);
+    } else if (pi.region_log2 == 19) {
+        if (iloads == 2) BF_APPLY_TEST(19, kApplyLanes, 2);
+        else BF_APPLY_TEST(19, kApplyLanes, 8);
+    } else {
+        if (iloads == 2) BF_APPLY_TEST(20, kApplyLanes, 2);
+        else BF_APPLY_TEST(20, kApplyLanes, 8);
+    }
+#undef BF_APPLY_TEST
+    bf_mark(mk, s, "apply_test");
+    hipLaunchKernelGGL(chunk_unsort_kernel, dim3(pt.ngroups, cit.nh), dim3(1024), 0, s, cit, pt.ngroups, pt.nsup,
+                       ct.base, ct.level2_key, ct.ans2, packed, cap8);
+    bf_mark(mk, s, "unsort_packed");
+    return hipGetLastError();
+}
+
+uint64_t bf_chunk_scratch_bytes(const BfBinPlan& p) { return carve(p, nullptr).bytes; }
 
 hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,
@@ -2496,6 +2783,38 @@ hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint
     if (e != hipSuccess) return e;
     if ((e = launch_chunk_mid(p, c, ci, out8, s, mk)) != hipSuccess) return e;
     return launch_test(g, p, c, bitset_bytes, out8, s, mk);
+}
+
+hipError_t bf_launch_shard_test_chunks_packed(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                              BfChunkIn ci, void* scratch, uint8_t* packed, hipStream_t s,
+                                              BfMarks* mk) {
+    if (!p.chunked || !p.with_keys || !p.ordered || !packed || p.tiles != ci.tiles || p.nwin != ci.nh * ci.nsrc)
+        return hipErrorInvalidValue;
+    const Carve c = carve(p, scratch);
+    ci.ranked = true;
+    ci.cps = p.cps;
+    const uint64_t cap8 = (ci.cap + 7) / 8;
+    hipError_t e = hipMemsetAsync(packed, 0, (uint64_t)p.nwin * cap8, s);   // entries with no level-2 entry answer 0
+    if (e != hipSuccess) return e;
+    if ((e = launch_chunk_mid(p, c, ci, nullptr, s, mk)) != hipSuccess) return e;
+    const uint64_t nwords = bitset_bytes / 4;
+    if (p.region_log2 == 18)
+        hipLaunchKernelGGL((bin_test_kernel<18, kApplyLanes / 2, true>), dim3(p.nbins), dim3(kApplyLanes / 2), 0, s,
+                           g.bits, nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks,
+                           p.ngroups, p.rel_log2, c.ans2);
+    else if (p.region_log2 == 19)
+        hipLaunchKernelGGL((bin_test_kernel<19, kApplyLanes, true>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
+                           p.rel_log2, c.ans2);
+    else
+        hipLaunchKernelGGL((bin_test_kernel<20, kApplyLanes, true>), dim3(p.nbins), dim3(kApplyLanes), 0, s, g.bits,
+                           nwords, c.level2, c.level2_key, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups,
+                           p.rel_log2, c.ans2);
+    bf_mark(mk, s, "bin_test_l2order");
+    hipLaunchKernelGGL(chunk_unsort_kernel, dim3(p.ngroups, ci.nh), dim3(1024), 0, s, ci, p.ngroups, p.nsup, c.base,
+                       c.level2_key, c.ans2, packed, cap8);
+    bf_mark(mk, s, "unsort_packed");
+    return hipGetLastError();
 }
 
 hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t nh, const BfChunks& cg,

@@ -105,7 +105,24 @@ struct BfChunkIn {
     uint64_t dir_bytes = 0, tiles = 0, cap = 0, limit = 0;
     const unsigned long long* counts = nullptr;
     uint32_t cstride = 1, nsrc = 1, nh = 1, S = 1, sup_log2 = 0;
+    // Ranked chunks (the sorted owner test with packed answers): chunk c = src * cps + r is the
+    // tile whose run has rank r in window (h, src) — the order the route claimed the window's
+    // runs in, recorded in the directory's rank table — and cps = tiles rounded up to whole
+    // run-table passes, so every group of chunks lies in one window and its runs are ONE
+    // contiguous range of it.  Unranked: chunk c = src * tiles + tile.
+    bool ranked = false;
+    uint64_t cps = 0;
 };
+// Directory of window w (BfChunks / bf_route_chunks_dev), after start[tiles] and tab[(S + 1) *
+// tiles]: rank[tiles] (uint16: 1 + the tile whose run the route claimed r-th in the window, 0 =
+// none) and an 8-byte claim counter (runs claimed << kClaimRankShift | entries claimed).
+constexpr uint32_t kClaimRankShift = 40;
+__host__ __device__ inline uint64_t bf_chunk_dir_rank_offset(const BfChunks& cg, uint64_t tiles) {
+    return 4 * tiles + 2 * (uint64_t)(cg.S + 1) * tiles;
+}
+__host__ __device__ inline uint64_t bf_chunk_dir_claim_offset(const BfChunks& cg, uint64_t tiles) {
+    return (bf_chunk_dir_rank_offset(cg, tiles) + 2 * tiles + 7) & ~(uint64_t)7;
+}
 
 enum BfOp : int {
     BF_OP_INDEXES      = 0,  // write the k offsets of each key (ruby.rb:41-55)
@@ -152,6 +169,10 @@ struct BfBinPlan {
     uint64_t scratch_bytes; // device scratch the launch needs
     bool     chunked;       // level 1 = received chunked windows (no front pass, no level-1 arrays)
     bool     l2test;        // chunked include?: the superbin-major L2-local test (no mid sort, no level 2)
+    bool     ordered;       // chunked include? with packed answers: chunks ranked by run start (BfChunkIn::ranked)
+    uint64_t cps;           // ... chunks per source (tiles rounded up to whole groups)
+    uint32_t nwin;          // ... received windows (nh * nsrc)
+    uint64_t tiles;         // ... directory tiles
 };
 // Optional per-kernel timing: when a BfMarks is passed, a launcher records
 // marks->ev[i] after its i-th kernel (ev[0] before the first), named names[i].
@@ -237,7 +258,10 @@ hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const ui
 // windows of cap entries and `tiles` chunks each; insert (any_flag nullable) or test (out8[i]
 // = bit of recv entry i, for every live entry; plan with_keys).
 bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint32_t nsrc, uint64_t cap,
-                   bool with_keys, BfBinPlan* plan, bool l2test = false);
+                   bool with_keys, BfBinPlan* plan, bool l2test = false, bool ordered = false);
+// Whether the ranked (packed-answer) test takes this geometry: a tile index fits the directory's
+// uint16 rank table and each window's packed answers start on a 4-byte word.
+bool bf_chunk_ordered_ok(uint64_t tiles, uint64_t cap);
 hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                          const BfChunkIn& ci, void* scratch, uint32_t* any_flag, hipStream_t s,
                                          BfMarks* marks = nullptr);
@@ -254,6 +278,21 @@ struct BfSideHash {
 hipError_t bf_launch_shard_test_chunks(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
                                        const BfChunkIn& ci, void* scratch, uint8_t* out8, hipStream_t s,
                                        BfMarks* marks = nullptr, const BfSideHash& side = BfSideHash{});
+// The same test with the answers as packed bits in the return trip's layout (window (h, src) at
+// packed + (src * nh + h) * ceil(cap / 8), LSB first): ordered chunks, answers stored in level-2
+// order and moved to receive order per group in LDS (plan: bf_chunk_plan(..., ordered = true)).
+hipError_t bf_launch_shard_test_chunks_packed(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                              BfChunkIn ci, void* scratch, uint8_t* packed, hipStream_t s,
+                                              BfMarks* marks = nullptr);
+// One step's owner work in one pass over the shard: the insert windows (plan pi, as
+// bf_launch_shard_insert_chunks) ORed in and the include? windows (plan pt, ordered, as
+// bf_launch_shard_test_chunks_packed) tested against the result, region by region.  Scratch:
+// bf_chunk_scratch_bytes(pi) + bf_chunk_scratch_bytes(pt).
+uint64_t bf_chunk_scratch_bytes(const BfBinPlan& p);
+hipError_t bf_launch_shard_insert_test_chunks_packed(const BfGeom& g, const BfBinPlan& pi, const BfBinPlan& pt,
+                                                     uint64_t bitset_bytes, const BfChunkIn& cii, BfChunkIn cit,
+                                                     void* scratch, uint32_t* any_flag, uint8_t* packed, hipStream_t s,
+                                                     BfMarks* marks = nullptr);
 // Requester side: the window route with directories (cg.dir zeroed here first; slot16
 // nullable: tile-relative key indices).
 // dig: keys16 holds the keys' SHA-1 words (uint4 per key; offsets unused) instead of key bytes.

@@ -277,6 +277,29 @@ class HipEngine:
         self.filter.shard_test_chunks_dev(recv.data_ptr(), cap, nsrc, rdir.data_ptr(), dir_bytes, tiles,
                                           counts.data_ptr(), cstride, out.data_ptr(), stream=self._stream())
 
+    def shard_test_chunks_packed(self, recv: torch.Tensor, cap: int, nsrc: int, rdir: torch.Tensor, dir_bytes: int,
+                                 tiles: int, counts: torch.Tensor, cstride: int) -> torch.Tensor:
+        """The owner test's answers as packed bits, laid out as the return trip sends them:
+        window (h, src) at (src * nh + h) * ceil(cap / 8) (no pack pass)."""
+        cap8 = (cap + 7) // 8
+        packed = torch.empty(max(nsrc * self.nh * cap8, 1), dtype=torch.uint8, device=self.device)
+        self.filter.shard_test_chunks_packed_dev(recv.data_ptr(), cap, nsrc, rdir.data_ptr(), dir_bytes, tiles,
+                                                 counts.data_ptr(), cstride, packed.data_ptr(), stream=self._stream())
+        return packed
+
+    def shard_insert_test_chunks_packed(self, irecv: torch.Tensor, irdir: torch.Tensor, icounts: torch.Tensor,
+                                        trecv: torch.Tensor, trdir: torch.Tensor, tcounts: torch.Tensor, cap: int,
+                                        nsrc: int, dir_bytes: int, tiles: int, cstride: int) -> torch.Tensor:
+        """shard_insert_chunks then shard_test_chunks_packed, in one pass over the shard where
+        both take their sorted forms; returns the packed answers."""
+        cap8 = (cap + 7) // 8
+        packed = torch.empty(max(nsrc * self.nh * cap8, 1), dtype=torch.uint8, device=self.device)
+        self.filter.shard_insert_test_chunks_packed_dev(irecv.data_ptr(), irdir.data_ptr(), icounts.data_ptr(),
+                                                        trecv.data_ptr(), trdir.data_ptr(), tcounts.data_ptr(), cap,
+                                                        nsrc, dir_bytes, tiles, cstride, packed.data_ptr(),
+                                                        stream=self._stream())
+        return packed
+
     def combine_chunks_packed(self, packed: torch.Tensor, slot: torch.Tensor, cap: int, dirb: torch.Tensor,
                               dir_bytes: int, tiles: int, counts: torch.Tensor, n: int) -> torch.Tensor:
         out = torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)[:n]
@@ -736,6 +759,12 @@ class PartitionedFilter:
         e, P, nh, cap, n = self.engine, self.P, self.engine.nh, st["cap"], st["n"]
         for w in st["works"]:
             w.wait()
+        side = next_include is not None and next_include[2] and hasattr(e, "hash_keys")
+        if st["geo"] is not None and self.pack_answers and not side and hasattr(e, "shard_test_chunks_packed"):
+            # the owner test writes the return trip's packed bits itself (no answer bytes, no pack pass)
+            tiles, dbytes = st["geo"]
+            packed = e.shard_test_chunks_packed(st["recv"], cap, P, st["rdir"], dbytes, tiles, st["rmsg"], nh + 1)
+            return self._sf_return_packed(st, packed)
         bits = self._buf(nh * P * cap, torch.uint8, st["recv"].device, answers=True)
         if st["geo"] is not None:
             tiles, dbytes = st["geo"]
@@ -786,6 +815,35 @@ class PartitionedFilter:
             packed = e.pack_answers(back, self._pk_seg[key], cap, P * nh * cap8)
             return e.combine_chunks_packed(packed, st["slot"], cap, st["dir"], dbytes, tiles, st["counts"], n)
         return e.combine_windows(back, st["slot"], st["counts"], cap, n)
+
+    def _sf_return_packed(self, st: dict, packed: torch.Tensor) -> torch.Tensor:
+        """The owner's packed answers back to their requesters, then this rank's combine."""
+        e, P, nh, cap, n = self.engine, self.P, self.engine.nh, st["cap"], st["n"]
+        tiles, dbytes = st["geo"]
+        cap8 = (cap + 7) // 8
+        back = self._buf(P * nh * cap8, torch.uint8, packed.device, answers=True)
+        seg = [(src, (src * nh + h) * cap8, cap8) for src in range(P) for h in range(nh)]
+        for w in self._p2p(packed, seg, back, seg):
+            w.wait()
+        if not st["own_chunks"]:   # this rank's batch took plain windows declared overflowed: replayed
+            return torch.zeros(n, dtype=torch.uint8, device=packed.device)
+        return e.combine_chunks_packed(back, st["slot"], cap, st["dir"], dbytes, tiles, st["counts"], n)
+
+    def _sf_insert_answer(self, st_i: dict, st_q: dict) -> Optional[torch.Tensor]:
+        """_sf_insert(st_i) then _sf_answer(st_q) as ONE owner pass over the shard
+        (bf_shard_insert_test_chunks_packed_dev), when both batches took chunked windows of the
+        same geometry; None when they did not (the caller then makes the two calls)."""
+        e = self.engine
+        if (st_i["geo"] is None or st_q["geo"] is None or st_i["geo"] != st_q["geo"] or st_i["cap"] != st_q["cap"]
+                or not self.pack_answers or not hasattr(e, "shard_insert_test_chunks_packed")):
+            return None
+        for w in st_i["works"] + st_q["works"]:
+            w.wait()
+        tiles, dbytes = st_q["geo"]
+        packed = e.shard_insert_test_chunks_packed(st_i["recv"], st_i["rdir"], st_i["rmsg"], st_q["recv"],
+                                                   st_q["rdir"], st_q["rmsg"], st_q["cap"], self.P, dbytes, tiles,
+                                                   e.nh + 1)
+        return self._sf_return_packed(st_q, packed)
 
     def _synced_insert(self, kb, ko, n: int) -> None:
         recv, rt, works = self._exchange(kb, ko, n, want_slot=False)
@@ -869,8 +927,10 @@ class PartitionedFilter:
                 self._pending = self._sf_start(*next_insert, want_slot=False)
             self._sf_flag(st_i)
             self._sf_flag(st_q)
-            self._sf_insert(st_i)
-            out = self._sf_answer(st_q, next_include=next_include)
+            out = None if next_include is not None else self._sf_insert_answer(st_i, st_q)
+            if out is None:
+                self._sf_insert(st_i)
+                out = self._sf_answer(st_q, next_include=next_include)
             if self._sf_overflowed(st_i) or self._sf_overflowed(st_q):
                 self.replays += 1
                 self._synced_insert(ikb, iko, ni)

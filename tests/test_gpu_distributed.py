@@ -212,7 +212,9 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     assert geo is not None and all(e.chunk_info(n) == geo for e in shards)
     tiles, dbytes = geo
     S = shards[0].filter.route_chunk_info(n)[2]
-    assert dbytes == -(-(4 * tiles + 2 * (S + 1) * tiles) // 16) * 16
+    rank_off = 4 * tiles + 2 * (S + 1) * tiles          # start[tiles], tab[(S + 1) * tiles], then rank[tiles]
+    claim_off = -(-(rank_off + 2 * tiles) // 8) * 8    # ... and the 8-byte claim counter
+    assert dbytes == -(-(claim_off + 8) // 16) * 16
     tile_keys = 2048 if k <= 6 else 1024
     assert tiles == -(-n // tile_keys)
     A = 12288
@@ -258,6 +260,13 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
                 assert a == at
                 at = e
             assert at == int(want_c[w])
+            # the rank table lists the claimed runs in window order (the owner's ranked chunks)
+            rank = dw[rank_off: rank_off + 2 * tiles].view(np.uint16).astype(np.int64)
+            nclaim = int(dw[claim_off: claim_off + 8].view(np.uint64)[0]) >> 40
+            assert nclaim == int(live.sum()) and (rank[nclaim:] == 0).all()
+            ranked = rank[:nclaim] - 1
+            assert sorted(ranked.tolist()) == np.flatnonzero(live).tolist()
+            assert (np.diff(start[ranked]) > 0).all()
             got, keys_w = [], []
             for t in np.flatnonzero(live):
                 seg = slice(w * cap + int(start[t]), w * cap + int(start[t] + length[t]))
@@ -294,7 +303,7 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     for r in range(1, P, 2):
         check_route(*qs[r][:4], qs[r][4], qs[r][5])
     cap8 = (cap + 7) // 8
-    answers = []
+    answers, packed_by_owner = [], []
     for o in range(P):
         recv, rdir, rmsg = deliver(qs, o)
         out = torch.zeros(nh * P * cap, dtype=torch.uint8, device=dev)
@@ -304,6 +313,36 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
         shards[o].shard_test_chunks(recv, cap, P, rdir, dbytes, tiles, rmsg, nh + 1, out, nxt=(skb, sko, sn, sdig))
         torch.testing.assert_close(sdig, shards[o].hash_keys(skb, sko, sn), rtol=0, atol=0)
         answers.append(out)
+        # the packed form (bf_shard_test_chunks_packed_dev: ordered chunks + unsort for "sorted",
+        # bytes + pack for the others): every live entry's bit equals its answer byte
+        pk = shards[o].shard_test_chunks_packed(recv, cap, P, rdir, dbytes, tiles, rmsg, nh + 1).cpu().numpy()
+        ob = out.cpu().numpy()
+        cnt = rmsg.cpu().numpy()
+        for src in range(P):
+            for h in range(nh):
+                live = int(cnt[src, h])
+                bits_w = np.unpackbits(pk[(src * nh + h) * cap8:(src * nh + h + 1) * cap8], bitorder="little")
+                np.testing.assert_array_equal(bits_w[:live], ob[(h * P + src) * cap:(h * P + src) * cap + live])
+        packed_by_owner.append(torch.from_numpy(pk).to(dev))
+    for r in range(P):   # the requesters' answers from the packed owner tests
+        back = torch.cat([packed_by_owner[o][(r * nh) * cap8:(r * nh + nh) * cap8] for o in range(P)])
+        send, slot, counts, dirb, pb, po = qs[r]
+        got = shards[r].combine_chunks_packed(back, slot, cap, dirb, dbytes, tiles, counts, len(probes[r]))
+        np.testing.assert_array_equal(got.cpu().numpy(), oracle.include_many(bits, m, k, pb, po))
+    # the step's owner work in one pass (bf_shard_insert_test_chunks_packed_dev) on fresh shards:
+    # the inserts land as the separate insert's did and every answer sees them
+    fresh = [D.HipEngine(m, k, P, s_, b, dev) for s_ in range(P)]
+    packed_f = [fresh[o].shard_insert_test_chunks_packed(*deliver(ins, o), *deliver(qs, o), cap, P, dbytes, tiles,
+                                                         nh + 1) for o in range(P)]
+    torch.cuda.synchronize()
+    assert D.interleave_shards([e.shard_export() for e in fresh], fresh[0].filter.reach_bits, b) == got_str
+    for r in range(P):
+        back = torch.cat([packed_f[o][(r * nh) * cap8:(r * nh + nh) * cap8] for o in range(P)])
+        send, slot, counts, dirb, pb, po = qs[r]
+        got = fresh[r].combine_chunks_packed(back, slot, cap, dirb, dbytes, tiles, counts, len(probes[r]))
+        np.testing.assert_array_equal(got.cpu().numpy(), oracle.include_many(bits, m, k, pb, po))
+    for e in fresh:
+        e.close()
     for r in range(P):
         back = torch.zeros(nwin * cap8, dtype=torch.uint8, device=dev)
         for o in range(P):

@@ -27,6 +27,13 @@ import pkgload  # noqa: E402
 
 
 def main():
+    print(json.dumps(run(sys.argv[1:])))
+
+
+def run(argv) -> dict:
+    """The model for one command line (the CLI's flags); returns its JSON line as a dict.
+    bench.py calls this for its per-rank model legs (model_P8_nstar, model_P8_200b,
+    model_repl8_10b)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--config", default="nstar", choices=sorted(bench.CONFIGS))
@@ -67,6 +74,15 @@ def main():
     ap.add_argument("--dig-side", action="store_true",
                     help="--chunks --dig, but the next include? batch is hashed by bf_hash_many_dev on a second "
                          "stream (a second handle) beside the owner test, not inside it; read the wall time")
+    ap.add_argument("--hash-split", action="store_true",
+                    help="--chunks: each route as two kernels, the keys' SHA-1 (bf_hash_many_dev, full occupancy) "
+                         "then the route from the words (bf_route_chunks_digests_dev)")
+    ap.add_argument("--separate", action="store_true",
+                    help="--chunks: the owner's insert and include? as two calls (shard_insert_chunks, then "
+                         "shard_test_chunks_packed) instead of one pass over the shard")
+    ap.add_argument("--packed-bytes", action="store_true",
+                    help="--chunks: the owner test writes answer bytes and a pack pass makes the bits (the "
+                         "round-5 form) instead of bf_shard_test_chunks_packed_dev")
     ap.add_argument("--no-prefill", action="store_true",
                     help="partitioned: start from an empty shard (default: 50 %% random bit density, as "
                          "bench.py prefills every rank's shard; the owner test stores an answer per 0-probe)")
@@ -74,7 +90,7 @@ def main():
                     help="--chunks: route the NEXT step's insert batch on a second stream while this step's "
                          "owner kernels run (what PartitionedFilter's next_insert prefetch would do on a side "
                          "stream); the step's wall time is what to read")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     pkg = pkgload.load()
     if args.replicated:
         return replicated(args, pkg)
@@ -160,10 +176,17 @@ def main():
         if args.overlap:   # this step's insert batch was routed during the previous step, on side
             torch.cuda.current_stream(dev).wait_event(pre["ev"])
             send, counts, dirb = pre["send"], pre["counts"], pre["dirb"]
+        elif args.hash_split:   # SHA-1 in its own full-occupancy pass, then the route from the words
+            send, _, counts, dirb = eng.route_chunks(eng.hash_keys(ikb, iko, batch, digs["ins"]), None, batch, capsf,
+                                                     tiles, dbytes, want_slot=False)
         else:
             send, _, counts, dirb = eng.route_chunks(ikb, iko, batch, capsf, tiles, dbytes, want_slot=False)
         recv, rdir, rmsg = deliver(send, dirb, counts)
-        eng.shard_insert_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1)
+        fused = not (args.separate or args.dig or args.packed_bytes or args.overlap)
+        if fused:   # the owner's insert and include? in one pass (bf_shard_insert_test_chunks_packed_dev)
+            ins_recv = (recv, rdir, rmsg)
+        else:
+            eng.shard_insert_chunks(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1)
         if args.overlap:   # the next step's insert route, beside this step's owner kernels
             nb = nxt_batch[0]
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -174,9 +197,18 @@ def main():
             pre.update(send=s_, counts=c_, dirb=d_, ev=ev)
         if args.dig:   # this step's include? batch was hashed by the previous step's owner test
             send, slot, counts, dirb = eng.route_chunks(digs["cur"], None, batch, capsf, tiles, dbytes)
+        elif args.hash_split:
+            send, slot, counts, dirb = eng.route_chunks(eng.hash_keys(qkb, qko, batch, digs["inc"]), None, batch,
+                                                        capsf, tiles, dbytes)
         else:
             send, slot, counts, dirb = eng.route_chunks(qkb, qko, batch, capsf, tiles, dbytes)
         recv, rdir, rmsg = deliver(send, dirb, counts)
+        if fused:
+            packed = eng.shard_insert_test_chunks_packed(*ins_recv, recv, rdir, rmsg, capsf, P, dbytes, tiles, nh + 1)
+            return eng.combine_chunks_packed(packed, slot, capsf, dirb, dbytes, tiles, counts, batch)
+        if not args.dig and not args.packed_bytes:   # the owner test writes the packed answers itself
+            packed = eng.shard_test_chunks_packed(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1)
+            return eng.combine_chunks_packed(packed, slot, capsf, dirb, dbytes, tiles, counts, batch)
         bits = torch.empty(nh * P * capsf, dtype=torch.uint8, device=dev)
         nxt = None
         if args.dig:   # ... and this one hashes the next step's
@@ -208,6 +240,9 @@ def main():
     nxt_batch = [None]
     digs = {}
     hasher = pkg.Filter(1 << 20, k, device=0) if args.dig_side else None   # hash_many needs a handle
+    if args.hash_split:
+        digs["ins"] = torch.empty((batch, 4), dtype=torch.int32, device=dev)
+        digs["inc"] = torch.empty((batch, 4), dtype=torch.int32, device=dev)
     if args.dig:   # batch 0's include? words before the first step (the pipeline's fill)
         digs["cur"] = eng.hash_keys(batches[0][1][0], batches[0][1][1], batch)
         digs["spare"] = torch.empty_like(digs["cur"])
@@ -259,7 +294,12 @@ def main():
            "note": "per-rank compute = kernels_ms_sum; ms_per_step_compute also holds the stand-in receive "
                    "copies (--windows; --chunks with nh > 1: the windows permuted into the receive layout), "
                    "which are the exchange's job in a real run"}
-    print(json.dumps(out))
+    for e in (eng, router):
+        if e is not None:
+            e.close()
+    if hasher is not None:
+        hasher.close()
+    return out
 
 
 def replicated(args, pkg):
@@ -392,7 +432,6 @@ def replicated(args, pkg):
         enc.close()
     if os.environ.get("BFHIP_SETS_STOP", "0") == "0":   # (the encode stop-point A/B writes no sets)
         assert out.cpu().numpy()[: batch // 2].all(), "false negative"
-    one = None
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
            "fused_hash": bool(args.fused_hash), "overlap_encode": ovl or None, "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
@@ -406,8 +445,7 @@ def replicated(args, pkg):
            "note": "one replica's kernels per step at world size R; the key all-gather runs beside the "
                    "previous step and is not included"}
     f.close()
-    print(json.dumps(res))
-    return one
+    return res
 
 
 if __name__ == "__main__":
