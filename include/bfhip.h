@@ -404,6 +404,10 @@ int  bf_shard_test_windows_dev(bf_handle* h, const uint32_t* d_local32, uint64_t
  *                           both take their sorted forms (each region read once, its inserts
  *                           ORed in and written back, its include? probes tested against the
  *                           result); every answer sees every insert, as the two calls in order.
+ *                           d_next_keys / d_next_offsets / n_next (n_next = 0: none): another key
+ *                           batch whose SHA-1 words go to d_next_digests (16-byte aligned), hashed
+ *                           by the same pass while it streams the shard — this rank's next include?
+ *                           batch, which bf_route_chunks_digests_dev then routes without hashing.
  * bf_combine_chunks_packed_dev  requester: the include? answers from window w's answer bits
  *                           at d_packed + w*ceil(window_cap/8), through this rank's own
  *                           route directory and slots.  A window whose count exceeds
@@ -441,7 +445,9 @@ int  bf_shard_insert_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_ins_
                                             const uint8_t* d_tst_dir, const uint64_t* d_tst_counts,
                                             uint64_t window_cap, uint32_t nsrc, uint64_t dir_bytes, uint64_t tiles,
                                             uint32_t count_stride, uint32_t* d_any_new /* nullable */,
-                                            uint8_t* d_packed, void* stream);
+                                            uint8_t* d_packed, const uint8_t* d_next_keys,
+                                            const uint64_t* d_next_offsets, uint64_t n_next,
+                                            uint32_t* d_next_digests, void* stream);
 int  bf_combine_chunks_packed_dev(bf_handle* h, const uint8_t* d_packed, const uint16_t* d_slot16,
                                   uint64_t window_cap, const uint8_t* d_dir, uint64_t dir_bytes, uint64_t tiles,
                                   const uint64_t* d_counts /* nwin */, uint64_t n, uint8_t* d_out, void* stream);

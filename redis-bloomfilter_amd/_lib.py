@@ -21,6 +21,7 @@ BF_OK, BF_EINVAL, BF_ENOMEM, BF_EDEVICE, BF_ERCCL, BF_ERANGE = 0, 1, 2, 3, 4, 5
 BF_IMPORT_REPLACE, BF_IMPORT_OR = 0, 1
 BF_FLAG_ROUTE32 = 1
 BF_FLAG_ENGINE_MD5, BF_FLAG_ENGINE_SHA1 = 2, 4   # RubyTest hash engines (ruby_test.rb:43-61)
+BF_FLAG_ENCODER = 8   # no bitset: region-set encodes only (a replicated filter's second, encoding handle)
 BF_MAX_K = 64
 PROFILE_NAME_LEN = 64   # BF_PROFILE_NAME_LEN
 DIRTY_BLOCK_BYTES = 65536   # BF_DIRTY_BLOCK_BYTES
@@ -121,7 +122,7 @@ SIGNATURES = {
     "bf_shard_test_chunks_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
     "bf_shard_test_chunks_packed_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp, _vp]),
     "bf_shard_insert_test_chunks_packed_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _u64,
-                                                              _u64, _u32, _vp, _vp, _vp]),
+                                                              _u64, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
     "bf_route_chunks_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp]),
     "bf_shard_test_chunks_hash_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _vp, _u64, _u64, _vp, _u32, _vp,
                                                      _vp, _vp, _u64, _vp, _vp]),
@@ -587,12 +588,16 @@ class Filter:
     def shard_insert_test_chunks_packed_dev(self, d_ins_recv: int, d_ins_dir: int, d_ins_counts: int,
                                             d_tst_recv: int, d_tst_dir: int, d_tst_counts: int, window_cap: int,
                                             nsrc: int, dir_bytes: int, tiles: int, count_stride: int,
-                                            d_packed: int, d_any_new: int = 0, stream=None) -> None:
+                                            d_packed: int, d_any_new: int = 0, d_next_keys: int = 0,
+                                            d_next_offsets: int = 0, n_next: int = 0, d_next_digests: int = 0,
+                                            stream=None) -> None:
         """One step's owner work: the insert windows ORed in, then the include? windows tested
-        (packed answers as shard_test_chunks_packed_dev), in one pass over the shard."""
+        (packed answers as shard_test_chunks_packed_dev), in one pass over the shard; with
+        n_next, that pass also hashes another key batch into d_next_digests."""
         _check(self._lib.bf_shard_insert_test_chunks_packed_dev(
             self.handle, d_ins_recv, d_ins_dir, d_ins_counts, d_tst_recv, d_tst_dir, d_tst_counts, int(window_cap),
             int(nsrc), int(dir_bytes), int(tiles), int(count_stride), d_any_new or None, d_packed,
+            d_next_keys or None, d_next_offsets or None, int(n_next), d_next_digests or None,
             self._s(stream)), self._h)
 
     def shard_test_chunks_hash_dev(self, d_recv: int, window_cap: int, nsrc: int, d_dir: int, dir_bytes: int,

@@ -1403,7 +1403,14 @@ static bool handle_chunks(const bf_handle* h, BfChunks* cg, uint32_t* nh_out, bo
                (h->chunk_test_l2 == 1 || cg->sup_log2 <= kL2SweepMaxSupLog2)) {
         sweep = true;
     } else if (!bf_chunk_geometry(bits0, nwin, h->bin_region_log2, cg, 256)) {
-        return false;
+        return false;   // (shard counts whose windows take no geometry keep the plain windows)
+    } else {
+        // the sorted owner: 512 buckets where 256 fit, twice the superbins, so a region's runs in
+        // each sorted block are twice as long for the owner's apply / test (200B x 8: apply_test
+        // 1.78 -> 1.23 ms, the mids +0.32, per rank 6.96 -> 6.72 ms:
+        // profiles/r06h_ab_chunk_buckets.jsonl)
+        BfChunks c512;
+        if (bf_chunk_geometry(bits0, nwin, h->bin_region_log2, &c512, 512)) *cg = c512;
     }
     if (l2) *l2 = sweep;
     return true;
@@ -1668,11 +1675,17 @@ int bf_shard_insert_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_ins_r
                                            const uint8_t* d_tst_dir, const uint64_t* d_tst_counts,
                                            uint64_t window_cap, uint32_t nsrc, uint64_t dir_bytes, uint64_t tiles,
                                            uint32_t count_stride, uint32_t* d_any_new, uint8_t* d_packed,
-                                           void* stream) {
+                                           const uint8_t* d_next_keys, const uint64_t* d_next_offsets,
+                                           uint64_t n_next, uint32_t* d_next_digests, void* stream) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h) return BF_EINVAL;
     if (!d_packed) return set_err(h, BF_EINVAL, "d_packed is NULL");
-    if (!nsrc || !window_cap) return BF_OK;
+    if (n_next && (!d_next_keys || !d_next_offsets || !d_next_digests))
+        return set_err(h, BF_EINVAL, "NULL side-hash pointer");
+    if (n_next && (reinterpret_cast<uintptr_t>(d_next_digests) & 15u))
+        return set_err(h, BF_EINVAL, "d_next_digests must be 16-byte aligned");
+    if (!nsrc || !window_cap)
+        return n_next ? bf_hash_many_dev(h, d_next_keys, d_next_offsets, n_next, d_next_digests, stream) : BF_OK;
     if (!d_ins_recv || !d_ins_dir || !d_ins_counts || !d_tst_recv || !d_tst_dir || !d_tst_counts)
         return set_err(h, BF_EINVAL, "NULL device pointer");
     BfChunks cg;
@@ -1699,8 +1712,10 @@ int bf_shard_insert_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_ins_r
         rc = bf_shard_insert_chunks_dev(h, d_ins_recv, window_cap, nsrc, d_ins_dir, dir_bytes, tiles, d_ins_counts,
                                         count_stride, d_any_new, stream);
         if (rc) return rc;
-        return bf_shard_test_chunks_packed_dev(h, d_tst_recv, window_cap, nsrc, d_tst_dir, dir_bytes, tiles, d_tst_counts,
-                                               count_stride, d_packed, stream);
+        rc = bf_shard_test_chunks_packed_dev(h, d_tst_recv, window_cap, nsrc, d_tst_dir, dir_bytes, tiles, d_tst_counts,
+                                             count_stride, d_packed, stream);
+        if (rc) return rc;
+        return n_next ? bf_hash_many_dev(h, d_next_keys, d_next_offsets, n_next, d_next_digests, stream) : BF_OK;
     }
     BfChunkIn cii;
     cii.recv = d_ins_recv;
@@ -1725,9 +1740,17 @@ int bf_shard_insert_test_chunks_packed_dev(bf_handle* h, const uint32_t* d_ins_r
     StreamOrder so(h, pick_stream(h, stream));
     if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
     if ((rc = ensure_scratch(h, bf_chunk_scratch_bytes(pi) + bf_chunk_scratch_bytes(pt)))) return rc;
+    BfSideHash side;
+    if (n_next) {
+        side.keys16 = align_keys(d_next_keys, &side.bias);
+        side.offsets = d_next_offsets;
+        side.n = n_next;
+        side.dig = reinterpret_cast<uint4*>(d_next_digests);
+        side.key_status = h->g.key_status;
+    }
     BfMarks* mk = prof_begin(h, so.s);
     HIPCHK(h, bf_launch_shard_insert_test_chunks_packed(h->g, pi, pt, h->dev_bytes, cii, cit, h->d_bin_scratch,
-                                                        d_any_new, d_packed, so.s, mk));
+                                                        d_any_new, d_packed, so.s, mk, side));
     return BF_OK;
 }
 

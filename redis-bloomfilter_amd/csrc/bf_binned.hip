@@ -1456,12 +1456,16 @@ struct BfL2 {   // one plan's level-2 arrays and run tables
     uint64_t max_chunks;
     uint32_t nq;
 };
-template <uint32_t RLOG2, uint32_t LANES, int ILOADS>
-__global__ __launch_bounds__(LANES) void bin_apply_test_kernel(uint32_t* __restrict__ bits, uint64_t nwords, BfL2 ins,
+// SIDE: the workgroups also hash another key batch (the requester's next include? batch: sh),
+// an equal share each, staged through the LDS image before it is cleared, while the region's
+// vectors are in flight; the next step then routes that batch from its words.
+template <uint32_t RLOG2, uint32_t LANES, int ILOADS, bool SIDE = false>
+// (8 waves per SIMD = two 2^19-bit workgroups per CU: the SIDE form stays within 64 VGPRs)
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(RLOG2 == 19 ? 8 : 4, 8))) void bin_apply_test_kernel(uint32_t* __restrict__ bits, uint64_t nwords, BfL2 ins,
                                                                BfL2 tst, uint32_t rel_log2, uint32_t dense,
                                                                uint32_t* __restrict__ any_flag,
                                                                uint8_t* __restrict__ dirty, uint32_t store_fresh,
-                                                               uint8_t* __restrict__ ans2) {
+                                                               uint8_t* __restrict__ ans2, BfSideHash sh) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);
     constexpr uint32_t kPer = kVec / LANES;
     constexpr int kTLoads = 8;
@@ -1480,6 +1484,22 @@ __global__ __launch_bounds__(LANES) void bin_apply_test_kernel(uint32_t* __restr
     for (uint32_t c = 0; c < kPer; ++c) {
         const uint32_t v = c * LANES + t;
         old[c] = v0 + v < nvec ? apply_load(gv + v0 + v) : make_uint4(0, 0, 0, 0);
+    }
+    if constexpr (SIDE) {   // this workgroup's share of the side batch, LANES keys per tile
+        static_assert(8 * (LANES + 1) + 16 * (kStageVec + kStageSlackVec) <= 16 * kVec, "side stage fits the image");
+        const uint64_t per = (sh.n + gridDim.x - 1) / gridDim.x;
+        const uint64_t k0 = (uint64_t)blockIdx.x * per, k1 = k0 + per < sh.n ? k0 + per : sh.n;
+        uint64_t* s_off = reinterpret_cast<uint64_t*>(s_img4);
+        uint4* s_stage = s_img4 + (8 * (LANES + 1) + 15) / 16;
+        for (uint64_t j0 = k0; j0 < k1; j0 += LANES) {   // workgroup-uniform
+            const uint32_t cnt = (uint32_t)(k1 - j0 < LANES ? k1 - j0 : LANES);
+            for_key_tile<LANES, kStageVec>(sh.keys16, sh.offsets, sh.bias, j0, cnt, s_off, s_stage, sh.key_status,
+                [&](auto staged, uint32_t lane, const uint32_t* src, uint32_t s0, uint32_t L) {
+                    uint32_t H[5];
+                    sha1_any<decltype(staged)::value>(src, s0, L, H);
+                    sh.dig[j0 + lane] = make_uint4(H[0], H[1], H[2], H[3]);
+                });
+        }
     }
     for (uint32_t v = t; v < kVec; v += LANES) s_img4[v] = make_uint4(0, 0, 0, 0);
     __syncthreads();
@@ -2685,7 +2705,7 @@ hipError_t bf_launch_shard_insert_chunks(const BfGeom& g, const BfBinPlan& p, ui
 hipError_t bf_launch_shard_insert_test_chunks_packed(const BfGeom& g, const BfBinPlan& pi, const BfBinPlan& pt,
                                                      uint64_t bitset_bytes, const BfChunkIn& cii, BfChunkIn cit,
                                                      void* scratch, uint32_t* any_flag, uint8_t* packed, hipStream_t s,
-                                                     BfMarks* mk) {
+                                                     BfMarks* mk, const BfSideHash& side) {
     if (!pi.chunked || pi.with_keys || !pt.chunked || !pt.with_keys || !pt.ordered || !packed ||
         pi.region_log2 != pt.region_log2 || pi.rel_log2 != pt.rel_log2 || pi.nbins != pt.nbins ||
         pt.tiles != cit.tiles || pt.nwin != cit.nh * cit.nsrc)
@@ -2705,21 +2725,37 @@ hipError_t bf_launch_shard_insert_test_chunks_packed(const BfGeom& g, const BfBi
     const uint64_t vecs = (uint64_t)pi.nbins << (pi.region_log2 - 7);
     const uint32_t dense = pi.probes >= vecs ? 2u : (pi.probes >= vecs / 8 ? 1u : 0u);
     const int iloads = pi.probes <= (uint64_t)pi.nbins * 4096u ? 2 : 8;   // as launch_apply
-#define BF_APPLY_TEST(RL, LANES, LD)                                                                              \
-    hipLaunchKernelGGL((bin_apply_test_kernel<RL, LANES, LD>), dim3(pi.nbins), dim3(LANES), 0, s, g.bits, nwords, li, \
-                       lt, pi.rel_log2, dense, any_flag, g.dirty, apply_store_fresh(), ct.ans2)
-    if (pi.region_log2 == 18) {
-        if (iloads == 2) BF_APPLY_TEST(18, kApplyLanes / 2, 2);
-        else BF_APPLY_TEST(18, kApplyLanes / 2, 8);
+#define BF_APPLY_TEST(RL, LANES, LD, SD)                                                                          \
+    hipLaunchKernelGGL((bin_apply_test_kernel<RL, LANES, LD, SD>), dim3(pi.nbins), dim3(LANES), 0, s, g.bits, nwords, \
+                       li, lt, pi.rel_log2, dense, any_flag, g.dirty, apply_store_fresh(), ct.ans2, side)
+    const bool sd = side.n != 0;
+    if (pi.region_log2 == 18) {   // (a 2^18-bit image cannot hold the side stage: hashed in a pass of its own)
+        if (sd) {
+            hipError_t he = bf_launch_keys(BF_OP_HASH, g, side.keys16, side.offsets, side.bias, side.n, nullptr,
+                                           reinterpret_cast<uint64_t*>(side.dig), nullptr, s);
+            if (he != hipSuccess) return he;
+        }
+        if (iloads == 2) BF_APPLY_TEST(18, kApplyLanes / 2, 2, false);
+        else BF_APPLY_TEST(18, kApplyLanes / 2, 8, false);
     } else if (pi.region_log2 == 19) {
-        if (iloads == 2) BF_APPLY_TEST(19, kApplyLanes, 2);
-        else BF_APPLY_TEST(19, kApplyLanes, 8);
+        if (iloads == 2) {
+            if (sd) BF_APPLY_TEST(19, kApplyLanes, 2, true);
+            else BF_APPLY_TEST(19, kApplyLanes, 2, false);
+        } else {
+            if (sd) BF_APPLY_TEST(19, kApplyLanes, 8, true);
+            else BF_APPLY_TEST(19, kApplyLanes, 8, false);
+        }
     } else {
-        if (iloads == 2) BF_APPLY_TEST(20, kApplyLanes, 2);
-        else BF_APPLY_TEST(20, kApplyLanes, 8);
+        if (iloads == 2) {
+            if (sd) BF_APPLY_TEST(20, kApplyLanes, 2, true);
+            else BF_APPLY_TEST(20, kApplyLanes, 2, false);
+        } else {
+            if (sd) BF_APPLY_TEST(20, kApplyLanes, 8, true);
+            else BF_APPLY_TEST(20, kApplyLanes, 8, false);
+        }
     }
 #undef BF_APPLY_TEST
-    bf_mark(mk, s, "apply_test");
+    bf_mark(mk, s, sd ? "apply_test_hash" : "apply_test");
     hipLaunchKernelGGL(chunk_unsort_kernel, dim3(pt.ngroups, cit.nh), dim3(1024), 0, s, cit, pt.ngroups, pt.nsup,
                        ct.base, ct.level2_key, ct.ans2, packed, cap8);
     bf_mark(mk, s, "unsort_packed");

@@ -292,7 +292,7 @@ uint64_t bf_chunk_scratch_bytes(const BfBinPlan& p);
 hipError_t bf_launch_shard_insert_test_chunks_packed(const BfGeom& g, const BfBinPlan& pi, const BfBinPlan& pt,
                                                      uint64_t bitset_bytes, const BfChunkIn& cii, BfChunkIn cit,
                                                      void* scratch, uint32_t* any_flag, uint8_t* packed, hipStream_t s,
-                                                     BfMarks* marks = nullptr);
+                                                     BfMarks* marks, const BfSideHash& side);
 // Requester side: the window route with directories (cg.dir zeroed here first; slot16
 // nullable: tile-relative key indices).
 // dig: keys16 holds the keys' SHA-1 words (uint4 per key; offsets unused) instead of key bytes.

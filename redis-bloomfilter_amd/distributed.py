@@ -40,7 +40,7 @@ import torch
 import torch.distributed as dist
 
 from . import keys as _keys
-from ._lib import BF_EINVAL, BF_FLAG_ROUTE32, ArgumentError, BfHipError, Filter
+from ._lib import BF_EINVAL, BF_FLAG_ENCODER, BF_FLAG_ROUTE32, ArgumentError, BfHipError, Filter
 
 # -- collectives -------------------------------------------------------------------------
 # RCCL (backend "nccl") moves device tensors directly.  Under gloo the device tensors are
@@ -289,14 +289,19 @@ class HipEngine:
 
     def shard_insert_test_chunks_packed(self, irecv: torch.Tensor, irdir: torch.Tensor, icounts: torch.Tensor,
                                         trecv: torch.Tensor, trdir: torch.Tensor, tcounts: torch.Tensor, cap: int,
-                                        nsrc: int, dir_bytes: int, tiles: int, cstride: int) -> torch.Tensor:
+                                        nsrc: int, dir_bytes: int, tiles: int, cstride: int, nxt=None) -> torch.Tensor:
         """shard_insert_chunks then shard_test_chunks_packed, in one pass over the shard where
-        both take their sorted forms; returns the packed answers."""
+        both take their sorted forms; returns the packed answers.  nxt = (kb, ko, n, dig): the
+        pass also hashes that batch into dig (n x 4 int32)."""
         cap8 = (cap + 7) // 8
         packed = torch.empty(max(nsrc * self.nh * cap8, 1), dtype=torch.uint8, device=self.device)
+        kb, ko, nn, dig = nxt if nxt is not None and nxt[2] else (None, None, 0, None)
         self.filter.shard_insert_test_chunks_packed_dev(irecv.data_ptr(), irdir.data_ptr(), icounts.data_ptr(),
                                                         trecv.data_ptr(), trdir.data_ptr(), tcounts.data_ptr(), cap,
                                                         nsrc, dir_bytes, tiles, cstride, packed.data_ptr(),
+                                                        d_next_keys=kb.data_ptr() if nn else 0,
+                                                        d_next_offsets=ko.data_ptr() if nn else 0, n_next=nn,
+                                                        d_next_digests=dig.data_ptr() if nn else 0,
                                                         stream=self._stream())
         return packed
 
@@ -829,20 +834,27 @@ class PartitionedFilter:
             return torch.zeros(n, dtype=torch.uint8, device=packed.device)
         return e.combine_chunks_packed(back, st["slot"], cap, st["dir"], dbytes, tiles, st["counts"], n)
 
-    def _sf_insert_answer(self, st_i: dict, st_q: dict) -> Optional[torch.Tensor]:
+    def _sf_insert_answer(self, st_i: dict, st_q: dict, next_include=None) -> Optional[torch.Tensor]:
         """_sf_insert(st_i) then _sf_answer(st_q) as ONE owner pass over the shard
         (bf_shard_insert_test_chunks_packed_dev), when both batches took chunked windows of the
-        same geometry; None when they did not (the caller then makes the two calls)."""
+        same geometry; None when they did not (the caller then makes the two calls).
+        next_include = (kb, ko, n): the pass also hashes that batch (kept for the next call)."""
         e = self.engine
         if (st_i["geo"] is None or st_q["geo"] is None or st_i["geo"] != st_q["geo"] or st_i["cap"] != st_q["cap"]
                 or not self.pack_answers or not hasattr(e, "shard_insert_test_chunks_packed")):
             return None
         for w in st_i["works"] + st_q["works"]:
             w.wait()
+        nxt = None
+        if next_include is not None and next_include[2]:
+            nkb, nko, nn = next_include
+            dig = torch.empty((nn, 4), dtype=torch.int32, device=st_q["recv"].device)
+            nxt = (nkb, nko, nn, dig)
+            self._next_inc = dict(kb=nkb, ko=nko, n=nn, dig=dig)
         tiles, dbytes = st_q["geo"]
         packed = e.shard_insert_test_chunks_packed(st_i["recv"], st_i["rdir"], st_i["rmsg"], st_q["recv"],
                                                    st_q["rdir"], st_q["rmsg"], st_q["cap"], self.P, dbytes, tiles,
-                                                   e.nh + 1)
+                                                   e.nh + 1, nxt=nxt)
         return self._sf_return_packed(st_q, packed)
 
     def _synced_insert(self, kb, ko, n: int) -> None:
@@ -927,7 +939,7 @@ class PartitionedFilter:
                 self._pending = self._sf_start(*next_insert, want_slot=False)
             self._sf_flag(st_i)
             self._sf_flag(st_q)
-            out = None if next_include is not None else self._sf_insert_answer(st_i, st_q)
+            out = self._sf_insert_answer(st_i, st_q, next_include=next_include)
             if out is None:
                 self._sf_insert(st_i)
                 out = self._sf_answer(st_q, next_include=next_include)
@@ -1136,7 +1148,12 @@ class ReplicatedFilter:
 
     MODES = ("auto", "gather", "or", "digests", "sets")
 
-    def __init__(self, m: int, k: int, group=None, device=None, insert_mode: str = "auto"):
+    def __init__(self, m: int, k: int, group=None, device=None, insert_mode: str = "auto",
+                 side_encode: bool = True):
+        """side_encode ("sets" mode): a batch given as SHA-1 words (the pipelined step) is encoded
+        by a second, bitset-less handle (BF_FLAG_ENCODER) on a stream of its own, so it runs
+        beside this replica's apply of the previous batch instead of after it (one handle orders
+        all of its calls)."""
         if insert_mode not in self.MODES:
             raise ArgumentError("insert_mode must be one of %s" % (self.MODES,))
         self.group = group
@@ -1166,6 +1183,10 @@ class ReplicatedFilter:
             except (ArgumentError, BfHipError) as e:
                 self.filter.close()
                 raise ArgumentError("insert_mode='sets': this filter cannot take region sets (%s)" % e)
+        self.encoder = self.enc_stream = None
+        if insert_mode == "sets" and side_encode and self.device.type == "cuda":
+            self.encoder = Filter(m, k, device=self.device.index, flags=BF_FLAG_ENCODER)
+            self.enc_stream = torch.cuda.Stream(self.device)
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -1250,6 +1271,22 @@ class ReplicatedFilter:
             except ArgumentError:
                 mode = "digests"
         if mode == "sets":   # this rank sorts and encodes its batch once; the region sets travel
+            if digests is not None and n and self.encoder is not None:
+                # on the encoder's stream, beside whatever this replica's handle runs next (the
+                # previous batch's apply); it waits only for what is enqueued so far (the words)
+                side = self.enc_stream
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    mine = torch.empty(cap // 4, dtype=torch.int32, device=self.device)
+                    self.encoder.encode_region_sets_digests_dev(digests.data_ptr(), n, mine.data_ptr(), cap,
+                                                                stream=side.cuda_stream)
+                    gs = torch.empty(self.P * (cap // 4), dtype=torch.int32, device=self.device)
+                    works = [_all_gather_into_tensor(gs, mine, group=self.group, async_op=True)]
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                digests.record_stream(side)
+                return dict(mode="sets", kb=kb, ko=ko, n=n, gs=gs, send=mine, works=works, sizes=all_sizes, cap=cap,
+                            ev=ev)
             mine = torch.empty(cap // 4, dtype=torch.int32, device=self.device)
             if digests is not None and n:
                 self.filter.encode_region_sets_digests_dev(digests.data_ptr(), n, mine.data_ptr(), cap,
@@ -1297,6 +1334,9 @@ class ReplicatedFilter:
             return
         for w in st["works"]:
             w.wait()
+        if st.get("ev") is not None:   # encoded on the encoder's stream (a host-staged gather copies there too)
+            torch.cuda.current_stream(self.device).wait_event(st["ev"])
+            st["gs"].record_stream(torch.cuda.current_stream(self.device))
         if st["mode"] == "sets":   # every rank's sets ORed in by one pass over the bitset
             probes = sum(sz[1] for sz in st["sizes"]) * self.k
             if probes:
@@ -1371,6 +1411,9 @@ class ReplicatedFilter:
         return self.filter.export_redis()
 
     def close(self):
+        if self.encoder is not None:
+            self.enc_stream.synchronize()
+            self.encoder.close()
         self.filter.close()
 
 

@@ -332,8 +332,13 @@ def test_chunked_windows(pkg, oracle, monkeypatch, m, k, P, b, owner):
     # the step's owner work in one pass (bf_shard_insert_test_chunks_packed_dev) on fresh shards:
     # the inserts land as the separate insert's did and every answer sees them
     fresh = [D.HipEngine(m, k, P, s_, b, dev) for s_ in range(P)]
-    packed_f = [fresh[o].shard_insert_test_chunks_packed(*deliver(ins, o), *deliver(qs, o), cap, P, dbytes, tiles,
-                                                         nh + 1) for o in range(P)]
+    packed_f = []
+    for o in range(P):   # ... and the pass hashes a side batch (the requester's next include? batch)
+        skb, sko, sn, _, _ = dev_batch(pkg, torch, per_rank[o][: 2999 + 61 * o])
+        sdig = torch.full((sn, 4), -1, dtype=torch.int32, device=dev)
+        packed_f.append(fresh[o].shard_insert_test_chunks_packed(*deliver(ins, o), *deliver(qs, o), cap, P, dbytes,
+                                                                 tiles, nh + 1, nxt=(skb, sko, sn, sdig)))
+        torch.testing.assert_close(sdig, fresh[o].hash_keys(skb, sko, sn), rtol=0, atol=0)
     torch.cuda.synchronize()
     assert D.interleave_shards([e.shard_export() for e in fresh], fresh[0].filter.reach_bits, b) == got_str
     for r in range(P):

@@ -74,6 +74,10 @@ def run(argv) -> dict:
     ap.add_argument("--dig-side", action="store_true",
                     help="--chunks --dig, but the next include? batch is hashed by bf_hash_many_dev on a second "
                          "stream (a second handle) beside the owner test, not inside it; read the wall time")
+    ap.add_argument("--fused-dig", action="store_true",
+                    help="--chunks (one owner pass): that pass also hashes the next step's include? batch "
+                         "(bf_shard_insert_test_chunks_packed_dev with n_next), which the next step routes from "
+                         "its words")
     ap.add_argument("--hash-split", action="store_true",
                     help="--chunks: each route as two kernels, the keys' SHA-1 (bf_hash_many_dev, full occupancy) "
                          "then the route from the words (bf_route_chunks_digests_dev)")
@@ -195,7 +199,7 @@ def run(argv) -> dict:
                 ev = torch.cuda.Event()
                 ev.record(side)
             pre.update(send=s_, counts=c_, dirb=d_, ev=ev)
-        if args.dig:   # this step's include? batch was hashed by the previous step's owner test
+        if args.dig or args.fused_dig:   # this step's include? batch was hashed by the previous step's owner pass
             send, slot, counts, dirb = eng.route_chunks(digs["cur"], None, batch, capsf, tiles, dbytes)
         elif args.hash_split:
             send, slot, counts, dirb = eng.route_chunks(eng.hash_keys(qkb, qko, batch, digs["inc"]), None, batch,
@@ -204,7 +208,14 @@ def run(argv) -> dict:
             send, slot, counts, dirb = eng.route_chunks(qkb, qko, batch, capsf, tiles, dbytes)
         recv, rdir, rmsg = deliver(send, dirb, counts)
         if fused:
-            packed = eng.shard_insert_test_chunks_packed(*ins_recv, recv, rdir, rmsg, capsf, P, dbytes, tiles, nh + 1)
+            nxt = None
+            if args.fused_dig:   # ... and this pass hashes the next step's include? batch
+                nq = nxt_batch[0][1]
+                nxt = (nq[0], nq[1], batch, digs["spare"])
+            packed = eng.shard_insert_test_chunks_packed(*ins_recv, recv, rdir, rmsg, capsf, P, dbytes, tiles, nh + 1,
+                                                         nxt=nxt)
+            if args.fused_dig:
+                digs["spare"], digs["cur"] = digs["cur"], digs["spare"]
             return eng.combine_chunks_packed(packed, slot, capsf, dirb, dbytes, tiles, counts, batch)
         if not args.dig and not args.packed_bytes:   # the owner test writes the packed answers itself
             packed = eng.shard_test_chunks_packed(recv, capsf, P, rdir, dbytes, tiles, rmsg, nh + 1)
@@ -243,7 +254,7 @@ def run(argv) -> dict:
     if args.hash_split:
         digs["ins"] = torch.empty((batch, 4), dtype=torch.int32, device=dev)
         digs["inc"] = torch.empty((batch, 4), dtype=torch.int32, device=dev)
-    if args.dig:   # batch 0's include? words before the first step (the pipeline's fill)
+    if args.dig or args.fused_dig:   # batch 0's include? words before the first step (the pipeline's fill)
         digs["cur"] = eng.hash_keys(batches[0][1][0], batches[0][1][1], batch)
         digs["spare"] = torch.empty_like(digs["cur"])
 
@@ -367,8 +378,10 @@ def replicated(args, pkg):
     ovl = args.overlap_encode
     if ovl:
         assert args.gathered == "sets" and args.fused_hash
-        enc = pkg.Filter(m, k, device=0)   # the encoder: its own scratch, so its calls are not ordered
-        side = torch.cuda.Stream(dev)      # behind the main handle's
+        # the encoder: a bitset-less handle (BF_FLAG_ENCODER) with its own scratch, so its calls are
+        # not ordered behind the main handle's (ReplicatedFilter's side_encode)
+        enc = pkg.Filter(m, k, device=0, flags=pkg._lib.BF_FLAG_ENCODER)
+        side = torch.cuda.Stream(dev)
         owns = [own, torch.empty_like(own)]
         main_s = torch.cuda.current_stream(dev)
 
