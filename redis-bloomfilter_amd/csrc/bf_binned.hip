@@ -824,6 +824,138 @@ void route_front32_kernel(BF_ROUTE_FRONT_ARGS, BfChunks cg) {
 #undef BF_ROUTE_FRONT_PASS
 #undef BF_ROUTE_FRONT_ARGS
 
+// The chunked route from SHA-1 words (bf_route_chunks_digests_dev) in sorted-index form: the
+// tile's LDS sort moves one u16 per probe — (key within the tile) << 4 | probe index — instead
+// of its 32-bit offset and u16 slot, and the write loop derives the offset again from the key's
+// words, which stay in LDS.  Same buckets, claims, directory and window contents as
+// route_front_body<.., WIN, CHUNK, DIG>, whose sort buffers (72.8 KiB without slots, 105.5 KiB
+// with, 92-102 VGPRs at k = 13) hold one workgroup per CU: here 56-72 KiB and <= 64 VGPRs make
+// two, so one workgroup's claims and barriers hide behind the other's work.
+template <bool SLOT, int SLOTS>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void route_chunks_idx_kernel(BfGeom g, const uint4* __restrict__ dig, uint64_t n, uint32_t tile_keys,
+                             uint32_t tiles_per_block, uint32_t P, uint64_t wcap,
+                             unsigned long long* __restrict__ wcounts, uint32_t* __restrict__ wsend,
+                             uint16_t* __restrict__ wslot, uint32_t nh, BfChunks cg) {
+    static_assert(SLOTS <= 16 && kTile * SLOTS <= 65536, "a probe index is 4 bits, a sort slot 16");
+    constexpr uint32_t NB = kChunkBuckets;
+    __shared__ uint16_t s_idx[kTile * SLOTS];
+    __shared__ uint4 s_dig[SLOTS > kSlots ? kTile : 2 * kTile];   // k > 12: one key per lane
+    __shared__ uint32_t s_cnt[NB], s_lbase[NB];
+    __shared__ uint32_t s_w[16];
+    __shared__ unsigned long long s_gbase[kMaxOwners];
+    __shared__ uint32_t s_obase[kMaxOwners];
+    const uint32_t sub_log2 = cg.sub2, wS = cg.S;
+    const uint32_t t = threadIdx.x;
+    if (t < NB) s_cnt[t] = 0;
+    __syncthreads();
+    const uint32_t k = g.k;
+    const uint32_t kpl = tile_keys / kTile;
+    const uint64_t ntiles = (n + tile_keys - 1) / tile_keys;
+    const uint64_t tb0 = (uint64_t)blockIdx.x * tiles_per_block;
+    const uint64_t tb1 = (tb0 + tiles_per_block < ntiles) ? tb0 + tiles_per_block : ntiles;
+    for (uint64_t tile = tb0; tile < tb1; ++tile) {
+        const uint64_t key0 = tile * tile_keys;
+        const uint32_t tk = (uint32_t)((n - key0) < (uint64_t)tile_keys ? (n - key0) : tile_keys);
+        const bool live0 = t < tk;
+        const bool live1 = kpl == 2 && kTile + t < tk;
+        const uint4 H0 = live0 ? dig[key0 + t] : make_uint4(0, 0, 0, 0);
+        const uint4 H1 = live1 ? dig[key0 + kTile + t] : make_uint4(0, 0, 0, 0);
+        s_dig[t] = H0;
+        if (kpl == 2) s_dig[kTile + t] = H1;
+        uint32_t tag[SLOTS];
+        auto probes = [&](auto kplc) {
+            constexpr uint32_t KPL = decltype(kplc)::value;
+#pragma unroll
+            for (int q = 0; q < SLOTS; ++q) {
+                const bool second = KPL == 2 && q >= (int)kTwoKeys;
+                const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
+                tag[q] = 0xFFFFFFFFu;
+                if (i < k && (second ? live1 : live0)) {
+                    const uint4 H = second ? H1 : H0;
+                    uint32_t owner;
+                    uint64_t local;
+                    owner_local(g, probe_offset(g, H.x, H.y, H.z, H.w, i), owner, local);
+                    const uint32_t lo = (uint32_t)local;
+                    uint32_t sb = lo >> cg.sup_log2;
+                    if (sb >= cg.S) sb = cg.S - 1u;   // never for a valid offset (the geometry covers the shard)
+                    const uint32_t wb = (owner * nh + (uint32_t)(local >> 32)) * cg.S + sb;
+                    const uint32_t bkt = (wb << sub_log2) | (lo & ((1u << sub_log2) - 1u));
+                    tag[q] = (bkt << 16) | atomicAdd(s_cnt + bkt, 1u);
+                }
+            }
+        };
+        if (kpl == 2) probes(std::integral_constant<uint32_t, 2>{});
+        else probes(std::integral_constant<uint32_t, 1>{});
+        __syncthreads();
+        const uint32_t c = t < NB ? s_cnt[t] : 0u;
+        const uint32_t ex = block_excl_scan(c, s_w, nullptr);
+        if (t < NB) {
+            s_lbase[t] = ex;
+            s_cnt[t] = 0;
+        }
+        __syncthreads();
+        if (t < P) {   // claim this tile's window-t run: its place and its rank among the window's runs
+            const uint32_t lo_b = (t * wS) << sub_log2, hi_b = ((t + 1) * wS) << sub_log2;
+            const uint32_t ob = s_lbase[lo_b], oc = (hi_b < NB ? s_lbase[hi_b] : tk * k) - ob;
+            unsigned long long gb = 0;
+            if (oc) {
+                uint8_t* dw = cg.dir + (uint64_t)t * cg.dir_bytes;
+                const unsigned long long x = atomicAdd(
+                    reinterpret_cast<unsigned long long*>(dw + bf_chunk_dir_claim_offset(cg, cg.tiles)),
+                    (1ull << kClaimRankShift) | (unsigned long long)oc);
+                gb = x & ((1ull << kClaimRankShift) - 1ull);
+                reinterpret_cast<uint16_t*>(dw + bf_chunk_dir_rank_offset(cg, cg.tiles))[x >> kClaimRankShift] =
+                    (uint16_t)(tile + 1u);
+                atomicAdd(wcounts + t, (unsigned long long)oc);
+            }
+            s_gbase[t] = (gb + oc <= wcap) ? (unsigned long long)t * wcap + gb : ~0ull;
+            s_obase[t] = ob;
+            reinterpret_cast<uint32_t*>(cg.dir + (uint64_t)t * cg.dir_bytes)[tile] =
+                (gb + oc <= wcap) ? (uint32_t)gb : 0xFFFFFFFFu;
+        }
+        {   // the chunk's superbin run table in every window: [sb][tile], [S] = length
+            const uint32_t S1 = cg.S + 1u;
+            for (uint32_t e = t; e < P * S1; e += kTile) {
+                const uint32_t w = e / S1, sb = e - w * S1;
+                const uint32_t b0 = (w * cg.S) << sub_log2, b1 = (w * cg.S + sb) << sub_log2;
+                const uint32_t v = (b1 < NB ? s_lbase[b1] : tk * k) - s_lbase[b0];
+                reinterpret_cast<uint16_t*>(cg.dir + (uint64_t)w * cg.dir_bytes + 4 * cg.tiles)
+                    [(uint64_t)sb * cg.tiles + tile] = (uint16_t)v;
+            }
+        }
+        auto place = [&](auto kplc) {
+            constexpr uint32_t KPL = decltype(kplc)::value;
+#pragma unroll
+            for (int q = 0; q < SLOTS; ++q)
+                if (tag[q] != 0xFFFFFFFFu) {
+                    const bool second = KPL == 2 && q >= (int)kTwoKeys;
+                    const uint32_t i = second ? (uint32_t)q - kTwoKeys : (uint32_t)q;
+                    s_idx[s_lbase[tag[q] >> 16] + (tag[q] & 0xFFFFu)] = (uint16_t)(((second ? kTile + t : t) << 4) | i);
+                }
+        };
+        if (kpl == 2) place(std::integral_constant<uint32_t, 2>{});
+        else place(std::integral_constant<uint32_t, 1>{});
+        __syncthreads();
+        const uint32_t tp = tk * k;
+        uint32_t o = run_of(s_obase, P, t < tp ? t : 0u);
+        for (uint32_t j = t; j < tp; j += kTile) {
+            while (o + 1u < P && s_obase[o + 1u] <= j) ++o;
+            const unsigned long long gb = s_gbase[o];
+            if (gb == ~0ull) continue;   // the window overflows: the run is dropped
+            const uint32_t x = s_idx[j], key = x >> 4;
+            const uint4 H = s_dig[key];
+            uint32_t owner;
+            uint64_t local;
+            owner_local(g, probe_offset(g, H.x, H.y, H.z, H.w, x & 15u), owner, local);
+            const uint64_t d = gb + (j - s_obase[o]);
+            wsend[d] = (uint32_t)local;   // the window implies the high bits
+            if constexpr (SLOT) wslot[d] = (uint16_t)key;   // tile-relative
+        }
+        __syncthreads();   // s_gbase, s_dig and s_idx are rewritten by the next tile
+    }
+}
+
 // One workgroup per 8192-probe block of an (owner, group) window (the grid is an
 // upper bound; spare workgroups exit): the owner's runs from the group's tiles
 // are copied, in order, to the window's place in the send buffer (owner-major,
@@ -2866,7 +2998,30 @@ hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t 
     hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,      \
                        p.tiles_per_block, p.nsup, nullptr, nullptr, nullptr, nullptr, nullptr, wcap, counts, send, \
                        slot, nh, cg)
-    if (dig) {
+    // the sorted-index form (route_chunks_idx_kernel) where the offset form holds one workgroup
+    // per CU: k > 12 (200B x 8: 0.72 / 0.80 -> 0.62 / 0.66 ms insert / include? route); at k <= 12
+    // route_front32's form already runs two and measured the same or 8 % faster (nstar x 8:
+    // 0.331 vs 0.357 ms insert route), profiles/r06j_sim_P8.jsonl
+    bool idx = dig && g.k > (uint32_t)kSlots;
+#ifdef BFHIP_AB_KNOBS
+    if (const char* v = BF_AB_GETENV("BFHIP_ROUTE_IDX")) idx = dig && atoi(v) != 0;
+#endif
+    if (idx) {
+        const uint4* dg = reinterpret_cast<const uint4*>(keys16);
+        uint32_t* ws = static_cast<uint32_t*>(send);
+#define BF_ROUTE_IDX(KERNEL)                                                                                       \
+    hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, dg, n, p.tile_keys, p.tiles_per_block, p.nsup, \
+                       wcap, counts, ws, slot16, nh, cg)
+        if (g.k > (uint32_t)kSlots) {
+            if (slot16) BF_ROUTE_IDX((route_chunks_idx_kernel<true, kWideSlots>));
+            else BF_ROUTE_IDX((route_chunks_idx_kernel<false, kWideSlots>));
+        }
+#ifdef BFHIP_AB_KNOBS
+        else if (slot16) BF_ROUTE_IDX((route_chunks_idx_kernel<true, kSlots>));
+        else BF_ROUTE_IDX((route_chunks_idx_kernel<false, kSlots>));
+#endif
+#undef BF_ROUTE_IDX
+    } else if (dig) {
         if (g.k > (uint32_t)kSlots) {
             if (slot16) BF_ROUTE_CH((route_front_kernel<false, true, kWideSlots, true, true, true>));
             else BF_ROUTE_CH((route_front_kernel<false, false, kWideSlots, true, true, true>));

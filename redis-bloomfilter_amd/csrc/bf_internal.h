@@ -247,9 +247,11 @@ uint64_t bf_seq_chunk_keys(uint32_t k);
 uint64_t bf_seq_scratch_bytes(uint64_t n, uint32_t k, uint64_t m);
 hipError_t bf_launch_seq_candidates(const BfGeom& g, uint32_t i0, const uint8_t* keys16, const uint64_t* offsets,
                                     uint64_t bias, uint64_t n, void* scratch, hipStream_t s);
-// new(j) -> out8 / any_flag (nullable) for j < n; ORs the 0-probes of keys j < limit into g.bits.
+// new(j) -> out8 / any_flag (nullable) for j < n; ORs the 0-probes of keys j < limit into g.bits
+// (limit = min(limit, *d_limit) when d_limit is given: a cut the device computed).
 hipError_t bf_launch_seq_mark(const BfGeom& g, uint32_t i0, uint64_t n, uint64_t limit, void* scratch,
-                              uint8_t* out8, uint32_t* any_flag, hipStream_t s);
+                              uint8_t* out8, uint32_t* any_flag, hipStream_t s,
+                              const unsigned long long* d_limit = nullptr);
 hipError_t bf_launch_insert_seq(const BfGeom& g, const uint8_t* keys16, const uint64_t* offsets, uint64_t bias,
                                 uint64_t n, void* scratch, uint8_t* out8, uint32_t* any_flag, hipStream_t s,
                                 BfMarks* marks = nullptr);

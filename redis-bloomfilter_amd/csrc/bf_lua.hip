@@ -94,6 +94,43 @@ __global__ __launch_bounds__(256) void lua_count_kernel(const uint8_t* __restric
     }
 }
 
+// The cut of a chunk that may fill its layer (add.lua:48-50), on the device so the host reads
+// it back once, after the apply: cnt[0] holds the chunk's new keys (lua_count_kernel).  Below
+// `room` the whole chunk stays (cnt[1] = n); else cnt[1] = the index after the key whose INCR
+// brings the count to `room`, and cnt[0] = room.  One workgroup: a contiguous byte segment per
+// lane, a scan of the segment sums, then the lane whose segment holds the crossing walks it.
+__global__ __launch_bounds__(1024) void lua_cut_kernel(const uint8_t* __restrict__ flags, uint64_t n, uint64_t room,
+                                                       unsigned long long* __restrict__ cnt) {
+    __shared__ uint32_t s_sum[1024];
+    if (cnt[0] < room) {   // workgroup-uniform
+        if (threadIdx.x == 0) cnt[1] = n;
+        return;
+    }
+    const uint32_t t = threadIdx.x;
+    const uint64_t per = (n + 1023) / 1024;
+    const uint64_t a = min<uint64_t>((uint64_t)t * per, n), b = min<uint64_t>(a + per, n);
+    uint32_t loc = 0;
+    for (uint64_t i = a; i < b; ++i) loc += flags[i];
+    s_sum[t] = loc;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {   // inclusive scan
+        const uint32_t v = t >= d ? s_sum[t - d] : 0u;
+        __syncthreads();
+        s_sum[t] += v;
+        __syncthreads();
+    }
+    uint64_t c = s_sum[t] - loc;   // new keys before this segment
+    if (c >= room || c + loc < room) return;
+    for (uint64_t i = a; i < b; ++i) {
+        c += flags[i];
+        if (c == room) {
+            cnt[0] = room;
+            cnt[1] = i + 1;
+            return;
+        }
+    }
+}
+
 }  // namespace
 
 struct bf_lua {
@@ -198,7 +235,8 @@ uint64_t lua_layer_capacity(double entries, uint32_t layer, uint64_t from) {
     return lo;
 }
 
-int ensure_layer(bf_lua* h, uint32_t n) {
+// New layers are cleared on stream s (the call's stream: no cross-stream wait needed).
+int ensure_layer(bf_lua* h, uint32_t n, hipStream_t s) {
     if (n == 0 || n > kLuaMaxLayers) return lua_err(h, BF_EINVAL, "layer %u outside 1..%u", n, kLuaMaxLayers);
     while (h->layers.size() < n) {
         const uint32_t li = (uint32_t)h->layers.size() + 1;
@@ -219,7 +257,7 @@ int ensure_layer(bf_lua* h, uint32_t n) {
         } else {
             LUACHK(h, hipMalloc((void**)&g.bits, bytes));
         }
-        LUACHK(h, hipMemsetAsync(g.bits, 0, bytes, h->stream));
+        LUACHK(h, hipMemsetAsync(g.bits, 0, bytes, s));
         g.m = m;
         g.inv_m = 1.0 / (double)m;
         g.k = k;
@@ -537,7 +575,7 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     uint64_t s = 0;
     while (s < n) {
         const uint32_t layer = lua_index(h->entries, (double)(h->count + 1));   // add.lua:6-15
-        if ((rc = ensure_layer(h, layer))) return rc;
+        if ((rc = ensure_layer(h, layer, h->stream))) return rc;
         const BfGeom& g = h->layers[layer - 1];
         const uint64_t room = lua_layer_capacity(h->entries, layer, h->count + 1) - h->count;   // >= 1
         const uint64_t cn = std::min<uint64_t>(n - s, bf_seq_chunk_keys(g.k));
@@ -607,20 +645,13 @@ int lua_insert(bf_lua* h, const uint8_t* keys, const uint64_t* offsets, uint64_t
     return BF_OK;
 }
 
-// Layers up to n exist, and the caller's stream sees a new layer's clear (ensure_layer
-// clears on the handle's own stream).
-int ensure_layer_on(bf_lua* h, uint32_t n, hipStream_t s) {
-    const size_t had = h->layers.size();
-    int rc = ensure_layer(h, n);
-    if (rc) return rc;
-    if (h->layers.size() != had && s != h->stream) LUACHK(h, hipStreamSynchronize(h->stream));
-    return BF_OK;
-}
+// Layers up to n exist, cleared on the caller's stream (no host sync: VERDICT r05 item 5).
+int ensure_layer_on(bf_lua* h, uint32_t n, hipStream_t s) { return ensure_layer(h, n, s); }
 
 // bf_lua_insert_many on device-resident keys (the caller's stream): add.lua's sequential
 // semantics exactly as lua_insert, with the per-key flags left on the device and the count's
-// INCRs summed there (lua_count_kernel); the host reads 8 bytes per chunk to pick the next
-// layer, or — only for the chunk that fills a layer — the chunk's flags to find the cut.
+// INCRs summed there (lua_count_kernel) and a layer's cut found there (lua_cut_kernel); the
+// host reads 16 bytes per chunk, after its apply, to pick the next layer.
 int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, uint64_t n, uint8_t* d_per_key_new,
                    uint64_t* new_layers, hipStream_t s) {
     if (new_layers) *new_layers = 0;
@@ -649,47 +680,33 @@ int lua_insert_dev(bf_lua* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
         BfMarks* mk = lua_prof_begin(h, s);
         LUACHK(h, bf_launch_seq_candidates(g, 1, k16, d_offsets + done, bias, cn, h->scratch, s));
         bf_mark(mk, s, lua_prof_name(h, kLuaCand, layer));
-        uint64_t take = cn, fresh = 0;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((cn / 16 + 255) / 256 + 1, 256);
+        LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 16, s));
         if (room >= cn) {   // the whole chunk lands in this layer: flags and apply in one pass
             LUACHK(h, bf_launch_seq_mark(g, 1, cn, cn, h->scratch, flags, nullptr, s));
             bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
-            LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 8, s));
-            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn / 16 + 255) / 256 + 1, 256);
             hipLaunchKernelGGL(lua_count_kernel, dim3(grid), dim3(256), 0, s, flags, cn, h->d_cnt);
             LUACHK(h, hipGetLastError());
             bf_mark(mk, s, lua_prof_name(h, kLuaCount, layer));
             LUACHK(h, hipMemcpyAsync(h->h_cnt, h->d_cnt, 8, hipMemcpyDeviceToHost, s));
-            LUACHK(h, hipStreamSynchronize(s));
-            fresh = h->h_cnt[0];
+            h->h_cnt[1] = cn;
         } else {   // the chunk may fill the layer: cut after the key whose INCR fills it (add.lua:48-50)
+            // flags first; the INCRs summed and the cut found on the device (lua_cut_kernel),
+            // then the keys before the cut applied with that limit — one read-back, at the end
             LUACHK(h, bf_launch_seq_mark(g, 1, cn, 0, h->scratch, flags, nullptr, s));
             bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
-            // the chunk's INCRs summed first: below the room (a chunk longer than the room whose
-            // keys are not all new) nothing is cut and the flags stay on the device
-            LUACHK(h, hipMemsetAsync(h->d_cnt, 0, 8, s));
-            const uint32_t grid = (uint32_t)std::min<uint64_t>((cn / 16 + 255) / 256 + 1, 256);
             hipLaunchKernelGGL(lua_count_kernel, dim3(grid), dim3(256), 0, s, flags, cn, h->d_cnt);
+            hipLaunchKernelGGL(lua_cut_kernel, dim3(1), dim3(1024), 0, s, flags, cn, room, h->d_cnt);
             LUACHK(h, hipGetLastError());
             bf_mark(mk, s, lua_prof_name(h, kLuaCount, layer));
-            LUACHK(h, hipMemcpyAsync(h->h_cnt, h->d_cnt, 8, hipMemcpyDeviceToHost, s));
-            LUACHK(h, hipStreamSynchronize(s));
-            fresh = h->h_cnt[0];
-            if (fresh >= room) {   // the cut: the flags to the host to find it
-                LUACHK(h, hipMemcpyAsync(h->h_out, flags, cn, hipMemcpyDeviceToHost, s));
-                LUACHK(h, hipStreamSynchronize(s));
-                fresh = 0;
-                for (uint64_t j = 0; j < cn; ++j) {
-                    fresh += h->h_out[j];
-                    if (fresh == room) {
-                        take = j + 1;
-                        break;
-                    }
-                }
-            }
-            mk = lua_prof_begin(h, s);
-            LUACHK(h, bf_launch_seq_mark(g, 1, cn, take, h->scratch, nullptr, nullptr, s));
+            LUACHK(h, bf_launch_seq_mark(g, 1, cn, cn, h->scratch, nullptr, nullptr, s, h->d_cnt + 1));
             bf_mark(mk, s, lua_prof_name(h, kLuaMark, layer));
+            LUACHK(h, hipMemcpyAsync(h->h_cnt, h->d_cnt, 16, hipMemcpyDeviceToHost, s));
         }
+        LUACHK(h, hipStreamSynchronize(s));
+        const uint64_t fresh = h->h_cnt[0], take = h->h_cnt[1];
+        if (take == 0 || take > cn) return lua_err(h, BF_EDEVICE, "layer %u: cut at %llu of %llu keys", layer,
+                                                   (unsigned long long)take, (unsigned long long)cn);
         if (fresh && new_layers && layer <= 64) *new_layers |= 1ull << (layer - 1);
         h->count += fresh;
         done += take;
@@ -793,7 +810,7 @@ int bf_lua_include_many(bf_lua* h, const uint8_t* keys, const uint64_t* offsets,
     LuaOrder lo(h, h->stream);
     if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
     const uint32_t index = lua_index(h->entries, (double)h->count);   // check.lua:9-11
-    int rc = ensure_layer(h, index);
+    int rc = ensure_layer(h, index, h->stream);
     if (rc) return rc;
     if ((rc = stage_keys(h, keys, offsets, n))) return rc;
     if (h->d_layers_n < index) {   // upload the table only when a layer was added
@@ -847,7 +864,7 @@ int bf_lua_import_layer(bf_lua* h, uint32_t layer, const uint8_t* buf, uint64_t 
     LuaDeviceGuard dg(h->device);
     LuaOrder lo(h, h->stream);
     if (int krc = lua_take_key_status(h)) return krc;   // an earlier call's bad key offsets
-    int rc = ensure_layer(h, layer);
+    int rc = ensure_layer(h, layer, h->stream);
     if (rc) return rc;
     const BfGeom& g = h->layers[layer - 1];
     const uint64_t full = (g.m + 7) / 8;

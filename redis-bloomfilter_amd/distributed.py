@@ -445,7 +445,8 @@ class PartitionedFilter:
 
     def __init__(self, m: int, k: int, block_log2: int = 20, group=None, device=None, engine=None,
                  windows: bool = True, pack_answers: bool = True, sync_free: bool = True,
-                 batch_capacity: Optional[int] = None, poison: Optional[int] = None, chunks: bool = True):
+                 batch_capacity: Optional[int] = None, poison: Optional[int] = None, chunks: bool = True,
+                 hash_split: bool = True):
         self.group = group
         self.P = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -480,6 +481,11 @@ class PartitionedFilter:
         if self.chunks and engine.chunk_info(1) is None:
             self.chunks = False
         self._chunk_geo = {}
+        # chunked routes hash in a pass of their own (bf_hash_many_dev, full occupancy), then
+        # route from the words (bf_route_chunks_digests_dev): the route's LDS sort holds one
+        # workgroup per CU, too few waves to hide SHA-1 behind (200B x 8: 6.61 -> 6.17 ms per
+        # rank step, profiles/r06j_sim_P8.jsonl)
+        self.hash_split = bool(hash_split and hasattr(engine, "hash_keys"))
         # The sync-free windows are sized from a batch bound every rank agrees on, never from
         # the rank's own n: ranks that size them from different n would post p2p messages of
         # different sizes (undefined under RCCL).  ``batch_capacity`` (the same on every rank)
@@ -696,6 +702,9 @@ class PartitionedFilter:
         dirb = None
         if geo is not None and dig is not None:
             self.routed_from_digests += 1
+            send, slot, counts, dirb = e.route_chunks(dig, None, n, cap, geo[0], geo[1], want_slot=want_slot)
+        elif geo is not None and self.hash_split:
+            dig = e.hash_keys(kb, ko, n)
             send, slot, counts, dirb = e.route_chunks(dig, None, n, cap, geo[0], geo[1], want_slot=want_slot)
         elif geo is not None:
             send, slot, counts, dirb = e.route_chunks(kb, ko, n, cap, geo[0], geo[1], want_slot=want_slot)

@@ -21,7 +21,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PASSES = ("rd", "wr", "dram", "valu", "stall", "fs", "ws")   # tools/pmc_passes.sh
-BATCH = {"nstar": 1 << 24, "1m": 1 << 20, "1m_big": 1 << 24, "100m": 1 << 24, "10b": 1 << 24, "lua_1m": 1 << 20}
+BATCH = {"nstar": 1 << 24, "1m": 1 << 20, "1m_big": 1 << 24, "100m": 1 << 24, "10b": 1 << 24, "200b": 1 << 24,
+         "lua_1m": 1 << 20, "model_P8_nstar": 1 << 24, "model_P8_200b": 1 << 24, "model_repl8_10b": 1 << 24}
 
 
 def main():

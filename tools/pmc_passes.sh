@@ -9,16 +9,20 @@ CONFIG=${1:-nstar}
 TAG=${2:-$CONFIG}
 if [ $# -gt 2 ]; then shift 2; PASSES="$*"; else PASSES="rd wr dram valu"; fi
 # lua_1m: the Lua layout's secondary alone (bench.py lua_config), behind the tiny 10k config
-if [ "$CONFIG" = lua_1m ]; then
-    BENCH_ARGS="--config 10k --secondary lua_1m --steps 3 --warmup 1"
-else
-    BENCH_ARGS="--config $CONFIG --steps 3 --warmup 1 --no-secondary"
-fi
+# model_*: the per-rank models of bench.py's multi_gpu_models legs (tools/sim_rank.py, the same
+# argv as bench.MODEL_LEGS with fewer steps)
+PROG="bench.py"
+case "$CONFIG" in
+    lua_1m) BENCH_ARGS="--config 10k --secondary lua_1m --steps 3 --warmup 1 --no-cpu-baseline --no-host-api --no-reference-shapes" ;;
+    model_P8_nstar) PROG="tools/sim_rank.py"; BENCH_ARGS="--shards 8 --chunks --config nstar --steps 2" ;;
+    model_P8_200b) PROG="tools/sim_rank.py"; BENCH_ARGS="--shards 8 --chunks --config 200b --steps 2" ;;
+    model_repl8_10b) PROG="tools/sim_rank.py"; BENCH_ARGS="--replicated 8 --config 10b --gathered sets --fused-hash --overlap-encode apply --steps 2" ;;
+    *) BENCH_ARGS="--config $CONFIG --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-host-api --no-reference-shapes" ;;
+esac
 run() {   # pass, counters...
     local pass=$1; shift
     timeout -s KILL 180 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_${TAG}_${pass} -o run -- \
-        python bench.py $BENCH_ARGS --no-cpu-baseline --no-host-api --no-reference-shapes \
-        > gpurun_out/pmc_${TAG}_${pass}.log 2>&1
+        python $PROG $BENCH_ARGS > gpurun_out/pmc_${TAG}_${pass}.log 2>&1
 }
 for p in $PASSES; do
     case $p in

@@ -67,6 +67,9 @@ def run(argv) -> dict:
                     help="--replicated --gathered sets --fused-hash: the NEXT step's own encode runs on a second "
                          "stream (a second handle) from the start of this step's apply, or of its include?; "
                          "read the wall time")
+    ap.add_argument("--main-priority", action="store_true",
+                    help="--overlap-encode: the main step on a high-priority stream, the side encode at normal "
+                         "priority")
     ap.add_argument("--dig", action="store_true",
                     help="--chunks: route the include? batch from SHA-1 words that the previous step's owner "
                          "test hashed between its probe rounds (bf_shard_test_chunks_hash_dev + "
@@ -78,9 +81,12 @@ def run(argv) -> dict:
                     help="--chunks (one owner pass): that pass also hashes the next step's include? batch "
                          "(bf_shard_insert_test_chunks_packed_dev with n_next), which the next step routes from "
                          "its words")
-    ap.add_argument("--hash-split", action="store_true",
-                    help="--chunks: each route as two kernels, the keys' SHA-1 (bf_hash_many_dev, full occupancy) "
-                         "then the route from the words (bf_route_chunks_digests_dev)")
+    ap.add_argument("--hash-split", dest="hash_split", action="store_true", default=True,
+                    help="--chunks (default, as PartitionedFilter): each route as two kernels, the keys' SHA-1 "
+                         "(bf_hash_many_dev, full occupancy) then the route from the words "
+                         "(bf_route_chunks_digests_dev)")
+    ap.add_argument("--no-hash-split", dest="hash_split", action="store_false",
+                    help="--chunks: the route hashes the keys itself (the round-5 form)")
     ap.add_argument("--separate", action="store_true",
                     help="--chunks: the owner's insert and include? as two calls (shard_insert_chunks, then "
                          "shard_test_chunks_packed) instead of one pass over the shard")
@@ -297,6 +303,7 @@ def run(argv) -> dict:
     out = {"config": args.config, "shards": args.shards, "m": m, "k": k, "batch": batch,
            "prefill": None if args.no_prefill else "50% random bits",
            "shard_bytes": f.device_bytes, "route32": bool(eng.offset_dtype == torch.int32),
+           "hash_split": bool(args.chunks and args.hash_split),
            "route": "chunked windows" if args.chunks else
                     ("sync-free windows" if args.sync_free else ("windows" if args.windows else "contiguous")),
            "ms_per_step_compute": wall * 1e3,
@@ -384,6 +391,10 @@ def replicated(args, pkg):
         side = torch.cuda.Stream(dev)
         owns = [own, torch.empty_like(own)]
         main_s = torch.cuda.current_stream(dev)
+        if args.main_priority:   # the step's own kernels on a high-priority queue, the encode beside them
+            main_s = torch.cuda.Stream(dev, priority=-1)
+            main_s.wait_stream(torch.cuda.current_stream(dev))
+            sp = main_s.cuda_stream
 
         def step_ovl(j):
             s_, n1, n2 = steps[j % len(steps)], steps[(j + 1) % len(steps)], steps[(j + 2) % len(steps)]
@@ -446,7 +457,8 @@ def replicated(args, pkg):
     if os.environ.get("BFHIP_SETS_STOP", "0") == "0":   # (the encode stop-point A/B writes no sets)
         assert out.cpu().numpy()[: batch // 2].all(), "false negative"
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
-           "fused_hash": bool(args.fused_hash), "overlap_encode": ovl or None, "m": m, "k": k,
+           "fused_hash": bool(args.fused_hash), "overlap_encode": ovl or None,
+           "main_priority": bool(ovl and args.main_priority), "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
            "gathered_bytes_per_rank": (cap_sets if args.gathered == "sets" else
                                        batch * 16 if args.gathered == "digests" else None),
