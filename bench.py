@@ -591,8 +591,8 @@ def time_config(pkg, D: Dist, name: str, steps: int, warmup: int, want_host=Fals
 MODEL_LEGS = {
     "model_P8_nstar": (["--shards", "8", "--chunks", "--config", "nstar", "--steps", "5"], "nstar", "partitioned"),
     "model_P8_200b": (["--shards", "8", "--chunks", "--config", "200b", "--steps", "5"], "200b", "partitioned"),
-    "model_repl8_10b": (["--replicated", "8", "--config", "10b", "--gathered", "sets", "--fused-hash", "--steps", "3"],
-                        "10b", "replicated"),
+    "model_repl8_10b": (["--replicated", "8", "--config", "10b", "--gathered", "sets", "--fused-hash",
+                         "--overlap-encode", "apply", "--steps", "3"], "10b", "replicated"),
 }
 
 

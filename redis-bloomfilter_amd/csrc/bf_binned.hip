@@ -831,16 +831,24 @@ void route_front32_kernel(BF_ROUTE_FRONT_ARGS, BfChunks cg) {
 // route_front_body<.., WIN, CHUNK, DIG>, whose sort buffers (72.8 KiB without slots, 105.5 KiB
 // with, 92-102 VGPRs at k = 13) hold one workgroup per CU: here 56-72 KiB and <= 64 VGPRs make
 // two, so one workgroup's claims and barriers hide behind the other's work.
-template <bool SLOT, int SLOTS>
+// HASH (bf_route_chunks_dev, k > 12): the keys are hashed here, one per lane, their bytes staged
+// in the index buffer (dead until the tile's scan).
+template <bool SLOT, int SLOTS, bool HASH = false>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void route_chunks_idx_kernel(BfGeom g, const uint4* __restrict__ dig, uint64_t n, uint32_t tile_keys,
+void route_chunks_idx_kernel(BfGeom g, const uint8_t* __restrict__ keys16, const uint64_t* __restrict__ offsets,
+                             uint64_t bias, uint64_t n, uint32_t tile_keys,
                              uint32_t tiles_per_block, uint32_t P, uint64_t wcap,
                              unsigned long long* __restrict__ wcounts, uint32_t* __restrict__ wsend,
                              uint16_t* __restrict__ wslot, uint32_t nh, BfChunks cg) {
     static_assert(SLOTS <= 16 && kTile * SLOTS <= 65536, "a probe index is 4 bits, a sort slot 16");
     constexpr uint32_t NB = kChunkBuckets;
-    __shared__ uint16_t s_idx[kTile * SLOTS];
+    constexpr uint32_t kOffVec = (8 * (kTile + 1) + 15) / 16;
+    static_assert(!HASH || (SLOTS > kSlots && (kOffVec + kStageVec + kStageSlackVec) * 16 <= kTile * SLOTS * 2),
+                  "the key stage fits the index buffer (one key per lane)");
+    __shared__ uint4 s_idx4[kTile * SLOTS * 2 / 16];
+    uint16_t* s_idx = reinterpret_cast<uint16_t*>(s_idx4);
     __shared__ uint4 s_dig[SLOTS > kSlots ? kTile : 2 * kTile];   // k > 12: one key per lane
+    const uint4* dig = reinterpret_cast<const uint4*>(keys16);
     __shared__ uint32_t s_cnt[NB], s_lbase[NB];
     __shared__ uint32_t s_w[16];
     __shared__ unsigned long long s_gbase[kMaxOwners];
@@ -859,8 +867,19 @@ void route_chunks_idx_kernel(BfGeom g, const uint4* __restrict__ dig, uint64_t n
         const uint32_t tk = (uint32_t)((n - key0) < (uint64_t)tile_keys ? (n - key0) : tile_keys);
         const bool live0 = t < tk;
         const bool live1 = kpl == 2 && kTile + t < tk;
-        const uint4 H0 = live0 ? dig[key0 + t] : make_uint4(0, 0, 0, 0);
-        const uint4 H1 = live1 ? dig[key0 + kTile + t] : make_uint4(0, 0, 0, 0);
+        uint4 H0 = make_uint4(0, 0, 0, 0), H1 = make_uint4(0, 0, 0, 0);
+        if constexpr (HASH) {   // kpl == 1
+            for_key_tile<kTile, kStageVec>(keys16, offsets, bias, key0, tk, reinterpret_cast<uint64_t*>(s_idx4),
+                                           s_idx4 + kOffVec, g.key_status,
+                [&](auto staged, uint32_t, const uint32_t* src, uint32_t s0, uint32_t L) {
+                    uint32_t H[5];
+                    sha1_any<decltype(staged)::value>(src, s0, L, H);
+                    H0 = make_uint4(H[0], H[1], H[2], H[3]);
+                });
+        } else {
+            if (live0) H0 = dig[key0 + t];
+            if (live1) H1 = dig[key0 + kTile + t];
+        }
         s_dig[t] = H0;
         if (kpl == 2) s_dig[kTile + t] = H1;
         uint32_t tag[SLOTS];
@@ -3002,19 +3021,21 @@ hipError_t bf_launch_route_chunks(const BfGeom& g, const BfBinPlan& p, uint32_t 
     // per CU: k > 12 (200B x 8: 0.72 / 0.80 -> 0.62 / 0.66 ms insert / include? route); at k <= 12
     // route_front32's form already runs two and measured the same or 8 % faster (nstar x 8:
     // 0.331 vs 0.357 ms insert route), profiles/r06j_sim_P8.jsonl
-    bool idx = dig && g.k > (uint32_t)kSlots;
+    bool idx = g.k > (uint32_t)kSlots;
 #ifdef BFHIP_AB_KNOBS
-    if (const char* v = BF_AB_GETENV("BFHIP_ROUTE_IDX")) idx = dig && atoi(v) != 0;
+    if (const char* v = BF_AB_GETENV("BFHIP_ROUTE_IDX")) idx = atoi(v) != 0 && (g.k > (uint32_t)kSlots || dig);
 #endif
     if (idx) {
-        const uint4* dg = reinterpret_cast<const uint4*>(keys16);
         uint32_t* ws = static_cast<uint32_t*>(send);
 #define BF_ROUTE_IDX(KERNEL)                                                                                       \
-    hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, dg, n, p.tile_keys, p.tiles_per_block, p.nsup, \
-                       wcap, counts, ws, slot16, nh, cg)
+    hipLaunchKernelGGL(KERNEL, dim3(p.nblocks), dim3(kTile), 0, s, g, keys16, offsets, bias, n, p.tile_keys,          \
+                       p.tiles_per_block, p.nsup, wcap, counts, ws, slot16, nh, cg)
         if (g.k > (uint32_t)kSlots) {
-            if (slot16) BF_ROUTE_IDX((route_chunks_idx_kernel<true, kWideSlots>));
-            else BF_ROUTE_IDX((route_chunks_idx_kernel<false, kWideSlots>));
+            if (dig) {
+                if (slot16) BF_ROUTE_IDX((route_chunks_idx_kernel<true, kWideSlots>));
+                else BF_ROUTE_IDX((route_chunks_idx_kernel<false, kWideSlots>));
+            } else if (slot16) BF_ROUTE_IDX((route_chunks_idx_kernel<true, kWideSlots, true>));
+            else BF_ROUTE_IDX((route_chunks_idx_kernel<false, kWideSlots, true>));
         }
 #ifdef BFHIP_AB_KNOBS
         else if (slot16) BF_ROUTE_IDX((route_chunks_idx_kernel<true, kSlots>));

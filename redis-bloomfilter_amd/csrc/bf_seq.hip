@@ -111,13 +111,18 @@ __global__ __launch_bounds__(256) void seq_mark_kernel(BfGeom g, uint32_t i0, ui
                 }
                 isnew |= tvals[slot] == (uint32_t)j ? 1u : 0u;
                 if (j < limit) {
-                    __hip_atomic_fetch_or(g.bits + (o >> 5), 1u << ((uint32_t)(o ^ 7u) & 31u), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t bit = 1u << ((uint32_t)(o ^ 7u) & 31u);
                     if (g.dirty) g.dirty[o >> kDirtyShiftBits] = 1;
-                    // the bit flips once, reported by the first key of the batch that probes it
-                    if (g.flips && tvals[slot] == (uint32_t)j) {
-                        const unsigned long long at = atomicAdd(g.flip_count, 1ull);
-                        if (at < g.flip_cap) g.flips[at] = o | g.flip_tag;
+                    if (g.flips) {   // the bit flips once: reported by the one OR that set it (a key
+                                     // may probe one bit twice, and later keys probe it too)
+                        const uint32_t old = __hip_atomic_fetch_or(g.bits + (o >> 5), bit, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        if (!(old & bit)) {
+                            const unsigned long long at = atomicAdd(g.flip_count, 1ull);
+                            if (at < g.flip_cap) g.flips[at] = o | g.flip_tag;
+                        }
+                    } else {
+                        __hip_atomic_fetch_or(g.bits + (o >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
             }
@@ -287,7 +292,9 @@ __global__ __launch_bounds__(kSeqRegionLanes) void seq_region_kernel(BfGeom g, u
         if (out8) out8[j] = 1;
         if (j >= limit) continue;
         fresh = true;
-        atomicOr(&s_img[b >> 5], 1u << ((b ^ 7u) & 31u));
+        const uint32_t bit = 1u << ((b ^ 7u) & 31u);
+        const uint32_t old = atomicOr(&s_img[b >> 5], bit);
+        if (old & bit) continue;   // key j probes bit b twice: the other entry reports it
         const uint64_t o = ((uint64_t)r << kSeqRegionLog2) | b;
         if (g.dirty) g.dirty[o >> kDirtyShiftBits] = 1;
         if (g.flips) {   // the bit flips once, reported by its first key

@@ -171,3 +171,26 @@ def test_hip_lua_per_key_setbit_replay(pkg):
         want = set(np.flatnonzero(new_bits & ~old_bits).tolist())
         assert {o for (lay, o) in flips if lay == n} == want, n
     bf.driver.close()
+
+
+def test_lua_changes_binned_batch_across_layers(pkg):
+    """bf_lua_insert_many_changes on 6000 keys (the binned sequential form: 4096+ keys, layers
+    of <= 2^27 bits) that fill layer 1 and run into layer 2 within one call: the flips reported
+    are exactly the layers' new bits, one per bit, and the flags and layers match the script."""
+    rng = np.random.default_rng(23)
+    keys = ["b%d" % v for v in rng.integers(0, 9000, 6000)]
+    r, want_flags = script_run(pkg, keys, 2000, 0.01)
+    with pkg.LuaFilter(2000, 0.01) as f:
+        b, o = pkg.keys.pack(keys)
+        pk, touched, flips = f.insert_many_changes(b, o)
+        np.testing.assert_array_equal(pk.astype(bool), want_flags)
+        assert f.count == int(r.get("lbf:count")) and f.layers >= 2
+        got = {}
+        for lay, off in flips:
+            got.setdefault(lay, []).append(off)
+        for n, s in layers_of(r, "lbf").items():
+            assert f.export_layer(n) == s, n
+            offs = sorted(got.get(n, []))
+            assert len(offs) == len(set(offs)), n    # each bit reported once
+            bits = np.unpackbits(np.frombuffer(s, np.uint8))
+            assert offs == np.flatnonzero(bits).tolist(), n

@@ -192,11 +192,14 @@ def test_any_new_and_per_key(pkg, oracle):
 
 @pytest.mark.parametrize("m,k,n,chunk", [(9585, 6, 5000, 0), (95851, 7, 40_000, 0), (95851, 7, 40_000, 997),
                                          (2**32 + 17, 13, 20_000, 0), (9585058377, 6, 100_000, 0),
-                                         (1000, 64, 300, 0)])
+                                         (1000, 64, 300, 0), (70001, 64, 6000, 0), (2**27, 7, 50_000, 0)])
 def test_per_key_new_is_sequential(pkg, oracle, m, k, n, chunk):
     """per_key_new[j] == 1 iff inserting the batch key by key (ruby.rb:57-61), key j flipped a
     bit: exact against the oracle's sequential loop, with repeated keys, dense filters
-    (many keys sharing bits within the batch), host chunks (batch_keys) and a prefilled filter."""
+    (many keys sharing bits within the batch), host chunks (batch_keys) and a prefilled filter.
+    Batches of 4096+ keys on filters of up to 2^27 bits take the binned form (bf_seq.hip: the
+    first-index table per 2^14-bit region in LDS): 9585 / 95851 (a partial last region) / 70001
+    at k = 64 / 2^27 (8192 regions, the form's limit); the others the direct or hash forms."""
     rng = np.random.default_rng(RNG_SEED + 9)
     vals = rng.integers(0, n // 2, size=n)                 # ~half the batch repeats earlier keys
     b, o = pkg.keys.pack_decimal(vals)

@@ -70,6 +70,8 @@ def run(argv) -> dict:
     ap.add_argument("--main-priority", action="store_true",
                     help="--overlap-encode: the main step on a high-priority stream, the side encode at normal "
                          "priority")
+    ap.add_argument("--side-priority", action="store_true",
+                    help="--overlap-encode: the side encode on a high-priority stream")
     ap.add_argument("--dig", action="store_true",
                     help="--chunks: route the include? batch from SHA-1 words that the previous step's owner "
                          "test hashed between its probe rounds (bf_shard_test_chunks_hash_dev + "
@@ -388,7 +390,7 @@ def replicated(args, pkg):
         # the encoder: a bitset-less handle (BF_FLAG_ENCODER) with its own scratch, so its calls are
         # not ordered behind the main handle's (ReplicatedFilter's side_encode)
         enc = pkg.Filter(m, k, device=0, flags=pkg._lib.BF_FLAG_ENCODER)
-        side = torch.cuda.Stream(dev)
+        side = torch.cuda.Stream(dev, priority=-1 if args.side_priority else 0)
         owns = [own, torch.empty_like(own)]
         main_s = torch.cuda.current_stream(dev)
         if args.main_priority:   # the step's own kernels on a high-priority queue, the encode beside them
@@ -458,7 +460,8 @@ def replicated(args, pkg):
         assert out.cpu().numpy()[: batch // 2].all(), "false negative"
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
            "fused_hash": bool(args.fused_hash), "overlap_encode": ovl or None,
-           "main_priority": bool(ovl and args.main_priority), "m": m, "k": k,
+           "main_priority": bool(ovl and args.main_priority), "side_priority": bool(ovl and args.side_priority),
+           "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
            "gathered_bytes_per_rank": (cap_sets if args.gathered == "sets" else
                                        batch * 16 if args.gathered == "digests" else None),
