@@ -872,8 +872,9 @@ def load_traffic(workload: str, kernel: str):
 
 # every workload's counters from the round's final tree, one tag (tools/pmc_finalize.py;
 # tests/test_profiles_tagged.py checks the tag across these, pmc_traffic.json and the rocprof means)
-PMC_TAG = "r05f"
-PMC_FILES = {w: "pmc_%s_%s.json" % (PMC_TAG, w) for w in ("nstar", "1m", "1m_big", "100m", "10b", "lua_1m")}
+PMC_TAG = "r06n"
+PMC_FILES = {w: "pmc_%s_%s.json" % (PMC_TAG, w) for w in ("nstar", "1m", "1m_big", "100m", "10b", "200b", "lua_1m",
+                                                          "model_P8_nstar", "model_P8_200b", "model_repl8_10b")}
 # rocprofv3 --kernel-trace --stats of the bench command on the round's final tree
 # (tools/rocprof_means.py over profiles/<tag>_kernel_stats.csv): each kernel's mean launch
 ROCPROF_MEANS = "rocprof_means.json"
@@ -902,7 +903,8 @@ def load_pmc(workload: str):
             t = json.load(fh).get(workload) or {}
     except (OSError, ValueError):
         return None
-    keep = ("valu_busy", "valu_lane_insts_per_key", "hbm_bytes_per_launch", "profiled_ms_mean")
+    keep = ("valu_busy", "valu_lane_insts_per_key", "hbm_bytes_per_launch", "profiled_ms_mean", "frac_wait_any",
+            "frac_wait_inst_any", "frac_active_inst_any", "lds_bank_conflict_frac")
     return {"source": "profiles/" + name,
             "kernels": {kn: {x: rec.get(x) for x in keep} for kn, rec in t.items() if isinstance(rec, dict)}}
 
@@ -1045,7 +1047,7 @@ def main():
     if D.world == 1 and args.models and not args.no_secondary:
         single = {name: r["ms_per_step"] for name, r in secondary.items() if "ms_per_step" in r}
         single[args.config] = main_res["wall_s"] / args.steps * 1e3
-        models = model_legs([x for x in args.models.split(",") if x], single)
+        models = model_legs([x for x in args.models.split(",") if x and x != "none"], single)
     shapes = None
     if D.world == 1 and not args.no_reference_shapes:
         shapes = reference_shapes(pkg)

@@ -227,7 +227,15 @@ int  bf_include_hash_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_
  *                            d_status (nullable) gets 1 ORed in when a buffer's header does not
  *                            match this filter (that buffer is skipped), or a region's entry
  *                            would reach past its buffer (that region of that buffer is
- *                            skipped).  A set body is read only inside its own bounds. */
+ *                            skipped).  A set body is read only inside its own bounds.
+ *   bf_insert_encode_region_sets_dev  one replica step's two region passes in one call:
+ *                            bf_insert_region_sets_dev of the nsrc buffers, and
+ *                            bf_encode_region_sets_digests_dev of the NEXT batch (n_next SHA-1
+ *                            word quadruples) into d_next_sets, which must not overlap the
+ *                            buffers being inserted.  Region r is applied and then r's next
+ *                            set encoded by the same workgroup in the same LDS, so the apply's
+ *                            bitset stream and the encode's LDS / VALU work overlap inside each
+ *                            CU.  Results equal the two calls'. */
 int  bf_region_sets_capacity(const bf_handle* h, uint64_t n, uint64_t* bytes);
 int  bf_encode_region_sets_dev(bf_handle* h, const uint8_t* d_key_bytes, const uint64_t* d_offsets, uint64_t n,
                                uint32_t* d_sets, uint64_t sets_bytes, void* stream);
@@ -236,6 +244,10 @@ int  bf_encode_region_sets_digests_dev(bf_handle* h, const uint32_t* d_digests, 
 int  bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t stride_bytes, uint32_t nsrc,
                                uint64_t probes_hint, uint32_t* d_any_new /* nullable */,
                                uint32_t* d_status /* nullable */, void* stream);
+int  bf_insert_encode_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t stride_bytes, uint32_t nsrc,
+                                      uint64_t probes_hint, uint32_t* d_any_new /* nullable */,
+                                      uint32_t* d_status /* nullable */, const uint32_t* d_next_digests,
+                                      uint64_t n_next, uint32_t* d_next_sets, uint64_t next_sets_bytes, void* stream);
 /* The device bitset (Redis byte order, device_bytes long, zero past the reachable prefix). */
 int  bf_device_bits(bf_handle* h, void** d_bits, uint64_t* device_bytes);
 /* How an insert batch of n keys will run (no launch): *binned = 1 for the binned

@@ -93,6 +93,8 @@ SIGNATURES = {
     "bf_encode_region_sets_dev": (ctypes.c_int, [_vp, _vp, _vp, _u64, _vp, _u64, _vp]),
     "bf_encode_region_sets_digests_dev": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
     "bf_insert_region_sets_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _u64, _vp, _vp, _vp]),
+    "bf_insert_encode_region_sets_dev": (ctypes.c_int, [_vp, _vp, _u64, _u32, _u64, _vp, _vp, _vp, _u64, _vp, _u64,
+                                                        _vp]),
     "bf_insert_plan": (ctypes.c_int, [_vp, _u64, _u32p, _u64p]),
     "bf_track_dirty": (ctypes.c_int, [_vp, _u32]),
     "bf_dirty_ranges": (ctypes.c_int, [_vp, _u64p, _u32, _u32p, _u64p, _u32]),
@@ -485,6 +487,17 @@ class Filter:
         _check(self._lib.bf_insert_region_sets_dev(self.handle, d_sets, int(stride_bytes), int(nsrc),
                                                    int(probes_hint), d_any_new or None, d_status or None,
                                                    self._s(stream)), self._h)
+
+    def insert_encode_region_sets_dev(self, d_sets: int, stride_bytes: int, nsrc: int, probes_hint: int,
+                                      d_next_digests: int, n_next: int, d_next_sets: int, next_sets_bytes: int,
+                                      d_any_new: int = 0, d_status: int = 0, stream=None) -> None:
+        """insert_region_sets_dev of nsrc buffers and encode_region_sets_digests_dev of the next
+        batch's words into d_next_sets, in one pass over the regions
+        (bf_insert_encode_region_sets_dev)."""
+        _check(self._lib.bf_insert_encode_region_sets_dev(self.handle, d_sets or None, int(stride_bytes), int(nsrc),
+                                                          int(probes_hint), d_any_new or None, d_status or None,
+                                                          d_next_digests or None, int(n_next), d_next_sets,
+                                                          int(next_sets_bytes), self._s(stream)), self._h)
 
     def _s(self, stream):
         if stream is None:

@@ -2249,6 +2249,67 @@ int bf_insert_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t str
     return BF_OK;
 }
 
+int bf_insert_encode_region_sets_dev(bf_handle* h, const uint32_t* d_sets, uint64_t stride_bytes, uint32_t nsrc,
+                                     uint64_t probes_hint, uint32_t* d_any_new, uint32_t* d_status,
+                                     const uint32_t* d_next_digests, uint64_t n_next, uint32_t* d_next_sets,
+                                     uint64_t next_sets_bytes, void* stream) {
+    if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
+    if (!h) return BF_EINVAL;
+    if (nsrc == 0)   // nothing to apply: the encode alone
+        return encode_sets(h, reinterpret_cast<const uint8_t*>(d_next_digests), nullptr, n_next, true, d_next_sets,
+                           next_sets_bytes, stream);
+    if (!d_sets || (reinterpret_cast<uintptr_t>(d_sets) & 15u) || (stride_bytes & 15u))
+        return set_err(h, BF_EINVAL, "d_sets and stride_bytes must be 16-byte aligned");
+    if (!d_next_sets || (reinterpret_cast<uintptr_t>(d_next_sets) & 15u))
+        return set_err(h, BF_EINVAL, "d_next_sets must be 16-byte aligned");
+    if (n_next && (!d_next_digests || (reinterpret_cast<uintptr_t>(d_next_digests) & 15u)))
+        return set_err(h, BF_EINVAL, "d_next_digests must be a 16-byte aligned device pointer");
+    if (h->shards > 1) return set_err(h, BF_EINVAL, "handle holds one shard of a partitioned filter");
+    if (h->engine != BF_ENGINE_RUBY) return set_err(h, BF_EINVAL, "region sets carry the ruby driver's derivation only");
+    uint32_t rl = 0, nbins = 0;
+    if (!bf_sets_geometry(h->dev_bytes, h->bin_region_log2, &rl, &nbins))
+        return set_err(h, BF_EINVAL, "this filter's regions cannot take region sets");
+    if (stride_bytes < 4 * bf_sets_header_words(nbins))
+        return set_err(h, BF_EINVAL, "stride_bytes below a set buffer's header and tables");
+    // the next batch's buffer is written while the sets are read: it must not be one of them
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(d_sets), a1 = a0 + (uint64_t)nsrc * stride_bytes;
+    const uintptr_t b0 = reinterpret_cast<uintptr_t>(d_next_sets), b1 = b0 + next_sets_bytes;
+    if (b0 < a1 && a0 < b1) return set_err(h, BF_EINVAL, "d_next_sets overlaps the set buffers being inserted");
+    const uint64_t need = bf_sets_capacity_bytes(h->dev_bytes, h->bin_region_log2, n_next, h->k);
+    if (next_sets_bytes < need)
+        return set_err(h, BF_EINVAL, "next_sets_bytes %llu < bf_region_sets_capacity %llu",
+                       (unsigned long long)next_sets_bytes, (unsigned long long)need);
+    BfBinPlan plan{};
+    plan.region_log2 = rl;
+    plan.nbins = nbins;
+    if (!sets_one_pass(h, n_next, rl, &plan))
+        return set_err(h, BF_EINVAL, "a batch of %llu keys does not sort in one pass", (unsigned long long)n_next);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (!dg.ok) return set_err(h, BF_EDEVICE, "hipSetDevice(%d) failed", h->device);
+    StreamOrder so(h, pick_stream(h, stream));
+    if (int krc = op_check(h)) return krc;   // a bitset-less handle; an earlier call's bad key offsets
+    if (n_next) {
+        int rc = ensure_scratch(h, plan.scratch_bytes);
+        if (rc) return rc;
+    }
+    BfMarks* mk = prof_begin(h, so.s);
+    if (n_next == 0) {   // an empty next batch: its buffer is the header alone
+        HIPCHK(h, bf_launch_encode_sets(h->g, plan, h->dev_bytes, nullptr, nullptr, 0, 0, true, h->d_bin_scratch,
+                                        d_next_sets, std::min<uint64_t>(next_sets_bytes / 4, 0xFFFFFFFFull), so.s,
+                                        nullptr));
+        HIPCHK(h, bf_launch_insert_sets(h->g, h->dev_bytes, rl, nbins, d_sets, stride_bytes / 4, nsrc, probes_hint,
+                                        d_any_new, d_status, so.s, mk));
+        return BF_OK;
+    }
+    HIPCHK(h, bf_launch_insert_encode_sets(h->g, plan, h->dev_bytes, rl, nbins, d_sets, stride_bytes / 4, nsrc,
+                                           probes_hint, d_any_new, d_status,
+                                           reinterpret_cast<const uint8_t*>(d_next_digests), n_next, h->d_bin_scratch,
+                                           d_next_sets, std::min<uint64_t>(next_sets_bytes / 4, 0xFFFFFFFFull), so.s,
+                                           mk));
+    return BF_OK;
+}
+
 int bf_stream(bf_handle* h, void** stream) {
     if (h && h->multi) return bfm_fail(h->multi, BF_EINVAL, "multi-device handle: use the host-pointer API");
     if (!h || !stream) return BF_EINVAL;

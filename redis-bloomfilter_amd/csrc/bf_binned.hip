@@ -3196,27 +3196,34 @@ __global__ __launch_bounds__(1024) void sets_place_kernel(uint32_t* __restrict__
 //   l < 5 (dense) and bitmap sets: assembled in the bitmap's own LDS after every lane has taken
 //   its words into registers.
 // 78 KiB of LDS at 2^19-bit regions: two workgroups per CU.
-template <uint32_t RLOG2, uint32_t LANES, int LOADS>
-__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES / 256))) void sets_encode_kernel(const uint32_t* __restrict__ level2,
-                                                            const uint32_t* __restrict__ cb_base,
-                                                            const uint32_t* __restrict__ cb_start,
-                                                            const uint16_t* __restrict__ tabs, uint64_t max_chunks,
-                                                            uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
-                                                            const uint32_t* __restrict__ sb_first, uint32_t cap_words,
-                                                            uint32_t stop) {
-    constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
-    static_assert(WPL * LANES == NW && WPL % 4 == 0 && WPL <= 32, "region words must tile the lanes in vectors");
+// the LDS words the encode's run table / sparse-set image takes beside its bitmap
+template <uint32_t RLOG2>
+constexpr uint32_t sets_encode_run_lds() {
+    constexpr uint32_t NW = (1u << RLOG2) / 32;
     // the gather's run table, then a sparse set's image: at l >= 5 (n <= U / 2^l) the low bits
     // take at most 5 NW / 32 words (l = 5) and the upper bitmap 2 NW / 32
     constexpr uint32_t kSetLds = 5u * NW / 32u + 2u * NW / 32u + 2u;
-    constexpr uint32_t kRunLds = 2 * kRunsPerPass > kSetLds ? 2 * kRunsPerPass : kSetLds;
-    __shared__ uint4 s_m4[NW / 4];
-    __shared__ uint32_t s_runs[kRunLds], s_w[16];
+    return 2 * kRunsPerPass > kSetLds ? 2 * kRunsPerPass : kSetLds;
+}
+
+// Region r's set (nbins regions): the body of sets_encode_kernel, also run by
+// sets_apply_encode_kernel after its apply of the same region, in the same LDS.
+template <uint32_t RLOG2, uint32_t LANES, int LOADS>
+__device__ __forceinline__ void sets_encode_region(uint32_t r, uint32_t nbins, const uint32_t* __restrict__ level2,
+                                                   const uint32_t* __restrict__ cb_base,
+                                                   const uint32_t* __restrict__ cb_start,
+                                                   const uint16_t* __restrict__ tabs, uint64_t max_chunks,
+                                                   uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
+                                                   const uint32_t* __restrict__ sb_first, uint32_t cap_words,
+                                                   uint32_t stop, uint4* s_m4, uint32_t* s_runs, uint32_t* s_w) {
+    constexpr uint32_t U = 1u << RLOG2, NW = U / 32, WPL = NW / LANES;
+    static_assert(WPL * LANES == NW && WPL % 4 == 0 && WPL <= 32, "region words must tile the lanes in vectors");
+    constexpr uint32_t kSetLds = 5u * NW / 32u + 2u * NW / 32u + 2u;
     uint32_t* s_m = reinterpret_cast<uint32_t*>(s_m4);
     uint32_t* s_pre = s_runs;
     uint32_t* s_gst = s_runs + kRunsPerPass;
     uint32_t* s_set = s_runs;
-    const uint32_t t = threadIdx.x, r = blockIdx.x;
+    const uint32_t t = threadIdx.x;
     // the region's reserved place: its superbin's first word + its prefix in the superbin
     // (sets_size_kernel / sets_place_kernel); loaded while the LDS image is cleared
     const uint32_t rv = out[kSetsHdr + r], sbf = sb_first[r >> rel_log2];
@@ -3225,7 +3232,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES
     if (!(rv & 0x80000000u)) return;   // workgroup-uniform: no probes (out[4 + r] is already 0)
 #ifdef BFHIP_AB_KNOBS
     if (stop == 3) {   // (A/B: where the time goes; BFHIP_SETS_STOP) the region left absent
-        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;   // every lane read rv before the barrier
+        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + nbins + r] = 0;   // every lane read rv before the barrier
         return;
     }
 #endif
@@ -3243,7 +3250,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES
         });
 #ifdef BFHIP_AB_KNOBS
     if (stop == 2) {   // (A/B)
-        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
+        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + nbins + r] = 0;
         return;
     }
 #endif
@@ -3276,13 +3283,13 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES
     const bool fits = (uint64_t)st + words <= cap_words;
     if (t == 0) {   // every lane read rv before the barriers above
         out[kSetsHdr + r] = fits ? st : 0u;
-        out[kSetsHdr + gridDim.x + r] = fits ? n | ((bitmap ? kSetsBitmap : l) << 24) : 0u;
+        out[kSetsHdr + nbins + r] = fits ? n | ((bitmap ? kSetsBitmap : l) << 24) : 0u;
     }
     if (!fits) return;   // workgroup-uniform
     uint32_t* o = out + st;
 #ifdef BFHIP_AB_KNOBS
     if (stop == 1) {   // (A/B) the region left absent, so no reader decodes the unwritten set
-        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + gridDim.x + r] = 0;
+        if (t == 0) out[kSetsHdr + r] = out[kSetsHdr + nbins + r] = 0;
         return;
     }
 #else
@@ -3334,31 +3341,54 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES
     walk(o + 1, o + 1 + lw);
 }
 
+
+template <uint32_t RLOG2, uint32_t LANES, int LOADS>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES / 256))) void sets_encode_kernel(const uint32_t* __restrict__ level2,
+                                                            const uint32_t* __restrict__ cb_base,
+                                                            const uint32_t* __restrict__ cb_start,
+                                                            const uint16_t* __restrict__ tabs, uint64_t max_chunks,
+                                                            uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
+                                                            const uint32_t* __restrict__ sb_first, uint32_t cap_words,
+                                                            uint32_t stop) {
+    __shared__ uint4 s_m4[(1u << RLOG2) / 128];
+    __shared__ uint32_t s_runs[sets_encode_run_lds<RLOG2>()], s_w[16];
+    sets_encode_region<RLOG2, LANES, LOADS>(blockIdx.x, gridDim.x, level2, cb_base, cb_start, tabs, max_chunks, nq,
+                                            rel_log2, out, sb_first, cap_words, stop, s_m4, s_runs, s_w);
+}
+
 // One workgroup per region: every source's set for the region ORed into an LDS image (bitmap
 // sets word by word; Elias-Fano sets decoded one pass of LANES upper-bitmap words at a time
 // across all sources: an offset's rank in its set is its rank among all sources' upper bits
 // minus the offsets of the sources before it), then bin_apply's read-OR-write of the region.
 // A source whose header does not match (magic, region geometry, capacity) is skipped and
 // flagged in *status.
+// sets_apply_kernel's LDS tables beside the region image and the low-bit stage
+struct SetsApplyTabs {
+    uint32_t w[16];
+    uint32_t st[kMaxSetSrc], hdr[kMaxSetSrc], uw0[kMaxSetSrc + 1], np[kMaxSetSrc + 1], lw0[kMaxSetSrc + 1];
+};
+
+// Region r: the body of sets_apply_kernel, also run by sets_apply_encode_kernel.  Ends with every
+// lane past its last LDS access of the image but without a barrier.
 template <uint32_t RLOG2, uint32_t LANES, uint32_t STAGE>
-__global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
-                                                           const uint32_t* __restrict__ sets, uint64_t stride_words,
-                                                           uint32_t nsrc, uint32_t nbins, uint32_t dense,
-                                                           uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
-                                                           uint32_t store_fresh, uint32_t* __restrict__ status,
-                                                           uint32_t xg) {
+__device__ __forceinline__ void sets_apply_region(uint32_t r, uint32_t* __restrict__ bits, uint64_t nwords,
+                                                  const uint32_t* __restrict__ sets, uint64_t stride_words,
+                                                  uint32_t nsrc, uint32_t nbins, uint32_t dense,
+                                                  uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
+                                                  uint32_t store_fresh, uint32_t* __restrict__ status,
+                                                  uint4* s_mask4, uint32_t* s_lows, SetsApplyTabs& T) {
     constexpr uint32_t kVec = 1u << (RLOG2 - 7);
     constexpr uint32_t kPer = kVec / LANES;
     constexpr uint32_t U = 1u << RLOG2, NW = U / 32;
     static_assert(kPer * LANES == kVec, "region must tile the workgroup");
-    __shared__ uint4 s_mask4[kVec];
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_st[kMaxSetSrc], s_hdr[kMaxSetSrc], s_uw0[kMaxSetSrc + 1], s_np[kMaxSetSrc + 1];
-    __shared__ uint32_t s_lw0[kMaxSetSrc + 1];
-    __shared__ uint32_t s_lows[STAGE + 1];   // every Elias-Fano source's low-bit words, back to back
+    uint32_t* s_w = T.w;
+    uint32_t* s_st = T.st;
+    uint32_t* s_hdr = T.hdr;
+    uint32_t* s_uw0 = T.uw0;
+    uint32_t* s_np = T.np;
+    uint32_t* s_lw0 = T.lw0;
     uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_mask4);
     const uint32_t t = threadIdx.x;
-    const uint32_t r = apply_region(blockIdx.x, gridDim.x, xg);
     const uint64_t v0 = (uint64_t)r * kVec;
     const uint64_t nvec = nwords / 4;
     uint4* gv = reinterpret_cast<uint4*>(bits);
@@ -3511,6 +3541,49 @@ __global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict_
         if (dirty && fr) dirty[((v0 + v) * 128) >> kDirtyShiftBits] = 1;
     }
     if (any_flag) report_any_new(any_flag, fresh != 0);
+}
+
+template <uint32_t RLOG2, uint32_t LANES, uint32_t STAGE>
+__global__ __launch_bounds__(LANES) void sets_apply_kernel(uint32_t* __restrict__ bits, uint64_t nwords,
+                                                           const uint32_t* __restrict__ sets, uint64_t stride_words,
+                                                           uint32_t nsrc, uint32_t nbins, uint32_t dense,
+                                                           uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty,
+                                                           uint32_t store_fresh, uint32_t* __restrict__ status,
+                                                           uint32_t xg) {
+    __shared__ uint4 s_mask4[1u << (RLOG2 - 7)];
+    __shared__ SetsApplyTabs s_tabs;
+    __shared__ uint32_t s_lows[STAGE + 1];   // every Elias-Fano source's low-bit words, back to back
+    sets_apply_region<RLOG2, LANES, STAGE>(apply_region(blockIdx.x, gridDim.x, xg), bits, nwords, sets, stride_words,
+                                           nsrc, nbins, dense, any_flag, dirty, store_fresh, status, s_mask4, s_lows,
+                                           s_tabs);
+}
+
+// One step's two region passes in one launch (bf_insert_encode_region_sets_dev): region r's
+// sets from every source ORed into the bitset (sets_apply_region), then, in the same LDS, region
+// r's set of the NEXT batch encoded (sets_encode_region).  The two passes wait on different
+// things — the apply on the bitset stream, the encode on LDS atomics and its VALU walk — and
+// the two workgroups of a CU are at different points of their regions, so each hides the
+// other's stalls; as two kernels on two streams they take turns on whole CUs instead (DESIGN
+// §6b).  79.5 KiB of LDS at 2^19-bit regions: two workgroups per CU.
+template <uint32_t RLOG2, uint32_t LANES, uint32_t STAGE, int LOADS>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES / 256)))
+void sets_apply_encode_kernel(uint32_t* __restrict__ bits, uint64_t nwords, const uint32_t* __restrict__ sets,
+                              uint64_t stride_words, uint32_t nsrc, uint32_t nbins, uint32_t dense,
+                              uint32_t* __restrict__ any_flag, uint8_t* __restrict__ dirty, uint32_t store_fresh,
+                              uint32_t* __restrict__ status, uint32_t xg, const uint32_t* __restrict__ level2,
+                              const uint32_t* __restrict__ cb_base, const uint32_t* __restrict__ cb_start,
+                              const uint16_t* __restrict__ tabs, uint64_t max_chunks, uint32_t nq, uint32_t rel_log2,
+                              uint32_t* __restrict__ out, const uint32_t* __restrict__ sb_first, uint32_t cap_words) {
+    constexpr uint32_t kRun = sets_encode_run_lds<RLOG2>();
+    __shared__ uint4 s_mask4[1u << (RLOG2 - 7)];
+    __shared__ SetsApplyTabs s_tabs;
+    __shared__ uint32_t s_lows[(STAGE + 1) > kRun ? STAGE + 1 : kRun];
+    const uint32_t r = apply_region(blockIdx.x, gridDim.x, xg);
+    sets_apply_region<RLOG2, LANES, STAGE>(r, bits, nwords, sets, stride_words, nsrc, nbins, dense, any_flag, dirty,
+                                           store_fresh, status, s_mask4, s_lows, s_tabs);
+    __syncthreads();   // the image and the stage are reused by the encode
+    sets_encode_region<RLOG2, LANES, LOADS>(r, nbins, level2, cb_base, cb_start, tabs, max_chunks, nq, rel_log2, out,
+                                            sb_first, cap_words, 0u, s_mask4, s_lows, s_tabs.w);
 }
 
 #ifdef BFHIP_AB_KNOBS
@@ -3940,5 +4013,51 @@ hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_
 #undef BF_SETS_APPLY
     }
     bf_mark(mk, s, "sets_apply");
+    return hipGetLastError();
+}
+
+hipError_t bf_launch_insert_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                        uint32_t region_log2, uint32_t nbins, const uint32_t* sets,
+                                        uint64_t stride_words, uint32_t nsrc, uint64_t probes_hint, uint32_t* any_flag,
+                                        uint32_t* status, const uint8_t* next_dig, uint64_t n_next, void* scratch,
+                                        uint32_t* next_out, uint64_t cap_words, hipStream_t s, BfMarks* mk) {
+    if (cap_words >= (1ull << 32)) return hipErrorInvalidValue;
+    bool fuse = n_next && nsrc && nsrc <= kMaxSetSrc && !p.with_keys && p.region_log2 == region_log2 &&
+                p.nbins == nbins && (region_log2 == 19 || region_log2 == 18);
+#ifdef BFHIP_AB_KNOBS
+    if (const char* v = BF_AB_GETENV("BFHIP_SETS_FUSE")) fuse = fuse && atoi(v) != 0;   // (A/B: 0 = two kernels)
+#endif
+    if (!fuse) {   // the next batch's encode (no bitset read), then the apply: the two calls in order
+        hipError_t e = bf_launch_encode_sets(g, p, bitset_bytes, next_dig, nullptr, 0, n_next, true, scratch, next_out,
+                                             cap_words, s, mk);
+        if (e != hipSuccess) return e;
+        return bf_launch_insert_sets(g, bitset_bytes, region_log2, nbins, sets, stride_words, nsrc, probes_hint, any_flag,
+                                     status, s, mk);
+    }
+    const Carve c = carve(p, scratch);
+    hipError_t e = launch_partition(g, p, c, next_dig, nullptr, 0, n_next, nullptr, s, mk, true);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sets_size_kernel, dim3(p.nsup), dim3(1024), 0, s, c.tabs, c.cb_base, p.max_chunks, p.ngroups,
+                       p.rel_log2, p.nbins, 1u << p.region_log2, next_out, c.stot);
+    hipLaunchKernelGGL(sets_place_kernel, dim3(1), dim3(1024), 0, s, next_out, c.stot, p.nsup, p.region_log2, p.nbins);
+    const int loads = n_next * g.k <= (uint64_t)p.nbins * 4096u ? 2 : 8;   // as bf_launch_encode_sets
+    const uint64_t nwords = bitset_bytes / 4;
+    const uint64_t vecs = (uint64_t)nbins << (region_log2 - 7);
+    const uint32_t dense = probes_hint >= vecs ? 2u : (probes_hint >= vecs / 8 ? 1u : 0u);
+    const uint32_t xg = 2u;   // as bf_launch_insert_sets
+#define BF_SETS_APPLY_ENCODE(RL, LN, ST, LD)                                                                     \
+    hipLaunchKernelGGL((sets_apply_encode_kernel<RL, LN, ST, LD>), dim3(nbins), dim3(LN), 0, s, g.bits, nwords, sets, \
+                       stride_words, nsrc, nbins, dense, any_flag, g.dirty, apply_store_fresh(), status, xg, c.level2,  \
+                       c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, next_out, c.stot,           \
+                       (uint32_t)cap_words)
+    if (region_log2 == 19) {
+        if (loads == 8) BF_SETS_APPLY_ENCODE(19, kApplyLanes, kLowsStage, 8);
+        else BF_SETS_APPLY_ENCODE(19, kApplyLanes, kLowsStage, 2);
+    } else {
+        if (loads == 8) BF_SETS_APPLY_ENCODE(18, kApplyLanes / 2, kLowsStage / 2, 8);
+        else BF_SETS_APPLY_ENCODE(18, kApplyLanes / 2, kLowsStage / 2, 2);
+    }
+#undef BF_SETS_APPLY_ENCODE
+    bf_mark(mk, s, "sets_apply_encode");
     return hipGetLastError();
 }

@@ -236,6 +236,15 @@ uint64_t bf_sets_header_words(uint32_t nbins);
 hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,
                                  const uint64_t* offsets, uint64_t bias, uint64_t n, bool dig, void* scratch,
                                  uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* marks = nullptr);
+// One step of a replicated filter: nsrc set buffers ORed in (as bf_launch_insert_sets) and the
+// next batch (n_next SHA-1 word quadruples, plan p) encoded into next_out (as
+// bf_launch_encode_sets with dig), the two region passes in one kernel when they share the
+// region geometry and one launch takes every source.
+hipError_t bf_launch_insert_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes,
+                                        uint32_t region_log2, uint32_t nbins, const uint32_t* sets,
+                                        uint64_t stride_words, uint32_t nsrc, uint64_t probes_hint, uint32_t* any_flag,
+                                        uint32_t* status, const uint8_t* next_dig, uint64_t n_next, void* scratch,
+                                        uint32_t* next_out, uint64_t cap_words, hipStream_t s, BfMarks* marks = nullptr);
 hipError_t bf_launch_insert_sets(const BfGeom& g, uint64_t bitset_bytes, uint32_t region_log2, uint32_t nbins,
                                  const uint32_t* sets, uint64_t stride_words, uint32_t nsrc, uint64_t probes_hint,
                                  uint32_t* any_flag, uint32_t* status, hipStream_t s, BfMarks* marks = nullptr);

@@ -181,6 +181,57 @@ def test_insert_sets_into_prefilled_filter_and_include(pkg, oracle, m, k):
         np.testing.assert_array_equal(got_inc.astype(bool), want)
 
 
+@pytest.mark.parametrize("m,k,n", [(9585058377, 6, 100_000), (191701167547, 13, 60_000), (9585058, 6, 30_000)])
+def test_insert_encode_equals_the_two_calls(pkg, oracle, m, k, n):
+    """bf_insert_encode_region_sets_dev (the apply of one step's sets and the encode of the next
+    batch in one kernel) against the two calls: the same bitset (checked against the oracle too),
+    the same any_new and status, and a next-batch buffer whose sets decode to the oracle's
+    offsets (tests/sets_codec.py) exactly as the separate encode's."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(SEED + 31 * k)
+    batches = [_keys(pkg, rng, n, "p%d" % s) for s in range(3)]
+    nb, no = _keys(pkg, rng, n, "next")
+    with pkg.Filter(m, k) as fa, pkg.Filter(m, k) as fb:
+        cap = fa.region_sets_capacity(n)
+        sets = torch.cat([_encode(torch, fa, b, o, cap=cap) for b, o in batches])
+        kb, ko = _dev(torch, nb, no)
+        dig = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        fa.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, dig.data_ptr(), stream=0)
+        probes = 3 * n * k
+        flags = torch.zeros(2, dtype=torch.int32, device="cuda")
+        status = torch.zeros(2, dtype=torch.int32, device="cuda")
+        nxt_a = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+        nxt_b = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+        fa.encode_region_sets_digests_dev(dig.data_ptr(), n, nxt_a.data_ptr(), cap, stream=0)
+        fa.insert_region_sets_dev(sets.data_ptr(), cap, 3, probes, d_any_new=flags[0:].data_ptr(),
+                                  d_status=status[0:].data_ptr(), stream=0)
+        fb.insert_encode_region_sets_dev(sets.data_ptr(), cap, 3, probes, dig.data_ptr(), n, nxt_b.data_ptr(), cap,
+                                         d_any_new=flags[1:].data_ptr(), d_status=status[1:].data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert flags.tolist() == [1, 1] and status.tolist() == [0, 0]
+        pa, va = _nonzero_bytes(torch, fa)
+        pb, vb = _nonzero_bytes(torch, fb)
+        np.testing.assert_array_equal(pa, pb)
+        np.testing.assert_array_equal(va, vb)
+        idx = np.concatenate([oracle.indexes_many(b, o, m, k).reshape(-1) for b, o in batches])
+        want_p, want_v = _want_sparse(idx)
+        np.testing.assert_array_equal(pb, want_p)
+        np.testing.assert_array_equal(vb, want_v)
+        words = int(nxt_a[3].item())
+        assert words == int(nxt_b[3].item())
+        np.testing.assert_array_equal(nxt_a[:words].cpu().numpy(), nxt_b[:words].cpu().numpy())
+        # and that buffer inserts the next batch: both filters take it and stay equal to the oracle
+        fb.insert_region_sets_dev(nxt_b.data_ptr(), cap, 1, n * k, stream=0)
+        pb2, vb2 = _nonzero_bytes(torch, fb)
+        want_p2, want_v2 = _want_sparse(np.concatenate([idx, oracle.indexes_many(nb, no, m, k).reshape(-1)]))
+        np.testing.assert_array_equal(pb2, want_p2)
+        np.testing.assert_array_equal(vb2, want_v2)
+        # the next buffer may not overlap the buffers it is applied with
+        with pytest.raises(pkg.ArgumentError, match="overlaps"):
+            fb.insert_encode_region_sets_dev(sets.data_ptr(), cap, 3, probes, dig.data_ptr(), n,
+                                             sets[cap // 4:].data_ptr(), cap, stream=0)
+
+
 def test_foreign_set_buffer_is_skipped(pkg):
     """A buffer encoded for another filter size does not match this filter's regions: it is
     skipped (no bit set) and d_status flags it; the ABI refuses a short capacity."""

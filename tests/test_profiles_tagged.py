@@ -33,7 +33,8 @@ def test_nstar_counters_share_one_tag():
 
 def test_every_workload_has_final_tree_counters():
     import bench
-    want = {"nstar", "1m", "1m_big", "100m", "10b", "lua_1m"}
+    want = {"nstar", "1m", "1m_big", "100m", "10b", "200b", "lua_1m",
+            "model_P8_nstar", "model_P8_200b", "model_repl8_10b"}   # every secondary and per-rank model
     assert want <= set(bench.PMC_FILES)
     tags = {_tag(f) for f in bench.PMC_FILES.values()}
     assert tags == {bench.PMC_TAG}, tags

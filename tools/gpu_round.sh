@@ -13,8 +13,10 @@
 #   bench10b / bench200b / bench100m   the other single-GPU configs
 #   prof       kernel trace (rocprofv3 --kernel-trace --stats) of a short bench run
 #   pmc        the PMC passes of tools/pmc_passes.sh on the north-star bench
-#   pmcsec     the same passes for every secondary workload (PMC_WORKLOADS, default 1m 1m_big 100m
-#              10b lua_1m); then
+#   pmcstall   the stall / LDS pass of the per-rank models (PMC_WORKLOADS)
+#   pmcsum     the PMC summaries made on the box (gpurun_out/pmcsum/), raw counter files deleted
+#   pmcsec     the same passes for every secondary workload and per-rank model (PMC_WORKLOADS,
+#              default 1m 1m_big 100m 10b 200b lua_1m model_P8_nstar model_P8_200b model_repl8_10b); then
 #              python tools/pmc_finalize.py <tag> on the CPU host writes profiles/pmc_<tag>_*.json
 #   simP8      the P = 8 per-rank step (tools/sim_rank.py): time + stall/LDS + VALU counters
 #   simP8t     the P = 8 per-rank step, time only (SIMCFG=200b: BASELINE configs[4]'s filter)
@@ -75,11 +77,11 @@ for st in $STEPS; do
         seq)    timeout -k 10 500 $PYT tests/test_gpu_lua.py tests/test_gpu_parity.py tests/test_gpu_per_key.py \
                     tests/test_gpu_dirty_sync.py tests/test_gpu_engines.py tests/test_gpu_multi.py \
                     tests/test_gpu_reference_shapes.py > gpurun_out/tests_${TAG}_seq.log 2>&1 ;;
-        benchlua) timeout -k 10 200 python bench.py --config 10k --secondary lua_1m --steps 5 --warmup 2 \
+        benchlua) timeout -k 10 200 python bench.py --config 10k --secondary lua_1m --models none --steps 5 --warmup 2 \
                     --no-cpu-baseline --no-host-api --no-reference-shapes \
                     > gpurun_out/bench_lua_${TAG}.json 2> gpurun_out/bench_lua_${TAG}.err ;;
         smoke)  timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1 ;;
-        bench)  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
+        bench)  timeout -k 10 700 python bench.py --gpus 1 --steps 20 --warmup 5 \
                     > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err ;;
         bench10b|bench200b|bench100m)
                 timeout -k 10 300 python bench.py --config ${st#bench} --steps 20 --warmup 5 $NOEXTRA \
@@ -88,8 +90,14 @@ for st in $STEPS; do
                     python bench.py --steps 5 --warmup 2 $NOEXTRA \
                     > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/bench_prof_${TAG}.err ;;
         pmc)    bash tools/pmc_passes.sh nstar ${TAG}_nstar ;;
-        pmcsec) for w in ${PMC_WORKLOADS:-1m 1m_big 100m 10b lua_1m}; do
+        pmcsec) for w in ${PMC_WORKLOADS:-1m 1m_big 100m 10b 200b lua_1m model_P8_nstar model_P8_200b model_repl8_10b}; do
                     bash tools/pmc_passes.sh $w ${TAG}_$w || exit 1
+                done ;;
+        pmcsum) python tools/pmc_finalize.py ${TAG} --box > gpurun_out/pmcsum_${TAG}.log 2>&1 ;;   # (on the box:
+                # summaries to gpurun_out/pmcsum/, raw CSVs deleted so the call's output comes back)
+        pmcstall)   # the stall / LDS pass of the per-rank models (VERDICT r05 item 1's counters)
+                for w in ${PMC_WORKLOADS:-model_P8_200b model_P8_nstar model_repl8_10b}; do
+                    bash tools/pmc_passes.sh $w ${TAG}_$w stall || exit 1
                 done ;;
         simP8t) timeout -k 10 180 python tools/sim_rank.py --config $SIMCFG --shards 8 --chunks --steps 5 \
                     > gpurun_out/sim_P8${SIMSFX}_${TAG}.json 2> gpurun_out/sim_P8${SIMSFX}_${TAG}.err ;;

@@ -15,6 +15,7 @@ bench.PMC_FILES must then name the same tag (tests/test_profiles_tagged.py check
 import glob
 import json
 import os
+import shutil
 import subprocess
 import sys
 
@@ -27,16 +28,26 @@ BATCH = {"nstar": 1 << 24, "1m": 1 << 20, "1m_big": 1 << 24, "100m": 1 << 24, "1
 
 def main():
     tag = sys.argv[1]
+    # --box: run on the GPU box itself (tools/gpu_round.sh pmcsum): the summaries go to
+    # gpurun_out/pmcsum/ and the raw counter CSVs are deleted, since a call's gpurun_out/ comes
+    # back only below 64 MiB (the per-rank models' passes hold every torch kernel's rows too)
+    box = "--box" in sys.argv[2:]
+    outdir = os.path.join(ROOT, "gpurun_out", "pmcsum") if box else os.path.join(ROOT, "profiles")
+    os.makedirs(outdir, exist_ok=True)
     for wl, batch in BATCH.items():
         # exactly this workload's passes ("1m_*" would also take "1m_big_*")
         dirs = [os.path.join(ROOT, "gpurun_out", "pmc_%s_%s_%s" % (tag, wl, p)) for p in PASSES]
         dirs = [d for d in dirs if os.path.isdir(d)]
         if not dirs:
             continue
-        out = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (tag, wl))
+        out = os.path.join(outdir, "pmc_%s_%s.json" % (tag, wl))
         subprocess.check_call([sys.executable, os.path.join(HERE, "pmc_summary.py"), *dirs, "--workload", wl,
                                "--batch", str(batch), "--json", out], stdout=subprocess.DEVNULL)
         print("wrote", os.path.relpath(out, ROOT))
+        if box:
+            for d in dirs:
+                shutil.rmtree(d)
+            continue
         if wl == "nstar":
             rec = json.load(open(out))["nstar"]
             k = rec.get("bf_include_hash_kernel") or {}
@@ -47,7 +58,7 @@ def main():
                 fh.write("\n")
             print("wrote profiles/pmc_traffic.json")
     stats = os.path.join(ROOT, "profiles", "%s_kernel_stats.csv" % tag)
-    if os.path.exists(stats):
+    if not box and os.path.exists(stats):
         txt = subprocess.check_output([sys.executable, os.path.join(HERE, "rocprof_means.py"),
                                        os.path.relpath(stats, ROOT), "--workload", "nstar"], cwd=ROOT, text=True)
         with open(os.path.join(ROOT, "profiles", "rocprof_means.json"), "w") as fh:

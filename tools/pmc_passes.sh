@@ -13,7 +13,7 @@ if [ $# -gt 2 ]; then shift 2; PASSES="$*"; else PASSES="rd wr dram valu"; fi
 # argv as bench.MODEL_LEGS with fewer steps)
 PROG="bench.py"
 case "$CONFIG" in
-    lua_1m) BENCH_ARGS="--config 10k --secondary lua_1m --steps 3 --warmup 1 --no-cpu-baseline --no-host-api --no-reference-shapes" ;;
+    lua_1m) BENCH_ARGS="--config 10k --secondary lua_1m --models none --steps 3 --warmup 1 --no-cpu-baseline --no-host-api --no-reference-shapes" ;;
     model_P8_nstar) PROG="tools/sim_rank.py"; BENCH_ARGS="--shards 8 --chunks --config nstar --steps 2" ;;
     model_P8_200b) PROG="tools/sim_rank.py"; BENCH_ARGS="--shards 8 --chunks --config 200b --steps 2" ;;
     model_repl8_10b) PROG="tools/sim_rank.py"; BENCH_ARGS="--replicated 8 --config 10b --gathered sets --fused-hash --overlap-encode apply --steps 2" ;;

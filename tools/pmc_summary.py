@@ -35,8 +35,22 @@ KERNELS = {
     "bin_test": re.compile(r"bin_test_kernel"),
     # the Lua layout (bf_lua.hip, bench.py lua_config)
     "lua_check": re.compile(r"lua_check_kernel"),
-    "lua_seq_candidates": re.compile(r"seq_candidates_kernel"),
-    "lua_seq_mark": re.compile(r"seq_mark_kernel"),
+    "lua_seq_candidates": re.compile(r"seq_candidates_kernel|seq_bin_count_kernel|seq_bin_place_kernel"),
+    "lua_seq_mark": re.compile(r"seq_mark_kernel|seq_region_kernel"),
+    # the per-rank models (tools/sim_rank.py: bench.py's multi_gpu_models legs), named as their
+    # bf_profile marks
+    "route_chunks_dig": re.compile(r"route_chunks_idx_kernel<false|route_front32_kernel<false, true, true, true>"),
+    "route_chunks_slot_dig": re.compile(r"route_chunks_idx_kernel<true|route_front32_kernel<true, true, true, true>"),
+    "chunk_group": re.compile(r"chunk_group_sum_kernel"),
+    "mid_chunks": re.compile(r"bin_mid_chunks_kernel<false>"),
+    "mid_chunks_keys": re.compile(r"bin_mid_chunks_kernel<true>"),
+    "apply_test": re.compile(r"bin_apply_test_kernel"),
+    "unsort_packed": re.compile(r"chunk_unsort_kernel"),
+    "test_l2": re.compile(r"chunk_test_l2_kernel"),
+    "pack_answers": re.compile(r"pack_segments_kernel"),
+    "combine_chunks": re.compile(r"combine_chunks_packed_kernel"),
+    "sets_encode": re.compile(r"sets_encode_kernel"),
+    "sets_apply": re.compile(r"sets_apply_kernel"),
 }
 FULL_BATCH = ("bf_keys_kernel", "digest_kernel")   # grid = one lane per key: keep full-batch launches only
 

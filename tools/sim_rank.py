@@ -70,6 +70,9 @@ def run(argv) -> dict:
     ap.add_argument("--main-priority", action="store_true",
                     help="--overlap-encode: the main step on a high-priority stream, the side encode at normal "
                          "priority")
+    ap.add_argument("--fused-encode", action="store_true",
+                    help="--replicated --gathered sets --fused-hash: this step's sets applied and the next batch's "
+                         "own set encoded by one kernel (bf_insert_encode_region_sets_dev)")
     ap.add_argument("--side-priority", action="store_true",
                     help="--overlap-encode: the side encode on a high-priority stream")
     ap.add_argument("--dig", action="store_true",
@@ -385,7 +388,33 @@ def replicated(args, pkg):
         f.include_many_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), stream=sp)
 
     ovl = args.overlap_encode
-    if ovl:
+    if args.fused_encode:
+        assert args.gathered == "sets" and args.fused_hash and not ovl
+        # one kernel per step for this step's sets (apply) and the next batch's own set (encode,
+        # bf_insert_encode_region_sets_dev); the include? hashes the batch after next
+        owns = [own, torch.empty_like(own)]
+
+        def step_fe(j):
+            s_, n1, n2 = steps[j % len(steps)], steps[(j + 1) % len(steps)], steps[(j + 2) % len(steps)]
+            _, _, (qkb, qko), dg = s_
+            f.insert_encode_region_sets_dev(dg.data_ptr(), cap_sets, R, R * batch * k, owns[(j + 1) % 2].data_ptr(),
+                                            batch, n1[3].data_ptr(), cap_sets, d_any_new=flag.data_ptr(), stream=sp)
+            f.include_hash_dev(qkb.data_ptr(), qko.data_ptr(), batch, out.data_ptr(), n2[0].data_ptr(),
+                               n2[1].data_ptr(), batch, owns[j % 2].data_ptr(), stream=sp)
+
+        # the pipeline's fill: batch 0's words and set, batch 1's words
+        f.hash_many_dev(steps[0][0].data_ptr(), steps[0][1].data_ptr(), batch, owns[0].data_ptr(), stream=sp)
+        f.encode_region_sets_digests_dev(owns[0].data_ptr(), batch, steps[0][3].data_ptr(), cap_sets, stream=sp)
+        f.hash_many_dev(steps[1][0].data_ptr(), steps[1][1].data_ptr(), batch, owns[1].data_ptr(), stream=sp)
+        step_fe(0)
+        torch.cuda.synchronize()
+        f.profile(True)
+        f.profile_read(reset=True)
+        t0 = time.perf_counter()
+        for j in range(1, args.steps + 1):
+            step_fe(j)
+        torch.cuda.synchronize()
+    elif ovl:
         assert args.gathered == "sets" and args.fused_hash
         # the encoder: a bitset-less handle (BF_FLAG_ENCODER) with its own scratch, so its calls are
         # not ordered behind the main handle's (ReplicatedFilter's side_encode)
@@ -461,6 +490,7 @@ def replicated(args, pkg):
     res = {"config": args.config, "layout": "replicated", "world": R, "gathered": args.gathered,
            "fused_hash": bool(args.fused_hash), "overlap_encode": ovl or None,
            "main_priority": bool(ovl and args.main_priority), "side_priority": bool(ovl and args.side_priority),
+           "fused_encode": bool(args.fused_encode),
            "m": m, "k": k,
            "batch": batch, "merged_insert_keys": nm, "bitset_bytes": f.device_bytes,
            "gathered_bytes_per_rank": (cap_sets if args.gathered == "sets" else
