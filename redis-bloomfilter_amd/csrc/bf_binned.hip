@@ -1909,7 +1909,8 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
                            const uint32_t* __restrict__ base, const uint32_t* __restrict__ cb_base,
                            uint64_t max_chunks, uint16_t* __restrict__ tabs, uint32_t* __restrict__ level2,
-                           uint32_t* __restrict__ level2_key, uint8_t* __restrict__ out8) {
+                           uint32_t* __restrict__ level2_key, uint8_t* __restrict__ out8,
+                           const uint2* __restrict__ runs) {
     __shared__ uint32_t s_pre[kRunsPerPass], s_gst[kRunsPerPass];
     __shared__ uint32_t s_cnt[1u << kMaxRel];
     __shared__ uint32_t s_w[16];
@@ -1937,15 +1938,24 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
     const uint32_t h = sb / ci.S, lsb = sb - h * ci.S;
     const uint64_t hoff = (uint64_t)h << 32;
     const uint32_t smask = (1u << ci.sup_log2) - 1u;
-    // run table of the group's chunks
+    // run table of the group's chunks: chunk_group_sum_kernel's (one coalesced load), or built
+    // here from the directories (dependent reads: rank table, start, run table)
     const uint64_t nch = (uint64_t)ci.nsrc * chunks_per_src(ci), c0 = (uint64_t)q * kRunsPerPass;
     const uint32_t nt = (uint32_t)(nch - c0 < kRunsPerPass ? nch - c0 : kRunsPerPass);
-    uint32_t len = 0, st = 0;
-    if (t < nt) chunk_run(ci, h, lsb, c0 + t, &len, &st);
-    const uint32_t ex = block_excl_scan(len, s_w, nullptr);
-    if (t < nt) {
-        s_pre[t] = ex;
-        s_gst[t] = st;
+    if (runs) {
+        if (t < nt) {
+            const uint2 r = runs[(uint64_t)w * kRunsPerPass + t];
+            s_pre[t] = r.x;
+            s_gst[t] = r.y;
+        }
+    } else {
+        uint32_t len = 0, st = 0;
+        if (t < nt) chunk_run(ci, h, lsb, c0 + t, &len, &st);
+        const uint32_t ex = block_excl_scan(len, s_w, nullptr);
+        if (t < nt) {
+            s_pre[t] = ex;
+            s_gst[t] = st;
+        }
     }
     __syncthreads();
     auto load = [&](uint32_t f0, uint32_t* lv, uint32_t* kv) {
@@ -2229,6 +2239,8 @@ Carve carve(const BfBinPlan& p, void* at0) {
         c.bytes = off;
         return c;
     }
+    if (p.chunked)   // the window run tables chunk_group_sum_kernel writes for bin_mid_chunks_kernel
+        c.runs = reinterpret_cast<uint2*>(take(N * kRunsPerPass * sizeof(uint2)));
     c.tabs = reinterpret_cast<uint16_t*>(take(p.max_chunks * ((1ull << p.rel_log2) + 1) * 2));   // [region][block]
     if (p.ordered) c.ans2 = take(p.probes + 16);   // the unsort reads whole 4-byte quads
     c.bytes = off;
@@ -2826,18 +2838,24 @@ bool bf_chunk_plan(uint64_t bitset_bytes, const BfChunks& cg, uint32_t nh, uint3
 namespace {
 hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn& ci, uint8_t* out8, hipStream_t s,
                             BfMarks* mk) {
+    // the group sums also write each window's run table, which the mid's workgroups then read
+    // in one coalesced load instead of walking the directories themselves
+    uint2* runs = c.runs;
+#ifdef BFHIP_AB_KNOBS
+    if (const char* v = BF_AB_GETENV("BFHIP_MID_RUNS")) runs = atoi(v) ? runs : nullptr;   // (A/B)
+#endif
     hipLaunchKernelGGL(chunk_group_sum_kernel, dim3(p.nsup, p.ngroups), dim3(kRunsPerPass), 0, s, ci, p.ngroups,
-                       c.gsum, (uint2*)nullptr, 0u, (uint16_t*)nullptr);
+                       c.gsum, runs, 0u, (uint16_t*)nullptr);
     launch_scan(p, c, s);
     bf_mark(mk, s, "chunk_group");
     if (p.with_keys)
         hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
                            p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
-                           c.level2_key, out8);
+                           c.level2_key, out8, runs);
     else
         hipLaunchKernelGGL(bin_mid_chunks_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
                            p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
-                           c.level2_key, out8);
+                           c.level2_key, out8, runs);
     bf_mark(mk, s, p.with_keys ? "mid_chunks_keys" : "mid_chunks");
     return hipGetLastError();
 }
