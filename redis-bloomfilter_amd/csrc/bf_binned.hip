@@ -1904,7 +1904,10 @@ __global__ __launch_bounds__(kL2Lanes) void chunk_test_l2_kernel(BfChunkIn ci, c
 // The received entries are window-local offsets: an entry outside its superbin or past the
 // shard is dropped (KEYS: answered 0), so peer data never addresses outside the bitset.  KEYS:
 // each probe's position is its index in the receive buffer (no level-1 key array).
-template <bool KEYS>
+// CONTIG: lane t takes entries t * kChunkPerLane .. + kChunkPerLane - 1 of a block (its run walk
+// rarely steps: runs average ~26 entries at 200B x 8), instead of entries 64 apart (a wave's
+// loads 64 consecutive entries, and each lane's walk crosses ~2.5 runs per load).
+template <bool KEYS, bool CONTIG = false>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8)))
 void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t region_log2, uint32_t rel_log2,
                            const uint32_t* __restrict__ base, const uint32_t* __restrict__ cb_base,
@@ -1959,11 +1962,11 @@ void bin_mid_chunks_kernel(BfChunkIn ci, uint32_t nsup, uint32_t nq, uint32_t re
     }
     __syncthreads();
     auto load = [&](uint32_t f0, uint32_t* lv, uint32_t* kv) {
-        const uint32_t fw = f0 + (t >> 6) * (64u * kChunkPerLane);
+        const uint32_t fw = CONTIG ? f0 + t * (uint32_t)kChunkPerLane : f0 + (t >> 6) * (64u * kChunkPerLane);
         uint32_t i = run_of(s_pre, nt, fw < E ? fw : E - 1);
 #pragma unroll
         for (int u = 0; u < kChunkPerLane; ++u) {
-            const uint32_t f = fw + u * 64 + (t & 63u);
+            const uint32_t f = CONTIG ? fw + u : fw + u * 64 + (t & 63u);
             lv[u] = 0xFFFFFFFFu;
             kv[u] = 0;
             if (f < E) {
@@ -2848,14 +2851,26 @@ hipError_t launch_chunk_mid(const BfBinPlan& p, const Carve& c, const BfChunkIn&
                        c.gsum, runs, 0u, (uint16_t*)nullptr);
     launch_scan(p, c, s);
     bf_mark(mk, s, "chunk_group");
-    if (p.with_keys)
-        hipLaunchKernelGGL(bin_mid_chunks_kernel<true>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
-                           p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
-                           c.level2_key, out8, runs);
-    else
-        hipLaunchKernelGGL(bin_mid_chunks_kernel<false>, dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,
-                           p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2,
-                           c.level2_key, out8, runs);
+#define BF_MID_CHUNKS(K, C)                                                                                     \
+    hipLaunchKernelGGL((bin_mid_chunks_kernel<K, C>), dim3(p.nsup * p.ngroups * kMidParts), dim3(kTile), 0, s, ci,   \
+                       p.nsup, p.ngroups, p.region_log2, p.rel_log2, c.base, c.cb_base, p.max_chunks, c.tabs, c.level2, \
+                       c.level2_key, out8, runs)
+    // lane-contiguous entries where the shard spans several 2^32-bit sub-ranges: 200B x 8, mids
+    // 1.00 / 1.19 -> 0.93 / 1.12 ms; the north star x 8 (one sub-range) keeps the strided form,
+    // 0.371 vs 0.393 ms (profiles/r06t_ab_mid_contig.jsonl)
+    bool contig = ci.nh > 1;
+#ifdef BFHIP_AB_KNOBS
+    if (const char* e = BF_AB_GETENV("BFHIP_MID_CONTIG")) contig = e[0] == '1';   // (A/B)
+#endif
+    if (contig) {
+        if (p.with_keys) BF_MID_CHUNKS(true, true);
+        else BF_MID_CHUNKS(false, true);
+    } else if (p.with_keys) {
+        BF_MID_CHUNKS(true, false);
+    } else {
+        BF_MID_CHUNKS(false, false);
+    }
+#undef BF_MID_CHUNKS
     bf_mark(mk, s, p.with_keys ? "mid_chunks_keys" : "mid_chunks");
     return hipGetLastError();
 }
