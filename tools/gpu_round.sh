@@ -65,7 +65,7 @@ ab_cmd() {   # one A/B line's command, stdout = its JSON
 
 for st in $STEPS; do
     case $st in
-        tests)  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        tests)  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
                     ${PYTEST_EXTRA:-} > gpurun_out/tests_${TAG}.log 2>&1 ;;
         parity) timeout -k 10 560 $PYT tests/test_gpu_parity.py tests/test_gpu_distributed.py tests/test_gpu_digests.py \
                     tests/test_gpu_region_sets.py > gpurun_out/tests_${TAG}_parity.log 2>&1 ;;
