@@ -42,8 +42,8 @@ KERNELS = {
     "route_chunks_dig": re.compile(r"route_chunks_idx_kernel<false|route_front32_kernel<false, true, true, true>"),
     "route_chunks_slot_dig": re.compile(r"route_chunks_idx_kernel<true|route_front32_kernel<true, true, true, true>"),
     "chunk_group": re.compile(r"chunk_group_sum_kernel"),
-    "mid_chunks": re.compile(r"bin_mid_chunks_kernel<false>"),
-    "mid_chunks_keys": re.compile(r"bin_mid_chunks_kernel<true>"),
+    "mid_chunks": re.compile(r"bin_mid_chunks_kernel<false"),
+    "mid_chunks_keys": re.compile(r"bin_mid_chunks_kernel<true"),
     "apply_test": re.compile(r"bin_apply_test_kernel"),
     "unsort_packed": re.compile(r"chunk_unsort_kernel"),
     "test_l2": re.compile(r"chunk_test_l2_kernel"),
