@@ -232,6 +232,45 @@ def test_insert_encode_equals_the_two_calls(pkg, oracle, m, k, n):
                                              sets[cap // 4:].data_ptr(), cap, stream=0)
 
 
+@pytest.mark.parametrize("nsrc,n_next", [(17, 4000), (2, 0)])
+def test_insert_encode_other_shapes(pkg, oracle, nsrc, n_next):
+    """bf_insert_encode_region_sets_dev where the one-kernel form does not apply: 17 sources (more
+    than one apply launch takes: the two calls run instead) and an empty next batch (its buffer is
+    the header alone).  The bitset equals the oracle's, the next buffer inserts its batch."""
+    torch = pytest.importorskip("torch")
+    m, k = 9585058377, 6
+    rng = np.random.default_rng(SEED + 61 + nsrc)
+    batches = [_keys(pkg, rng, 3000, "q%d" % s) for s in range(nsrc)]
+    nb, no = _keys(pkg, rng, n_next, "nx")
+    with pkg.Filter(m, k) as f:
+        cap = f.region_sets_capacity(max(3000, n_next))
+        sets = torch.cat([_encode(torch, f, b, o, cap=cap) for b, o in batches])
+        dig = torch.zeros((max(n_next, 1), 4), dtype=torch.int32, device="cuda")
+        if n_next:
+            kb, ko = _dev(torch, nb, no)
+            f.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n_next, dig.data_ptr(), stream=0)
+        nxt = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        f.insert_encode_region_sets_dev(sets.data_ptr(), cap, nsrc, nsrc * 3000 * k, dig.data_ptr(), n_next,
+                                        nxt.data_ptr(), cap, d_status=status.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(status.item()) == 0
+        idx = np.concatenate([oracle.indexes_many(b, o, m, k).reshape(-1) for b, o in batches])
+        got_p, got_v = _nonzero_bytes(torch, f)
+        want_p, want_v = _want_sparse(idx)
+        np.testing.assert_array_equal(got_p, want_p)
+        np.testing.assert_array_equal(got_v, want_v)
+        f.insert_region_sets_dev(nxt.data_ptr(), cap, 1, max(n_next, 1) * k, d_status=status.data_ptr(), stream=0)
+        torch.cuda.synchronize()
+        assert int(status.item()) == 0
+        if n_next:
+            idx = np.concatenate([idx, oracle.indexes_many(nb, no, m, k).reshape(-1)])
+        got_p, got_v = _nonzero_bytes(torch, f)
+        want_p, want_v = _want_sparse(idx)
+        np.testing.assert_array_equal(got_p, want_p)
+        np.testing.assert_array_equal(got_v, want_v)
+
+
 def test_foreign_set_buffer_is_skipped(pkg):
     """A buffer encoded for another filter size does not match this filter's regions: it is
     skipped (no bit set) and d_status flags it; the ABI refuses a short capacity."""
