@@ -2206,8 +2206,17 @@ int encode_sets(bf_handle* h, const uint8_t* d_keys, const uint64_t* d_offsets, 
     uint64_t bias = 0;
     const uint8_t* k16 = (n && !dig) ? align_keys(d_keys, &bias) : d_keys;
     BfMarks* mk = n ? prof_begin(h, so.s) : nullptr;
+    // an encoder handle encodes beside another stream's apply: a persistent encode on 3/4 of the
+    // CUs (bf_binned.hip sets_encode_persistent_kernel)
+    uint32_t pgrid = 0;
+    if (!h->g.bits) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        pgrid = std::max<uint32_t>(1u, (uint32_t)cus * 3u / 4u);
+    }
     HIPCHK(h, bf_launch_encode_sets(h->g, plan, h->dev_bytes, k16, d_offsets, bias, n, dig, h->d_bin_scratch, d_sets,
-                                    std::min<uint64_t>(sets_bytes / 4, 0xFFFFFFFFull), so.s, mk));
+                                    std::min<uint64_t>(sets_bytes / 4, 0xFFFFFFFFull), so.s, mk, pgrid));
     return BF_OK;
 }
 }  // namespace

@@ -3395,6 +3395,27 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES
 // minus the offsets of the sources before it), then bin_apply's read-OR-write of the region.
 // A source whose header does not match (magic, region geometry, capacity) is skipped and
 // flagged in *status.
+// sets_encode_kernel as a persistent grid: workgroup b encodes regions b, b + G, ... (G =
+// gridDim.x).  An encoder handle's encode runs beside another stream's apply: with G = 3/4 of
+// the CUs it holds one of the two workgroup slots of those CUs for the whole encode, and the
+// apply keeps the rest, instead of the two kernels taking turns on whole CUs (the replicated
+// 10B x 8 replica step 9.78 / 9.83 -> 9.54 / 9.59 ms; G = 224 / 256 / 320: 9.64 / 9.70 / 9.77,
+// profiles/r06y_ab_sets_enc_grid.jsonl).
+template <uint32_t RLOG2, uint32_t LANES, int LOADS>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(2 * LANES / 256)))
+void sets_encode_persistent_kernel(const uint32_t* __restrict__ level2, const uint32_t* __restrict__ cb_base,
+                                   const uint32_t* __restrict__ cb_start, const uint16_t* __restrict__ tabs,
+                                   uint64_t max_chunks, uint32_t nq, uint32_t rel_log2, uint32_t* __restrict__ out,
+                                   const uint32_t* __restrict__ sb_first, uint32_t cap_words, uint32_t nbins) {
+    __shared__ uint4 s_m4[(1u << RLOG2) / 128];
+    __shared__ uint32_t s_runs[sets_encode_run_lds<RLOG2>()], s_w[16];
+    for (uint32_t r = blockIdx.x; r < nbins; r += gridDim.x) {
+        sets_encode_region<RLOG2, LANES, LOADS>(r, nbins, level2, cb_base, cb_start, tabs, max_chunks, nq, rel_log2,
+                                                out, sb_first, cap_words, 0u, s_m4, s_runs, s_w);
+        __syncthreads();   // every lane is past the region's LDS before the next one clears it
+    }
+}
+
 // sets_apply_kernel's LDS tables beside the region image and the low-bit stage
 struct SetsApplyTabs {
     uint32_t w[16];
@@ -3933,7 +3954,8 @@ uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2
 
 hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,
                                  const uint64_t* offsets, uint64_t bias, uint64_t n, bool dig, void* scratch,
-                                 uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* mk) {
+                                 uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* mk,
+                                 uint32_t persistent_grid) {
     (void)bitset_bytes;
     if (cap_words >= (1ull << 32)) return hipErrorInvalidValue;
     if (n == 0) {
@@ -3959,6 +3981,22 @@ hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t b
         return v == 8 || v == 4 || v == 2 || v == 1 ? v : 0;
     }();
     const int loads = forced ? forced : (n * g.k <= (uint64_t)p.nbins * 4096u ? 2 : 8);
+    uint32_t enc_grid = persistent_grid;
+#ifdef BFHIP_AB_KNOBS
+    if (const char* e = BF_AB_GETENV("BFHIP_SETS_ENC_GRID")) enc_grid = (uint32_t)std::strtoul(e, nullptr, 10);   // (A/B)
+#endif
+    if (enc_grid && p.region_log2 == 19) {
+        if (loads == 8)
+            hipLaunchKernelGGL((sets_encode_persistent_kernel<19, kApplyLanes, 8>), dim3(enc_grid), dim3(kApplyLanes),
+                               0, s, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out,
+                               c.stot, (uint32_t)cap_words, p.nbins);
+        else
+            hipLaunchKernelGGL((sets_encode_persistent_kernel<19, kApplyLanes, 2>), dim3(enc_grid), dim3(kApplyLanes),
+                               0, s, c.level2, c.cb_base, c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out,
+                               c.stot, (uint32_t)cap_words, p.nbins);
+        bf_mark(mk, s, "sets_encode");
+        return hipGetLastError();
+    }
 #define BF_SETS_ENCODE(RL, LN, LD)                                                                              \
     hipLaunchKernelGGL((sets_encode_kernel<RL, LN, LD>), dim3(p.nbins), dim3(LN), 0, s, c.level2, c.cb_base,    \
                        c.cb_start, c.tabs, p.max_chunks, p.ngroups, p.rel_log2, out, c.stot, (uint32_t)cap_words, \

@@ -233,9 +233,12 @@ bool bf_sets_geometry(uint64_t bitset_bytes, uint32_t pref_region_log2, uint32_t
 uint64_t bf_sets_capacity_bytes(uint64_t bitset_bytes, uint32_t pref_region_log2, uint64_t n, uint32_t k);
 // Words before a set buffer's first set: the header and the two per-region tables.
 uint64_t bf_sets_header_words(uint32_t nbins);
+// persistent_grid > 0: the encode pass as a persistent grid of that many workgroups (an encoder
+// handle's, beside another stream's apply; 2^19-bit regions), 0: one workgroup per region.
 hipError_t bf_launch_encode_sets(const BfGeom& g, const BfBinPlan& p, uint64_t bitset_bytes, const uint8_t* keys16,
                                  const uint64_t* offsets, uint64_t bias, uint64_t n, bool dig, void* scratch,
-                                 uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* marks = nullptr);
+                                 uint32_t* out, uint64_t cap_words, hipStream_t s, BfMarks* marks = nullptr,
+                                 uint32_t persistent_grid = 0);
 // One step of a replicated filter: nsrc set buffers ORed in (as bf_launch_insert_sets) and the
 // next batch (n_next SHA-1 word quadruples, plan p) encoded into next_out (as
 // bf_launch_encode_sets with dig), the two region passes in one kernel when they share the

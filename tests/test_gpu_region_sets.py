@@ -271,6 +271,29 @@ def test_insert_encode_other_shapes(pkg, oracle, nsrc, n_next):
         np.testing.assert_array_equal(got_v, want_v)
 
 
+@pytest.mark.parametrize("m,k,n", [(9585058377, 6, 200_000), (191701167547, 13, 100_000)])
+def test_encoder_handle_writes_the_same_sets(pkg, m, k, n):
+    """An encoder handle (BF_FLAG_ENCODER) encodes with a persistent grid on part of the CUs
+    (it runs beside another stream's apply); its buffer is word for word the filter handle's."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(SEED + 71 + k)
+    b, o = _keys(pkg, rng, n, "enc")
+    with pkg.Filter(m, k) as f, pkg.Filter(m, k, flags=pkg._lib.BF_FLAG_ENCODER) as enc:
+        cap = f.region_sets_capacity(n)
+        assert enc.region_sets_capacity(n) == cap
+        kb, ko = _dev(torch, b, o)
+        dig = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        f.hash_many_dev(kb.data_ptr(), ko.data_ptr(), n, dig.data_ptr(), stream=0)
+        sa = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+        sb = torch.zeros(cap // 4, dtype=torch.int32, device="cuda")
+        f.encode_region_sets_digests_dev(dig.data_ptr(), n, sa.data_ptr(), cap, stream=0)
+        enc.encode_region_sets_digests_dev(dig.data_ptr(), n, sb.data_ptr(), cap, stream=0)
+        torch.cuda.synchronize()
+        words = int(sa[3].item())
+        assert words == int(sb[3].item()) and words > 4
+        np.testing.assert_array_equal(sa[:words].cpu().numpy(), sb[:words].cpu().numpy())
+
+
 def test_foreign_set_buffer_is_skipped(pkg):
     """A buffer encoded for another filter size does not match this filter's regions: it is
     skipped (no bit set) and d_status flags it; the ABI refuses a short capacity."""

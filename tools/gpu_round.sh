@@ -30,7 +30,8 @@
 #              (interleaved, e.g. "old ab old ab"); lines appended to gpurun_out/ablib_<tag>.jsonl
 #   ab         an A/B over one environment variable: AB_VAR, AB_VALUES (interleaved, e.g.
 #              "1 0 1 0"), AB_CMD in {nstar, 10b, 200b, simP8, simP4, simP8_200b, repl10b, replnstar,
-#              repl10bf, replnstarf (the fused-hash region-set steps)}; lines appended to
+#              repl10bf, replnstarf (the fused-hash region-set steps), repl10bo (... with the next
+#              encode on a second stream)}; lines appended to
 #              gpurun_out/ab_${AB_VAR}_<tag>.jsonl.  The shipped library reads no A/B knob: the step
 #              loads AB_LIB (default ab_libs/ab/libbfhip.so, built on the box by
 #              `bash tools/build_ab_libs.sh ${AB_BUILD:-ab=-DBFHIP_AB_KNOBS}` when absent)
@@ -59,6 +60,8 @@ ab_cmd() {   # one A/B line's command, stdout = its JSON
                       --steps 3 2>>"$ABERR" ;;
         replnstarf) timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --fused-hash \
                       --steps 5 2>>"$ABERR" ;;
+        repl10bo) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash \
+                      --overlap-encode apply --steps 3 2>>"$ABERR" ;;
         *) echo "unknown AB_CMD $1" >&2; return 2 ;;
     esac
 }
