@@ -50,6 +50,7 @@ KERNELS = {
     "pack_answers": re.compile(r"pack_segments_kernel"),
     "combine_chunks": re.compile(r"combine_chunks_packed_kernel"),
     "sets_encode": re.compile(r"sets_encode_kernel"),
+    "sets_encode_persistent": re.compile(r"sets_encode_persistent_kernel"),   # (an encoder handle's)
     "sets_apply": re.compile(r"sets_apply_kernel"),
 }
 FULL_BATCH = ("bf_keys_kernel", "digest_kernel")   # grid = one lane per key: keep full-batch launches only
