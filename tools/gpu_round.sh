@@ -60,6 +60,8 @@ ab_cmd() {   # one A/B line's command, stdout = its JSON
                       --steps 3 2>>"$ABERR" ;;
         replnstarf) timeout -k 10 120 python tools/sim_rank.py --replicated 2 --config nstar --gathered sets --fused-hash \
                       --steps 5 2>>"$ABERR" ;;
+        simP8digside) timeout -k 10 120 python tools/sim_rank.py --shards 8 --chunks --steps 5 --dig --dig-side \
+                      --no-hash-split 2>>"$ABERR" ;;
         repl10bo) timeout -k 10 200 python tools/sim_rank.py --replicated 8 --config 10b --gathered sets --fused-hash \
                       --overlap-encode apply --steps 3 2>>"$ABERR" ;;
         *) echo "unknown AB_CMD $1" >&2; return 2 ;;
