@@ -872,7 +872,7 @@ def load_traffic(workload: str, kernel: str):
 
 # every workload's counters from the round's final tree, one tag (tools/pmc_finalize.py;
 # tests/test_profiles_tagged.py checks the tag across these, pmc_traffic.json and the rocprof means)
-PMC_TAG = "r06n"
+PMC_TAG = "r06ac"
 PMC_FILES = {w: "pmc_%s_%s.json" % (PMC_TAG, w) for w in ("nstar", "1m", "1m_big", "100m", "10b", "200b", "lua_1m",
                                                           "model_P8_nstar", "model_P8_200b", "model_repl8_10b")}
 # rocprofv3 --kernel-trace --stats of the bench command on the round's final tree

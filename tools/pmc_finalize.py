@@ -6,7 +6,8 @@ the passes' gpurun_out/ came back):
 
 * profiles/pmc_<tag>_<workload>.json for every workload whose PMC passes exist
   (gpurun_out/pmc_<tag>_<workload>_{rd,wr,dram,valu}/, tools/pmc_passes.sh), summarised by
-  tools/pmc_summary.py with the workload's batch;
+  tools/pmc_summary.py with the workload's batch, or copied from gpurun_out/pmcsum/ where the
+  box summarised them (tools/gpu_round.sh pmcsum);
 * profiles/pmc_traffic.json: the north-star include? kernel's HBM bytes per launch (the
   line's roofline.traffic), with its source;
 * profiles/rocprof_means.json from profiles/<tag>_kernel_stats.csv (tools/rocprof_means.py).
@@ -38,11 +39,15 @@ def main():
         # exactly this workload's passes ("1m_*" would also take "1m_big_*")
         dirs = [os.path.join(ROOT, "gpurun_out", "pmc_%s_%s_%s" % (tag, wl, p)) for p in PASSES]
         dirs = [d for d in dirs if os.path.isdir(d)]
-        if not dirs:
-            continue
         out = os.path.join(outdir, "pmc_%s_%s.json" % (tag, wl))
-        subprocess.check_call([sys.executable, os.path.join(HERE, "pmc_summary.py"), *dirs, "--workload", wl,
-                               "--batch", str(batch), "--json", out], stdout=subprocess.DEVNULL)
+        made = os.path.join(ROOT, "gpurun_out", "pmcsum", "pmc_%s_%s.json" % (tag, wl))
+        if dirs:
+            subprocess.check_call([sys.executable, os.path.join(HERE, "pmc_summary.py"), *dirs, "--workload", wl,
+                                   "--batch", str(batch), "--json", out], stdout=subprocess.DEVNULL)
+        elif not box and os.path.exists(made):   # summarised on the box (pmcsum): take it as is
+            shutil.copyfile(made, out)
+        else:
+            continue
         print("wrote", os.path.relpath(out, ROOT))
         if box:
             for d in dirs:
